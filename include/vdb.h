@@ -1,0 +1,147 @@
+/*
+ * vdb.h — C-ABI of the MI355X (gfx950) brute-force vector-search core.
+ *
+ * This is the drop-in boundary for the hot path of Theseus-AT/mlx-vector-db.
+ * The reference has no FFI of its own: its "operator slot" is the Python
+ * callable `MLXVectorStore._compiled_similarity_fn(query, vectors) -> scores[N]`
+ * followed by `mx.argsort(...)[:k]`
+ * (reference service/optimized_vector_store.py:31-48, :149-192, :211-213) and
+ * the batched variant in performance/mlx_optimized.py:59-88, :217-248.
+ * Each entry point below names the reference interface it replaces.
+ * A ctypes binding (mlx-vector-db_amd/service/_vdb.py) is the host side; the
+ * binding a maintainer would add to the reference is shown in INTEGRATION.md.
+ *
+ * Conventions
+ *   - Every function returns an int32 status (VDB_OK = 0, negative = error
+ *     class); vdb_last_error() returns a thread-local message for the last
+ *     failing call on the calling thread.
+ *   - Plain pointers and sizes only.  `mem` says whether the query / output
+ *     pointers of a call are host (VDB_MEM_HOST) or device (VDB_MEM_DEVICE)
+ *     memory.  Host-memory calls are synchronous; device-memory calls are
+ *     stream-ordered on `stream` (a hipStream_t, or NULL for the index's own
+ *     stream) and return without waiting.
+ *   - The library never frees caller memory.  An index owns its device-resident
+ *     corpus (tiled fp32 layout) and a per-call workspace pool.
+ *   - All entry points are thread-safe; searches on one index may run from
+ *     several threads at once (the reference serves from a 4-thread executor,
+ *     api/routes/vectors.py:43).
+ *
+ * Result contract:
+ *   cosine    score = (q/max(|q|,1e-8)) . (x/max(|x|,1e-8))   higher first
+ *   euclidean score = sqrt(sum((x-q)^2))                        lower first
+ *   Ranking is by the exact (fp64, canonical summation order) value with ties
+ *   broken by the lower row index; returned scores are that value rounded to
+ *   fp32.  Rows beyond the number of eligible rows are returned as index -1.
+ */
+#ifndef VDB_H
+#define VDB_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+    VDB_OK = 0,
+    VDB_ERR_INVALID = -1,     /* bad argument -> Python ValueError          */
+    VDB_ERR_HIP = -2,         /* HIP runtime error -> RuntimeError          */
+    VDB_ERR_OOM = -3,         /* device allocation failed                   */
+    VDB_ERR_NONFINITE = -4,   /* NaN/Inf in vectors or queries -> ValueError */
+    VDB_ERR_UNSUPPORTED = -5, /* e.g. metric "dot_product" (reference raises,
+                                 service/optimized_vector_store.py:153-154)   */
+    VDB_ERR_NODEVICE = -6     /* no gfx950 device visible                    */
+};
+
+enum { VDB_METRIC_COSINE = 0, VDB_METRIC_EUCLIDEAN = 1 };
+enum { VDB_MEM_HOST = 0, VDB_MEM_DEVICE = 1 };
+
+/* Candidate-pass arithmetic for an index (vdb_index_set_param "precision"). */
+enum { VDB_PREC_FP32 = 0, VDB_PREC_BF16 = 1 };
+
+typedef struct vdb_index vdb_index;
+
+/* --- library -------------------------------------------------------------- */
+const char* vdb_last_error(void);
+int32_t vdb_version(void);
+/* Number of visible HIP devices (0 on a host without a GPU). */
+int32_t vdb_device_count(int32_t* n);
+
+/* --- index lifecycle -------------------------------------------------------
+ * Replaces MLXVectorStore's corpus state `self._vectors` (mx.array [N,D] f32)
+ * and `_compile_critical_functions` (service/optimized_vector_store.py:59-83,
+ * :211-213).  metric: VDB_METRIC_*.  Any other metric -> VDB_ERR_UNSUPPORTED,
+ * matching the reference, where "dot_product" leaves no operator and every
+ * query raises. */
+int32_t vdb_index_create(int32_t dim, int32_t metric, int32_t device, vdb_index** out);
+int32_t vdb_index_destroy(vdb_index* idx);
+/* Pre-size the device corpus for `rows` rows (capacity otherwise doubles). */
+int32_t vdb_index_reserve(vdb_index* idx, int64_t rows);
+/* Tuning / test knobs: "precision" (VDB_PREC_*), "margin" (extra candidates
+ * per query), "force_exact" (0/1), "n_wg" (candidate-pass workgroups). */
+int32_t vdb_index_set_param(vdb_index* idx, const char* name, int64_t value);
+int32_t vdb_index_get_stat(const vdb_index* idx, const char* name, int64_t* value);
+
+/* --- ingest ------------------------------------------------------------------
+ * Replaces MLXVectorStore.add_vectors' `mx.concatenate([old, new])`
+ * (service/optimized_vector_store.py:96-106; mlx_optimized.py:127-137).
+ * Appends n rows of `dim` fp32 (row-major) in place (capacity doubling), packs
+ * them into the MFMA-tiled layout and computes the per-row norms once.
+ * Non-finite input -> VDB_ERR_NONFINITE and nothing is appended. */
+int32_t vdb_index_add(vdb_index* idx, const float* vectors, int64_t n, int32_t mem, void* stream);
+int32_t vdb_index_count(const vdb_index* idx, int64_t* n);
+/* Replaces MLXVectorStore.clear (service/optimized_vector_store.py:198-209). */
+int32_t vdb_index_clear(vdb_index* idx);
+/* Copy rows [start, start+n) back out, row-major fp32, to host memory (used for
+ * vectors.npz persistence, service/optimized_vector_store.py:218-223). */
+int32_t vdb_index_get_vectors(vdb_index* idx, int64_t start, int64_t n, float* out_host);
+
+/* --- search ------------------------------------------------------------------
+ * Replaces `_brute_force_search`: similarity fn + mx.argsort(...)[:k] + gather
+ * (service/optimized_vector_store.py:149-192) for B=1, and
+ * `optimized_batch_similarity_search` (performance/mlx_optimized.py:217-248)
+ * for B>1.
+ *   queries      [n_queries, dim] fp32 row-major (host or device per `mem`)
+ *   k            1..1024 results per query (min(k, eligible rows) are valid)
+ *   row_mask     NULL, or a bitmap of ceil(count/32) uint32 words (bit r of
+ *                word r/32 = row r eligible): the metadata filter
+ *                (service/optimized_vector_store.py:159-167); same memory kind
+ *                as `mem`.
+ *   out_scores   [n_queries, k] fp32 (cosine similarity / euclidean distance)
+ *   out_indices  [n_queries, k] int64 row ids (+ index_offset), -1 = no result
+ *   out_keys     NULL or [n_queries, k] fp64 exact ranking keys (cosine: the
+ *                similarity; euclidean: minus the squared distance) — what a
+ *                multi-GPU merge needs to stay bit-identical to one GPU.
+ */
+int32_t vdb_index_search(vdb_index* idx, const float* queries, int32_t n_queries, int32_t k,
+                         const uint32_t* row_mask, int32_t mem,
+                         float* out_scores, int64_t* out_indices, double* out_keys,
+                         int64_t index_offset, void* stream);
+
+/* --- multi-GPU merge -----------------------------------------------------------
+ * Merge per-shard top-k lists (all device memory, already all-gathered):
+ *   keys [n_lists, n_queries, k_in] fp64 ranking keys (higher first),
+ *   idx  [n_lists, n_queries, k_in] int64 global row ids (-1 = empty)
+ * into the global top-k_out per query, ordered by (key desc, index asc) —
+ * bit-identical to a single-GPU search.  No reference counterpart (the
+ * reference is single device); SURVEY.md §8e. */
+int32_t vdb_merge_topk(const double* keys, const int64_t* idx, int32_t n_lists, int32_t n_queries,
+                       int32_t k_in, int32_t k_out, int32_t metric,
+                       float* out_scores, int64_t* out_indices, double* out_keys, void* stream);
+
+/* --- stateless operator slot ---------------------------------------------------
+ * The reference's similarity functions themselves, returning every score
+ * (no top-k): `_compiled_cosine_similarity` / `_compiled_euclidean_distance`
+ * (service/optimized_vector_store.py:31-48) for n_queries = 1 and
+ * `compute_cosine_similarity_batch` (performance/mlx_optimized.py:59-88) for
+ * n_queries > 1.  All pointers are device memory: corpus [n, dim] row-major
+ * fp32, queries [n_queries, dim], out [n_queries, n] fp32.  fp32 arithmetic
+ * (normalise, then MFMA dot), within 1e-4 of the reference. */
+int32_t vdb_similarity_matrix(const float* corpus, int64_t n, int32_t dim,
+                              const float* queries, int32_t n_queries, int32_t metric,
+                              float* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VDB_H */

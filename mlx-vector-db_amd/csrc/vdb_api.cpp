@@ -1,0 +1,609 @@
+// vdb_api.cpp — the C-ABI (include/vdb.h): index object, workspace pool and the
+// search driver that sequences the kernels of vdb_kernels.hip.
+//
+// Host-side restatement of the reference store's operator flow
+// (service/optimized_vector_store.py:96-192): ingest appends rows in place and
+// computes norms once (instead of re-normalising the corpus on every query,
+// :31-41); search = candidate pass + exact rerank instead of a full argsort
+// (:176-183).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <shared_mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/vdb.h"
+#include "vdb_internal.h"
+
+using namespace vdb;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int set_error(int code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                                  \
+    do {                                                                                               \
+        hipError_t _e = (expr);                                                                        \
+        if (_e != hipSuccess)                                                                          \
+            return set_error(_e == hipErrorOutOfMemory ? VDB_ERR_OOM : VDB_ERR_HIP, "%s failed: %s (%s:%d)", \
+                             #expr, hipGetErrorString(_e), __FILE__, __LINE__);                        \
+    } while (0)
+
+constexpr int64_t kStepRows = STEP_ROWS;   // rows per scan step (4 waves x 2 row tiles x 32)
+constexpr int kMaxApproxK = 200;          // k above this uses the exact path
+
+inline int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
+inline int next_pow2(int v) {
+    int p = 1;
+    while (p < v) p <<= 1;
+    return p;
+}
+
+// Bump allocator over one device buffer (256-B aligned carve).
+struct Carver {
+    char* base;
+    size_t off = 0;
+    template <typename T>
+    T* take(size_t count) {
+        off = (off + 255) & ~size_t(255);
+        T* p = reinterpret_cast<T*>(base + off);
+        off += count * sizeof(T);
+        return p;
+    }
+};
+
+struct Workspace {
+    char* dev = nullptr;
+    size_t dev_bytes = 0;
+    char* exact = nullptr;  // exact-path lists, grown on demand
+    size_t exact_bytes = 0;
+    int* host_flag = nullptr;  // pinned
+    hipEvent_t done = nullptr;
+    bool busy = false;
+    bool used = false;
+};
+
+}  // namespace
+
+struct vdb_index {
+    int dim = 0, metric = 0, device = 0;
+    int Dp = 0, G = 0;
+    int64_t count = 0;
+    int64_t cap_rows = 0;  // multiple of kStepRows
+    float* X = nullptr;
+    double* nrm64 = nullptr;
+    float* inv32 = nullptr;
+    float* sq32 = nullptr;
+    unsigned long long* d_xmax = nullptr;
+    int* d_nonfinite = nullptr;
+    double xmax = 0.0;
+    hipStream_t stream = nullptr;
+    int n_cu = 256;
+    // knobs
+    int64_t precision = VDB_PREC_FP32;
+    int64_t margin = -1;  // -1 = default
+    int64_t force_exact = 0;
+    int64_t n_wg_override = 0;
+    // stats
+    std::atomic<int64_t> n_searches{0}, n_queries{0}, n_fallback{0};
+    std::shared_mutex mu;  // add/clear/reserve exclusive; search shared
+    std::mutex ws_mu;
+    std::vector<Workspace*> pool;
+};
+
+namespace {
+
+int ensure_capacity(vdb_index* ix, int64_t rows) {
+    if (rows <= ix->cap_rows) return VDB_OK;
+    int64_t cap = std::max<int64_t>(ix->cap_rows * 2, kStepRows);
+    while (cap < rows) cap *= 2;
+    cap = round_up(cap, kStepRows);
+    const size_t tile_floats = (size_t)ix->G * BLOCK_FLOATS;
+    float* X = nullptr;
+    double* n64 = nullptr;
+    float *i32 = nullptr, *s32 = nullptr;
+    HIP_TRY(hipMalloc(&X, (size_t)(cap / 32) * tile_floats * sizeof(float)));
+    HIP_TRY(hipMalloc(&n64, cap * sizeof(double)));
+    HIP_TRY(hipMalloc(&i32, cap * sizeof(float)));
+    HIP_TRY(hipMalloc(&s32, cap * sizeof(float)));
+    HIP_TRY(hipMemsetAsync(X, 0, (size_t)(cap / 32) * tile_floats * sizeof(float), ix->stream));
+    HIP_TRY(hipMemsetAsync(n64, 0, cap * sizeof(double), ix->stream));
+    HIP_TRY(hipMemsetAsync(i32, 0, cap * sizeof(float), ix->stream));
+    HIP_TRY(hipMemsetAsync(s32, 0, cap * sizeof(float), ix->stream));
+    if (ix->X) {
+        // all searches that might read the old buffers must be finished
+        HIP_TRY(hipDeviceSynchronize());
+        const int64_t used_tiles = round_up(ix->count, 32) / 32;
+        HIP_TRY(hipMemcpyAsync(X, ix->X, (size_t)used_tiles * tile_floats * sizeof(float), hipMemcpyDeviceToDevice,
+                               ix->stream));
+        HIP_TRY(hipMemcpyAsync(n64, ix->nrm64, ix->count * sizeof(double), hipMemcpyDeviceToDevice, ix->stream));
+        HIP_TRY(hipMemcpyAsync(i32, ix->inv32, ix->count * sizeof(float), hipMemcpyDeviceToDevice, ix->stream));
+        HIP_TRY(hipMemcpyAsync(s32, ix->sq32, ix->count * sizeof(float), hipMemcpyDeviceToDevice, ix->stream));
+        HIP_TRY(hipStreamSynchronize(ix->stream));
+        (void)hipFree(ix->X);
+        (void)hipFree(ix->nrm64);
+        (void)hipFree(ix->inv32);
+        (void)hipFree(ix->sq32);
+    }
+    ix->X = X;
+    ix->nrm64 = n64;
+    ix->inv32 = i32;
+    ix->sq32 = s32;
+    ix->cap_rows = cap;
+    HIP_TRY(hipStreamSynchronize(ix->stream));
+    return VDB_OK;
+}
+
+Workspace* acquire_ws(vdb_index* ix) {
+    std::lock_guard<std::mutex> g(ix->ws_mu);
+    for (Workspace* w : ix->pool) {
+        if (!w->busy) {
+            w->busy = true;
+            return w;
+        }
+    }
+    Workspace* w = new Workspace();
+    w->busy = true;
+    ix->pool.push_back(w);
+    return w;
+}
+
+void release_ws(vdb_index* ix, Workspace* w, hipStream_t st) {
+    if (w->done == nullptr) (void)hipEventCreateWithFlags(&w->done, hipEventDisableTiming);
+    (void)hipEventRecord(w->done, st);
+    w->used = true;
+    std::lock_guard<std::mutex> g(ix->ws_mu);
+    w->busy = false;
+}
+
+// Make the workspace at least `bytes` large and stream-ordered after its last use.
+int ws_reserve(Workspace* w, size_t bytes, hipStream_t st) {
+    if (w->used && w->done) HIP_TRY(hipStreamWaitEvent(st, w->done, 0));
+    if (!w->host_flag) HIP_TRY(hipHostMalloc(&w->host_flag, 64 * sizeof(int), hipHostMallocDefault));
+    if (bytes > w->dev_bytes) {
+        if (w->dev) {
+            HIP_TRY(hipStreamSynchronize(st));
+            (void)hipFree(w->dev);
+            w->dev = nullptr;
+        }
+        size_t nb = std::max(bytes, w->dev_bytes * 2);
+        HIP_TRY(hipMalloc(&w->dev, nb));
+        w->dev_bytes = nb;
+    }
+    return VDB_OK;
+}
+
+int ws_reserve_exact(Workspace* w, size_t bytes, hipStream_t st) {
+    if (bytes > w->exact_bytes) {
+        if (w->exact) {
+            HIP_TRY(hipStreamSynchronize(st));
+            (void)hipFree(w->exact);
+            w->exact = nullptr;
+        }
+        HIP_TRY(hipMalloc(&w->exact, bytes));
+        w->exact_bytes = bytes;
+    }
+    return VDB_OK;
+}
+
+bool all_finite(const float* p, int64_t n) {
+    for (int64_t i = 0; i < n; ++i)
+        if (!std::isfinite(p[i])) return false;
+    return true;
+}
+
+// Exact full scan for queries qlist[0..nq) (device list) -> writes outputs.
+int run_exact(vdb_index* ix, Workspace* w, const float* Qd, const double* qn64, const int* qlist_dev, int nq, int k,
+              const uint32_t* mask_dev, float* out_s, int64_t* out_i, double* out_k, int64_t index_offset,
+              hipStream_t st) {
+    const int KE = std::max(32, next_pow2(k));
+    const int64_t N = ix->count;
+    // ~8 workgroups per CU of rows, at least 64 rows per wave
+    int n_wg = (int)std::min<int64_t>(std::max<int64_t>(1, ix->n_cu * 2), std::max<int64_t>(1, N / 256));
+    const int64_t rpw = (N + n_wg - 1) / n_wg;
+    n_wg = (int)((N + rpw - 1) / rpw);
+    const int n_lists = n_wg * 4;
+    const size_t list_elems = (size_t)nq * n_lists * KE;
+    const size_t bytes = list_elems * (sizeof(double) + sizeof(uint32_t)) + (size_t)nq * KE * 12 + 4096;
+    int rc = ws_reserve_exact(w, bytes, st);
+    if (rc) return rc;
+    Carver c{w->exact};
+    double* lk = c.take<double>(list_elems);
+    uint32_t* li = c.take<uint32_t>(list_elems);
+    double* mk = c.take<double>((size_t)nq * KE);
+    uint32_t* mi = c.take<uint32_t>((size_t)nq * KE);
+    HIP_TRY(launch_exact_scan(ix->metric, KE, Qd, qn64, qlist_dev, nq, ix->X, ix->G, ix->dim, ix->nrm64, mask_dev, N,
+                              n_wg, rpw, lk, li, st));
+    HIP_TRY(launch_merge_f64_u32(KE, lk, li, n_lists, KE, (int64_t)n_lists * KE, KE, nq, mk, mi, st));
+    HIP_TRY(launch_finalize_u32(ix->metric, mk, mi, KE, nq, qlist_dev, k, index_offset, out_s, out_i, out_k, st));
+    return VDB_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* vdb_last_error(void) { return g_last_error.c_str(); }
+
+int32_t vdb_version(void) { return 1; }
+
+int32_t vdb_device_count(int32_t* n) {
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    if (e != hipSuccess) c = 0;
+    if (n) *n = c;
+    return VDB_OK;
+}
+
+int32_t vdb_index_create(int32_t dim, int32_t metric, int32_t device, vdb_index** out) {
+    if (!out) return set_error(VDB_ERR_INVALID, "out is NULL");
+    *out = nullptr;
+    if (dim <= 0 || dim > 65536) return set_error(VDB_ERR_INVALID, "dimension must be in [1, 65536], got %d", dim);
+    if (metric != VDB_METRIC_COSINE && metric != VDB_METRIC_EUCLIDEAN)
+        return set_error(VDB_ERR_UNSUPPORTED, "unsupported metric id %d (cosine=0, euclidean=1)", metric);
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return set_error(VDB_ERR_NODEVICE, "no HIP device visible: the vdb core needs an MI355X (gfx950)");
+    if (device < 0 || device >= ndev) return set_error(VDB_ERR_INVALID, "device %d out of range [0,%d)", device, ndev);
+    HIP_TRY(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return set_error(VDB_ERR_NODEVICE, "device %d is %s; this build targets gfx950 only", device,
+                         prop.gcnArchName);
+    vdb_index* ix = new vdb_index();
+    ix->dim = dim;
+    ix->metric = metric;
+    ix->device = device;
+    ix->Dp = (int)round_up(dim, 32);
+    ix->G = ix->Dp / GROUP_DIMS;
+    ix->n_cu = prop.multiProcessorCount;
+    hipError_t e = hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc(&ix->d_xmax, 64);
+    if (e == hipSuccess) e = hipMemset(ix->d_xmax, 0, 64);
+    if (e != hipSuccess) {
+        delete ix;
+        return set_error(VDB_ERR_HIP, "index setup failed: %s", hipGetErrorString(e));
+    }
+    ix->d_nonfinite = reinterpret_cast<int*>(reinterpret_cast<char*>(ix->d_xmax) + 32);
+    *out = ix;
+    return VDB_OK;
+}
+
+int32_t vdb_index_destroy(vdb_index* ix) {
+    if (!ix) return VDB_OK;
+    (void)hipSetDevice(ix->device);
+    (void)hipDeviceSynchronize();
+    for (Workspace* w : ix->pool) {
+        if (w->dev) (void)hipFree(w->dev);
+        if (w->exact) (void)hipFree(w->exact);
+        if (w->host_flag) (void)hipHostFree(w->host_flag);
+        if (w->done) (void)hipEventDestroy(w->done);
+        delete w;
+    }
+    if (ix->X) (void)hipFree(ix->X);
+    if (ix->nrm64) (void)hipFree(ix->nrm64);
+    if (ix->inv32) (void)hipFree(ix->inv32);
+    if (ix->sq32) (void)hipFree(ix->sq32);
+    if (ix->d_xmax) (void)hipFree(ix->d_xmax);
+    if (ix->stream) (void)hipStreamDestroy(ix->stream);
+    delete ix;
+    return VDB_OK;
+}
+
+int32_t vdb_index_reserve(vdb_index* ix, int64_t rows) {
+    if (!ix) return set_error(VDB_ERR_INVALID, "index is NULL");
+    if (rows < 0) return set_error(VDB_ERR_INVALID, "rows must be >= 0");
+    HIP_TRY(hipSetDevice(ix->device));
+    std::unique_lock<std::shared_mutex> g(ix->mu);
+    return ensure_capacity(ix, rows);
+}
+
+int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
+    if (!ix || !name) return set_error(VDB_ERR_INVALID, "NULL argument");
+    std::string n(name);
+    if (n == "precision") {
+        if (value != VDB_PREC_FP32) return set_error(VDB_ERR_UNSUPPORTED, "precision %lld not built yet", (long long)value);
+        ix->precision = value;
+    } else if (n == "margin") {
+        ix->margin = value;
+    } else if (n == "force_exact") {
+        ix->force_exact = value != 0;
+    } else if (n == "n_wg") {
+        ix->n_wg_override = value;
+    } else {
+        return set_error(VDB_ERR_INVALID, "unknown parameter '%s'", name);
+    }
+    return VDB_OK;
+}
+
+int32_t vdb_index_get_stat(const vdb_index* ix, const char* name, int64_t* value) {
+    if (!ix || !name || !value) return set_error(VDB_ERR_INVALID, "NULL argument");
+    std::string n(name);
+    if (n == "searches") *value = ix->n_searches.load();
+    else if (n == "queries") *value = ix->n_queries.load();
+    else if (n == "fallback_queries") *value = ix->n_fallback.load();
+    else if (n == "capacity") *value = ix->cap_rows;
+    else if (n == "count") *value = ix->count;
+    else if (n == "device_bytes") *value = (int64_t)(ix->cap_rows / 32) * ix->G * BLOCK_FLOATS * 4 + ix->cap_rows * 16;
+    else return set_error(VDB_ERR_INVALID, "unknown stat '%s'", name);
+    return VDB_OK;
+}
+
+int32_t vdb_index_add(vdb_index* ix, const float* vectors, int64_t n, int32_t mem, void* stream) {
+    if (!ix) return set_error(VDB_ERR_INVALID, "index is NULL");
+    if (n < 0) return set_error(VDB_ERR_INVALID, "n must be >= 0");
+    if (n == 0) return VDB_OK;
+    if (!vectors) return set_error(VDB_ERR_INVALID, "vectors is NULL");
+    if (ix->count + n > (int64_t)0xFFFFFFFE) return set_error(VDB_ERR_INVALID, "index is limited to 2^32-2 rows");
+    HIP_TRY(hipSetDevice(ix->device));
+    std::unique_lock<std::shared_mutex> g(ix->mu);
+    hipStream_t st = ix->stream;
+    int rc = ensure_capacity(ix, ix->count + n);
+    if (rc) return rc;
+    HIP_TRY(hipMemsetAsync(ix->d_nonfinite, 0, sizeof(int), st));
+    const int D = ix->dim;
+    const int64_t chunk = std::max<int64_t>(1, (int64_t)(256ll << 20) / ((int64_t)D * 4));
+    float* staging = nullptr;
+    if (mem == VDB_MEM_HOST) HIP_TRY(hipMalloc(&staging, (size_t)std::min(chunk, n) * D * sizeof(float)));
+    for (int64_t r = 0; r < n; r += chunk) {
+        const int64_t m = std::min(chunk, n - r);
+        const float* src = vectors + r * D;
+        if (mem == VDB_MEM_HOST) {
+            hipError_t e = hipMemcpyAsync(staging, src, (size_t)m * D * sizeof(float), hipMemcpyHostToDevice, st);
+            if (e == hipSuccess) e = launch_pack_rows(staging, m, D, ix->G, ix->X, ix->count + r, ix->nrm64,
+                                                      ix->inv32, ix->sq32, ix->d_xmax, ix->d_nonfinite, st);
+            if (e == hipSuccess) e = hipStreamSynchronize(st);  // staging reuse
+            if (e != hipSuccess) {
+                (void)hipFree(staging);
+                return set_error(VDB_ERR_HIP, "ingest failed: %s", hipGetErrorString(e));
+            }
+        } else {
+            HIP_TRY(launch_pack_rows(src, m, D, ix->G, ix->X, ix->count + r, ix->nrm64, ix->inv32, ix->sq32,
+                                     ix->d_xmax, ix->d_nonfinite, st));
+        }
+    }
+    if (staging) (void)hipFree(staging);
+    (void)stream;  // ingest always runs on the index's own stream (serialised with growth)
+    int nonfinite = 0;
+    unsigned long long xb = 0;
+    HIP_TRY(hipMemcpyAsync(&nonfinite, ix->d_nonfinite, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(&xb, ix->d_xmax, sizeof(xb), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (nonfinite) {
+        // rows past `count` are never read; the next add overwrites them
+        const int64_t used_tiles = round_up(ix->count + n, 32) / 32;
+        (void)used_tiles;
+        return set_error(VDB_ERR_NONFINITE, "%d row(s) contain NaN or Inf; nothing was added", nonfinite);
+    }
+    double xm;
+    std::memcpy(&xm, &xb, sizeof(xm));
+    ix->xmax = xm;
+    ix->count += n;
+    return VDB_OK;
+}
+
+int32_t vdb_index_count(const vdb_index* ix, int64_t* n) {
+    if (!ix || !n) return set_error(VDB_ERR_INVALID, "NULL argument");
+    *n = ix->count;
+    return VDB_OK;
+}
+
+int32_t vdb_index_clear(vdb_index* ix) {
+    if (!ix) return set_error(VDB_ERR_INVALID, "index is NULL");
+    HIP_TRY(hipSetDevice(ix->device));
+    std::unique_lock<std::shared_mutex> g(ix->mu);
+    HIP_TRY(hipDeviceSynchronize());
+    if (ix->X) {
+        HIP_TRY(hipMemsetAsync(ix->X, 0, (size_t)(ix->cap_rows / 32) * ix->G * BLOCK_FLOATS * sizeof(float),
+                               ix->stream));
+        HIP_TRY(hipMemsetAsync(ix->nrm64, 0, ix->cap_rows * sizeof(double), ix->stream));
+    }
+    HIP_TRY(hipMemsetAsync(ix->d_xmax, 0, 64, ix->stream));
+    HIP_TRY(hipStreamSynchronize(ix->stream));
+    ix->count = 0;
+    ix->xmax = 0.0;
+    return VDB_OK;
+}
+
+int32_t vdb_index_get_vectors(vdb_index* ix, int64_t start, int64_t n, float* out_host) {
+    if (!ix || (!out_host && n > 0)) return set_error(VDB_ERR_INVALID, "NULL argument");
+    if (start < 0 || n < 0 || start + n > ix->count)
+        return set_error(VDB_ERR_INVALID, "rows [%lld, %lld) out of range [0, %lld)", (long long)start,
+                         (long long)(start + n), (long long)ix->count);
+    if (n == 0) return VDB_OK;
+    HIP_TRY(hipSetDevice(ix->device));
+    std::shared_lock<std::shared_mutex> g(ix->mu);
+    const int D = ix->dim;
+    const int64_t chunk = std::max<int64_t>(1, (int64_t)(256ll << 20) / ((int64_t)D * 4));
+    float* tmp = nullptr;
+    HIP_TRY(hipMalloc(&tmp, (size_t)std::min(chunk, n) * D * sizeof(float)));
+    for (int64_t r = 0; r < n; r += chunk) {
+        const int64_t m = std::min(chunk, n - r);
+        hipError_t e = launch_unpack_rows(ix->X, ix->G, D, start + r, m, tmp, ix->stream);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(out_host + r * D, tmp, (size_t)m * D * sizeof(float), hipMemcpyDeviceToHost, ix->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(ix->stream);
+        if (e != hipSuccess) {
+            (void)hipFree(tmp);
+            return set_error(VDB_ERR_HIP, "export failed: %s", hipGetErrorString(e));
+        }
+    }
+    (void)hipFree(tmp);
+    return VDB_OK;
+}
+
+int32_t vdb_index_search(vdb_index* ix, const float* queries, int32_t B, int32_t k, const uint32_t* row_mask,
+                         int32_t mem, float* out_scores, int64_t* out_indices, double* out_keys,
+                         int64_t index_offset, void* stream) {
+    if (!ix) return set_error(VDB_ERR_INVALID, "index is NULL");
+    if (B <= 0) return set_error(VDB_ERR_INVALID, "n_queries must be >= 1, got %d", B);
+    if (k <= 0 || k > 1024) return set_error(VDB_ERR_INVALID, "k must be in [1, 1024], got %d", k);
+    if (!queries || !out_scores || !out_indices) return set_error(VDB_ERR_INVALID, "NULL query/output pointer");
+    if (mem != VDB_MEM_HOST && mem != VDB_MEM_DEVICE) return set_error(VDB_ERR_INVALID, "bad mem kind %d", mem);
+    const int D = ix->dim;
+    if (mem == VDB_MEM_HOST && !all_finite(queries, (int64_t)B * D))
+        return set_error(VDB_ERR_NONFINITE, "query contains NaN or Inf");
+    HIP_TRY(hipSetDevice(ix->device));
+    std::shared_lock<std::shared_mutex> g(ix->mu);
+    hipStream_t st = stream ? (hipStream_t)stream : ix->stream;
+    const int64_t N = ix->count;
+    ix->n_searches++;
+    ix->n_queries += B;
+
+    // ---- sizes ----------------------------------------------------------------
+    const int margin = ix->margin >= 0 ? (int)ix->margin : std::max(16, k / 4);
+    int KP = std::max(32, next_pow2(k + margin));
+    const bool exact_all = ix->force_exact || k > kMaxApproxK || KP > 256;
+    if (KP > 256) KP = 256;
+    const int QB = KP == 256 ? 32 : 64;
+    const int Bp = (int)round_up(B, 64);
+    const int n_qblocks = Bp / QB;
+    const int64_t n_steps = std::max<int64_t>(1, round_up(N, kStepRows) / kStepRows);
+    int target = ix->n_wg_override > 0 ? (int)ix->n_wg_override : std::max(1, ix->n_cu * 2 / n_qblocks);
+    int spw = (int)std::max<int64_t>(1, (n_steps + target - 1) / target);
+    int n_wg = (int)((n_steps + spw - 1) / spw);
+    const int64_t mask_words = round_up(N, 32) / 32;
+
+    Workspace* w = acquire_ws(ix);
+    struct Releaser {
+        vdb_index* ix; Workspace* w; hipStream_t st;
+        ~Releaser() { release_ws(ix, w, st); }
+    } rel{ix, w, st};
+
+    size_t bytes = 0;
+    bytes += (size_t)B * D * 4 + 256;                       // Qraw (host mode)
+    bytes += (size_t)(mask_words + 64) * 4 + 256;           // mask (host mode)
+    bytes += (size_t)Bp * ix->Dp * 4 + 256;                 // Qt
+    bytes += (size_t)Bp * 8 + 256;                          // qn64
+    bytes += (size_t)Bp * n_wg * KP * 8 + 512;              // candidate lists
+    bytes += (size_t)Bp * KP * 8 + 512;                     // merged approx lists
+    bytes += (size_t)B * k * 20 + 768;                      // outputs (host mode)
+    bytes += (size_t)(B + 64) * 4 + 256;                    // flags
+    int rc = ws_reserve(w, bytes, st);
+    if (rc) return rc;
+    Carver c{w->dev};
+    float* Qraw = c.take<float>((size_t)B * D);
+    uint32_t* maskd = c.take<uint32_t>(mask_words + 64);
+    float* Qt = c.take<float>((size_t)Bp * ix->Dp);
+    double* qn64 = c.take<double>(Bp);
+    float* cs = c.take<float>((size_t)Bp * n_wg * KP);
+    uint32_t* ci = c.take<uint32_t>((size_t)Bp * n_wg * KP);
+    float* as = c.take<float>((size_t)Bp * KP);
+    uint32_t* ai = c.take<uint32_t>((size_t)Bp * KP);
+    float* os = c.take<float>((size_t)B * k);
+    int64_t* oi = c.take<int64_t>((size_t)B * k);
+    double* ok = c.take<double>((size_t)B * k);
+    int* flags = c.take<int>(B + 64);
+
+    const float* Qd = queries;
+    const uint32_t* md = row_mask;
+    float* out_s = out_scores;
+    int64_t* out_i = out_indices;
+    double* out_k = out_keys;
+    if (mem == VDB_MEM_HOST) {
+        HIP_TRY(hipMemcpyAsync(Qraw, queries, (size_t)B * D * 4, hipMemcpyHostToDevice, st));
+        Qd = Qraw;
+        if (row_mask && N > 0) {
+            HIP_TRY(hipMemcpyAsync(maskd, row_mask, (size_t)mask_words * 4, hipMemcpyHostToDevice, st));
+            md = maskd;
+        }
+        out_s = os;
+        out_i = oi;
+        out_k = out_keys ? ok : nullptr;
+    }
+
+    if (N == 0) {
+        // empty store: every slot "no result" (reference returns ([],[],[]), :117)
+        HIP_TRY(hipMemsetAsync(out_i, 0xFF, (size_t)B * k * 8, st));
+        HIP_TRY(hipMemsetAsync(out_s, 0, (size_t)B * k * 4, st));
+        if (out_k) HIP_TRY(hipMemsetAsync(out_k, 0, (size_t)B * k * 8, st));
+    } else {
+        HIP_TRY(hipMemsetAsync(Qt, 0, (size_t)Bp * ix->Dp * 4, st));
+        HIP_TRY(hipMemsetAsync(qn64, 0, (size_t)Bp * 8, st));
+        HIP_TRY(launch_prep_queries(Qd, B, D, ix->G, ix->metric, Qt, qn64, st));
+        int n_flag = 0;
+        if (!exact_all) {
+            HIP_TRY(hipMemsetAsync(flags, 0, sizeof(int), st));
+            HIP_TRY(launch_scan_topk(ix->metric, KP, ix->X, ix->metric == 0 ? ix->inv32 : ix->sq32, md, Qt, ix->G, N,
+                                     B, n_qblocks, n_steps, n_wg, spw, cs, ci, st));
+            HIP_TRY(launch_merge_f32(KP, cs, ci, n_wg, B, as, ai, st));
+            RerankArgs ra;
+            ra.Q = Qd; ra.qn64 = qn64; ra.X = ix->X; ra.G = ix->G; ra.D = D;
+            ra.nrm64 = ix->nrm64; ra.app_s = as; ra.app_i = ai; ra.k = k;
+            ra.eps_rel = 1.01 * (double)(ix->Dp + 8) * std::ldexp(1.0, -24);
+            ra.xmax = ix->xmax;
+            ra.out_s = out_s; ra.out_i = out_i; ra.out_k = out_k; ra.index_offset = index_offset;
+            ra.flag_count = flags; ra.flag_list = flags + 1;
+            HIP_TRY(launch_rerank(ix->metric, KP, ra, B, st));
+            HIP_TRY(hipMemcpyAsync(w->host_flag, flags, sizeof(int), hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+            n_flag = w->host_flag[0];
+            if (n_flag > 0) {
+                ix->n_fallback += n_flag;
+                rc = run_exact(ix, w, Qd, qn64, flags + 1, n_flag, k, md, out_s, out_i, out_k, index_offset, st);
+                if (rc) return rc;
+            }
+        } else {
+            ix->n_fallback += B;
+            rc = run_exact(ix, w, Qd, qn64, nullptr, B, k, md, out_s, out_i, out_k, index_offset, st);
+            if (rc) return rc;
+        }
+    }
+    if (mem == VDB_MEM_HOST) {
+        HIP_TRY(hipMemcpyAsync(out_scores, out_s, (size_t)B * k * 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(out_indices, out_i, (size_t)B * k * 8, hipMemcpyDeviceToHost, st));
+        if (out_keys) HIP_TRY(hipMemcpyAsync(out_keys, out_k, (size_t)B * k * 8, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+    }
+    return VDB_OK;
+}
+
+int32_t vdb_merge_topk(const double* keys, const int64_t* idx, int32_t n_lists, int32_t nq, int32_t k_in,
+                       int32_t k_out, int32_t metric, float* out_scores, int64_t* out_indices, double* out_keys,
+                       void* stream) {
+    if (!keys || !idx || !out_scores || !out_indices) return set_error(VDB_ERR_INVALID, "NULL argument");
+    if (n_lists <= 0 || nq <= 0 || k_in <= 0 || k_out <= 0 || k_out > 1024 || k_in > 1024)
+        return set_error(VDB_ERR_INVALID, "bad sizes n_lists=%d nq=%d k_in=%d k_out=%d", n_lists, nq, k_in, k_out);
+    if (metric != 0 && metric != 1) return set_error(VDB_ERR_UNSUPPORTED, "metric %d", metric);
+    hipStream_t st = (hipStream_t)stream;
+    const int KP = std::max(32, next_pow2(std::max(k_in, k_out)));
+    double* mk = nullptr;
+    int64_t* mi = nullptr;
+    HIP_TRY(hipMallocAsync((void**)&mk, (size_t)nq * KP * 8, st));
+    HIP_TRY(hipMallocAsync((void**)&mi, (size_t)nq * KP * 8, st));
+    // input [n_lists][nq][k_in]: list j of query q at j*nq*k_in + q*k_in
+    HIP_TRY(launch_merge_f64_i64(KP, keys, idx, n_lists, k_in, k_in, (int64_t)nq * k_in, nq, mk, mi, st));
+    HIP_TRY(launch_finalize_i64(metric, mk, mi, KP, nq, nullptr, k_out, out_scores, out_indices, out_keys, st));
+    HIP_TRY(hipFreeAsync(mk, st));
+    HIP_TRY(hipFreeAsync(mi, st));
+    return VDB_OK;
+}
+
+int32_t vdb_similarity_matrix(const float* corpus, int64_t n, int32_t dim, const float* queries, int32_t nq,
+                              int32_t metric, float* out, void* stream) {
+    if (!corpus || !queries || !out) return set_error(VDB_ERR_INVALID, "NULL argument");
+    if (n < 0 || dim <= 0 || nq <= 0) return set_error(VDB_ERR_INVALID, "bad sizes");
+    if (metric != 0 && metric != 1) return set_error(VDB_ERR_UNSUPPORTED, "metric %d", metric);
+    HIP_TRY(launch_similarity_matrix(corpus, n, dim, queries, nq, metric, out, (hipStream_t)stream));
+    return VDB_OK;
+}
+
+}  // extern "C"

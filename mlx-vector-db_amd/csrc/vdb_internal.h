@@ -1,0 +1,75 @@
+// vdb_internal.h — host-side launchers for the kernels in vdb_kernels.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace vdb {
+
+// Tiling constants (layout documented in vdb_common.h / DESIGN.md §2).
+constexpr int TILE_ROWS = 32;      // rows per row tile
+constexpr int GROUP_DIMS = 8;      // dims per (tile, group) block
+constexpr int BLOCK_FLOATS = 256;  // floats per (tile, group) block = 1 KiB
+constexpr int STEP_ROWS = 256;     // rows one scan workgroup consumes per step
+
+// Ingest: row-major fp32 [n][D] (device) -> tiled corpus rows [row0, row0+n),
+// canonical fp64 norms, fp32 inverse norms and squared norms, running max norm
+// (as fp64 bits) and a non-finite counter.
+hipError_t launch_pack_rows(const float* src, int64_t n, int D, int G, float* X, int64_t row0,
+                            double* nrm64, float* inv32, float* sq32,
+                            unsigned long long* xmax_bits, int* nonfinite, hipStream_t st);
+
+// Tiled corpus rows -> row-major fp32 (export for persistence).
+hipError_t launch_unpack_rows(const float* X, int G, int D, int64_t row0, int64_t n, float* dst, hipStream_t st);
+
+// Queries: row-major [B][D] -> tiled Qt (cosine: pre-normalised in fp32) and
+// canonical fp64 norms.  Qt must be zeroed by the caller (padding).
+hipError_t launch_prep_queries(const float* Q, int B, int D, int G, int metric,
+                               float* Qt, double* qn64, hipStream_t st);
+
+// Candidate pass: MFMA fp32 scores fused with a per-workgroup top-KP.
+// Output lists cand_[s|i][B][n_wg][KP], each sorted best first.
+hipError_t launch_scan_topk(int metric, int KP, const float* X, const float* rowscale, const uint32_t* mask,
+                            const float* Qt, int G, int64_t N, int B, int n_qblocks, int64_t n_steps,
+                            int n_wg, int steps_per_wg, float* cand_s, uint32_t* cand_i, hipStream_t st);
+
+// Merge sorted per-workgroup lists -> sorted top-KP per query (fp32 keys).
+hipError_t launch_merge_f32(int KP, const float* ls, const uint32_t* li, int n_lists, int B,
+                            float* out_s, uint32_t* out_i, hipStream_t st);
+
+// Exact fp64 rerank of the KP candidates + certificate check.
+struct RerankArgs {
+    const float* Q; const double* qn64; const float* X; int G; int D;
+    const double* nrm64; const float* app_s; const uint32_t* app_i;
+    int k; double eps_rel; double xmax;
+    float* out_s; int64_t* out_i; double* out_k; int64_t index_offset;
+    int* flag_count; int* flag_list;
+};
+hipError_t launch_rerank(int metric, int KP, const RerankArgs& a, int B, hipStream_t st);
+
+// Exact fp64 scan of the whole corpus for the queries in qlist[0..nq):
+// per-wave sorted top-KE lists [nq][n_wg*4][KE] (fp64 keys, local rows).
+hipError_t launch_exact_scan(int metric, int KE, const float* Q, const double* qn64, const int* qlist, int nq,
+                             const float* X, int G, int D, const double* nrm64, const uint32_t* mask,
+                             int64_t N, int n_wg, int64_t rows_per_wg,
+                             double* lk, uint32_t* li, hipStream_t st);
+
+// Merge sorted fp64-key lists.  Element (q, j, e) lives at q*sq + j*sj + e, lists
+// have Lk entries; output [nq][KP] sorted.
+hipError_t launch_merge_f64_u32(int KP, const double* lk, const uint32_t* li, int n_lists, int Lk,
+                                int64_t sq, int64_t sj, int nq, double* out_k, uint32_t* out_i, hipStream_t st);
+hipError_t launch_merge_f64_i64(int KP, const double* lk, const int64_t* li, int n_lists, int Lk,
+                                int64_t sq, int64_t sj, int nq, double* out_k, int64_t* out_i, hipStream_t st);
+
+// Write final results for query rows qmap[q] (or q if qmap == nullptr) from
+// sorted [nq][KP] fp64-key lists.
+hipError_t launch_finalize_u32(int metric, const double* sk, const uint32_t* si, int KP, int nq, const int* qmap,
+                               int k, int64_t index_offset, float* out_s, int64_t* out_i, double* out_k,
+                               hipStream_t st);
+hipError_t launch_finalize_i64(int metric, const double* sk, const int64_t* si, int KP, int nq, const int* qmap,
+                               int k, float* out_s, int64_t* out_i, double* out_k, hipStream_t st);
+
+// Operator slot: full score matrix out[B][N] (fp32 reference arithmetic).
+hipError_t launch_similarity_matrix(const float* X, int64_t N, int D, const float* Q, int B, int metric,
+                                    float* out, hipStream_t st);
+
+}  // namespace vdb

@@ -1,0 +1,237 @@
+"""ctypes binding of the gfx950 vector-search core (include/vdb.h, lib/libvdb_amd.so).
+
+This is the only way the store reaches the device.  There is no CPU fallback:
+if the shared library is missing, or no gfx950 device is visible, every
+constructor here raises.  (The CPU oracle under ``oracle/`` is test
+infrastructure and is never imported by this package.)
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from pathlib import Path
+from typing import Optional, Tuple
+
+import numpy as np
+
+_PKG_ROOT = Path(__file__).resolve().parent.parent
+_DEFAULT_LIB = _PKG_ROOT / "lib" / "libvdb_amd.so"
+
+VDB_OK = 0
+VDB_ERR_INVALID = -1
+VDB_ERR_HIP = -2
+VDB_ERR_OOM = -3
+VDB_ERR_NONFINITE = -4
+VDB_ERR_UNSUPPORTED = -5
+VDB_ERR_NODEVICE = -6
+
+METRIC_IDS = {"cosine": 0, "euclidean": 1}
+MEM_HOST = 0
+MEM_DEVICE = 1
+
+# Every symbol include/vdb.h declares (tests/test_abi.py checks the .so exports them).
+EXPORTED_SYMBOLS = (
+    "vdb_last_error", "vdb_version", "vdb_device_count",
+    "vdb_index_create", "vdb_index_destroy", "vdb_index_reserve",
+    "vdb_index_set_param", "vdb_index_get_stat",
+    "vdb_index_add", "vdb_index_count", "vdb_index_clear", "vdb_index_get_vectors",
+    "vdb_index_search", "vdb_merge_topk", "vdb_similarity_matrix",
+)
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+class VDBError(RuntimeError):
+    """A failing vdb_* call (HIP error, out of memory, no device)."""
+
+
+def library_path() -> Path:
+    return Path(os.environ.get("VDB_LIB", str(_DEFAULT_LIB)))
+
+
+def _prefer_torch_runtime() -> None:
+    # torch bundles its own libamdhip64.so.7; load it first so the process has
+    # one HIP runtime whichever of torch / this library is imported first.
+    try:  # pragma: no cover - depends on the environment
+        import torch  # noqa: F401
+    except Exception:
+        pass
+
+
+def load_library():
+    """Load (once) and type the C-ABI.  Raises ImportError if it is not built."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None:
+            return _lib
+        path = library_path()
+        if not path.exists():
+            raise ImportError(
+                f"vdb HIP library not found at {path}; build it with "
+                f"`make -C {_PKG_ROOT}` (hipcc --offload-arch=gfx950)")
+        _prefer_torch_runtime()
+        lib = ctypes.CDLL(str(path))
+        c_i32, c_i64, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_void_p
+        p_i64 = ctypes.POINTER(ctypes.c_int64)
+        sig = {
+            "vdb_last_error": (ctypes.c_char_p, []),
+            "vdb_version": (c_i32, []),
+            "vdb_device_count": (c_i32, [ctypes.POINTER(ctypes.c_int32)]),
+            "vdb_index_create": (c_i32, [c_i32, c_i32, c_i32, ctypes.POINTER(c_vp)]),
+            "vdb_index_destroy": (c_i32, [c_vp]),
+            "vdb_index_reserve": (c_i32, [c_vp, c_i64]),
+            "vdb_index_set_param": (c_i32, [c_vp, ctypes.c_char_p, c_i64]),
+            "vdb_index_get_stat": (c_i32, [c_vp, ctypes.c_char_p, p_i64]),
+            "vdb_index_add": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_vp]),
+            "vdb_index_count": (c_i32, [c_vp, p_i64]),
+            "vdb_index_clear": (c_i32, [c_vp]),
+            "vdb_index_get_vectors": (c_i32, [c_vp, c_i64, c_i64, c_vp]),
+            "vdb_index_search": (c_i32, [c_vp, c_vp, c_i32, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp, c_i64, c_vp]),
+            "vdb_merge_topk": (c_i32, [c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp]),
+            "vdb_similarity_matrix": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i32, c_i32, c_vp, c_vp]),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+        return lib
+
+
+def _check(rc: int) -> None:
+    if rc == VDB_OK:
+        return
+    msg = _lib.vdb_last_error().decode("utf-8", "replace")
+    if rc in (VDB_ERR_INVALID, VDB_ERR_NONFINITE):
+        raise ValueError(msg)
+    raise VDBError(f"vdb error {rc}: {msg}")
+
+
+def device_count() -> int:
+    lib = load_library()
+    n = ctypes.c_int32(0)
+    lib.vdb_device_count(ctypes.byref(n))
+    return int(n.value)
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+class NativeIndex:
+    """One device-resident corpus (tiled fp32 + norms) on one GPU."""
+
+    def __init__(self, dim: int, metric: str = "cosine", device: int = 0):
+        if metric not in METRIC_IDS:
+            raise ValueError(f"unsupported metric {metric!r}; the vdb core implements {sorted(METRIC_IDS)}")
+        self._lib = load_library()
+        self.dim = int(dim)
+        self.metric = metric
+        self.device = int(device)
+        h = ctypes.c_void_p()
+        _check(self._lib.vdb_index_create(self.dim, METRIC_IDS[metric], self.device, ctypes.byref(h)))
+        self._h = h
+
+    # -- lifecycle -------------------------------------------------------------
+    def close(self) -> None:
+        h, self._h = getattr(self, "_h", None), None
+        if h:
+            self._lib.vdb_index_destroy(h)
+
+    def __del__(self):  # pragma: no cover - GC timing
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def reserve(self, rows: int) -> None:
+        _check(self._lib.vdb_index_reserve(self._h, int(rows)))
+
+    def set_param(self, name: str, value: int) -> None:
+        _check(self._lib.vdb_index_set_param(self._h, name.encode(), int(value)))
+
+    def stat(self, name: str) -> int:
+        v = ctypes.c_int64(0)
+        _check(self._lib.vdb_index_get_stat(self._h, name.encode(), ctypes.byref(v)))
+        return int(v.value)
+
+    # -- data ------------------------------------------------------------------
+    def add(self, vectors: np.ndarray) -> None:
+        v = np.ascontiguousarray(vectors, dtype=np.float32)
+        if v.ndim != 2 or v.shape[1] != self.dim:
+            raise ValueError(f"vectors must have shape (n, {self.dim}), got {v.shape}")
+        if v.shape[0] == 0:
+            return
+        _check(self._lib.vdb_index_add(self._h, _ptr(v), v.shape[0], MEM_HOST, None))
+
+    def add_device(self, ptr: int, n: int, stream: int = 0) -> None:
+        _check(self._lib.vdb_index_add(self._h, ctypes.c_void_p(ptr), int(n), MEM_DEVICE, ctypes.c_void_p(stream)))
+
+    def count(self) -> int:
+        n = ctypes.c_int64(0)
+        _check(self._lib.vdb_index_count(self._h, ctypes.byref(n)))
+        return int(n.value)
+
+    def clear(self) -> None:
+        _check(self._lib.vdb_index_clear(self._h))
+
+    def get_vectors(self, start: int = 0, n: Optional[int] = None) -> np.ndarray:
+        total = self.count()
+        n = total - start if n is None else n
+        out = np.empty((max(n, 0), self.dim), dtype=np.float32)
+        if n > 0:
+            _check(self._lib.vdb_index_get_vectors(self._h, int(start), int(n), _ptr(out)))
+        return out
+
+    # -- search ----------------------------------------------------------------
+    def search(self, queries: np.ndarray, k: int, row_mask: Optional[np.ndarray] = None,
+               with_keys: bool = False, index_offset: int = 0):
+        """Host-memory search.  Returns (scores f32 [B,k], indices i64 [B,k][, keys f64 [B,k]])."""
+        q = np.ascontiguousarray(queries, dtype=np.float32)
+        if q.ndim == 1:
+            q = q[None, :]
+        if q.ndim != 2 or q.shape[1] != self.dim:
+            raise ValueError(f"queries must have shape (B, {self.dim}), got {np.shape(queries)}")
+        B = q.shape[0]
+        k = int(k)
+        scores = np.empty((B, k), dtype=np.float32)
+        idx = np.empty((B, k), dtype=np.int64)
+        keys = np.empty((B, k), dtype=np.float64) if with_keys else None
+        mask_p = None
+        if row_mask is not None:
+            m = np.ascontiguousarray(row_mask, dtype=np.uint32)
+            need = (self.count() + 31) // 32
+            if m.size < need:
+                raise ValueError(f"row_mask needs {need} uint32 words, got {m.size}")
+            mask_p = _ptr(m)
+        _check(self._lib.vdb_index_search(self._h, _ptr(q), B, k, mask_p, MEM_HOST, _ptr(scores), _ptr(idx),
+                                          _ptr(keys) if keys is not None else None, int(index_offset), None))
+        return (scores, idx, keys) if with_keys else (scores, idx)
+
+    def search_device(self, q_ptr: int, n_queries: int, k: int, out_scores_ptr: int, out_idx_ptr: int,
+                      out_keys_ptr: int = 0, mask_ptr: int = 0, index_offset: int = 0, stream: int = 0) -> None:
+        """Device-memory search (pointers from torch tensors); stream-ordered."""
+        _check(self._lib.vdb_index_search(
+            self._h, ctypes.c_void_p(q_ptr), int(n_queries), int(k), ctypes.c_void_p(mask_ptr or None),
+            MEM_DEVICE, ctypes.c_void_p(out_scores_ptr), ctypes.c_void_p(out_idx_ptr),
+            ctypes.c_void_p(out_keys_ptr or None), int(index_offset), ctypes.c_void_p(stream or None)))
+
+
+def merge_topk_device(keys_ptr: int, idx_ptr: int, n_lists: int, n_queries: int, k_in: int, k_out: int,
+                      metric: str, out_scores_ptr: int, out_idx_ptr: int, out_keys_ptr: int = 0,
+                      stream: int = 0) -> None:
+    lib = load_library()
+    _check(lib.vdb_merge_topk(ctypes.c_void_p(keys_ptr), ctypes.c_void_p(idx_ptr), int(n_lists), int(n_queries),
+                              int(k_in), int(k_out), METRIC_IDS[metric], ctypes.c_void_p(out_scores_ptr),
+                              ctypes.c_void_p(out_idx_ptr), ctypes.c_void_p(out_keys_ptr or None),
+                              ctypes.c_void_p(stream or None)))
+
+
+def similarity_matrix_device(corpus_ptr: int, n: int, dim: int, q_ptr: int, n_queries: int, metric: str,
+                             out_ptr: int, stream: int = 0) -> None:
+    lib = load_library()
+    _check(lib.vdb_similarity_matrix(ctypes.c_void_p(corpus_ptr), int(n), int(dim), ctypes.c_void_p(q_ptr),
+                                     int(n_queries), METRIC_IDS[metric], ctypes.c_void_p(out_ptr),
+                                     ctypes.c_void_p(stream or None)))

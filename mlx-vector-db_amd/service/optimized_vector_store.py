@@ -1,0 +1,363 @@
+"""Drop-in store for the brute-force hot path, backed by the gfx950 vdb core.
+
+Mirrors the reference module ``service/optimized_vector_store.py`` (same class
+and function names, argument meaning, return shapes and error behaviour) so
+that existing callers — the REST routes (api/routes/vectors.py:57-64, :193,
+:229-233, :291), the admin routes, the RAG pipeline and the benchmarks — run
+unchanged with ``mlx-vector-db_amd/`` first on ``sys.path``.
+
+What differs underneath:
+  * the corpus lives on the GPU in an MFMA-tiled fp32 layout with norms
+    computed once at ingest (the reference re-normalises every row on every
+    query, service/optimized_vector_store.py:31-41);
+  * search is a fused fp32-MFMA candidate pass + exact fp64 rerank instead of
+    a full argsort (:176-183); ranking is exact with ties to the lower row;
+  * ``batch_query``, ``optimize`` and ``health_check`` exist (callers expect
+    them: api/routes/vectors.py:291, api/routes/admin.py:230, tests/demo.py:134,
+    :248, :254) and the functional API of tests/test_vector_store.py:15-18.
+"""
+from __future__ import annotations
+
+import json
+import logging
+import os
+import shutil
+import threading
+import time
+from dataclasses import dataclass
+from pathlib import Path
+from typing import Any, Dict, List, Optional, Tuple, Union
+
+import numpy as np
+
+from . import _vdb
+
+logger = logging.getLogger("mlx_vector_db.optimized_store")
+
+# Raised by the reference when no similarity operator exists (jit_compile=False
+# or metric="dot_product"): service/optimized_vector_store.py:153-154.
+_NO_OPERATOR_MSG = "Keine kompilierte Ähnlichkeitsfunktion verfügbar."
+
+
+@dataclass
+class MLXVectorStoreConfig:
+    """service/optimized_vector_store.py:51-56, plus two MI355X knobs."""
+    dimension: int = 384
+    metric: str = "cosine"
+    enable_hnsw: bool = False
+    jit_compile: bool = True
+    device: int = 0          # GPU ordinal holding this store's corpus
+    persist: bool = True     # write vectors.npz / metadata.jsonl on every add (reference behaviour)
+
+
+def _as_matrix(vectors: Any) -> np.ndarray:
+    """mx.array(vectors, float32) restated (service/optimized_vector_store.py:215-216)."""
+    if hasattr(vectors, "detach") and hasattr(vectors, "cpu"):  # torch tensor
+        vectors = vectors.detach().cpu().numpy()
+    a = np.asarray(vectors, dtype=np.float32)
+    return a
+
+
+def _filter_mask(metadata: List[Dict], filt: Dict, n: int) -> Tuple[np.ndarray, int]:
+    """AND of exact `meta.get(key) == value` (service/optimized_vector_store.py:159-165),
+    as a row bitmap for the device top-k.  Returns (uint32 words, matches)."""
+    hits = np.fromiter((all(m.get(k) == v for k, v in filt.items()) for m in metadata[:n]),
+                       dtype=bool, count=n)
+    bits = np.zeros(((n + 31) // 32) * 32, dtype=bool)
+    bits[:n] = hits
+    words = np.packbits(bits, bitorder="little").view("<u4").astype(np.uint32)
+    return words, int(hits.sum())
+
+
+class MLXVectorStore:
+    """service/optimized_vector_store.py:59-242, MI355X-native."""
+
+    def __init__(self, store_path: str, config: Optional[MLXVectorStoreConfig] = None):
+        self.store_path = Path(store_path).expanduser()
+        self.config = config or MLXVectorStoreConfig()
+        self._lock = threading.RLock()
+        self.store_path.mkdir(parents=True, exist_ok=True)
+        self._is_dirty = False
+        self._compiled_similarity_fn = None
+        self._index: Optional[_vdb.NativeIndex] = None
+        self._dim: Optional[int] = None
+        self._metadata: List[Dict] = []
+        self._vector_count = 0
+        self._hnsw_index = None  # the HNSW graph path is not built yet
+        self._initialize_store()
+        if self.config.jit_compile:
+            self._compile_critical_functions()
+        logger.info("vdb store initialised: %s | HNSW: %s", self.store_path, self.config.enable_hnsw)
+
+    # ---- state -----------------------------------------------------------------
+    def _create_empty_store(self):
+        if self._index is not None:
+            self._index.clear()
+        self._metadata = []
+        self._vector_count = 0
+        self._is_dirty = False
+
+    def _initialize_store(self):
+        self._load_store()
+
+    def _compile_critical_functions(self):
+        # the operator slot: which device kernel family serves brute force (:211-213)
+        if self.config.metric in _vdb.METRIC_IDS:
+            self._compiled_similarity_fn = self.config.metric
+
+    def _ensure_index(self, dim: int) -> _vdb.NativeIndex:
+        if self._index is None:
+            metric = self.config.metric if self.config.metric in _vdb.METRIC_IDS else "cosine"
+            self._index = _vdb.NativeIndex(dim, metric, self.config.device)
+            self._dim = dim
+        elif dim != self._dim:
+            raise ValueError(f"Dimension mismatch: store holds {self._dim}-d vectors, got {dim}-d")
+        return self._index
+
+    @property
+    def _vectors(self) -> Optional[np.ndarray]:
+        """The corpus as [N, D] float32 (copied back from the GPU), or None if empty."""
+        if self._index is None or self._vector_count == 0:
+            return None
+        return self._index.get_vectors()
+
+    # ---- ingest ------------------------------------------------------------------
+    def add_vectors(self, vectors: Union[np.ndarray, Any], metadata: List[Dict]):
+        """service/optimized_vector_store.py:96-114."""
+        with self._lock:
+            v = _as_matrix(vectors)
+            if v.ndim == 1:
+                v = v[None, :]
+            if v.ndim != 2:
+                raise ValueError(f"vectors must be 2-D (n, dim), got shape {v.shape}")
+            if v.shape[0] > 0:
+                self._ensure_index(v.shape[1]).add(v)
+            self._metadata.extend(metadata)
+            self._vector_count = self._index.count() if self._index is not None else 0
+            self._is_dirty = True
+            self._save_store()
+            return {"vectors_added": len(metadata), "total_vectors": self._vector_count}
+
+    # ---- query ---------------------------------------------------------------------
+    def query(self, query_vector: Union[np.ndarray, Any], k: int = 10,
+              filter_metadata: Optional[Dict] = None, use_hnsw: bool = True) -> Tuple:
+        """service/optimized_vector_store.py:116-145 -> (indices, scores, metadata)."""
+        if self._vector_count == 0:
+            return [], [], []
+        q = _as_matrix(query_vector)
+        if q.ndim == 2 and q.shape[0] == 1:
+            q = q[0]
+        if q.ndim != 1:
+            raise ValueError(f"query takes one vector of shape (dim,) or (1, dim), got {q.shape}; "
+                             "use batch_query for several")
+        return self._brute_force_search(q[None, :], k, filter_metadata)[0]
+
+    def batch_query(self, query_vectors: Union[np.ndarray, Any], k: int = 10,
+                    filter_metadata: Optional[Dict] = None) -> List[Tuple]:
+        """The batched path (performance/mlx_optimized.py:217-248) behind the store API that
+        api/routes/vectors.py:291 and tests/demo.py:134 call: one (indices, scores, metadata)
+        tuple per query, each exactly what ``query`` returns for that row."""
+        q = _as_matrix(query_vectors)
+        if q.ndim == 1:
+            q = q[None, :]
+        if q.ndim != 2:
+            raise ValueError(f"query_vectors must be 2-D (B, dim), got {q.shape}")
+        if self._vector_count == 0 or q.shape[0] == 0:
+            return [([], [], []) for _ in range(q.shape[0])]
+        return self._brute_force_search(q, k, filter_metadata)
+
+    def _brute_force_search(self, Q: np.ndarray, k: int, filter_metadata: Optional[Dict] = None):
+        """service/optimized_vector_store.py:149-192 for a [B, D] block of queries."""
+        if not self._compiled_similarity_fn:
+            raise RuntimeError(_NO_OPERATOR_MSG)
+        B = Q.shape[0]
+        empty = [([], [], []) for _ in range(B)]
+        if Q.shape[1] != self._dim:
+            raise ValueError(f"Dimension mismatch: query has {Q.shape[1]} dims, store holds {self._dim}")
+        k = int(k)
+        if k <= 0:
+            return empty
+        n = self._vector_count
+        mask = None
+        eligible = n
+        if filter_metadata:
+            mask, eligible = _filter_mask(self._metadata, filter_metadata, n)
+            if eligible == 0:
+                return empty
+        kk = min(k, eligible)
+        if kk > 1024:
+            raise ValueError(f"k={k} exceeds the device top-k limit of 1024")
+        scores, idx = self._index.search(Q, kk, row_mask=mask)
+        out = []
+        meta = self._metadata
+        for b in range(B):
+            valid = idx[b] >= 0
+            ib = idx[b][valid].tolist()
+            sb = scores[b][valid].astype(np.float64).tolist()
+            out.append((ib, sb, [meta[i] if i < len(meta) else {} for i in ib]))
+        return out
+
+    # ---- misc API ----------------------------------------------------------------------
+    def _warmup_kernels(self):
+        """service/optimized_vector_store.py:194-196 (a no-op there); here: one tiny search."""
+        if self._vector_count and self._compiled_similarity_fn:
+            self._index.search(np.zeros((1, self._dim), np.float32) + 1.0, 1)
+
+    def clear(self):
+        """service/optimized_vector_store.py:198-209."""
+        with self._lock:
+            try:
+                if self.store_path.exists():
+                    shutil.rmtree(self.store_path)
+                self.store_path.mkdir(parents=True, exist_ok=True)
+                self._create_empty_store()
+            except Exception as e:  # the reference logs and swallows (:208-209)
+                logger.error("clearing store %s failed: %s", self.store_path, e)
+
+    def optimize(self) -> Dict[str, Any]:
+        """Callers: api/routes/admin.py:230, api/routes/performance.py:188, tests/demo.py:248.
+        Flushes persistence and pre-sizes the device corpus to a 256-row multiple."""
+        t0 = time.time()
+        with self._lock:
+            if self._index is not None:
+                self._index.reserve(self._vector_count)
+            self._is_dirty = True
+            self._save_store(force=True)
+            self._warmup_kernels()
+        return {"optimized": True, "vector_count": self._vector_count,
+                "optimization_time_ms": (time.time() - t0) * 1000.0}
+
+    def health_check(self) -> Dict[str, Any]:
+        """Caller: tests/demo.py:254 (reads 'healthy' and 'issues')."""
+        issues = []
+        if len(self._metadata) != self._vector_count:
+            issues.append(f"metadata rows ({len(self._metadata)}) != vectors ({self._vector_count})")
+        if self._vector_count and self._index is None:
+            issues.append("device index missing")
+        if self._index is not None and self._index.count() != self._vector_count:
+            issues.append("device row count out of sync")
+        if not self._compiled_similarity_fn:
+            issues.append(_NO_OPERATOR_MSG)
+        return {"healthy": not issues, "issues": issues, "vector_count": self._vector_count,
+                "metric": self.config.metric, "device": self.config.device}
+
+    def get_stats(self):
+        """service/optimized_vector_store.py:241-242 (+ memory_usage_mb, read by
+        api/routes/monitoring.py:153 and tests/demo.py:146)."""
+        mem = 0.0
+        if self._index is not None:
+            mem = self._index.stat("device_bytes") / (1024.0 * 1024.0)
+        return {"vector_count": self._vector_count, "dimension": self.config.dimension,
+                "metric": self.config.metric,
+                "index_type": "hnsw" if self.config.enable_hnsw else "flat",
+                "memory_usage_mb": mem}
+
+    # ---- persistence: vectors.npz + metadata.jsonl (service/optimized_vector_store.py:218-239)
+    def _save_store(self, force: bool = False):
+        if not (self.config.persist or force):
+            return
+        if self._vector_count == 0 or not self._is_dirty:
+            return
+        vecs = self._index.get_vectors()
+        np.savez(str(self.store_path / "vectors.npz"), vectors=vecs)
+        with open(self.store_path / "metadata.jsonl", "w") as f:
+            for meta in self._metadata:
+                f.write(json.dumps(meta) + "\n")
+        self._is_dirty = False
+
+    def _load_store(self):
+        vectors_path = self.store_path / "vectors.npz"
+        if not vectors_path.exists():
+            self._create_empty_store()
+            return
+        try:
+            with np.load(str(vectors_path), allow_pickle=False) as z:
+                vecs = np.asarray(z["vectors"], dtype=np.float32)
+            meta: List[Dict] = []
+            metadata_path = self.store_path / "metadata.jsonl"
+            if metadata_path.exists():
+                with open(metadata_path, "r") as f:
+                    meta = [json.loads(line) for line in f]
+            if vecs.ndim != 2:
+                raise ValueError(f"vectors.npz holds shape {vecs.shape}")
+            if vecs.shape[0]:
+                self._ensure_index(vecs.shape[1]).add(vecs)
+            self._metadata = meta
+            self._vector_count = self._index.count() if self._index is not None else 0
+        except Exception as e:  # reference: log and start empty (:237-239)
+            logger.error("loading store %s failed, starting empty: %s", self.store_path, e)
+            self._create_empty_store()
+
+
+def create_optimized_vector_store(store_path: str, dimension: int = 384, jit_compile: bool = True,
+                                  enable_hnsw: bool = False, **kwargs) -> MLXVectorStore:
+    """service/optimized_vector_store.py:244-246."""
+    config = MLXVectorStoreConfig(dimension=dimension, jit_compile=jit_compile, enable_hnsw=enable_hnsw, **kwargs)
+    return MLXVectorStore(store_path, config)
+
+
+# ---- functional API (tests/test_vector_store.py:15-43 imports these) -----------------------
+_STORES: Dict[str, MLXVectorStore] = {}
+_STORES_LOCK = threading.Lock()
+
+
+def _base_dir() -> Path:
+    # the REST manager's layout, api/routes/vectors.py:57
+    return Path(os.environ.get("VECTOR_STORE_BASE", "~/.team_mind_data/vector_stores")).expanduser()
+
+
+def _store_path(user_id: str, model_id: str) -> Path:
+    return _base_dir() / user_id / model_id
+
+
+def _key(user_id: str, model_id: str) -> str:
+    return f"{user_id}_{model_id}"  # api/routes/vectors.py:45-46
+
+
+def store_exists(user_id: str, model_id: str) -> bool:
+    return _key(user_id, model_id) in _STORES or _store_path(user_id, model_id).exists()
+
+
+def create_store(user_id: str, model_id: str, dimension: int = 384, metric: str = "cosine",
+                 **kwargs) -> MLXVectorStore:
+    with _STORES_LOCK:
+        key = _key(user_id, model_id)
+        if key not in _STORES:
+            cfg = MLXVectorStoreConfig(dimension=dimension, metric=metric, **kwargs)
+            _STORES[key] = MLXVectorStore(str(_store_path(user_id, model_id)), cfg)
+        return _STORES[key]
+
+
+def _get_store(user_id: str, model_id: str) -> MLXVectorStore:
+    key = _key(user_id, model_id)
+    if key not in _STORES:
+        return create_store(user_id, model_id)  # lazy creation, api/routes/vectors.py:53-69
+    return _STORES[key]
+
+
+def add_vectors(user_id: str, model_id: str, vectors, metadata: List[Dict]) -> Dict[str, int]:
+    return _get_store(user_id, model_id).add_vectors(vectors, metadata)
+
+
+def query_vectors(user_id: str, model_id: str, query_vector, k: int = 10,
+                  filter_metadata: Optional[Dict] = None) -> List[Dict[str, Any]]:
+    """-> [{"index", "score", "metadata"}] (service/models.py SearchResult shape)."""
+    idx, scores, meta = _get_store(user_id, model_id).query(query_vector, k=k, filter_metadata=filter_metadata)
+    return [{"index": i, "score": s, "metadata": m} for i, s, m in zip(idx, scores, meta)]
+
+
+def count_vectors(user_id: str, model_id: str) -> Dict[str, int]:
+    st = _get_store(user_id, model_id)
+    return {"vectors": st._vector_count, "metadata": len(st._metadata)}
+
+
+def delete_store(user_id: str, model_id: str) -> bool:
+    with _STORES_LOCK:
+        st = _STORES.pop(_key(user_id, model_id), None)
+    path = _store_path(user_id, model_id)
+    if st is not None and st._index is not None:
+        st._index.close()
+    if path.exists():
+        shutil.rmtree(path)
+        return True
+    return st is not None

@@ -1,0 +1,272 @@
+"""CPU oracle for the brute-force distance + top-k hot path.  TEST INFRASTRUCTURE.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline``
+leg may import this module, and only as the checker / the timed CPU baseline.
+The product (``mlx-vector-db_amd/``) never imports it: its only compute path is
+the gfx950 HIP library.
+
+What it restates (reference = /root/reference, Theseus-AT/mlx-vector-db):
+  * ``reference_*`` functions: the reference's own fp32 arithmetic, line for
+    line, with numpy standing in for MLX (MLX is not installable here:
+    ``import performance.mlx_optimized`` -> ModuleNotFoundError 'mlx', an
+    ordinary import error, not a permission denial).
+  * ``canonical_*`` / ``exact_*``: the ranking contract the GPU path is held to
+    bit for bit — fp64 keys in the one summation order the kernels use
+    (mlx-vector-db_amd/csrc/vdb_common.h), ties to the lower row index.
+
+Parity pinning.  The reference ships no golden vectors, fixtures or seeded
+tests for this path: its known-answer checks are behavioural —
+P1 self-query top-1 with similarity > 0.999 (tests/test_integration.py:81-136),
+P2/P3 metadata-filter AND semantics (test_integration.py:139-160,
+tests/demo.py:217-243), P4 counts, P5 result length k (tests/test_vector_store.py:35-40),
+P6 batch shape (demo.py:130-139), P7 empty store.  tests/test_oracle.py checks
+this module against all of them, against hand-derived known answers
+(orthogonal / parallel / scaled vectors whose cosine and L2 are exact), and
+against the committed fixtures in tests/golden/ (made by
+tests/golden/gen_golden.py from this module).  MLX's own argsort cannot be run
+here, so the reference's order among fp32 near-ties is "parity unpinned"
+beyond those pins; the exact fp64 order is the contract instead.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+EPS = 1e-8  # service/optimized_vector_store.py:36, performance/mlx_optimized.py:45
+
+
+# =============================================================================
+# 1. Reference arithmetic (fp32), restated from the reference sources
+# =============================================================================
+def reference_cosine_scores(query: np.ndarray, vectors: np.ndarray) -> np.ndarray:
+    """`_compiled_cosine_similarity` (service/optimized_vector_store.py:31-41):
+    norms (mx.linalg.norm, :34-35), max with 1e-8 (:36-38), divide (:39-40),
+    matmul(vectors_normalized, query_normalized.T).flatten() (:41).  fp32."""
+    q = np.asarray(query, dtype=np.float32)
+    if q.ndim == 1:
+        q = q[None, :]
+    v = np.asarray(vectors, dtype=np.float32)
+    qn = np.maximum(np.linalg.norm(q, axis=1, keepdims=True), np.float32(EPS)).astype(np.float32)
+    vn = np.maximum(np.linalg.norm(v, axis=1, keepdims=True), np.float32(EPS)).astype(np.float32)
+    return ((v / vn) @ (q / qn).T).reshape(-1).astype(np.float32)
+
+
+def reference_euclidean_distances(query: np.ndarray, vectors: np.ndarray) -> np.ndarray:
+    """`_compiled_euclidean_distance` (service/optimized_vector_store.py:43-48):
+    sqrt(sum((vectors - query)^2, axis=1)), fp32."""
+    q = np.asarray(query, dtype=np.float32).reshape(1, -1)
+    d = np.asarray(vectors, dtype=np.float32) - q
+    return np.sqrt(np.sum(d * d, axis=1, dtype=np.float32)).astype(np.float32)
+
+
+def reference_cosine_batch(queries: np.ndarray, vectors: np.ndarray) -> np.ndarray:
+    """`compute_cosine_similarity_batch` (performance/mlx_optimized.py:59-88): [B, N] fp32,
+    with its ValueError checks (:65-72)."""
+    Q = np.asarray(queries, dtype=np.float32)
+    V = np.asarray(vectors, dtype=np.float32)
+    if Q.ndim != 2:
+        raise ValueError(f"query_vectors muss 2D sein, erhielt Shape {Q.shape}")
+    if V.ndim != 2:
+        raise ValueError(f"db_vectors muss 2D sein, erhielt Shape {V.shape}")
+    if Q.shape[1] != V.shape[1]:
+        raise ValueError(f"Dimension Mismatch: query_vectors Dim {Q.shape[1]}, db_vectors Dim {V.shape[1]}")
+    qn = np.maximum(np.sqrt(np.sum(Q * Q, axis=1, keepdims=True)), np.float32(EPS))
+    vn = np.maximum(np.sqrt(np.sum(V * V, axis=1, keepdims=True)), np.float32(EPS))
+    return ((Q / qn) @ (V / vn).T).astype(np.float32)
+
+
+def reference_topk_indices(scores: np.ndarray, k: int, metric: str = "cosine") -> np.ndarray:
+    """mx.argsort(-s)[:k] (cosine, :181) / mx.argsort(s)[:k] (euclidean, :178), as a
+    STABLE sort (ties -> lower row); empty for k <= 0
+    (performance/mlx_optimized.py:98-105)."""
+    if k <= 0:
+        return np.zeros(0, dtype=np.int64)
+    key = -scores if metric != "euclidean" else scores
+    return np.argsort(key, kind="stable")[:k].astype(np.int64)
+
+
+def reference_store_search(query, vectors, k=10, metric="cosine", metadata=None, filter_metadata=None):
+    """`MLXVectorStore.query` -> `_brute_force_search` (service/optimized_vector_store.py:116-192),
+    HNSW disabled.  Returns (indices, scores, metadata) Python lists."""
+    V = np.asarray(vectors, dtype=np.float32)
+    if V.shape[0] == 0:
+        return [], [], []
+    original = None
+    target = V
+    if filter_metadata:
+        original = [i for i, m in enumerate(metadata) if all(m.get(a) == b for a, b in filter_metadata.items())]
+        if not original:
+            return [], [], []
+        target = V[original]
+    if metric == "cosine":
+        s = reference_cosine_scores(query, target)
+    elif metric == "euclidean":
+        s = reference_euclidean_distances(query, target)
+    else:
+        raise RuntimeError("Keine kompilierte Ähnlichkeitsfunktion verfügbar.")
+    local = reference_topk_indices(s, k, metric)
+    top = s[local]
+    idx = [original[i] for i in local.tolist()] if original is not None else local.tolist()
+    meta = [metadata[i] for i in idx] if metadata is not None else [None] * len(idx)
+    return idx, top.tolist(), meta
+
+
+def reference_batch_search(queries, vectors, k=10):
+    """`optimized_batch_similarity_search` (performance/mlx_optimized.py:217-248):
+    (indices [B,k'], scores [B,k']) with k' = min(k, N)."""
+    S = reference_cosine_batch(queries, vectors)
+    B, N = S.shape
+    if N == 0:
+        return np.zeros((B, 0), np.int64), np.zeros((B, 0), np.float32)
+    kk = min(k, N)
+    if kk <= 0:
+        return np.zeros((B, 0), np.int64), np.zeros((B, 0), np.float32)
+    idx = np.argsort(-S, axis=1, kind="stable")[:, :kk]
+    return idx.astype(np.int64), np.take_along_axis(S, idx, axis=1)
+
+
+# =============================================================================
+# 2. The exact ranking contract (fp64, canonical order) the GPU path must match
+# =============================================================================
+def _pad64(A: np.ndarray) -> np.ndarray:
+    A = np.asarray(A)
+    D = A.shape[-1]
+    Dp = (D + 63) // 64 * 64
+    if Dp == D:
+        return A
+    pad = [(0, 0)] * (A.ndim - 1) + [(0, Dp - D)]
+    return np.pad(A, pad)
+
+
+def _butterfly(acc: np.ndarray) -> np.ndarray:
+    """xor-butterfly over the last axis (64 lanes), offsets 32..1; returns lane 0."""
+    lanes = np.arange(64)
+    for off in (32, 16, 8, 4, 2, 1):
+        acc = acc + acc[..., lanes ^ off]
+    return acc[..., 0]
+
+
+def canonical_sumsq64(A: np.ndarray) -> np.ndarray:
+    """Per-row sum of squares in fp64, lane order of vdb_common.h (pack_rows_kernel)."""
+    X = _pad64(np.asarray(A, dtype=np.float32)).astype(np.float64)
+    X = X.reshape(X.shape[0], -1, 64)
+    acc = np.zeros((X.shape[0], 64))
+    for m in range(X.shape[1]):
+        v = X[:, m, :]
+        acc = acc + v * v
+    return _butterfly(acc)
+
+
+def canonical_norm64(A: np.ndarray) -> np.ndarray:
+    return np.sqrt(canonical_sumsq64(A))
+
+
+def canonical_dot64(q: np.ndarray, X: np.ndarray) -> np.ndarray:
+    """fp64 q.x for every row of X, canonical order (exact_key<cosine> in vdb_kernels.hip)."""
+    qp = _pad64(np.asarray(q, dtype=np.float32).reshape(1, -1)).astype(np.float64).reshape(-1, 64)
+    Xp = _pad64(np.asarray(X, dtype=np.float32)).astype(np.float64)
+    Xp = Xp.reshape(Xp.shape[0], -1, 64)
+    acc = np.zeros((Xp.shape[0], 64))
+    for m in range(Xp.shape[1]):
+        acc = acc + qp[m] * Xp[:, m, :]
+    return _butterfly(acc)
+
+
+def canonical_sqdist64(q: np.ndarray, X: np.ndarray) -> np.ndarray:
+    """fp64 sum((x-q)^2) for every row of X, canonical order (exact_key<euclidean>)."""
+    qp = _pad64(np.asarray(q, dtype=np.float32).reshape(1, -1)).astype(np.float64).reshape(-1, 64)
+    Xp = _pad64(np.asarray(X, dtype=np.float32)).astype(np.float64)
+    Xp = Xp.reshape(Xp.shape[0], -1, 64)
+    acc = np.zeros((Xp.shape[0], 64))
+    for m in range(Xp.shape[1]):
+        d = Xp[:, m, :] - qp[m]
+        acc = acc + d * d
+    return _butterfly(acc)
+
+
+def exact_keys(q: np.ndarray, X: np.ndarray, metric: str, xnorm64: np.ndarray | None = None) -> np.ndarray:
+    """Ranking keys, higher = better: cosine similarity / minus squared L2 (fp64)."""
+    if metric == "cosine":
+        qn = canonical_norm64(np.asarray(q, np.float32).reshape(1, -1))[0]
+        xn = canonical_norm64(X) if xnorm64 is None else xnorm64
+        return canonical_dot64(q, X) / (np.maximum(qn, EPS) * np.maximum(xn, EPS))
+    if metric == "euclidean":
+        return -canonical_sqdist64(q, X)
+    raise RuntimeError("Keine kompilierte Ähnlichkeitsfunktion verfügbar.")
+
+
+def exact_topk_from_keys(keys: np.ndarray, k: int):
+    """Stable order by (key desc, row asc); returns local positions."""
+    order = np.lexsort((np.arange(keys.shape[0]), -keys))
+    return order[:k]
+
+
+def keys_to_scores(keys: np.ndarray, metric: str) -> np.ndarray:
+    """What the store returns: cosine similarity, or sqrt of the squared distance (fp32)."""
+    if metric == "cosine":
+        return keys.astype(np.float32)
+    return np.sqrt(-keys).astype(np.float32)
+
+
+def exact_search(queries: np.ndarray, vectors: np.ndarray, k: int, metric: str = "cosine",
+                 row_mask: np.ndarray | None = None, chunk: int = 1 << 16):
+    """The contract for B queries: (scores f32 [B,k], indices i64 [B,k], keys f64 [B,k]);
+    slots past the eligible row count are index -1 / score 0 / key -inf.
+
+    Scales past the sizes where keying every row canonically is slow: a fp64 BLAS
+    prefilter (|error| < 1e-9 relative to the score scale) keeps every row within
+    a safe margin of the k-th prefilter value, and only those get canonical keys."""
+    Q = np.asarray(queries, dtype=np.float32)
+    if Q.ndim == 1:
+        Q = Q[None, :]
+    V = np.asarray(vectors, dtype=np.float32)
+    B, N = Q.shape[0], V.shape[0]
+    rows = np.arange(N) if row_mask is None else np.nonzero(row_mask)[0]
+    out_s = np.zeros((B, k), np.float32)
+    out_i = np.full((B, k), -1, np.int64)
+    out_k = np.full((B, k), -np.inf)
+    if rows.size == 0:
+        return out_s, out_i, out_k
+    Vr = V[rows]
+    xn = canonical_norm64(Vr)
+    V64 = Vr.astype(np.float64)
+    sq64 = np.sum(V64 * V64, axis=1)
+    kk = min(k, rows.size)
+    for b in range(B):
+        q = Q[b]
+        q64 = q.astype(np.float64)
+        if rows.size <= 4096:
+            cand = np.arange(rows.size)
+        else:
+            approx = np.empty(rows.size)
+            for s in range(0, rows.size, chunk):
+                blk = V64[s:s + chunk] @ q64
+                if metric == "cosine":
+                    approx[s:s + chunk] = blk / np.maximum(xn[s:s + chunk], EPS)
+                else:
+                    approx[s:s + chunk] = 2.0 * blk - sq64[s:s + chunk]
+            scale = (np.abs(approx).max() + (sq64.max() if metric != "cosine" else 1.0)) + 1.0
+            kth = np.partition(approx, -kk)[-kk]
+            cand = np.nonzero(approx >= kth - 1e-9 * scale)[0]
+        keys = exact_keys(q, Vr[cand], metric, xn[cand] if metric == "cosine" else None)
+        sel = exact_topk_from_keys(keys, kk)
+        pos = cand[sel]
+        out_i[b, :kk] = rows[pos]
+        out_k[b, :kk] = keys[sel]
+        out_s[b, :kk] = keys_to_scores(keys[sel], metric)
+    return out_s, out_i, out_k
+
+
+def merge_topk(keys_lists: np.ndarray, idx_lists: np.ndarray, k: int):
+    """Merge per-shard lists [G, B, k_in] by (key desc, index asc) -> [B, k] (multi-GPU check)."""
+    G, B, kin = keys_lists.shape
+    keys = np.transpose(keys_lists, (1, 0, 2)).reshape(B, G * kin)
+    idx = np.transpose(idx_lists, (1, 0, 2)).reshape(B, G * kin)
+    out_k = np.full((B, k), -np.inf)
+    out_i = np.full((B, k), -1, np.int64)
+    for b in range(B):
+        valid = idx[b] >= 0
+        kb, ib = keys[b][valid], idx[b][valid]
+        order = np.lexsort((ib, -kb))[:k]
+        out_k[b, :order.size] = kb[order]
+        out_i[b, :order.size] = ib[order]
+    return out_k, out_i

@@ -1,0 +1,235 @@
+"""Parity of the gfx950 path (through the C-ABI) against the CPU oracle.
+
+Bar: indices bit-exact against the exact contract (fp64 keys in
+the canonical order, ties to the lower row), fp64 keys bit-exact, returned fp32
+scores within 1e-4 of the reference's own fp32 arithmetic.
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+from oracle import ref_cpu
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "*.npz")))
+
+
+@pytest.fixture(scope="module")
+def vdb():
+    from service import _vdb
+    assert _vdb.device_count() >= 1, "no GPU visible"
+    return _vdb
+
+
+def _mask_words(mask_bool):
+    n = mask_bool.size
+    bits = np.zeros(((n + 31) // 32) * 32, bool)
+    bits[:n] = mask_bool
+    return np.packbits(bits, bitorder="little").view("<u4").astype(np.uint32)
+
+
+def _check(vdb, V, Q, k, metric, mask=None, force_exact=False, margin=None, chunked_add=False):
+    ix = vdb.NativeIndex(V.shape[1], metric)
+    if force_exact:
+        ix.set_param("force_exact", 1)
+    if margin is not None:
+        ix.set_param("margin", margin)
+    if chunked_add:
+        for s in range(0, V.shape[0], 777):
+            ix.add(V[s:s + 777])
+    else:
+        ix.add(V)
+    assert ix.count() == V.shape[0]
+    mw = _mask_words(mask) if mask is not None else None
+    s, i, kk = ix.search(Q, k, row_mask=mw, with_keys=True)
+    es, ei, ek = ref_cpu.exact_search(Q, V, k, metric, row_mask=mask)
+    np.testing.assert_array_equal(i, ei)
+    valid = ei >= 0
+    # fp64 keys: bit-exact with the canonical order
+    np.testing.assert_array_equal(kk[valid], ek[valid])
+    np.testing.assert_array_equal(s[valid], es[valid])
+    return ix, s, i
+
+
+@pytest.mark.parametrize("path", GOLDEN, ids=[os.path.basename(p) for p in GOLDEN])
+def test_golden_fixtures(vdb, path):
+    z = np.load(path, allow_pickle=False)
+    V, Q, k, metric = z["vectors"], z["queries"], int(z["k"]), str(z["metric"])
+    mask = z["mask"] if z["mask"].size else None
+    ix = vdb.NativeIndex(V.shape[1], metric)
+    ix.add(V)
+    s, i, kk = ix.search(Q, k, row_mask=_mask_words(mask) if mask is not None else None, with_keys=True)
+    np.testing.assert_array_equal(i, z["exact_idx"])
+    valid = i >= 0
+    np.testing.assert_array_equal(kk[valid], z["exact_keys"][valid])
+    # scores vs the reference's fp32 arithmetic, same rows
+    np.testing.assert_allclose(s[valid], z["ref_scores"][valid], atol=1e-4, rtol=0)
+
+
+@pytest.mark.parametrize("metric", ["cosine", "euclidean"])
+@pytest.mark.parametrize("N,D,B,k", [(5000, 384, 7, 10), (3000, 100, 3, 5), (4096, 128, 64, 100),
+                                     (1234, 33, 65, 32), (700, 1536, 9, 10)])
+def test_random_uniform(vdb, metric, N, D, B, k):
+    rng = np.random.default_rng(N + D)
+    V = rng.random((N, D), dtype=np.float32)
+    Q = rng.random((B, D), dtype=np.float32)
+    _check(vdb, V, Q, k, metric)
+
+
+@pytest.mark.parametrize("metric", ["cosine", "euclidean"])
+def test_normal_with_mask_and_chunked_add(vdb, metric):
+    rng = np.random.default_rng(7)
+    V = rng.standard_normal((6000, 200)).astype(np.float32)
+    Q = rng.standard_normal((5, 200)).astype(np.float32)
+    mask = rng.random(6000) < 0.3
+    _check(vdb, V, Q, 10, metric, mask=mask, chunked_add=True)
+
+
+def test_duplicates_force_certificate_fallback(vdb):
+    """50 copies of the nearest row: the candidate list cannot certify the top-k,
+    so the exact scan must take over and keep the lower-index-first order."""
+    rng = np.random.default_rng(3)
+    V = rng.random((20000, 64), dtype=np.float32)
+    V[1000:1050] = V[7]
+    Q = np.stack([V[7], rng.random(64, dtype=np.float32)])
+    ix, s, i = _check(vdb, V, Q, 10, "cosine")
+    assert i[0, 0] == 7 and list(i[0, 1:]) == list(range(1000, 1009))
+    assert ix.stat("fallback_queries") >= 1
+
+
+@pytest.mark.parametrize("metric", ["cosine", "euclidean"])
+def test_exact_path_large_k(vdb, metric):
+    rng = np.random.default_rng(11)
+    V = rng.random((9000, 96), dtype=np.float32)
+    Q = rng.random((3, 96), dtype=np.float32)
+    _check(vdb, V, Q, 300, metric)          # k > 200 -> exact path
+    _check(vdb, V, Q, 10, metric, force_exact=True)
+
+
+def test_k_larger_than_n_and_tiny(vdb):
+    rng = np.random.default_rng(5)
+    V = rng.random((7, 16), dtype=np.float32)
+    Q = rng.random((2, 16), dtype=np.float32)
+    ix, s, i = _check(vdb, V, Q, 20, "cosine")
+    assert (i[:, 7:] == -1).all() and (i[:, :7] >= 0).all()
+
+
+def test_empty_index_returns_no_results(vdb):
+    ix = vdb.NativeIndex(8, "cosine")
+    s, i = ix.search(np.ones((3, 8), np.float32), 5)
+    assert (i == -1).all()
+
+
+def test_nonfinite_rejected(vdb):
+    ix = vdb.NativeIndex(4, "cosine")
+    bad = np.ones((3, 4), np.float32)
+    bad[1, 2] = np.nan
+    with pytest.raises(ValueError):
+        ix.add(bad)
+    assert ix.count() == 0
+    ix.add(np.ones((2, 4), np.float32))
+    with pytest.raises(ValueError):
+        ix.search(np.full((1, 4), np.inf, np.float32), 1)
+
+
+def test_export_roundtrip(vdb):
+    rng = np.random.default_rng(9)
+    V = rng.standard_normal((1000, 77)).astype(np.float32)
+    ix = vdb.NativeIndex(77, "euclidean")
+    ix.add(V[:300])
+    ix.add(V[300:])
+    np.testing.assert_array_equal(ix.get_vectors(), V)
+    ix.clear()
+    assert ix.count() == 0
+    ix.add(V[:10])
+    np.testing.assert_array_equal(ix.get_vectors(), V[:10])
+
+
+def test_merge_topk_matches_single_device(vdb):
+    """Shard a corpus in 4, search shards with index offsets, merge on device:
+    identical to one search over everything."""
+    import torch
+    rng = np.random.default_rng(13)
+    V = rng.random((8000, 128), dtype=np.float32)
+    V[5000:5020] = V[123]  # ties across shards
+    Q = rng.random((16, 128), dtype=np.float32)
+    Q[0] = V[123]
+    k, G = 25, 4
+    bounds = np.linspace(0, V.shape[0], G + 1).astype(int)
+    keys, idx = [], []
+    for g in range(G):
+        ix = vdb.NativeIndex(128, "euclidean")
+        ix.add(V[bounds[g]:bounds[g + 1]])
+        _, i, kk = ix.search(Q, k, with_keys=True, index_offset=int(bounds[g]))
+        keys.append(kk)
+        idx.append(i)
+    kd = torch.from_numpy(np.stack(keys)).cuda()
+    idd = torch.from_numpy(np.stack(idx)).cuda()
+    os_ = torch.empty((16, k), dtype=torch.float32, device="cuda")
+    oi = torch.empty((16, k), dtype=torch.int64, device="cuda")
+    ok = torch.empty((16, k), dtype=torch.float64, device="cuda")
+    vdb.merge_topk_device(kd.data_ptr(), idd.data_ptr(), G, 16, k, k, "euclidean", os_.data_ptr(), oi.data_ptr(),
+                          ok.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    es, ei, ek = ref_cpu.exact_search(Q, V, k, "euclidean")
+    np.testing.assert_array_equal(oi.cpu().numpy(), ei)
+    np.testing.assert_array_equal(ok.cpu().numpy(), ek)
+
+
+def test_device_pointer_search_matches_host(vdb):
+    import torch
+    rng = np.random.default_rng(17)
+    V = rng.random((10000, 256), dtype=np.float32)
+    Q = rng.random((64, 256), dtype=np.float32)
+    ix = vdb.NativeIndex(256, "cosine")
+    ix.add(V)
+    s_h, i_h = ix.search(Q, 10)
+    qd = torch.from_numpy(Q).cuda()
+    sd = torch.empty((64, 10), dtype=torch.float32, device="cuda")
+    idd = torch.empty((64, 10), dtype=torch.int64, device="cuda")
+    ix.search_device(qd.data_ptr(), 64, 10, sd.data_ptr(), idd.data_ptr(),
+                     stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(idd.cpu().numpy(), i_h)
+    np.testing.assert_array_equal(sd.cpu().numpy(), s_h)
+
+
+def test_similarity_matrix_operator_slot(vdb):
+    import torch
+    rng = np.random.default_rng(19)
+    V = rng.random((3000, 384), dtype=np.float32)
+    Q = rng.random((4, 384), dtype=np.float32)
+    for metric in ("cosine", "euclidean"):
+        out = torch.empty((4, 3000), dtype=torch.float32, device="cuda")
+        vt, qt = torch.from_numpy(V).cuda(), torch.from_numpy(Q).cuda()
+        vdb.similarity_matrix_device(vt.data_ptr(), 3000, 384, qt.data_ptr(), 4, metric, out.data_ptr())
+        torch.cuda.synchronize()
+        if metric == "cosine":
+            ref = ref_cpu.reference_cosine_batch(Q, V)
+        else:
+            ref = np.stack([ref_cpu.reference_euclidean_distances(q, V) for q in Q])
+        np.testing.assert_allclose(out.cpu().numpy(), ref, atol=1e-4, rtol=0)
+
+
+@pytest.mark.slow
+def test_full_size_c2_subset(vdb):
+    """BASELINE.json configs[1]: 1M x 768 fp32 cosine, B=64, k=10.  The oracle
+    checks 8 of the 64 queries exactly; every query checks size-independent
+    properties (sorted scores, planted self-queries on top)."""
+    N, D, B, k = 1_000_000, 768, 64, 10
+    V = np.random.default_rng(0).random((N, D), dtype=np.float32)
+    Q = np.random.default_rng(1).random((B, D), dtype=np.float32)
+    Q[5] = V[777_777]
+    Q[6] = V[3]
+    ix = vdb.NativeIndex(D, "cosine")
+    ix.add(V)
+    s, i = ix.search(Q, k)
+    assert (np.diff(s, axis=1) <= 0).all()
+    assert i[5, 0] == 777_777 and i[6, 0] == 3
+    sub = [0, 1, 2, 5, 6, 31, 32, 63]
+    es, ei, ek = ref_cpu.exact_search(Q[sub], V, k, "cosine")
+    np.testing.assert_array_equal(i[sub], ei)
+    np.testing.assert_allclose(s[sub], es, atol=1e-6, rtol=0)
