@@ -1,0 +1,233 @@
+#!/usr/bin/env python3
+"""Headline benchmark: brute-force cosine / L2 top-k on MI355X (BASELINE.json).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c1|c3|c4]
+
+One "step" = one batch of queries searched against the whole corpus (fused
+fp32-MFMA candidate scan + exact fp64 rerank; queries, corpus and outputs
+resident in HBM).  N=1 runs BASELINE.json configs[1] (C2: 1M x 768 fp32
+cosine, batch 64, top-10).  N>1 (torchrun, one rank per GPU, RCCL) row-shards
+the SAME corpus over the ranks — each rank searches its shard, the per-shard
+top-k lists (fp64 keys + global row ids) are all-gathered over xGMI and merged
+on device, bit-identical to one GPU — so total work is fixed ("strong").
+
+Rank 0 prints one JSON line: QPS (whole job), p50 batch latency, the roofline
+of the dominant kernel (scan_topk, HIP-event timed inside the library on the
+stream it runs on) and, at N=1, the CPU baseline: the reference's batched path
+(performance/mlx_optimized.py:217-248) restated in numpy (oracle/ref_cpu.py),
+timed on this host on one full batch.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "mlx-vector-db_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402  (loaded before the HIP library: one HIP runtime per process)
+import torch.distributed as dist  # noqa: E402
+
+from service import _vdb  # noqa: E402
+
+METRIC = "QPS + p50 latency, cosine top-10 batch=64: 1M×768D @1 GPU; 10M×128D @8 GPU"
+CONFIGS = {
+    # name: (N, D, B, k, metric, description)
+    "c1": (10_000, 384, 1, 10, "cosine", "10K x 384 cosine top-10, single query"),
+    "c2": (1_000_000, 768, 64, 10, "cosine", "1M x 768 fp32 cosine top-10, batch 64"),
+    "c3": (1_000_000, 1536, 256, 10, "cosine", "1M x 1536 cosine top-10, batch 256 (fp32 candidate pass)"),
+    "c4": (10_000_000, 128, 512, 100, "euclidean", "10M x 128 L2 top-100, batch 512, row-sharded"),
+}
+FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md, Peak FP32 (matrix)
+HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md, HBM3E peak (spec)
+CHUNK_ROWS = 1 << 16
+
+
+def corpus_rows(N, D, start, stop, seed=0):
+    """Rows [start, stop) of the synthetic corpus: uniform [0,1) fp32 like the
+    reference harness (benchmarks/large_scale_benchmark.py:59), generated per
+    65536-row chunk from SeedSequence([seed, chunk]) so any shard is reproducible
+    without generating the others."""
+    out = np.empty((stop - start, D), np.float32)
+    c0, c1 = start // CHUNK_ROWS, (stop - 1) // CHUNK_ROWS
+    for c in range(c0, c1 + 1):
+        lo, hi = c * CHUNK_ROWS, min((c + 1) * CHUNK_ROWS, N)
+        blk = np.random.Generator(np.random.PCG64(np.random.SeedSequence([seed, c]))).random((hi - lo, D),
+                                                                                            dtype=np.float32)
+        a, b = max(lo, start), min(hi, stop)
+        out[a - start:b - start] = blk[a - lo:b - lo]
+    return out
+
+
+def shard_bounds(N, world, rank):
+    per = (N + world - 1) // world
+    return min(rank * per, N), min((rank + 1) * per, N)
+
+
+def cpu_baseline(V, Q, k):
+    """The reference's batched path restated in numpy (oracle/ref_cpu.py), one full batch."""
+    from oracle import ref_cpu
+    try:
+        from threadpoolctl import threadpool_info
+        threads = max([p.get("num_threads", 1) for p in threadpool_info() if p.get("user_api") == "blas"] or [1])
+    except Exception:
+        threads = int(os.environ.get("OMP_NUM_THREADS", "1"))
+    t0 = time.perf_counter()
+    ref_cpu.reference_batch_search(Q, V, k)
+    dt = time.perf_counter() - t0
+    return {"value": Q.shape[0] / dt, "unit": "queries/s", "cores": threads, "kind": "port",
+            "sample": f"1 batch of {Q.shape[0]} queries x full {V.shape[0]}x{V.shape[1]} corpus, numpy restatement "
+                      f"of optimized_batch_similarity_search (normalise + fp32 BLAS matmul + stable argsort); "
+                      f"{dt:.2f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--scan-variant", type=int, default=None, help="candidate-pass kernel variant (tuning)")
+    ap.add_argument("--n-wg", type=int, default=None, help="candidate-pass workgroups (tuning)")
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_scan_latest.json"),
+                    help="HBM traffic of scan_topk from a separate rocprofv3 --pmc pass (see profiles/)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    N, D, B, k, metric, desc = CONFIGS[args.config]
+    lo, hi = shard_bounds(N, world, rank)
+    n_local = hi - lo
+
+    # ---- data: this rank's shard of the corpus, replicated queries -------------------
+    keep_host = world == 1 and rank == 0 and not args.no_cpu_baseline
+    ix = _vdb.NativeIndex(D, metric, local)
+    if args.scan_variant is not None:
+        ix.set_param("scan_variant", args.scan_variant)
+    if args.n_wg is not None:
+        ix.set_param("n_wg", args.n_wg)
+    ix.reserve(n_local)
+    host_parts = []
+    for s in range(lo, hi, 8 * CHUNK_ROWS):
+        part = corpus_rows(N, D, s, min(s + 8 * CHUNK_ROWS, hi))
+        ix.add(part)
+        if keep_host:
+            host_parts.append(part)
+    assert ix.count() == n_local
+    Q = np.random.default_rng(1).random((B, D), dtype=np.float32)  # large_scale_benchmark.py:61
+    q_dev = torch.from_numpy(Q).to(dev)
+    out_s = torch.empty((B, k), dtype=torch.float32, device=dev)
+    out_i = torch.empty((B, k), dtype=torch.int64, device=dev)
+    out_k = torch.empty((B, k), dtype=torch.float64, device=dev)
+    if world > 1:
+        g_keys = torch.empty((world, B, k), dtype=torch.float64, device=dev)
+        g_idx = torch.empty((world, B, k), dtype=torch.int64, device=dev)
+        fin_s = torch.empty((B, k), dtype=torch.float32, device=dev)
+        fin_i = torch.empty((B, k), dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def step():
+        ix.search_device(q_dev.data_ptr(), B, k, out_s.data_ptr(), out_i.data_ptr(),
+                         out_k.data_ptr() if world > 1 else 0, index_offset=lo, stream=stream)
+        if world > 1:
+            dist.all_gather_into_tensor(g_keys, out_k)
+            dist.all_gather_into_tensor(g_idx, out_i)
+            _vdb.merge_topk_device(g_keys.data_ptr(), g_idx.data_ptr(), world, B, k, k, metric,
+                                   fin_s.data_ptr(), fin_i.data_ptr(), 0, stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    ix.set_param("timing", 1)
+    scan0, pipe0, n0 = ix.stat("scan_ns"), ix.stat("pipeline_ns"), ix.stat("timed_searches")
+    lat = []
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        t0 = time.perf_counter()
+        step()
+        torch.cuda.synchronize()
+        lat.append(time.perf_counter() - t0)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    n_t = ix.stat("timed_searches") - n0
+    scan_ms = (ix.stat("scan_ns") - scan0) / 1e6 / max(n_t, 1)
+    pipe_ms = (ix.stat("pipeline_ns") - pipe0) / 1e6 / max(n_t, 1)
+    ix.set_param("timing", 0)
+    if world > 1:
+        t = torch.tensor([elapsed, scan_ms, pipe_ms, float(np.median(lat))], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, scan_ms, pipe_ms, p50 = t.tolist()
+    else:
+        p50 = float(np.median(lat))
+
+    fallback = ix.stat("fallback_queries")
+    if rank == 0:
+        flops = 2.0 * B * n_local * D  # per rank per launch of scan_topk (algorithmic)
+        achieved_tf = flops / (scan_ms * 1e-3) / 1e12
+        hbm_bytes = n_local * D * 4 + n_local * 4 + B * D * 4  # corpus + row scales + queries, once
+        traffic = None
+        traffic_src = None
+        try:
+            pm = json.load(open(args.pmc_json))
+            if pm.get("config") == args.config and pm.get("n_gpus") == world:
+                traffic = pm["hbm_bytes_per_launch"]
+                traffic_src = os.path.relpath(args.pmc_json, ROOT)
+        except Exception:
+            pass
+        rec = {
+            "metric": METRIC,
+            "value": B * args.steps / elapsed,
+            "unit": "queries/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "p50_ms": p50 * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic uniform [0,1) fp32 (numpy PCG64, corpus seed 0 per 65536-row chunk, queries seed 1)",
+            "config": {"workload": f"{args.config}: {desc}", "n_rows": N, "dim": D, "batch": B, "k": k,
+                       "metric": metric, "parallelism": f"row-shard x{world}" if world > 1 else "single GPU",
+                       "rows_per_gpu": n_local},
+            "roofline": {"bound": "mfma", "kernel": "scan_topk", "achieved": achieved_tf,
+                         "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved_tf / FP32_MFMA_PEAK_TFLOPS,
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "algorithmic_bytes": hbm_bytes, "avg_launch_ms": scan_ms,
+                         "hbm_gbs_algorithmic": hbm_bytes / (scan_ms * 1e-3) / 1e9},
+            "pipeline_ms": pipe_ms,
+            "fallback_queries_total": fallback,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            V = np.concatenate(host_parts) if len(host_parts) > 1 else host_parts[0]
+            del host_parts
+            rec["cpu_baseline"] = cpu_baseline(V, Q, k)
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -17,9 +17,11 @@
  *     failing call on the calling thread.
  *   - Plain pointers and sizes only.  `mem` says whether the query / output
  *     pointers of a call are host (VDB_MEM_HOST) or device (VDB_MEM_DEVICE)
- *     memory.  Host-memory calls are synchronous; device-memory calls are
- *     stream-ordered on `stream` (a hipStream_t, or NULL for the index's own
- *     stream) and return without waiting.
+ *     memory.  Work is stream-ordered on `stream` (a hipStream_t, or NULL for
+ *     the index's own stream).  Host-memory calls return when the results are
+ *     in host memory; a device-memory search synchronises `stream` once (to
+ *     read the exactness certificate, see vdb_index_search) and returns with
+ *     the results in device memory.
  *   - The library never frees caller memory.  An index owns its device-resident
  *     corpus (tiled fp32 layout) and a per-call workspace pool.
  *   - All entry points are thread-safe; searches on one index may run from
@@ -78,7 +80,10 @@ int32_t vdb_index_destroy(vdb_index* idx);
 /* Pre-size the device corpus for `rows` rows (capacity otherwise doubles). */
 int32_t vdb_index_reserve(vdb_index* idx, int64_t rows);
 /* Tuning / test knobs: "precision" (VDB_PREC_*), "margin" (extra candidates
- * per query), "force_exact" (0/1), "n_wg" (candidate-pass workgroups). */
+ * per query), "force_exact" (0/1), "n_wg" (candidate-pass workgroups),
+ * "timing" (0/1: HIP events around the candidate pass; stats "scan_ns",
+ * "pipeline_ns", "timed_searches").  Stats also: "searches", "queries",
+ * "fallback_queries", "capacity", "count", "device_bytes". */
 int32_t vdb_index_set_param(vdb_index* idx, const char* name, int64_t value);
 int32_t vdb_index_get_stat(const vdb_index* idx, const char* name, int64_t* value);
 

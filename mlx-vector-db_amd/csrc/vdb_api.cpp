@@ -46,7 +46,7 @@ int set_error(int code, const char* fmt, ...) {
                              #expr, hipGetErrorString(_e), __FILE__, __LINE__);                        \
     } while (0)
 
-constexpr int64_t kStepRows = STEP_ROWS;   // rows per scan step (4 waves x 2 row tiles x 32)
+constexpr int64_t kRowAlign = ROW_ALIGN;   // capacity granule, a multiple of every scan step
 constexpr int kMaxApproxK = 200;          // k above this uses the exact path
 
 inline int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
@@ -76,6 +76,7 @@ struct Workspace {
     size_t exact_bytes = 0;
     int* host_flag = nullptr;  // pinned
     hipEvent_t done = nullptr;
+    hipEvent_t tev[3] = {nullptr, nullptr, nullptr};  // timing: scan start / scan end / rerank end
     bool busy = false;
     bool used = false;
 };
@@ -86,7 +87,7 @@ struct vdb_index {
     int dim = 0, metric = 0, device = 0;
     int Dp = 0, G = 0;
     int64_t count = 0;
-    int64_t cap_rows = 0;  // multiple of kStepRows
+    int64_t cap_rows = 0;  // multiple of kRowAlign
     float* X = nullptr;
     double* nrm64 = nullptr;
     float* inv32 = nullptr;
@@ -101,8 +102,11 @@ struct vdb_index {
     int64_t margin = -1;  // -1 = default
     int64_t force_exact = 0;
     int64_t n_wg_override = 0;
+    int64_t timing = 0;  // record HIP events around the candidate pass
+    int64_t scan_variant = 0;
     // stats
     std::atomic<int64_t> n_searches{0}, n_queries{0}, n_fallback{0};
+    std::atomic<int64_t> scan_ns{0}, pipe_ns{0}, n_timed{0};
     std::shared_mutex mu;  // add/clear/reserve exclusive; search shared
     std::mutex ws_mu;
     std::vector<Workspace*> pool;
@@ -112,9 +116,9 @@ namespace {
 
 int ensure_capacity(vdb_index* ix, int64_t rows) {
     if (rows <= ix->cap_rows) return VDB_OK;
-    int64_t cap = std::max<int64_t>(ix->cap_rows * 2, kStepRows);
+    int64_t cap = std::max<int64_t>(ix->cap_rows * 2, kRowAlign);
     while (cap < rows) cap *= 2;
-    cap = round_up(cap, kStepRows);
+    cap = round_up(cap, kRowAlign);
     const size_t tile_floats = (size_t)ix->G * BLOCK_FLOATS;
     float* X = nullptr;
     double* n64 = nullptr;
@@ -130,7 +134,7 @@ int ensure_capacity(vdb_index* ix, int64_t rows) {
     if (ix->X) {
         // all searches that might read the old buffers must be finished
         HIP_TRY(hipDeviceSynchronize());
-        const int64_t used_tiles = round_up(ix->count, 32) / 32;
+        const int64_t used_tiles = round_up(ix->count, 128) / 32;  // whole super tiles (prefix of the layout)
         HIP_TRY(hipMemcpyAsync(X, ix->X, (size_t)used_tiles * tile_floats * sizeof(float), hipMemcpyDeviceToDevice,
                                ix->stream));
         HIP_TRY(hipMemcpyAsync(n64, ix->nrm64, ix->count * sizeof(double), hipMemcpyDeviceToDevice, ix->stream));
@@ -219,7 +223,7 @@ int run_exact(vdb_index* ix, Workspace* w, const float* Qd, const double* qn64, 
     int n_wg = (int)std::min<int64_t>(std::max<int64_t>(1, ix->n_cu * 2), std::max<int64_t>(1, N / 256));
     const int64_t rpw = (N + n_wg - 1) / n_wg;
     n_wg = (int)((N + rpw - 1) / rpw);
-    const int n_lists = n_wg * 4;
+    const int n_lists = n_wg;
     const size_t list_elems = (size_t)nq * n_lists * KE;
     const size_t bytes = list_elems * (sizeof(double) + sizeof(uint32_t)) + (size_t)nq * KE * 12 + 4096;
     int rc = ws_reserve_exact(w, bytes, st);
@@ -272,7 +276,7 @@ int32_t vdb_index_create(int32_t dim, int32_t metric, int32_t device, vdb_index*
     ix->dim = dim;
     ix->metric = metric;
     ix->device = device;
-    ix->Dp = (int)round_up(dim, 32);
+    ix->Dp = (int)round_up(dim, 64);  // G = Dp/8 is a multiple of the scan prefetch depth
     ix->G = ix->Dp / GROUP_DIMS;
     ix->n_cu = prop.multiProcessorCount;
     hipError_t e = hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking);
@@ -296,6 +300,8 @@ int32_t vdb_index_destroy(vdb_index* ix) {
         if (w->exact) (void)hipFree(w->exact);
         if (w->host_flag) (void)hipHostFree(w->host_flag);
         if (w->done) (void)hipEventDestroy(w->done);
+        for (int e = 0; e < 3; ++e)
+            if (w->tev[e]) (void)hipEventDestroy(w->tev[e]);
         delete w;
     }
     if (ix->X) (void)hipFree(ix->X);
@@ -328,6 +334,11 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
         ix->force_exact = value != 0;
     } else if (n == "n_wg") {
         ix->n_wg_override = value;
+    } else if (n == "scan_variant") {
+        if (value < 0 || value > 2) return set_error(VDB_ERR_INVALID, "scan_variant must be 0, 1 or 2");
+        ix->scan_variant = value;
+    } else if (n == "timing") {
+        ix->timing = value != 0;
     } else {
         return set_error(VDB_ERR_INVALID, "unknown parameter '%s'", name);
     }
@@ -341,6 +352,9 @@ int32_t vdb_index_get_stat(const vdb_index* ix, const char* name, int64_t* value
     else if (n == "queries") *value = ix->n_queries.load();
     else if (n == "fallback_queries") *value = ix->n_fallback.load();
     else if (n == "capacity") *value = ix->cap_rows;
+    else if (n == "scan_ns") *value = ix->scan_ns.load();
+    else if (n == "pipeline_ns") *value = ix->pipe_ns.load();
+    else if (n == "timed_searches") *value = ix->n_timed.load();
     else if (n == "count") *value = ix->count;
     else if (n == "device_bytes") *value = (int64_t)(ix->cap_rows / 32) * ix->G * BLOCK_FLOATS * 4 + ix->cap_rows * 16;
     else return set_error(VDB_ERR_INVALID, "unknown stat '%s'", name);
@@ -474,9 +488,11 @@ int32_t vdb_index_search(vdb_index* ix, const float* queries, int32_t B, int32_t
     const bool exact_all = ix->force_exact || k > kMaxApproxK || KP > 256;
     if (KP > 256) KP = 256;
     const int QB = KP == 256 ? 32 : 64;
-    const int Bp = (int)round_up(B, 64);
-    const int n_qblocks = Bp / QB;
-    const int64_t n_steps = std::max<int64_t>(1, round_up(N, kStepRows) / kStepRows);
+    const int Bp = (int)round_up(B, 128);  // whole query super tiles (tiled layout)
+    const int n_qblocks = (B + QB - 1) / QB;
+    const int variant = (int)ix->scan_variant;
+    const int64_t step_rows = scan_rows_per_step(variant);
+    const int64_t n_steps = std::max<int64_t>(1, round_up(N, step_rows) / step_rows);
     int target = ix->n_wg_override > 0 ? (int)ix->n_wg_override : std::max(1, ix->n_cu * 2 / n_qblocks);
     int spw = (int)std::max<int64_t>(1, (n_steps + target - 1) / target);
     int n_wg = (int)((n_steps + spw - 1) / spw);
@@ -491,18 +507,19 @@ int32_t vdb_index_search(vdb_index* ix, const float* queries, int32_t B, int32_t
     size_t bytes = 0;
     bytes += (size_t)B * D * 4 + 256;                       // Qraw (host mode)
     bytes += (size_t)(mask_words + 64) * 4 + 256;           // mask (host mode)
-    bytes += (size_t)Bp * ix->Dp * 4 + 256;                 // Qt
+    bytes += (size_t)Bp * (ix->Dp + 8 * QG_EXTRA) * 4 + 256;  // Qt (tiled, duplicated groups)
     bytes += (size_t)Bp * 8 + 256;                          // qn64
     bytes += (size_t)Bp * n_wg * KP * 8 + 512;              // candidate lists
     bytes += (size_t)Bp * KP * 8 + 512;                     // merged approx lists
     bytes += (size_t)B * k * 20 + 768;                      // outputs (host mode)
     bytes += (size_t)(B + 64) * 4 + 256;                    // flags
+    bytes += (size_t)Bp * 4 + 256;                          // shared thresholds
     int rc = ws_reserve(w, bytes, st);
     if (rc) return rc;
     Carver c{w->dev};
     float* Qraw = c.take<float>((size_t)B * D);
     uint32_t* maskd = c.take<uint32_t>(mask_words + 64);
-    float* Qt = c.take<float>((size_t)Bp * ix->Dp);
+    float* Qt = c.take<float>((size_t)Bp * (ix->Dp + 8 * QG_EXTRA));
     double* qn64 = c.take<double>(Bp);
     float* cs = c.take<float>((size_t)Bp * n_wg * KP);
     uint32_t* ci = c.take<uint32_t>((size_t)Bp * n_wg * KP);
@@ -512,6 +529,7 @@ int32_t vdb_index_search(vdb_index* ix, const float* queries, int32_t B, int32_t
     int64_t* oi = c.take<int64_t>((size_t)B * k);
     double* ok = c.take<double>((size_t)B * k);
     int* flags = c.take<int>(B + 64);
+    uint32_t* gthr = c.take<uint32_t>(Bp);
 
     const float* Qd = queries;
     const uint32_t* md = row_mask;
@@ -536,14 +554,18 @@ int32_t vdb_index_search(vdb_index* ix, const float* queries, int32_t B, int32_t
         HIP_TRY(hipMemsetAsync(out_s, 0, (size_t)B * k * 4, st));
         if (out_k) HIP_TRY(hipMemsetAsync(out_k, 0, (size_t)B * k * 8, st));
     } else {
-        HIP_TRY(hipMemsetAsync(Qt, 0, (size_t)Bp * ix->Dp * 4, st));
-        HIP_TRY(hipMemsetAsync(qn64, 0, (size_t)Bp * 8, st));
-        HIP_TRY(launch_prep_queries(Qd, B, D, ix->G, ix->metric, Qt, qn64, st));
+        HIP_TRY(launch_prep_queries(Qd, B, Bp, D, ix->G, ix->metric, Qt, qn64, flags, gthr, st));
         int n_flag = 0;
         if (!exact_all) {
-            HIP_TRY(hipMemsetAsync(flags, 0, sizeof(int), st));
-            HIP_TRY(launch_scan_topk(ix->metric, KP, ix->X, ix->metric == 0 ? ix->inv32 : ix->sq32, md, Qt, ix->G, N,
-                                     B, n_qblocks, n_steps, n_wg, spw, cs, ci, st));
+            const bool timed = ix->timing != 0;
+            if (timed) {
+                for (int e = 0; e < 3; ++e)
+                    if (!w->tev[e]) HIP_TRY(hipEventCreate(&w->tev[e]));
+                HIP_TRY(hipEventRecord(w->tev[0], st));
+            }
+            HIP_TRY(launch_scan_topk(ix->metric, KP, variant, ix->X, ix->metric == 0 ? ix->inv32 : ix->sq32, md, Qt, ix->G, N,
+                                     B, n_qblocks, n_steps, n_wg, spw, cs, ci, gthr, st));
+            if (timed) HIP_TRY(hipEventRecord(w->tev[1], st));
             HIP_TRY(launch_merge_f32(KP, cs, ci, n_wg, B, as, ai, st));
             RerankArgs ra;
             ra.Q = Qd; ra.qn64 = qn64; ra.X = ix->X; ra.G = ix->G; ra.D = D;
@@ -553,9 +575,18 @@ int32_t vdb_index_search(vdb_index* ix, const float* queries, int32_t B, int32_t
             ra.out_s = out_s; ra.out_i = out_i; ra.out_k = out_k; ra.index_offset = index_offset;
             ra.flag_count = flags; ra.flag_list = flags + 1;
             HIP_TRY(launch_rerank(ix->metric, KP, ra, B, st));
+            if (timed) HIP_TRY(hipEventRecord(w->tev[2], st));
             HIP_TRY(hipMemcpyAsync(w->host_flag, flags, sizeof(int), hipMemcpyDeviceToHost, st));
             HIP_TRY(hipStreamSynchronize(st));
             n_flag = w->host_flag[0];
+            if (timed) {
+                float ms_scan = 0.f, ms_pipe = 0.f;
+                HIP_TRY(hipEventElapsedTime(&ms_scan, w->tev[0], w->tev[1]));
+                HIP_TRY(hipEventElapsedTime(&ms_pipe, w->tev[0], w->tev[2]));
+                ix->scan_ns += (int64_t)(ms_scan * 1e6);
+                ix->pipe_ns += (int64_t)(ms_pipe * 1e6);
+                ix->n_timed++;
+            }
             if (n_flag > 0) {
                 ix->n_fallback += n_flag;
                 rc = run_exact(ix, w, Qd, qn64, flags + 1, n_flag, k, md, out_s, out_i, out_k, index_offset, st);

@@ -8,6 +8,7 @@
 #include <stdint.h>
 #include <math.h>
 #include <type_traits>
+#include <algorithm>
 #include "vdb_internal.h"
 
 namespace vdb {
@@ -16,20 +17,25 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 // ---- corpus / query tiling -------------------------------------------------
-// A "row tile" is 32 rows; a "group" is 8 dimensions.  Tile (t, g) is one
-// 1 KiB block laid out in MFMA lane order: lane l holds the 4 floats
-//   X[32 t + (l & 31)][8 g + 4 (l >> 5) + j],  j = 0..3
+// A "row tile" is 32 rows, a "super tile" 4 row tiles (128 rows), a "group" 8
+// dimensions.  Block (super tile st, group g, sub tile u) is 1 KiB in MFMA lane
+// order: lane l holds the 4 floats
+//   X[128 st + 32 u + (l & 31)][8 g + 4 (l >> 5) + j],  j = 0..3
 // so one global_load_dwordx4 per lane fetches exactly the A operand of four
-// consecutive v_mfma_f32_32x32x2_f32 k-steps (k index = l >> 5), and a whole
-// wave reads 1 KiB of contiguous HBM.  Dimensions are padded to Dp (multiple
-// of 32, zeros), rows to the capacity (multiple of 256, zeros).
+// consecutive v_mfma_f32_32x32x2_f32 k-steps (k index = l >> 5); a whole wave
+// reads 1 KiB of contiguous HBM, and the 4 sub tiles of one group are adjacent
+// (a wave owning several row tiles addresses them with immediate offsets).
+// Layout: [T/4][G][4][64][4].  Dimensions are padded to Dp (multiple of 64,
+// zeros), rows to the capacity (multiple of ROW_ALIGN, zeros).  Queries use the
+// same layout.
+__device__ __forceinline__ size_t tiled_block(uint64_t t, int g, int G) {
+    return (((size_t)(t >> 2) * G + g) * 4 + (t & 3)) * BLOCK_FLOATS;
+}
+
 __device__ __forceinline__ size_t tiled_offset(uint64_t r, int d, int G) {
-    const uint64_t t = r >> 5;
     const int i = (int)(r & 31);
-    const int g = d >> 3;
     const int kk = (d >> 2) & 1;
-    const int j = d & 3;
-    return (((size_t)t * G + g) * 64 + i + 32 * kk) * 4 + j;
+    return tiled_block(r >> 5, d >> 3, G) + (i + 32 * kk) * 4 + (d & 3);
 }
 
 // ---- ordering ----------------------------------------------------------------
@@ -111,14 +117,124 @@ __device__ __forceinline__ void wave_merge_desc(K (&s)[E], I (&ix)[E]) {
 
 // ---- canonical fp64 arithmetic ---------------------------------------------------
 // The exact ranking keys are computed in ONE fixed order so that the numpy
-// oracle (oracle/ref_cpu.py: canonical_dot64) reproduces them bit for bit:
-// lane l accumulates dims d = l, l+64, l+128, ... (zero beyond the data) with
-// separate multiply and add (the file is built with -ffp-contract=off), then a
-// xor-butterfly over offsets 32,16,8,4,2,1.
+// oracle (oracle/ref_cpu.py, canonical_*) reproduces them bit for bit:
+//   lane l owns the 4-dim "pieces" p = 64 m + l (dims 4p .. 4p+3), m = 0, 1, ...
+//   (dims past D are zero; D is padded to a multiple of 256), and accumulates
+//   them in (m, j) order with separate multiply and add (the library is built
+//   with -ffp-contract=off); then an xor-butterfly over offsets 32,16,8,4,2,1.
+// In the tiled corpus a piece is one aligned 16-byte load.
 __device__ __forceinline__ double wave_sum_butterfly(double v) {
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) v = v + __shfl_xor(v, off, 64);
     return v;
 }
+
+// float offset of piece p (dims 4p..4p+3) of row r in the tiled corpus
+__device__ __forceinline__ size_t tiled_piece_offset(uint64_t r, int p, int G) {
+    return tiled_block(r >> 5, p >> 1, G) + (size_t)(r & 31) * 4 + (size_t)(p & 1) * 128;
+}
+
+// Write one result slot (fp32 score, int64 row, optional fp64 key).
+__device__ __forceinline__ void write_result(int metric, double key, uint64_t row_plus_off, bool valid, float* os,
+                                             int64_t* oi, double* ok) {
+    if (valid) {
+        *os = metric == 0 ? (float)key : (float)sqrt(-key);
+        *oi = (int64_t)row_plus_off;
+        if (ok) *ok = key;
+    } else {
+        *os = 0.0f;
+        *oi = -1;
+        if (ok) *ok = -INFINITY;
+    }
+}
+
+// ---- LDS-resident sorting / streaming selection (runtime sizes, one wave) --------
+// Used where a register network would be large (hundreds+ of elements): the
+// loops are not unrolled, so code size and compile time stay small.  Only the
+// calling wave touches the buffer; LDS accesses of one wave complete in order,
+// the wave_barrier only stops the compiler from moving them across stages.
+template <typename K, typename I>
+__device__ __attribute__((noinline)) void wave_lds_sort_desc(K* k, I* ix, int n /* power of two */) {
+    const int lane = threadIdx.x & 63;
+    for (int size = 2; size <= n; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int e = lane; e < (n >> 1); e += 64) {
+                const int lo = 2 * stride * (e / stride) + (e % stride);
+                const int hi = lo + stride;
+                const bool desc = (lo & size) == 0;
+                const K a = k[lo], b = k[hi];
+                const I ia = ix[lo], ib = ix[hi];
+                const bool sw = desc ? better(b, ib, a, ia) : better(a, ia, b, ib);
+                if (sw) {
+                    k[lo] = b; k[hi] = a;
+                    ix[lo] = ib; ix[hi] = ia;
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+}
+
+__host__ __device__ __forceinline__ int pow2_at_least(int v) {
+    int p = 1;
+    while (p < v) p <<= 1;
+    return p;
+}
+
+// Streaming top-KP for ONE wave over batches of up to 64 candidates (one per
+// lane), with an LDS buffer of capacity(KP) entries: candidates that beat the current
+// threshold are appended; a full buffer is sorted and cut back to KP, which
+// raises the threshold (the KP-th best so far).  Any KP (power of two).
+template <typename K, typename I>
+struct WaveTopK {
+    K* bk;
+    I* bi;
+    int KP;
+    int cap;  // buffer entries: power of two >= max(2 KP, KP + 64)
+    int cnt;
+    K tk;
+    I ti;
+    static __host__ __device__ int capacity(int kp) { return pow2_at_least(2 * kp > kp + 64 ? 2 * kp : kp + 64); }
+    __device__ void init(K* k, I* i, int kp) {
+        bk = k; bi = i; KP = kp; cap = capacity(kp); cnt = 0;
+        tk = (K)-INFINITY; ti = sentinel_idx<I>();
+    }
+    __device__ void compact() {
+        const int lane = threadIdx.x & 63;
+        for (int e = cnt + lane; e < cap; e += 64) {
+            bk[e] = (K)-INFINITY;
+            bi[e] = sentinel_idx<I>();
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        wave_lds_sort_desc<K, I>(bk, bi, cap);
+        cnt = cnt < KP ? cnt : KP;
+        if (cnt == KP) {
+            tk = bk[KP - 1];
+            ti = bi[KP - 1];
+        }
+    }
+    __device__ void offer(bool valid, K key, I idx) {
+        const int lane = threadIdx.x & 63;
+        bool pass = valid && better(key, idx, tk, ti);
+        unsigned long long m = __ballot(pass);
+        if (m == 0) return;
+        if (cnt + __popcll(m) > cap) {
+            compact();
+            pass = valid && better(key, idx, tk, ti);
+            m = __ballot(pass);
+        }
+        const int pos = cnt + __popcll(m & ((1ull << lane) - 1ull));
+        if (pass) {
+            bk[pos] = key;
+            bi[pos] = idx;
+        }
+        cnt += __popcll(m);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    }
+    // sort what is kept; afterwards bk[0..min(cnt,KP)) is the sorted result and
+    // the rest of [0, KP) holds sentinels
+    __device__ void finish() { compact(); }
+};
 
 }  // namespace vdb

@@ -1,0 +1,177 @@
+// vdb_ingest.hip: ingest (pack/unpack), query preparation and the operator-slot score matrix — part of the gfx950 kernels of the brute-force distance + top-k path
+// (pipeline overview: vdb_scan.hip).  Built with -ffp-contract=off.
+#include "vdb_common.h"
+#include "vdb_internal.h"
+
+namespace vdb {
+
+// =============================================================================
+// Ingest
+// =============================================================================
+// One wave per row.  Canonical fp64 norm (vdb_common.h), tiled store of whole
+// 16-byte pieces (padding dims of the row are written as zeros).
+__global__ void __launch_bounds__(256) pack_rows_kernel(const float* __restrict__ src, int64_t n, int D, int G,
+                                                        float* __restrict__ X, int64_t row0,
+                                                        double* __restrict__ nrm64, float* __restrict__ inv32,
+                                                        float* __restrict__ sq32,
+                                                        unsigned long long* __restrict__ xmax_bits,
+                                                        int* __restrict__ nonfinite) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= n) return;
+    const int Dp = G * GROUP_DIMS;
+    const int np = (D + 255) / 256;
+    const float* s = src + row * (int64_t)D;
+    const uint64_t r = (uint64_t)(row0 + row);
+    double acc = 0.0;
+    int bad = 0;
+    for (int m = 0; m < np; ++m) {
+        const int p = m * 64 + lane;
+        f32x4 v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int d = 4 * p + j;
+            v[j] = d < D ? s[d] : 0.0f;
+            bad |= !isfinite(v[j]);
+            const double dv = (double)v[j];
+            acc = acc + dv * dv;
+        }
+        if (4 * p < Dp) *(f32x4*)(X + tiled_piece_offset(r, p, G)) = v;
+    }
+    acc = wave_sum_butterfly(acc);
+    const int anybad = __any(bad);
+    if (lane == 0) {
+        const double nr = sqrt(acc);
+        nrm64[r] = nr;
+        inv32[r] = (float)(1.0 / fmax(nr, 1e-8));
+        sq32[r] = (float)acc;
+        if (anybad) atomicAdd(nonfinite, 1);
+        else atomicMax(xmax_bits, (unsigned long long)__double_as_longlong(nr));
+    }
+}
+
+hipError_t launch_pack_rows(const float* src, int64_t n, int D, int G, float* X, int64_t row0, double* nrm64,
+                            float* inv32, float* sq32, unsigned long long* xmax_bits, int* nonfinite,
+                            hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    const int64_t blocks = (n + 3) / 4;
+    hipLaunchKernelGGL(pack_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, st, src, n, D, G, X, row0, nrm64,
+                       inv32, sq32, xmax_bits, nonfinite);
+    return hipGetLastError();
+}
+
+__global__ void __launch_bounds__(256) unpack_rows_kernel(const float* __restrict__ X, int G, int D, int64_t row0,
+                                                          int64_t n, float* __restrict__ dst) {
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= n) return;
+    const int lane = threadIdx.x & 63;
+    for (int d = lane; d < D; d += 64) dst[row * D + d] = X[tiled_offset((uint64_t)(row0 + row), d, G)];
+}
+
+hipError_t launch_unpack_rows(const float* X, int G, int D, int64_t row0, int64_t n, float* dst, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(unpack_rows_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, X, G, D, row0, n, dst);
+    return hipGetLastError();
+}
+
+// =============================================================================
+// Queries
+// =============================================================================
+// One wave per padded query slot: canonical fp64 norm, tiled (cosine:
+// pre-normalised in fp32) query block including its zero padding, and the
+// certificate counter reset (one fewer memset per search).
+__global__ void __launch_bounds__(256) prep_queries_kernel(const float* __restrict__ Q, int B, int Bp, int D, int G,
+                                                           int metric, float* __restrict__ Qt,
+                                                           double* __restrict__ qn64, int* __restrict__ flag_count,
+                                                           uint32_t* __restrict__ gthr) {
+    const int lane = threadIdx.x & 63;
+    const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (b == 0 && lane == 0 && flag_count) *flag_count = 0;
+    if (b >= Bp) return;
+    if (lane == 0 && gthr) gthr[b] = 0u;
+    const int Dp = G * GROUP_DIMS;
+    const int np = (D + 255) / 256;
+    const bool real = b < B;
+    const float* q = Q + (int64_t)(real ? b : 0) * D;
+    double acc = 0.0;
+    for (int m = 0; m < np; ++m) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int d = 4 * (m * 64 + lane) + j;
+            const double v = (real && d < D) ? (double)q[d] : 0.0;
+            acc = acc + v * v;
+        }
+    }
+    acc = wave_sum_butterfly(acc);
+    const double nq = sqrt(acc);
+    if (lane == 0) qn64[b] = nq;
+    // cosine: the candidate pass works on q/max(|q|,1e-8) rounded to fp32.
+    const float scale = metric == 0 ? (float)(1.0 / fmax(nq, 1e-8)) : 1.0f;
+    const int GQ = G + QG_EXTRA;
+    for (int p = lane; 4 * p < Dp + 8 * QG_EXTRA; p += 64) {
+        const int ps = 4 * p < Dp ? p : p - 2 * G;  // source piece (duplicated groups wrap)
+        f32x4 v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int d = 4 * ps + j;
+            v[j] = (real && d < D) ? q[d] * scale : 0.0f;
+        }
+        *(f32x4*)(Qt + tiled_piece_offset((uint64_t)b, p, GQ)) = v;
+    }
+}
+
+hipError_t launch_prep_queries(const float* Q, int B, int Bp, int D, int G, int metric, float* Qt, double* qn64,
+                               int* flag_count, uint32_t* gthr, hipStream_t st) {
+    hipLaunchKernelGGL(prep_queries_kernel, dim3((Bp + 3) / 4), dim3(256), 0, st, Q, B, Bp, D, G, metric, Qt, qn64,
+                       flag_count, gthr);
+    return hipGetLastError();
+}
+// =============================================================================
+// Operator slot: the full score matrix, reference fp32 arithmetic
+// =============================================================================
+// cosine: x/max(|x|,1e-8) and q/max(|q|,1e-8) in fp32, then the dot product;
+// euclidean: sqrt(sum((x-q)^2)).  One wave per corpus row, looping queries; not
+// the hot path (service/optimized_vector_store.py:31-48 materialise [N] per
+// query, performance/mlx_optimized.py:59-88 [B,N]).
+__global__ void __launch_bounds__(256) similarity_matrix_kernel(const float* __restrict__ X, int64_t N, int D,
+                                                                const float* __restrict__ Q, int B, int metric,
+                                                                float* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= N) return;
+    const float* x = X + r * D;
+    float xs = 0.0f;
+    for (int d = lane; d < D; d += 64) xs = fmaf(x[d], x[d], xs);
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) xs += __shfl_xor(xs, off, 64);
+    const float xinv = 1.0f / fmaxf(sqrtf(xs), 1e-8f);
+    for (int b = 0; b < B; ++b) {
+        const float* q = Q + (int64_t)b * D;
+        float acc = 0.0f, qs = 0.0f;
+        for (int d = lane; d < D; d += 64) {
+            if (metric == 0) {
+                acc = fmaf(q[d], x[d] * xinv, acc);
+                qs = fmaf(q[d], q[d], qs);
+            } else {
+                const float df = x[d] - q[d];
+                acc = fmaf(df, df, acc);
+            }
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            acc += __shfl_xor(acc, off, 64);
+            qs += __shfl_xor(qs, off, 64);
+        }
+        if (lane == 0) out[(int64_t)b * N + r] = metric == 0 ? acc / fmaxf(sqrtf(qs), 1e-8f) : sqrtf(acc);
+    }
+}
+
+hipError_t launch_similarity_matrix(const float* X, int64_t N, int D, const float* Q, int B, int metric, float* out,
+                                    hipStream_t st) {
+    if (N <= 0 || B <= 0) return hipSuccess;
+    hipLaunchKernelGGL(similarity_matrix_kernel, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, st, X, N, D, Q, B,
+                       metric, out);
+    return hipGetLastError();
+}
+
+}  // namespace vdb

@@ -9,7 +9,8 @@ namespace vdb {
 constexpr int TILE_ROWS = 32;      // rows per row tile
 constexpr int GROUP_DIMS = 8;      // dims per (tile, group) block
 constexpr int BLOCK_FLOATS = 256;  // floats per (tile, group) block = 1 KiB
-constexpr int STEP_ROWS = 256;     // rows one scan workgroup consumes per step
+constexpr int QG_EXTRA = 8;        // duplicated leading dim-groups at the end of each query tile
+constexpr int ROW_ALIGN = 1024;    // corpus capacity granule (>= rows per scan step of any variant)
 
 // Ingest: row-major fp32 [n][D] (device) -> tiled corpus rows [row0, row0+n),
 // canonical fp64 norms, fp32 inverse norms and squared norms, running max norm
@@ -21,16 +22,21 @@ hipError_t launch_pack_rows(const float* src, int64_t n, int D, int G, float* X,
 // Tiled corpus rows -> row-major fp32 (export for persistence).
 hipError_t launch_unpack_rows(const float* X, int G, int D, int64_t row0, int64_t n, float* dst, hipStream_t st);
 
-// Queries: row-major [B][D] -> tiled Qt (cosine: pre-normalised in fp32) and
-// canonical fp64 norms.  Qt must be zeroed by the caller (padding).
-hipError_t launch_prep_queries(const float* Q, int B, int D, int G, int metric,
-                               float* Qt, double* qn64, hipStream_t st);
+// gthr[B]: per-query shared threshold (order-preserving score key, 0 = none),
+// zeroed by prep_queries; workgroups publish their KP-th best with atomicMax.
+// Queries: row-major [B][D] -> tiled Qt [Bp/32 tiles] with G + QG_EXTRA groups
+// (the first QG_EXTRA groups repeated at the end; cosine: pre-normalised in
+// fp32; zero padding written), canonical fp64 norms [Bp]; resets *flag_count.
+hipError_t launch_prep_queries(const float* Q, int B, int Bp, int D, int G, int metric,
+                               float* Qt, double* qn64, int* flag_count, uint32_t* gthr, hipStream_t st);
 
 // Candidate pass: MFMA fp32 scores fused with a per-workgroup top-KP.
 // Output lists cand_[s|i][B][n_wg][KP], each sorted best first.
-hipError_t launch_scan_topk(int metric, int KP, const float* X, const float* rowscale, const uint32_t* mask,
+int scan_rows_per_step(int variant);
+hipError_t launch_scan_topk(int metric, int KP, int variant, const float* X, const float* rowscale, const uint32_t* mask,
                             const float* Qt, int G, int64_t N, int B, int n_qblocks, int64_t n_steps,
-                            int n_wg, int steps_per_wg, float* cand_s, uint32_t* cand_i, hipStream_t st);
+                            int n_wg, int steps_per_wg, float* cand_s, uint32_t* cand_i, uint32_t* gthr,
+                            hipStream_t st);
 
 // Merge sorted per-workgroup lists -> sorted top-KP per query (fp32 keys).
 hipError_t launch_merge_f32(int KP, const float* ls, const uint32_t* li, int n_lists, int B,
@@ -47,7 +53,7 @@ struct RerankArgs {
 hipError_t launch_rerank(int metric, int KP, const RerankArgs& a, int B, hipStream_t st);
 
 // Exact fp64 scan of the whole corpus for the queries in qlist[0..nq):
-// per-wave sorted top-KE lists [nq][n_wg*4][KE] (fp64 keys, local rows).
+// per-workgroup sorted top-KE lists [nq][n_wg][KE] (fp64 keys, local rows).
 hipError_t launch_exact_scan(int metric, int KE, const float* Q, const double* qn64, const int* qlist, int nq,
                              const float* X, int G, int D, const double* nrm64, const uint32_t* mask,
                              int64_t N, int n_wg, int64_t rows_per_wg,

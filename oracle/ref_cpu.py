@@ -127,14 +127,17 @@ def reference_batch_search(queries, vectors, k=10):
 # =============================================================================
 # 2. The exact ranking contract (fp64, canonical order) the GPU path must match
 # =============================================================================
-def _pad64(A: np.ndarray) -> np.ndarray:
-    A = np.asarray(A)
-    D = A.shape[-1]
-    Dp = (D + 63) // 64 * 64
-    if Dp == D:
-        return A
-    pad = [(0, 0)] * (A.ndim - 1) + [(0, Dp - D)]
-    return np.pad(A, pad)
+def _pieces(A: np.ndarray) -> np.ndarray:
+    """[M, D] -> fp64 [M, np, 64, 4]: zero-pad D to a multiple of 256; lane l of
+    pass m owns dims 256 m + 4 l + j (the canonical order, vdb_common.h)."""
+    A = np.asarray(A, dtype=np.float32)
+    if A.ndim == 1:
+        A = A[None, :]
+    M, D = A.shape
+    Dp = (D + 255) // 256 * 256
+    if Dp != D:
+        A = np.pad(A, [(0, 0), (0, Dp - D)])
+    return A.astype(np.float64).reshape(M, Dp // 256, 64, 4)
 
 
 def _butterfly(acc: np.ndarray) -> np.ndarray:
@@ -146,13 +149,13 @@ def _butterfly(acc: np.ndarray) -> np.ndarray:
 
 
 def canonical_sumsq64(A: np.ndarray) -> np.ndarray:
-    """Per-row sum of squares in fp64, lane order of vdb_common.h (pack_rows_kernel)."""
-    X = _pad64(np.asarray(A, dtype=np.float32)).astype(np.float64)
-    X = X.reshape(X.shape[0], -1, 64)
+    """Per-row sum of squares in fp64, canonical order (pack_rows_kernel, prep_queries_kernel)."""
+    X = _pieces(A)
     acc = np.zeros((X.shape[0], 64))
     for m in range(X.shape[1]):
-        v = X[:, m, :]
-        acc = acc + v * v
+        for j in range(4):
+            v = X[:, m, :, j]
+            acc = acc + v * v
     return _butterfly(acc)
 
 
@@ -161,25 +164,25 @@ def canonical_norm64(A: np.ndarray) -> np.ndarray:
 
 
 def canonical_dot64(q: np.ndarray, X: np.ndarray) -> np.ndarray:
-    """fp64 q.x for every row of X, canonical order (exact_key<cosine> in vdb_kernels.hip)."""
-    qp = _pad64(np.asarray(q, dtype=np.float32).reshape(1, -1)).astype(np.float64).reshape(-1, 64)
-    Xp = _pad64(np.asarray(X, dtype=np.float32)).astype(np.float64)
-    Xp = Xp.reshape(Xp.shape[0], -1, 64)
+    """fp64 q.x for every row of X, canonical order (exact_key<cosine>, vdb_exact.hip)."""
+    qp = _pieces(np.asarray(q).reshape(1, -1))[0]
+    Xp = _pieces(X)
     acc = np.zeros((Xp.shape[0], 64))
     for m in range(Xp.shape[1]):
-        acc = acc + qp[m] * Xp[:, m, :]
+        for j in range(4):
+            acc = acc + qp[m, :, j] * Xp[:, m, :, j]
     return _butterfly(acc)
 
 
 def canonical_sqdist64(q: np.ndarray, X: np.ndarray) -> np.ndarray:
     """fp64 sum((x-q)^2) for every row of X, canonical order (exact_key<euclidean>)."""
-    qp = _pad64(np.asarray(q, dtype=np.float32).reshape(1, -1)).astype(np.float64).reshape(-1, 64)
-    Xp = _pad64(np.asarray(X, dtype=np.float32)).astype(np.float64)
-    Xp = Xp.reshape(Xp.shape[0], -1, 64)
+    qp = _pieces(np.asarray(q).reshape(1, -1))[0]
+    Xp = _pieces(X)
     acc = np.zeros((Xp.shape[0], 64))
     for m in range(Xp.shape[1]):
-        d = Xp[:, m, :] - qp[m]
-        acc = acc + d * d
+        for j in range(4):
+            d = Xp[:, m, :, j] - qp[m, :, j]
+            acc = acc + d * d
     return _butterfly(acc)
 
 
