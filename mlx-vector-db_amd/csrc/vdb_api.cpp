@@ -493,7 +493,9 @@ int32_t vdb_index_search(vdb_index* ix, const float* queries, int32_t B, int32_t
     const int variant = (int)ix->scan_variant;
     const int64_t step_rows = scan_rows_per_step(variant);
     const int64_t n_steps = std::max<int64_t>(1, round_up(N, step_rows) / step_rows);
-    int target = ix->n_wg_override > 0 ? (int)ix->n_wg_override : std::max(1, ix->n_cu * 2 / n_qblocks);
+    // one 4-wave workgroup per CU (1 wave per SIMD, all of its 512 registers):
+    // measured faster than two per CU, whose top-k epilogues then overlap (profiles/)
+    int target = ix->n_wg_override > 0 ? (int)ix->n_wg_override : std::max(1, ix->n_cu / n_qblocks);
     int spw = (int)std::max<int64_t>(1, (n_steps + target - 1) / target);
     int n_wg = (int)((n_steps + spw - 1) / spw);
     const int64_t mask_words = round_up(N, 32) / 32;
@@ -514,6 +516,7 @@ int32_t vdb_index_search(vdb_index* ix, const float* queries, int32_t B, int32_t
     bytes += (size_t)B * k * 20 + 768;                      // outputs (host mode)
     bytes += (size_t)(B + 64) * 4 + 256;                    // flags
     bytes += (size_t)Bp * 4 + 256;                          // shared thresholds
+    bytes += (size_t)Bp * KP_MAX * 4 + 256;                 // shared threshold slots
     int rc = ws_reserve(w, bytes, st);
     if (rc) return rc;
     Carver c{w->dev};
@@ -530,6 +533,7 @@ int32_t vdb_index_search(vdb_index* ix, const float* queries, int32_t B, int32_t
     double* ok = c.take<double>((size_t)B * k);
     int* flags = c.take<int>(B + 64);
     uint32_t* gthr = c.take<uint32_t>(Bp);
+    uint32_t* gslots = c.take<uint32_t>((size_t)Bp * KP_MAX);
 
     const float* Qd = queries;
     const uint32_t* md = row_mask;
@@ -554,7 +558,7 @@ int32_t vdb_index_search(vdb_index* ix, const float* queries, int32_t B, int32_t
         HIP_TRY(hipMemsetAsync(out_s, 0, (size_t)B * k * 4, st));
         if (out_k) HIP_TRY(hipMemsetAsync(out_k, 0, (size_t)B * k * 8, st));
     } else {
-        HIP_TRY(launch_prep_queries(Qd, B, Bp, D, ix->G, ix->metric, Qt, qn64, flags, gthr, st));
+        HIP_TRY(launch_prep_queries(Qd, B, Bp, D, ix->G, ix->metric, Qt, qn64, flags, gthr, gslots, st));
         int n_flag = 0;
         if (!exact_all) {
             const bool timed = ix->timing != 0;
@@ -564,7 +568,7 @@ int32_t vdb_index_search(vdb_index* ix, const float* queries, int32_t B, int32_t
                 HIP_TRY(hipEventRecord(w->tev[0], st));
             }
             HIP_TRY(launch_scan_topk(ix->metric, KP, variant, ix->X, ix->metric == 0 ? ix->inv32 : ix->sq32, md, Qt, ix->G, N,
-                                     B, n_qblocks, n_steps, n_wg, spw, cs, ci, gthr, st));
+                                     B, n_qblocks, n_steps, n_wg, spw, cs, ci, gthr, gslots, st));
             if (timed) HIP_TRY(hipEventRecord(w->tev[1], st));
             HIP_TRY(launch_merge_f32(KP, cs, ci, n_wg, B, as, ai, st));
             RerankArgs ra;

@@ -83,12 +83,15 @@ hipError_t launch_unpack_rows(const float* X, int G, int D, int64_t row0, int64_
 __global__ void __launch_bounds__(256) prep_queries_kernel(const float* __restrict__ Q, int B, int Bp, int D, int G,
                                                            int metric, float* __restrict__ Qt,
                                                            double* __restrict__ qn64, int* __restrict__ flag_count,
-                                                           uint32_t* __restrict__ gthr) {
+                                                           uint32_t* __restrict__ gthr,
+                                                           uint32_t* __restrict__ gslots) {
     const int lane = threadIdx.x & 63;
     const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (b == 0 && lane == 0 && flag_count) *flag_count = 0;
     if (b >= Bp) return;
     if (lane == 0 && gthr) gthr[b] = 0u;
+    if (gslots)
+        for (int j = lane; j < KP_MAX; j += 64) gslots[(size_t)b * KP_MAX + j] = 0u;
     const int Dp = G * GROUP_DIMS;
     const int np = (D + 255) / 256;
     const bool real = b < B;
@@ -121,9 +124,9 @@ __global__ void __launch_bounds__(256) prep_queries_kernel(const float* __restri
 }
 
 hipError_t launch_prep_queries(const float* Q, int B, int Bp, int D, int G, int metric, float* Qt, double* qn64,
-                               int* flag_count, uint32_t* gthr, hipStream_t st) {
+                               int* flag_count, uint32_t* gthr, uint32_t* gslots, hipStream_t st) {
     hipLaunchKernelGGL(prep_queries_kernel, dim3((Bp + 3) / 4), dim3(256), 0, st, Q, B, Bp, D, G, metric, Qt, qn64,
-                       flag_count, gthr);
+                       flag_count, gthr, gslots);
     return hipGetLastError();
 }
 // =============================================================================

@@ -22,13 +22,16 @@ hipError_t launch_pack_rows(const float* src, int64_t n, int D, int G, float* X,
 // Tiled corpus rows -> row-major fp32 (export for persistence).
 hipError_t launch_unpack_rows(const float* X, int G, int D, int64_t row0, int64_t n, float* dst, hipStream_t st);
 
-// gthr[B]: per-query shared threshold (order-preserving score key, 0 = none),
-// zeroed by prep_queries; workgroups publish their KP-th best with atomicMax.
+// gthr[B]: per-query shared threshold (order-preserving score key, 0 = none) and
+// gslots[B][KP_MAX]: per-query slots of published workgroup bests; both zeroed by
+// prep_queries (see the publish step of scan_topk_kernel).
+constexpr int KP_MAX = 256;
 // Queries: row-major [B][D] -> tiled Qt [Bp/32 tiles] with G + QG_EXTRA groups
 // (the first QG_EXTRA groups repeated at the end; cosine: pre-normalised in
 // fp32; zero padding written), canonical fp64 norms [Bp]; resets *flag_count.
 hipError_t launch_prep_queries(const float* Q, int B, int Bp, int D, int G, int metric,
-                               float* Qt, double* qn64, int* flag_count, uint32_t* gthr, hipStream_t st);
+                               float* Qt, double* qn64, int* flag_count, uint32_t* gthr, uint32_t* gslots,
+                               hipStream_t st);
 
 // Candidate pass: MFMA fp32 scores fused with a per-workgroup top-KP.
 // Output lists cand_[s|i][B][n_wg][KP], each sorted best first.
@@ -36,7 +39,7 @@ int scan_rows_per_step(int variant);
 hipError_t launch_scan_topk(int metric, int KP, int variant, const float* X, const float* rowscale, const uint32_t* mask,
                             const float* Qt, int G, int64_t N, int B, int n_qblocks, int64_t n_steps,
                             int n_wg, int steps_per_wg, float* cand_s, uint32_t* cand_i, uint32_t* gthr,
-                            hipStream_t st);
+                            uint32_t* gslots, hipStream_t st);
 
 // Merge sorted per-workgroup lists -> sorted top-KP per query (fp32 keys).
 hipError_t launch_merge_f32(int KP, const float* ls, const uint32_t* li, int n_lists, int B,

@@ -155,7 +155,8 @@ template <int METRIC, int QT, int RT, int PX, int PQ, int KP, int CAP, int WPS>
 __global__ void __launch_bounds__(256, WPS)
 scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale, const uint32_t* __restrict__ mask,
                  const float* __restrict__ Qt, int G, int64_t N, int B, int64_t n_steps, int steps_per_wg,
-                 float* __restrict__ cand_s, uint32_t* __restrict__ cand_i, uint32_t* __restrict__ gthr) {
+                 float* __restrict__ cand_s, uint32_t* __restrict__ cand_i, uint32_t* __restrict__ gthr,
+                 uint32_t* __restrict__ gslots) {
     static_assert(PX % PQ == 0, "query prefetch depth must divide the corpus prefetch depth");
     static_assert(PQ <= QG_EXTRA, "query prefetch deeper than the duplicated groups");
     constexpr int QB = 32 * QT;
@@ -164,6 +165,8 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
     __shared__ uint32_t s_ix[QB * CAP];
     __shared__ int s_cnt[QB];
     __shared__ float s_thr[QB];
+    __shared__ uint32_t s_best[QB];  // order key of the best score appended so far
+    __shared__ uint32_t s_pub[QB];   // ... and of the last one published
     __shared__ float s_rs[2][SR];  // row scales, double-buffered by step parity
 
     const int lane = threadIdx.x & 63;
@@ -177,6 +180,8 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
 
     for (int i = threadIdx.x; i < QB; i += 256) {
         s_cnt[i] = 0;
+        s_best[i] = 0;
+        s_pub[i] = 0;
         s_thr[i] = -INFINITY;
     }
 
@@ -214,6 +219,7 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
 #ifdef VDB_STAMP
     unsigned long long st_k = 0, st_e = 0, st_e0 = 0, st_t0 = STAMP_NOW();
     unsigned long long st_bar = 0, st_sc = 0, st_ins = 0, st_rt = 0, st_rounds = 0, st_compacts = 0;
+    unsigned long long st_pub_start = 0, st_pub = 0;
 #endif
     for (int64_t s = s_begin; s < s_end; ++s) {
 #ifdef VDB_STAMP
@@ -337,6 +343,10 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
             if (!__any(pm != 0)) return 0u;
             const int ql = qt * 32 + (lane & 31);
             const int base = pm ? atomicAdd(&s_cnt[ql], __popc(pm)) : 0;
+            float mx = -INFINITY;
+#pragma unroll
+            for (int v = 0; v < 16; ++v) mx = ((pm >> v) & 1u) ? fmaxf(mx, acc[rt][qt][v]) : mx;
+            if (pm) atomicMax(&s_best[ql], order_key(mx));
             uint32_t left = 0;
 #pragma unroll
             for (int v = 0; v < 16; ++v) {
@@ -394,8 +404,47 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
             }
         }
 #ifdef VDB_STAMP
+        const unsigned long long st_b5 = STAMP_NOW();
+        st_pub_start = st_b5;
+#endif
+        // ---- publish: slot (query, wg % KP) of gslots holds the max over a fixed set
+        // of workgroups of their best score, so the KP slots of a query are scores of
+        // KP distinct rows and their minimum is a lower bound of the global KP-th best
+        // (DESIGN.md §3.2).  Only queries whose best improved are republished.
+        // Published after this workgroup's steps 1, 2, 4, 8, ... (each costs a global
+        // round trip, and the bound moves little once every slot is filled).
+        const int64_t sd = s - s_begin + 1;
+        if ((sd & (sd - 1)) == 0 || s + 1 == s_end) {
+            constexpr int QPW = QB / 4;
+            bool improved = false;
+            uint32_t best = 0;
+            int qg = 0;
+            if (lane < QPW) {
+                const int q = wv + 4 * lane;
+                qg = qb * QB + q;
+                best = s_best[q];
+                improved = qg < B && best > s_pub[q];
+                if (improved) {
+                    s_pub[q] = best;
+                    atomicMax(gslots + (size_t)qg * KP + (wg % KP), best);
+                }
+            }
+            if (__any(improved) && improved) {
+                // all KP slot loads in flight at once (one round trip)
+                const uint32_t* sl = gslots + (size_t)qg * KP;
+                uint32_t mn = 0xFFFFFFFFu;
+#pragma unroll
+                for (int j = 0; j < KP; j += 4) {
+                    const uint4 v4 = *(const uint4*)(sl + j);
+                    mn = min(min(mn, min(v4.x, v4.y)), min(v4.z, v4.w));
+                }
+                atomicMax(gthr + qg, mn);
+            }
+        }
+#ifdef VDB_STAMP
         const unsigned long long st_c = STAMP_NOW();
-        st_rt += st_c - st_b4;
+        st_pub += st_c - st_pub_start;
+        st_rt += st_pub_start - st_b4;
         st_e += st_c - st_b;
         if (s == s_begin) st_e0 = st_c - st_b;
 #endif
@@ -405,7 +454,7 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
         const int w = wg * 4 + wv;
         g_scan_stamps[w][0] = st_k;
         g_scan_stamps[w][1] = st_e;
-        g_scan_stamps[w][2] = st_rounds * 1000000ull + st_compacts;
+        g_scan_stamps[w][2] = st_pub;
         g_scan_stamps[w][3] = STAMP_NOW() - st_t0;
         g_scan_stamps[w][4] = st_bar;
         g_scan_stamps[w][5] = st_sc;
@@ -427,9 +476,9 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
 template <int METRIC, int QT, int RT, int PX, int PQ, int KP, int CAP, int WPS>
 static hipError_t scan_dispatch(const float* X, const float* rowscale, const uint32_t* mask, const float* Qt, int G,
                                 int64_t N, int B, int n_qblocks, int64_t n_steps, int n_wg, int spw, float* cs,
-                                uint32_t* ci, uint32_t* gthr, hipStream_t st) {
+                                uint32_t* ci, uint32_t* gthr, uint32_t* gslots, hipStream_t st) {
     hipLaunchKernelGGL((scan_topk_kernel<METRIC, QT, RT, PX, PQ, KP, CAP, WPS>), dim3(n_wg, n_qblocks), dim3(256), 0, st,
-                       X, rowscale, mask, Qt, G, N, B, n_steps, spw, cs, ci, gthr);
+                       X, rowscale, mask, Qt, G, N, B, n_steps, spw, cs, ci, gthr, gslots);
     return hipGetLastError();
 }
 
@@ -440,14 +489,14 @@ int scan_waves_per_simd(int variant) { return variant == 2 ? 1 : 2; }
 hipError_t launch_scan_topk(int metric, int KP, int variant, const float* X, const float* rowscale,
                             const uint32_t* mask, const float* Qt, int G, int64_t N, int B, int n_qblocks,
                             int64_t n_steps, int n_wg, int spw, float* cs, uint32_t* ci, uint32_t* gthr,
-                            hipStream_t st) {
+                            uint32_t* gslots, hipStream_t st) {
     // variant 0: RT=2 (64 rows/wave), corpus 4 groups ahead, 2 waves/SIMD
     // variant 1: RT=4 (128 rows/wave), corpus 4 groups ahead, 2 waves/SIMD
     // variant 2: RT=4, corpus 8 groups ahead, 1 wave/SIMD (accumulators in AGPRs)
 #define VDB_SCAN(M, QT, KPV, V, RT, PX, PQ, W)                                                                 \
     if (metric == M && KP == KPV && variant == V)                                                             \
         return scan_dispatch<M, QT, RT, PX, PQ, KPV, (KPV == 32 ? 4 : 2) * KPV, W>(X, rowscale, mask, Qt, G, N, B, n_qblocks, n_steps, \
-                                                              n_wg, spw, cs, ci, gthr, st);
+                                                              n_wg, spw, cs, ci, gthr, gslots, st);
 #define VDB_SCAN_ALL(M)                                                                                  \
     VDB_SCAN(M, 2, 32, 0, 2, 4, 4, 2) VDB_SCAN(M, 2, 64, 0, 2, 4, 4, 2) VDB_SCAN(M, 2, 128, 0, 2, 4, 4, 1) \
     VDB_SCAN(M, 1, 256, 0, 2, 4, 4, 1)                                                                   \

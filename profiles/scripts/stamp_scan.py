@@ -26,6 +26,6 @@ lib.vdb_debug_scan_stamps(buf, n)
 a = np.array(buf, dtype=np.uint64).reshape(n, 8).astype(np.float64)
 a = a[a[:, 3] > 0]
 print(f"variant {variant} nwg {nwg}: waves {len(a)}")
-for i, name in enumerate(["k-loop", "epilogue", "rounds*1e6+compactions", "total", "barrier after k-loop", "scoring", "first insert pass", "retry loop (+barrier)"]):
+for i, name in enumerate(["k-loop", "epilogue", "publish", "total", "barrier after k-loop", "scoring", "first insert pass", "retry loop (+barrier,-pub)"]):
     print(f"  {name:22s} mean {a[:, i].mean():12.0f}  max {a[:, i].max():12.0f}  (ticks)")
 print("  k-loop share", a[:, 0].sum() / a[:, 3].sum(), "epilogue share", a[:, 1].sum() / a[:, 3].sum())
