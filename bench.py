@@ -18,6 +18,7 @@ stream it runs on) and, at N=1, the CPU baseline: the reference's batched path
 timed on this host on one full batch.
 """
 import argparse
+import glob
 import json
 import os
 import sys
@@ -94,8 +95,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--scan-variant", type=int, default=None, help="candidate-pass kernel variant (tuning)")
     ap.add_argument("--n-wg", type=int, default=None, help="candidate-pass workgroups (tuning)")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_scan_latest.json"),
-                    help="HBM traffic of scan_topk from a separate rocprofv3 --pmc pass (see profiles/)")
+    ap.add_argument("--pmc-json", default=None,
+                    help="HBM traffic of the scan kernel from a separate rocprofv3 --pmc pass "
+                         "(default: newest profiles/*/pmc.json for this config, see profiles/scripts/)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -187,13 +189,16 @@ def main():
         hbm_bytes = n_local * D * 4 + n_local * 4 + B * D * 4  # corpus + row scales + queries, once
         traffic = None
         traffic_src = None
-        try:
-            pm = json.load(open(args.pmc_json))
-            if pm.get("config") == args.config and pm.get("n_gpus") == world:
+        cands = [args.pmc_json] if args.pmc_json else sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc.json")))
+        for path in reversed(cands):
+            try:
+                pm = json.load(open(path))
+            except (OSError, ValueError):
+                continue
+            if pm.get("config") == args.config and pm.get("n_gpus") == world and "hbm_bytes_per_launch" in pm:
                 traffic = pm["hbm_bytes_per_launch"]
-                traffic_src = os.path.relpath(args.pmc_json, ROOT)
-        except Exception:
-            pass
+                traffic_src = os.path.relpath(path, ROOT)
+                break
         rec = {
             "metric": METRIC,
             "value": B * args.steps / elapsed,

@@ -1,0 +1,15 @@
+#!/bin/bash
+# One GPU call: parity tests, smoke, bench (N=1), rocprofv3 kernel-trace summary.
+# Usage (from the repo root, via gpurun): bash profiles/scripts/gpu_check.sh [tag]
+set -o pipefail
+export TMPDIR=/tmp
+TAG=${1:-r01}
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu_$TAG.log 2>&1 || { echo "pytest failed"; tail -40 gpurun_out/pytest_gpu_$TAG.log; exit 1; }
+tail -3 gpurun_out/pytest_gpu_$TAG.log
+timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || { echo "smoke failed"; cat gpurun_out/smoke_$TAG.log; exit 1; }
+cat gpurun_out/smoke_$TAG.log
+timeout -k 10 400 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { echo "bench failed"; tail -30 gpurun_out/bench_$TAG.err; exit 1; }
+cat gpurun_out/bench_$TAG.json
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run -- python bench.py --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/prof_bench_$TAG.json 2> gpurun_out/prof_$TAG.err || { echo "rocprof failed"; tail -30 gpurun_out/prof_$TAG.err; exit 1; }
+find gpurun_out/prof_$TAG -name '*stats*'
