@@ -1,21 +1,23 @@
 #!/usr/bin/env python3
 """Headline benchmark: brute-force cosine / L2 top-k on MI355X (BASELINE.json).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c1|c3|c4]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c1|c3|c4] [--scaling weak|strong]
 
 One "step" = one batch of queries searched against the whole corpus (fused
-fp32-MFMA candidate scan + exact fp64 rerank; queries, corpus and outputs
-resident in HBM).  N=1 runs BASELINE.json configs[1] (C2: 1M x 768 fp32
-cosine, batch 64, top-10).  N>1 (torchrun, one rank per GPU, RCCL) row-shards
-the SAME corpus over the ranks — each rank searches its shard, the per-shard
+MFMA candidate scan + exact fp64 rerank; queries, corpus and outputs resident
+in HBM).  N=1 runs BASELINE.json configs[1] (C2: 1M x 768 fp32 cosine, batch
+64, top-10).  N>1 (torchrun, one rank per GPU, RCCL) row-shards the corpus over
+the ranks (service/sharded.py): each rank searches its shard, the per-shard
 top-k lists (fp64 keys + global row ids) are all-gathered over xGMI and merged
-on device, bit-identical to one GPU — so total work is fixed ("strong").
+on device, bit-identical to one GPU.  Default "weak" scaling keeps the work per
+GPU fixed: the global batch is B x N queries against the same corpus (each rank:
+B x N queries x N_rows/N rows); "strong" keeps the batch at B.
 
 Rank 0 prints one JSON line: QPS (whole job), p50 batch latency, the roofline
-of the dominant kernel (scan_topk, HIP-event timed inside the library on the
-stream it runs on) and, at N=1, the CPU baseline: the reference's batched path
-(performance/mlx_optimized.py:217-248) restated in numpy (oracle/ref_cpu.py),
-timed on this host on one full batch.
+of the dominant kernel (the scan kernel, HIP-event timed inside the library on
+the stream it runs on) and, at N=1, the CPU baseline: the reference's batched
+path (performance/mlx_optimized.py:217-248) restated in numpy
+(oracle/ref_cpu.py), timed on this host on one bounded sample.
 """
 import argparse
 import glob
@@ -34,6 +36,7 @@ import torch  # noqa: E402  (loaded before the HIP library: one HIP runtime per 
 import torch.distributed as dist  # noqa: E402
 
 from service import _vdb  # noqa: E402
+from service.sharded import ShardedSearcher, shard_bounds  # noqa: E402
 
 METRIC = "QPS + p50 latency, cosine top-10 batch=64: 1M×768D @1 GPU; 10M×128D @8 GPU"
 CONFIGS = {
@@ -44,6 +47,7 @@ CONFIGS = {
     "c4": (10_000_000, 128, 512, 100, "euclidean", "10M x 128 L2 top-100, batch 512, row-sharded"),
 }
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md, Peak FP32 (matrix)
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md, Peak BF16 MFMA, dense
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md, HBM3E peak (spec)
 CHUNK_ROWS = 1 << 16
 
@@ -62,11 +66,6 @@ def corpus_rows(N, D, start, stop, seed=0):
         a, b = max(lo, start), min(hi, stop)
         out[a - start:b - start] = blk[a - lo:b - lo]
     return out
-
-
-def shard_bounds(N, world, rank):
-    per = (N + world - 1) // world
-    return min(rank * per, N), min((rank + 1) * per, N)
 
 
 def cpu_baseline(V, Q, k):
@@ -93,6 +92,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="N>1: weak = global batch B*N (fixed work per GPU), strong = global batch B")
+    ap.add_argument("--precision", default="bf16x3", choices=["bf16x3", "fp32"],
+                    help="candidate-pass arithmetic (results identical; DESIGN.md §3)")
     ap.add_argument("--scan-variant", type=int, default=None, help="candidate-pass kernel variant (tuning)")
     ap.add_argument("--n-wg", type=int, default=None, help="candidate-pass workgroups (tuning)")
     ap.add_argument("--pmc-json", default=None,
@@ -117,9 +120,9 @@ def main():
 
     # ---- data: this rank's shard of the corpus, replicated queries -------------------
     keep_host = world == 1 and rank == 0 and not args.no_cpu_baseline
-    ix = _vdb.NativeIndex(D, metric, local)
+    ix = _vdb.NativeIndex(D, metric, local, precision=args.precision)
     if args.scan_variant is not None:
-        ix.set_param("scan_variant", args.scan_variant)
+        ix.set_param("scan_variant" if args.precision == "fp32" else "scan_variant_bf16x3", args.scan_variant)
     if args.n_wg is not None:
         ix.set_param("n_wg", args.n_wg)
     ix.reserve(n_local)
@@ -130,26 +133,19 @@ def main():
         if keep_host:
             host_parts.append(part)
     assert ix.count() == n_local
-    Q = np.random.default_rng(1).random((B, D), dtype=np.float32)  # large_scale_benchmark.py:61
+    Bg = B * world if (world > 1 and args.scaling == "weak") else B  # global batch
+    Q = np.random.default_rng(1).random((Bg, D), dtype=np.float32)  # large_scale_benchmark.py:61
     q_dev = torch.from_numpy(Q).to(dev)
-    out_s = torch.empty((B, k), dtype=torch.float32, device=dev)
-    out_i = torch.empty((B, k), dtype=torch.int64, device=dev)
-    out_k = torch.empty((B, k), dtype=torch.float64, device=dev)
-    if world > 1:
-        g_keys = torch.empty((world, B, k), dtype=torch.float64, device=dev)
-        g_idx = torch.empty((world, B, k), dtype=torch.int64, device=dev)
-        fin_s = torch.empty((B, k), dtype=torch.float32, device=dev)
-        fin_i = torch.empty((B, k), dtype=torch.int64, device=dev)
+    out_s = torch.empty((Bg, k), dtype=torch.float32, device=dev)
+    out_i = torch.empty((Bg, k), dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
+    searcher = ShardedSearcher.from_index(ix, lo) if world > 1 else None
 
     def step():
-        ix.search_device(q_dev.data_ptr(), B, k, out_s.data_ptr(), out_i.data_ptr(),
-                         out_k.data_ptr() if world > 1 else 0, index_offset=lo, stream=stream)
-        if world > 1:
-            dist.all_gather_into_tensor(g_keys, out_k)
-            dist.all_gather_into_tensor(g_idx, out_i)
-            _vdb.merge_topk_device(g_keys.data_ptr(), g_idx.data_ptr(), world, B, k, k, metric,
-                                   fin_s.data_ptr(), fin_i.data_ptr(), 0, stream)
+        if searcher is None:
+            ix.search_device(q_dev.data_ptr(), Bg, k, out_s.data_ptr(), out_i.data_ptr(), 0, stream=stream)
+        else:
+            searcher.search(q_dev, k, out_s, out_i)
 
     for _ in range(args.warmup):
         step()
@@ -184,9 +180,25 @@ def main():
 
     fallback = ix.stat("fallback_queries")
     if rank == 0:
-        flops = 2.0 * B * n_local * D  # per rank per launch of scan_topk (algorithmic)
-        achieved_tf = flops / (scan_ms * 1e-3) / 1e12
-        hbm_bytes = n_local * D * 4 + n_local * 4 + B * D * 4  # corpus + row scales + queries, once
+        # algorithmic work of one scan launch on this rank: every corpus row read once
+        # (fp32 tiles or the split hi/lo tiles: 4 B per element either way), its row
+        # scale, the queries; flops = 2 B N D (x3 bf16 MFMA flops for the split product)
+        Dp = (D + 63) // 64 * 64
+        hbm_bytes = n_local * Dp * 4 + n_local * 4 + Bg * Dp * 4
+        if args.precision == "fp32":
+            mfma_flops, mfma_peak = 2.0 * Bg * n_local * D, FP32_MFMA_PEAK_TFLOPS
+        else:
+            mfma_flops, mfma_peak = 3 * 2.0 * Bg * n_local * D, BF16_MFMA_PEAK_TFLOPS
+        t_hbm = hbm_bytes / (HBM_PEAK_GBS * 1e9)
+        t_mfma = mfma_flops / (mfma_peak * 1e12)
+        achieved_gbs = hbm_bytes / (scan_ms * 1e-3) / 1e9
+        achieved_tf = mfma_flops / (scan_ms * 1e-3) / 1e12
+        if t_hbm >= t_mfma:
+            roof = {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": achieved_gbs / HBM_PEAK_GBS}
+        else:
+            roof = {"bound": "mfma", "achieved": achieved_tf, "peak": mfma_peak, "unit": "TFLOP/s",
+                    "frac": achieved_tf / mfma_peak}
         traffic = None
         traffic_src = None
         cands = [args.pmc_json] if args.pmc_json else sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc.json")))
@@ -195,13 +207,14 @@ def main():
                 pm = json.load(open(path))
             except (OSError, ValueError):
                 continue
-            if pm.get("config") == args.config and pm.get("n_gpus") == world and "hbm_bytes_per_launch" in pm:
+            if (pm.get("config") == args.config and pm.get("n_gpus") == world and "hbm_bytes_per_launch" in pm
+                    and pm.get("precision", "fp32") == args.precision):
                 traffic = pm["hbm_bytes_per_launch"]
                 traffic_src = os.path.relpath(path, ROOT)
                 break
         rec = {
             "metric": METRIC,
-            "value": B * args.steps / elapsed,
+            "value": Bg * args.steps / elapsed,
             "unit": "queries/s",
             "n_gpus": world,
             "steps": args.steps,
@@ -209,18 +222,18 @@ def main():
             "ms_per_step": elapsed / args.steps * 1e3,
             "p50_ms": p50 * 1e3,
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": args.scaling if world > 1 else "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "f32" if args.precision == "fp32" else "f32 (bf16x3 split MFMA candidates, fp64 exact rerank)",
             "data": "synthetic uniform [0,1) fp32 (numpy PCG64, corpus seed 0 per 65536-row chunk, queries seed 1)",
-            "config": {"workload": f"{args.config}: {desc}", "n_rows": N, "dim": D, "batch": B, "k": k,
+            "config": {"workload": f"{args.config}: {desc}", "n_rows": N, "dim": D, "global_batch": Bg,
+                       "batch_per_gpu_equiv": B, "k": k,
                        "metric": metric, "parallelism": f"row-shard x{world}" if world > 1 else "single GPU",
                        "rows_per_gpu": n_local},
-            "roofline": {"bound": "mfma", "kernel": "scan_topk", "achieved": achieved_tf,
-                         "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved_tf / FP32_MFMA_PEAK_TFLOPS,
-                         "traffic": traffic, "traffic_source": traffic_src,
-                         "algorithmic_bytes": hbm_bytes, "avg_launch_ms": scan_ms,
-                         "hbm_gbs_algorithmic": hbm_bytes / (scan_ms * 1e-3) / 1e9},
+            "roofline": dict(roof, traffic=traffic, kernel="scan_topk", precision=args.precision,
+                             traffic_source=traffic_src, algorithmic_bytes=hbm_bytes, algorithmic_flops=mfma_flops,
+                             avg_launch_ms=scan_ms, hbm_gbs=achieved_gbs, mfma_tflops=achieved_tf,
+                             hbm_frac=achieved_gbs / HBM_PEAK_GBS, mfma_frac=achieved_tf / mfma_peak),
             "pipeline_ms": pipe_ms,
             "fallback_queries_total": fallback,
         }

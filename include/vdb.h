@@ -58,8 +58,16 @@ enum {
 enum { VDB_METRIC_COSINE = 0, VDB_METRIC_EUCLIDEAN = 1 };
 enum { VDB_MEM_HOST = 0, VDB_MEM_DEVICE = 1 };
 
-/* Candidate-pass arithmetic for an index (vdb_index_set_param "precision"). */
-enum { VDB_PREC_FP32 = 0, VDB_PREC_BF16 = 1 };
+/* Candidate-pass arithmetic for an index (vdb_index_set_param "precision").
+ * The returned results are identical for both (the exact fp64 rerank decides);
+ * only the speed of the candidate pass differs.
+ *   VDB_PREC_FP32    fp32 v_mfma_f32_32x32x2_f32 (MFMA-bound, 157 TF peak)
+ *   VDB_PREC_BF16X3  split-bf16 "x3": x = hi + lo, q = hi + lo,
+ *                    x.q ~ xh.qh + xh.ql + xl.qh on v_mfma_f32_32x32x16_bf16,
+ *                    fp32 accumulate; error bound of the same order as fp32
+ *                    (HBM-bound).  Default.  Keeps a split copy of the corpus
+ *                    (same bytes as the fp32 copy). */
+enum { VDB_PREC_FP32 = 0, VDB_PREC_BF16X3 = 1 };
 
 typedef struct vdb_index vdb_index;
 
@@ -81,9 +89,10 @@ int32_t vdb_index_destroy(vdb_index* idx);
 int32_t vdb_index_reserve(vdb_index* idx, int64_t rows);
 /* Tuning / test knobs: "precision" (VDB_PREC_*), "margin" (extra candidates
  * per query), "force_exact" (0/1), "n_wg" (candidate-pass workgroups),
+ * "scan_variant" / "scan_variant_bf16x3" (0..2, kernel tiling variants),
  * "timing" (0/1: HIP events around the candidate pass; stats "scan_ns",
  * "pipeline_ns", "timed_searches").  Stats also: "searches", "queries",
- * "fallback_queries", "capacity", "count", "device_bytes". */
+ * "fallback_queries", "capacity", "count", "device_bytes", "precision". */
 int32_t vdb_index_set_param(vdb_index* idx, const char* name, int64_t value);
 int32_t vdb_index_get_stat(const vdb_index* idx, const char* name, int64_t* value);
 

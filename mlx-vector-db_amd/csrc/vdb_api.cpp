@@ -88,7 +88,8 @@ struct vdb_index {
     int Dp = 0, G = 0;
     int64_t count = 0;
     int64_t cap_rows = 0;  // multiple of kRowAlign
-    float* X = nullptr;
+    float* X = nullptr;      // fp32 tiles (rerank, exact scan, export, fp32 candidate pass)
+    float* Xs = nullptr;     // split-bf16 tiles (bf16x3 candidate pass), same bytes as X
     double* nrm64 = nullptr;
     float* inv32 = nullptr;
     float* sq32 = nullptr;
@@ -98,12 +99,13 @@ struct vdb_index {
     hipStream_t stream = nullptr;
     int n_cu = 256;
     // knobs
-    int64_t precision = VDB_PREC_FP32;
+    int64_t precision = VDB_PREC_BF16X3;
     int64_t margin = -1;  // -1 = default
     int64_t force_exact = 0;
     int64_t n_wg_override = 0;
     int64_t timing = 0;  // record HIP events around the candidate pass
-    int64_t scan_variant = 0;
+    int64_t scan_variant = 0;     // fp32 candidate pass variant (vdb_scan.hip)
+    int64_t scan_variant_b3 = 0;  // bf16x3 candidate pass variant
     // stats
     std::atomic<int64_t> n_searches{0}, n_queries{0}, n_fallback{0};
     std::atomic<int64_t> scan_ns{0}, pipe_ns{0}, n_timed{0};
@@ -120,10 +122,17 @@ int ensure_capacity(vdb_index* ix, int64_t rows) {
     while (cap < rows) cap *= 2;
     cap = round_up(cap, kRowAlign);
     const size_t tile_floats = (size_t)ix->G * BLOCK_FLOATS;
+    const size_t x_bytes = (size_t)(cap / 32) * tile_floats * sizeof(float);
+    const bool split = ix->precision == VDB_PREC_BF16X3;
     float* X = nullptr;
+    float* Xs = nullptr;
     double* n64 = nullptr;
     float *i32 = nullptr, *s32 = nullptr;
-    HIP_TRY(hipMalloc(&X, (size_t)(cap / 32) * tile_floats * sizeof(float)));
+    HIP_TRY(hipMalloc(&X, x_bytes));
+    if (split) {
+        HIP_TRY(hipMalloc(&Xs, x_bytes));
+        HIP_TRY(hipMemsetAsync(Xs, 0, x_bytes, ix->stream));
+    }
     HIP_TRY(hipMalloc(&n64, cap * sizeof(double)));
     HIP_TRY(hipMalloc(&i32, cap * sizeof(float)));
     HIP_TRY(hipMalloc(&s32, cap * sizeof(float)));
@@ -137,16 +146,23 @@ int ensure_capacity(vdb_index* ix, int64_t rows) {
         const int64_t used_tiles = round_up(ix->count, 128) / 32;  // whole super tiles (prefix of the layout)
         HIP_TRY(hipMemcpyAsync(X, ix->X, (size_t)used_tiles * tile_floats * sizeof(float), hipMemcpyDeviceToDevice,
                                ix->stream));
+        if (split && ix->Xs)
+            HIP_TRY(hipMemcpyAsync(Xs, ix->Xs, (size_t)used_tiles * tile_floats * sizeof(float),
+                                   hipMemcpyDeviceToDevice, ix->stream));
+        else if (split)
+            HIP_TRY(launch_split_rows(X, ix->G, 0, ix->count, Xs, ix->stream));
         HIP_TRY(hipMemcpyAsync(n64, ix->nrm64, ix->count * sizeof(double), hipMemcpyDeviceToDevice, ix->stream));
         HIP_TRY(hipMemcpyAsync(i32, ix->inv32, ix->count * sizeof(float), hipMemcpyDeviceToDevice, ix->stream));
         HIP_TRY(hipMemcpyAsync(s32, ix->sq32, ix->count * sizeof(float), hipMemcpyDeviceToDevice, ix->stream));
         HIP_TRY(hipStreamSynchronize(ix->stream));
         (void)hipFree(ix->X);
+        if (ix->Xs) (void)hipFree(ix->Xs);
         (void)hipFree(ix->nrm64);
         (void)hipFree(ix->inv32);
         (void)hipFree(ix->sq32);
     }
     ix->X = X;
+    ix->Xs = Xs;
     ix->nrm64 = n64;
     ix->inv32 = i32;
     ix->sq32 = s32;
@@ -305,6 +321,7 @@ int32_t vdb_index_destroy(vdb_index* ix) {
         delete w;
     }
     if (ix->X) (void)hipFree(ix->X);
+    if (ix->Xs) (void)hipFree(ix->Xs);
     if (ix->nrm64) (void)hipFree(ix->nrm64);
     if (ix->inv32) (void)hipFree(ix->inv32);
     if (ix->sq32) (void)hipFree(ix->sq32);
@@ -326,7 +343,23 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
     if (!ix || !name) return set_error(VDB_ERR_INVALID, "NULL argument");
     std::string n(name);
     if (n == "precision") {
-        if (value != VDB_PREC_FP32) return set_error(VDB_ERR_UNSUPPORTED, "precision %lld not built yet", (long long)value);
+        if (value != VDB_PREC_FP32 && value != VDB_PREC_BF16X3)
+            return set_error(VDB_ERR_INVALID, "precision must be %d (fp32) or %d (bf16x3), got %lld", VDB_PREC_FP32,
+                             VDB_PREC_BF16X3, (long long)value);
+        HIP_TRY(hipSetDevice(ix->device));
+        std::unique_lock<std::shared_mutex> g(ix->mu);
+        if (value == ix->precision) return VDB_OK;
+        HIP_TRY(hipDeviceSynchronize());
+        if (value == VDB_PREC_FP32) {
+            if (ix->Xs) (void)hipFree(ix->Xs);  // the split copy is only read by the bf16x3 pass
+            ix->Xs = nullptr;
+        } else if (ix->cap_rows > 0) {
+            const size_t x_bytes = (size_t)(ix->cap_rows / 32) * ix->G * BLOCK_FLOATS * sizeof(float);
+            HIP_TRY(hipMalloc(&ix->Xs, x_bytes));
+            HIP_TRY(hipMemsetAsync(ix->Xs, 0, x_bytes, ix->stream));
+            HIP_TRY(launch_split_rows(ix->X, ix->G, 0, ix->count, ix->Xs, ix->stream));
+            HIP_TRY(hipStreamSynchronize(ix->stream));
+        }
         ix->precision = value;
     } else if (n == "margin") {
         ix->margin = value;
@@ -337,6 +370,9 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
     } else if (n == "scan_variant") {
         if (value < 0 || value > 2) return set_error(VDB_ERR_INVALID, "scan_variant must be 0, 1 or 2");
         ix->scan_variant = value;
+    } else if (n == "scan_variant_bf16x3") {
+        if (value < 0 || value > 2) return set_error(VDB_ERR_INVALID, "scan_variant_bf16x3 must be 0, 1 or 2");
+        ix->scan_variant_b3 = value;
     } else if (n == "timing") {
         ix->timing = value != 0;
     } else {
@@ -356,7 +392,9 @@ int32_t vdb_index_get_stat(const vdb_index* ix, const char* name, int64_t* value
     else if (n == "pipeline_ns") *value = ix->pipe_ns.load();
     else if (n == "timed_searches") *value = ix->n_timed.load();
     else if (n == "count") *value = ix->count;
-    else if (n == "device_bytes") *value = (int64_t)(ix->cap_rows / 32) * ix->G * BLOCK_FLOATS * 4 + ix->cap_rows * 16;
+    else if (n == "precision") *value = ix->precision;
+    else if (n == "device_bytes")
+        *value = (int64_t)(ix->cap_rows / 32) * ix->G * BLOCK_FLOATS * 4 * (ix->Xs ? 2 : 1) + ix->cap_rows * 16;
     else return set_error(VDB_ERR_INVALID, "unknown stat '%s'", name);
     return VDB_OK;
 }
@@ -384,6 +422,7 @@ int32_t vdb_index_add(vdb_index* ix, const float* vectors, int64_t n, int32_t me
             hipError_t e = hipMemcpyAsync(staging, src, (size_t)m * D * sizeof(float), hipMemcpyHostToDevice, st);
             if (e == hipSuccess) e = launch_pack_rows(staging, m, D, ix->G, ix->X, ix->count + r, ix->nrm64,
                                                       ix->inv32, ix->sq32, ix->d_xmax, ix->d_nonfinite, st);
+            if (e == hipSuccess && ix->Xs) e = launch_split_rows(ix->X, ix->G, ix->count + r, m, ix->Xs, st);
             if (e == hipSuccess) e = hipStreamSynchronize(st);  // staging reuse
             if (e != hipSuccess) {
                 (void)hipFree(staging);
@@ -392,6 +431,7 @@ int32_t vdb_index_add(vdb_index* ix, const float* vectors, int64_t n, int32_t me
         } else {
             HIP_TRY(launch_pack_rows(src, m, D, ix->G, ix->X, ix->count + r, ix->nrm64, ix->inv32, ix->sq32,
                                      ix->d_xmax, ix->d_nonfinite, st));
+            if (ix->Xs) HIP_TRY(launch_split_rows(ix->X, ix->G, ix->count + r, m, ix->Xs, st));
         }
     }
     if (staging) (void)hipFree(staging);
@@ -429,6 +469,9 @@ int32_t vdb_index_clear(vdb_index* ix) {
         HIP_TRY(hipMemsetAsync(ix->X, 0, (size_t)(ix->cap_rows / 32) * ix->G * BLOCK_FLOATS * sizeof(float),
                                ix->stream));
         HIP_TRY(hipMemsetAsync(ix->nrm64, 0, ix->cap_rows * sizeof(double), ix->stream));
+        if (ix->Xs)
+            HIP_TRY(hipMemsetAsync(ix->Xs, 0, (size_t)(ix->cap_rows / 32) * ix->G * BLOCK_FLOATS * sizeof(float),
+                                   ix->stream));
     }
     HIP_TRY(hipMemsetAsync(ix->d_xmax, 0, 64, ix->stream));
     HIP_TRY(hipStreamSynchronize(ix->stream));
@@ -490,8 +533,11 @@ int32_t vdb_index_search(vdb_index* ix, const float* queries, int32_t B, int32_t
     const int QB = KP == 256 ? 32 : 64;
     const int Bp = (int)round_up(B, 128);  // whole query super tiles (tiled layout)
     const int n_qblocks = (B + QB - 1) / QB;
-    const int variant = (int)ix->scan_variant;
-    const int64_t step_rows = scan_rows_per_step(variant);
+    const int prec = ix->Xs && ix->precision == VDB_PREC_BF16X3 ? PREC_BF16X3 : PREC_FP32;
+    const int Gs = prec == PREC_FP32 ? ix->G : ix->G / 2;  // scan groups (8 or 16 dims)
+    int variant = (int)(prec == PREC_FP32 ? ix->scan_variant : ix->scan_variant_b3);
+    if (!scan_variant_ok(prec, variant, Gs)) variant = 0;  // e.g. PX=8 needs Dp % 128 == 0
+    const int64_t step_rows = scan_rows_per_step(prec, variant);
     const int64_t n_steps = std::max<int64_t>(1, round_up(N, step_rows) / step_rows);
     // one 4-wave workgroup per CU (1 wave per SIMD, all of its 512 registers):
     // measured faster than two per CU, whose top-k epilogues then overlap (profiles/)
@@ -509,7 +555,7 @@ int32_t vdb_index_search(vdb_index* ix, const float* queries, int32_t B, int32_t
     size_t bytes = 0;
     bytes += (size_t)B * D * 4 + 256;                       // Qraw (host mode)
     bytes += (size_t)(mask_words + 64) * 4 + 256;           // mask (host mode)
-    bytes += (size_t)Bp * (ix->Dp + 8 * QG_EXTRA) * 4 + 256;  // Qt (tiled, duplicated groups)
+    bytes += (size_t)Bp * (ix->Dp + 16 * QG_EXTRA) * 4 + 256;  // Qt (tiled fp32 or split, duplicated groups)
     bytes += (size_t)Bp * 8 + 256;                          // qn64
     bytes += (size_t)Bp * n_wg * KP * 8 + 512;              // candidate lists
     bytes += (size_t)Bp * KP * 8 + 512;                     // merged approx lists
@@ -522,7 +568,7 @@ int32_t vdb_index_search(vdb_index* ix, const float* queries, int32_t B, int32_t
     Carver c{w->dev};
     float* Qraw = c.take<float>((size_t)B * D);
     uint32_t* maskd = c.take<uint32_t>(mask_words + 64);
-    float* Qt = c.take<float>((size_t)Bp * (ix->Dp + 8 * QG_EXTRA));
+    float* Qt = c.take<float>((size_t)Bp * (ix->Dp + 16 * QG_EXTRA));
     double* qn64 = c.take<double>(Bp);
     float* cs = c.take<float>((size_t)Bp * n_wg * KP);
     uint32_t* ci = c.take<uint32_t>((size_t)Bp * n_wg * KP);
@@ -558,7 +604,8 @@ int32_t vdb_index_search(vdb_index* ix, const float* queries, int32_t B, int32_t
         HIP_TRY(hipMemsetAsync(out_s, 0, (size_t)B * k * 4, st));
         if (out_k) HIP_TRY(hipMemsetAsync(out_k, 0, (size_t)B * k * 8, st));
     } else {
-        HIP_TRY(launch_prep_queries(Qd, B, Bp, D, ix->G, ix->metric, Qt, qn64, flags, gthr, gslots, st));
+        HIP_TRY(launch_prep_queries(Qd, B, Bp, D, ix->G, ix->metric, prec == PREC_FP32 ? Qt : nullptr,
+                                    prec == PREC_FP32 ? nullptr : Qt, qn64, flags, gthr, gslots, st));
         int n_flag = 0;
         if (!exact_all) {
             const bool timed = ix->timing != 0;
@@ -567,14 +614,22 @@ int32_t vdb_index_search(vdb_index* ix, const float* queries, int32_t B, int32_t
                     if (!w->tev[e]) HIP_TRY(hipEventCreate(&w->tev[e]));
                 HIP_TRY(hipEventRecord(w->tev[0], st));
             }
-            HIP_TRY(launch_scan_topk(ix->metric, KP, variant, ix->X, ix->metric == 0 ? ix->inv32 : ix->sq32, md, Qt, ix->G, N,
+            HIP_TRY(launch_scan_topk(prec, ix->metric, KP, variant, prec == PREC_FP32 ? ix->X : ix->Xs,
+                                     ix->metric == 0 ? ix->inv32 : ix->sq32, md, Qt, Gs, N,
                                      B, n_qblocks, n_steps, n_wg, spw, cs, ci, gthr, gslots, st));
             if (timed) HIP_TRY(hipEventRecord(w->tev[1], st));
             HIP_TRY(launch_merge_f32(KP, cs, ci, n_wg, B, as, ai, st));
             RerankArgs ra;
             ra.Q = Qd; ra.qn64 = qn64; ra.X = ix->X; ra.G = ix->G; ra.D = D;
             ra.nrm64 = ix->nrm64; ra.app_s = as; ra.app_i = ai; ra.k = k;
-            ra.eps_rel = 1.01 * (double)(ix->Dp + 8) * std::ldexp(1.0, -24);
+            // |approx - exact| <= eps_rel * sum|q_i x_i| (relative to |q||x|):
+            //   fp32:   D fp32 MFMA additions + ~8 roundings of the normalisation / scaling
+            //   bf16x3: 3D additions (each counted at 2^-23 in case the bf16 MFMA adds
+            //           truncate) + the dropped hi*lo-order terms (< 3.1 2^-16) + the same 8
+            ra.eps_rel = prec == PREC_FP32
+                             ? 1.01 * (double)(D + 8) * std::ldexp(1.0, -24)
+                             : 1.01 * (3.0 * D * std::ldexp(1.0, -23) + 3.1 * std::ldexp(1.0, -16) +
+                                       8.0 * std::ldexp(1.0, -24));
             ra.xmax = ix->xmax;
             ra.out_s = out_s; ra.out_i = out_i; ra.out_k = out_k; ra.index_offset = index_offset;
             ra.flag_count = flags; ra.flag_list = flags + 1;

@@ -38,6 +38,45 @@ __device__ __forceinline__ size_t tiled_offset(uint64_t r, int d, int G) {
     return tiled_block(r >> 5, d >> 3, G) + (i + 32 * kk) * 4 + (d & 3);
 }
 
+// Split-bf16 corpus / query tiles (PREC_BF16X3): a group is 16 dims; block
+// (super tile st, group g, plane pl, sub tile u) is 1 KiB in the A/B operand
+// order of v_mfma_f32_32x32x16_bf16: lane l holds the 8 bf16
+//   plane(X[128 st + 32 u + (l & 31)][16 g + 8 (l >> 5) + j]),  j = 0..7
+// plane 0 = hi = bf16(x), plane 1 = lo = bf16(x - hi).  Layout [T/4][G16][2][4][64][8];
+// one (super tile, group) is 8 KiB contiguous.  Offsets in float units.
+__device__ __forceinline__ size_t split_block(uint64_t t, int g, int G16) {
+    return (((size_t)(t >> 2) * G16 + g) * 8 + (t & 3)) * BLOCK_FLOATS;
+}
+
+// Round-to-nearest-even fp32 -> bf16 bits for finite x (an overflow to inf falls
+// back to truncation so that hi stays finite and hi + lo still tracks x).
+__device__ __forceinline__ uint32_t bf16_rne_bits(float x) {
+    const uint32_t u = __float_as_uint(x);
+    const uint32_t r = (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+    return ((r & 0x7F80u) == 0x7F80u) ? (u >> 16) : r;
+}
+
+// x -> (hi, lo) bf16 pair, hi + lo = x within 2^-16 |x|
+__device__ __forceinline__ void split_bf16(float x, uint32_t& hi, uint32_t& lo) {
+    hi = bf16_rne_bits(x);
+    lo = bf16_rne_bits(x - __uint_as_float(hi << 16));
+}
+
+// Pack 8 floats (two f32x4) into the hi / lo operand vectors (16 B each)
+__device__ __forceinline__ void split8(const f32x4 a, const f32x4 b, f32x4& hi, f32x4& lo) {
+    uint32_t h[8], l[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        split_bf16(a[j], h[j], l[j]);
+        split_bf16(b[j], h[4 + j], l[4 + j]);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        hi[j] = __uint_as_float(h[2 * j] | (h[2 * j + 1] << 16));
+        lo[j] = __uint_as_float(l[2 * j] | (l[2 * j + 1] << 16));
+    }
+}
+
 // ---- ordering ----------------------------------------------------------------
 // Keys are "higher is better"; ties go to the LOWER row index.  Index types are
 // compared unsigned so that the sentinel (UINT32_MAX / int64 -1) sorts last.

@@ -60,6 +60,36 @@ hipError_t launch_pack_rows(const float* src, int64_t n, int D, int G, float* X,
     return hipGetLastError();
 }
 
+// fp32 tiles -> split-bf16 tiles.  Thread (tile t, fp32 group g8, row-in-tile i):
+// the 8 dims 8 g8 .. 8 g8 + 7 of row 32 t + i (two 16-byte pieces, lanes i and
+// i + 32 of the fp32 block) -> lane i + 32 (g8 & 1) of the hi and lo blocks of
+// 16-dim group g8 >> 1.  32 consecutive threads read and write 512 B runs.
+__global__ void __launch_bounds__(256) split_rows_kernel(const float* __restrict__ X, int G, int64_t t0,
+                                                         int64_t n_tiles, float* __restrict__ Xs) {
+    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= n_tiles * G * 32) return;
+    const int i = (int)(idx & 31);
+    const int g8 = (int)((idx >> 5) % G);
+    const uint64_t t = (uint64_t)(t0 + (idx >> 5) / G);
+    const float* src = X + tiled_block(t, g8, G);
+    const f32x4 a = *(const f32x4*)(src + i * 4);
+    const f32x4 b = *(const f32x4*)(src + (32 + i) * 4);
+    f32x4 hi, lo;
+    split8(a, b, hi, lo);
+    float* dst = Xs + split_block(t, g8 >> 1, G >> 1) + (size_t)(i + 32 * (g8 & 1)) * 4;
+    *(f32x4*)dst = hi;
+    *(f32x4*)(dst + 4 * BLOCK_FLOATS) = lo;
+}
+
+hipError_t launch_split_rows(const float* X, int G, int64_t row0, int64_t n, float* Xs, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    const int64_t t0 = row0 >> 5, t1 = (row0 + n + 31) >> 5;
+    const int64_t total = (t1 - t0) * G * 32;
+    hipLaunchKernelGGL(split_rows_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, X, G, t0, t1 - t0,
+                       Xs);
+    return hipGetLastError();
+}
+
 __global__ void __launch_bounds__(256) unpack_rows_kernel(const float* __restrict__ X, int G, int D, int64_t row0,
                                                           int64_t n, float* __restrict__ dst) {
     const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -81,7 +111,7 @@ hipError_t launch_unpack_rows(const float* X, int G, int D, int64_t row0, int64_
 // pre-normalised in fp32) query block including its zero padding, and the
 // certificate counter reset (one fewer memset per search).
 __global__ void __launch_bounds__(256) prep_queries_kernel(const float* __restrict__ Q, int B, int Bp, int D, int G,
-                                                           int metric, float* __restrict__ Qt,
+                                                           int metric, float* __restrict__ Qt, float* __restrict__ Qs,
                                                            double* __restrict__ qn64, int* __restrict__ flag_count,
                                                            uint32_t* __restrict__ gthr,
                                                            uint32_t* __restrict__ gslots) {
@@ -110,23 +140,45 @@ __global__ void __launch_bounds__(256) prep_queries_kernel(const float* __restri
     if (lane == 0) qn64[b] = nq;
     // cosine: the candidate pass works on q/max(|q|,1e-8) rounded to fp32.
     const float scale = metric == 0 ? (float)(1.0 / fmax(nq, 1e-8)) : 1.0f;
-    const int GQ = G + QG_EXTRA;
-    for (int p = lane; 4 * p < Dp + 8 * QG_EXTRA; p += 64) {
-        const int ps = 4 * p < Dp ? p : p - 2 * G;  // source piece (duplicated groups wrap)
-        f32x4 v;
+    if (Qt) {
+        const int GQ = G + QG_EXTRA;
+        for (int p = lane; 4 * p < Dp + 8 * QG_EXTRA; p += 64) {
+            const int ps = 4 * p < Dp ? p : p - 2 * G;  // source piece (duplicated groups wrap)
+            f32x4 v;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int d = 4 * ps + j;
-            v[j] = (real && d < D) ? q[d] * scale : 0.0f;
+            for (int j = 0; j < 4; ++j) {
+                const int d = 4 * ps + j;
+                v[j] = (real && d < D) ? q[d] * scale : 0.0f;
+            }
+            *(f32x4*)(Qt + tiled_piece_offset((uint64_t)b, p, GQ)) = v;
         }
-        *(f32x4*)(Qt + tiled_piece_offset((uint64_t)b, p, GQ)) = v;
+    }
+    if (Qs) {
+        // split-bf16 query tile: half-group h8 = 8 dims; 16-dim groups G/2 + QG_EXTRA, the
+        // trailing QG_EXTRA groups repeat the leading ones (modulo G/2)
+        const int G16 = G >> 1, GQ16 = G16 + QG_EXTRA;
+        for (int h8 = lane; h8 < 2 * GQ16; h8 += 64) {
+            const int g16 = h8 >> 1, h = h8 & 1;
+            const int d0 = 16 * (g16 % G16) + 8 * h;
+            f32x4 a, c;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                a[j] = (real && d0 + j < D) ? q[d0 + j] * scale : 0.0f;
+                c[j] = (real && d0 + 4 + j < D) ? q[d0 + 4 + j] * scale : 0.0f;
+            }
+            f32x4 hi, lo;
+            split8(a, c, hi, lo);
+            float* dst = Qs + split_block((uint64_t)(b >> 5), g16, GQ16) + (size_t)((b & 31) + 32 * h) * 4;
+            *(f32x4*)dst = hi;
+            *(f32x4*)(dst + 4 * BLOCK_FLOATS) = lo;
+        }
     }
 }
 
-hipError_t launch_prep_queries(const float* Q, int B, int Bp, int D, int G, int metric, float* Qt, double* qn64,
-                               int* flag_count, uint32_t* gthr, uint32_t* gslots, hipStream_t st) {
-    hipLaunchKernelGGL(prep_queries_kernel, dim3((Bp + 3) / 4), dim3(256), 0, st, Q, B, Bp, D, G, metric, Qt, qn64,
-                       flag_count, gthr, gslots);
+hipError_t launch_prep_queries(const float* Q, int B, int Bp, int D, int G, int metric, float* Qt, float* Qs,
+                               double* qn64, int* flag_count, uint32_t* gthr, uint32_t* gslots, hipStream_t st) {
+    hipLaunchKernelGGL(prep_queries_kernel, dim3((Bp + 3) / 4), dim3(256), 0, st, Q, B, Bp, D, G, metric, Qt, Qs,
+                       qn64, flag_count, gthr, gslots);
     return hipGetLastError();
 }
 // =============================================================================

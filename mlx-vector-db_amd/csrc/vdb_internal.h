@@ -12,12 +12,23 @@ constexpr int BLOCK_FLOATS = 256;  // floats per (tile, group) block = 1 KiB
 constexpr int QG_EXTRA = 8;        // duplicated leading dim-groups at the end of each query tile
 constexpr int ROW_ALIGN = 1024;    // corpus capacity granule (>= rows per scan step of any variant)
 
+// Candidate-pass arithmetic (vdb.h VDB_PREC_*):
+//   PREC_FP32   fp32 corpus tiles, v_mfma_f32_32x32x2_f32 (8-dim groups, 4 KiB per super-tile group)
+//   PREC_BF16X3 split-bf16 corpus (x = hi + lo + O(2^-16 x)), three v_mfma_f32_32x32x16_bf16 per
+//               16-dim group: hi*hi + hi*lo + lo*hi (8 KiB per super-tile group: [plane][sub tile])
+constexpr int PREC_FP32 = 0;
+constexpr int PREC_BF16X3 = 1;
+
 // Ingest: row-major fp32 [n][D] (device) -> tiled corpus rows [row0, row0+n),
 // canonical fp64 norms, fp32 inverse norms and squared norms, running max norm
 // (as fp64 bits) and a non-finite counter.
 hipError_t launch_pack_rows(const float* src, int64_t n, int D, int G, float* X, int64_t row0,
                             double* nrm64, float* inv32, float* sq32,
                             unsigned long long* xmax_bits, int* nonfinite, hipStream_t st);
+
+// fp32 tiles -> split-bf16 tiles (hi = bf16(x), lo = bf16(x - hi)) for the whole row tiles
+// covering rows [row0, row0 + n).  G = fp32 groups (Dp/8); the split copy has G/2 groups.
+hipError_t launch_split_rows(const float* X, int G, int64_t row0, int64_t n, float* Xs, hipStream_t st);
 
 // Tiled corpus rows -> row-major fp32 (export for persistence).
 hipError_t launch_unpack_rows(const float* X, int G, int D, int64_t row0, int64_t n, float* dst, hipStream_t st);
@@ -28,16 +39,19 @@ hipError_t launch_unpack_rows(const float* X, int G, int D, int64_t row0, int64_
 constexpr int KP_MAX = 256;
 // Queries: row-major [B][D] -> tiled Qt [Bp/32 tiles] with G + QG_EXTRA groups
 // (the first QG_EXTRA groups repeated at the end; cosine: pre-normalised in
-// fp32; zero padding written), canonical fp64 norms [Bp]; resets *flag_count.
+// fp32; zero padding written) and/or the split-bf16 tiles Qs (G/2 + QG_EXTRA
+// groups, same wrap), canonical fp64 norms [Bp]; resets *flag_count.
 hipError_t launch_prep_queries(const float* Q, int B, int Bp, int D, int G, int metric,
-                               float* Qt, double* qn64, int* flag_count, uint32_t* gthr, uint32_t* gslots,
-                               hipStream_t st);
+                               float* Qt, float* Qs, double* qn64, int* flag_count, uint32_t* gthr,
+                               uint32_t* gslots, hipStream_t st);
 
 // Candidate pass: MFMA fp32 scores fused with a per-workgroup top-KP.
 // Output lists cand_[s|i][B][n_wg][KP], each sorted best first.
-int scan_rows_per_step(int variant);
-hipError_t launch_scan_topk(int metric, int KP, int variant, const float* X, const float* rowscale, const uint32_t* mask,
-                            const float* Qt, int G, int64_t N, int B, int n_qblocks, int64_t n_steps,
+// X / Qt are the fp32 tiles (prec 0, G = Dp/8 groups) or the split tiles (prec 1, G = Dp/16).
+int scan_rows_per_step(int prec, int variant);
+bool scan_variant_ok(int prec, int variant, int G);
+hipError_t launch_scan_topk(int prec, int metric, int KP, int variant, const float* X, const float* rowscale,
+                            const uint32_t* mask, const float* Qt, int G, int64_t N, int B, int n_qblocks, int64_t n_steps,
                             int n_wg, int steps_per_wg, float* cand_s, uint32_t* cand_i, uint32_t* gthr,
                             uint32_t* gslots, hipStream_t st);
 

@@ -151,7 +151,37 @@ __device__ __forceinline__ void flush_query(float* sc, uint32_t* ix, int* cnt, f
     }
 }
 
-template <int METRIC, int QT, int RT, int PX, int PQ, int KP, int CAP, int WPS>
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+// Inner products of one 8-dim (fp32) or 16-dim (split-bf16) group of RT corpus
+// tiles against QT query tiles.  PREC_BF16X3: x.q ~ xh.qh + xh.ql + xl.qh, each
+// product exact in fp32, dropped terms <= ~3 2^-16 |x||q| per element.
+template <int PREC, int RT, int QT>
+__device__ __forceinline__ void group_mfma(const f32x4 (&x)[RT][PREC + 1], const f32x4 (&q)[QT][PREC + 1],
+                                           f32x16 (&acc)[RT][QT]) {
+    if constexpr (PREC == PREC_FP32) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+                for (int qt = 0; qt < QT; ++qt)
+                    acc[rt][qt] = __builtin_amdgcn_mfma_f32_32x32x2f32(x[rt][0][j], q[qt][0][j], acc[rt][qt], 0, 0, 0);
+    } else {
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt) {
+                const bf16x8 xh = __builtin_bit_cast(bf16x8, x[rt][0]), xl = __builtin_bit_cast(bf16x8, x[rt][1]);
+                const bf16x8 qh = __builtin_bit_cast(bf16x8, q[qt][0]), ql = __builtin_bit_cast(bf16x8, q[qt][1]);
+                acc[rt][qt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xl, qh, acc[rt][qt], 0, 0, 0);
+                acc[rt][qt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xh, ql, acc[rt][qt], 0, 0, 0);
+                acc[rt][qt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xh, qh, acc[rt][qt], 0, 0, 0);
+            }
+    }
+}
+
+template <int PREC, int METRIC, int QT, int RT, int PX, int PQ, int KP, int CAP, int WPS>
 __global__ void __launch_bounds__(256, WPS)
 scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale, const uint32_t* __restrict__ mask,
                  const float* __restrict__ Qt, int G, int64_t N, int B, int64_t n_steps, int steps_per_wg,
@@ -187,26 +217,37 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
 
     const int64_t s_begin = (int64_t)wg * steps_per_wg;
     const int64_t s_end = s_begin + steps_per_wg < n_steps ? s_begin + steps_per_wg : n_steps;
-    // super-tile addressing: group g of row tile t starts at tiled_block(t, g);
-    // consecutive groups are 4 blocks apart, sub tiles of one group adjacent.
-    constexpr size_t GSTEP = 4 * BLOCK_FLOATS;
+    // super-tile addressing: group g of row tile t starts at blk(t, g); consecutive
+    // groups are GBLK blocks apart (fp32: 4 sub tiles; split: 2 planes x 4 sub
+    // tiles), sub tiles of one group adjacent, the lo plane 4 blocks after hi.
+    constexpr int NPL = PREC + 1;
+    constexpr int GBLK = 4 * NPL;
+    constexpr size_t GSTEP = GBLK * BLOCK_FLOATS;
+    constexpr size_t PLANE = 4 * BLOCK_FLOATS;
+    auto blk = [](uint64_t t, int g, int GG) -> size_t {
+        return (((size_t)(t >> 2) * GG + g) * GBLK + (t & 3)) * BLOCK_FLOATS;
+    };
     // the query tiles carry QG_EXTRA duplicated leading groups after group G-1, so
     // the query stream of a step runs through groups PQ .. G+PQ-1 without a wrap
-    const float* Qbase = Qt + tiled_block((uint64_t)(qb * QT), 0, G + QG_EXTRA);
+    const float* Qbase = Qt + blk((uint64_t)(qb * QT), 0, G + QG_EXTRA);
 
-    f32x4 xr[PX][RT], qr[PQ][QT];
+    f32x4 xr[PX][RT][NPL], qr[PQ][QT][NPL];
     if (s_begin < s_end) {
-        const float* xs = X + tiled_block((uint64_t)((s_begin * 4 + wv) * RT), 0, G);
+        const float* xs = X + blk((uint64_t)((s_begin * 4 + wv) * RT), 0, G);
 #pragma unroll
         for (int p = 0; p < PX; ++p)
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt)
-                xr[p][rt] = *(const f32x4*)(xs + p * GSTEP + rt * BLOCK_FLOATS + lane4);
+#pragma unroll
+                for (int pl = 0; pl < NPL; ++pl)
+                    xr[p][rt][pl] = *(const f32x4*)(xs + p * GSTEP + pl * PLANE + rt * BLOCK_FLOATS + lane4);
 #pragma unroll
         for (int p = 0; p < PQ; ++p)
 #pragma unroll
             for (int qt = 0; qt < QT; ++qt)
-                qr[p][qt] = *(const f32x4*)(Qbase + p * GSTEP + qt * BLOCK_FLOATS + lane4);
+#pragma unroll
+                for (int pl = 0; pl < NPL; ++pl)
+                    qr[p][qt][pl] = *(const f32x4*)(Qbase + p * GSTEP + pl * PLANE + qt * BLOCK_FLOATS + lane4);
     }
 
     // row scales of the first step; later steps' are loaded one step ahead (next
@@ -231,8 +272,8 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
         const float* rs_buf = s_rs[s & 1];
 
         const int64_t t0 = (s * 4 + wv) * RT;
-        const float* xs = X + tiled_block((uint64_t)t0, 0, G);
-        const float* xn = (s + 1 < s_end) ? X + tiled_block((uint64_t)(t0 + 4 * RT), 0, G) : xs;
+        const float* xs = X + blk((uint64_t)t0, 0, G);
+        const float* xn = (s + 1 < s_end) ? X + blk((uint64_t)(t0 + 4 * RT), 0, G) : xs;
         f32x16 acc[RT][QT];
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt)
@@ -247,19 +288,18 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
         // shortens the prefetch distance.
         auto group = [&](const int p, const float* xsrc, const float* qsrc) {
             const int pq = p % PQ;
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-#pragma unroll
-                for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-                    for (int qt = 0; qt < QT; ++qt)
-                        acc[rt][qt] = __builtin_amdgcn_mfma_f32_32x32x2f32(xr[p][rt][j], qr[pq][qt][j], acc[rt][qt],
-                                                                           0, 0, 0);
+            group_mfma<PREC, RT, QT>(xr[p], qr[pq], acc);
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int rt = 0; rt < RT; ++rt) xr[p][rt] = *(const f32x4*)(xsrc + rt * BLOCK_FLOATS + lane4);
+            for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-            for (int qt = 0; qt < QT; ++qt) qr[pq][qt] = *(const f32x4*)(qsrc + qt * BLOCK_FLOATS + lane4);
+                for (int pl = 0; pl < NPL; ++pl)
+                    xr[p][rt][pl] = *(const f32x4*)(xsrc + pl * PLANE + rt * BLOCK_FLOATS + lane4);
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+                for (int pl = 0; pl < NPL; ++pl)
+                    qr[pq][qt][pl] = *(const f32x4*)(qsrc + pl * PLANE + qt * BLOCK_FLOATS + lane4);
             __builtin_amdgcn_sched_barrier(0);
         };
         int gb = 0;
@@ -473,35 +513,54 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
     }
 }
 
-template <int METRIC, int QT, int RT, int PX, int PQ, int KP, int CAP, int WPS>
+template <int PREC, int METRIC, int QT, int RT, int PX, int PQ, int KP, int CAP, int WPS>
 static hipError_t scan_dispatch(const float* X, const float* rowscale, const uint32_t* mask, const float* Qt, int G,
                                 int64_t N, int B, int n_qblocks, int64_t n_steps, int n_wg, int spw, float* cs,
                                 uint32_t* ci, uint32_t* gthr, uint32_t* gslots, hipStream_t st) {
-    hipLaunchKernelGGL((scan_topk_kernel<METRIC, QT, RT, PX, PQ, KP, CAP, WPS>), dim3(n_wg, n_qblocks), dim3(256), 0, st,
-                       X, rowscale, mask, Qt, G, N, B, n_steps, spw, cs, ci, gthr, gslots);
+    hipLaunchKernelGGL((scan_topk_kernel<PREC, METRIC, QT, RT, PX, PQ, KP, CAP, WPS>), dim3(n_wg, n_qblocks), dim3(256),
+                       0, st, X, rowscale, mask, Qt, G, N, B, n_steps, spw, cs, ci, gthr, gslots);
     return hipGetLastError();
 }
 
-int scan_rows_per_step(int variant) { return variant == 0 ? 256 : 512; }
+// Variants (RT row tiles of 32 per wave, corpus PX groups ahead, queries PQ ahead):
+//   fp32  0: RT=2 PX=4 PQ=4, 2 waves/SIMD     1: RT=4 PX=4 PQ=2, 2 waves/SIMD
+//         2: RT=4 PX=8 PQ=2, 1 wave/SIMD (accumulators in AGPRs)
+//   bf16x3 0: RT=2 PX=4 PQ=2, 1 wave/SIMD     1: RT=4 PX=4 PQ=2, 1 wave/SIMD
+//         2: RT=2 PX=8 PQ=2, 1 wave/SIMD
+static int variant_rt(int prec, int variant) {
+    if (prec == PREC_FP32) return variant == 0 ? 2 : 4;
+    return variant == 1 ? 4 : 2;
+}
+static int variant_px(int prec, int variant) {
+    if (prec == PREC_FP32) return variant == 2 ? 8 : 4;
+    return variant == 2 ? 8 : 4;
+}
 
-int scan_waves_per_simd(int variant) { return variant == 2 ? 1 : 2; }
+int scan_rows_per_step(int prec, int variant) { return 4 * 32 * variant_rt(prec, variant); }
 
-hipError_t launch_scan_topk(int metric, int KP, int variant, const float* X, const float* rowscale,
+bool scan_variant_ok(int prec, int variant, int G) {
+    return variant >= 0 && variant <= 2 && G % variant_px(prec, variant) == 0;
+}
+
+hipError_t launch_scan_topk(int prec, int metric, int KP, int variant, const float* X, const float* rowscale,
                             const uint32_t* mask, const float* Qt, int G, int64_t N, int B, int n_qblocks,
                             int64_t n_steps, int n_wg, int spw, float* cs, uint32_t* ci, uint32_t* gthr,
                             uint32_t* gslots, hipStream_t st) {
-    // variant 0: RT=2 (64 rows/wave), corpus 4 groups ahead, 2 waves/SIMD
-    // variant 1: RT=4 (128 rows/wave), corpus 4 groups ahead, 2 waves/SIMD
-    // variant 2: RT=4, corpus 8 groups ahead, 1 wave/SIMD (accumulators in AGPRs)
-#define VDB_SCAN(M, QT, KPV, V, RT, PX, PQ, W)                                                                 \
-    if (metric == M && KP == KPV && variant == V)                                                             \
-        return scan_dispatch<M, QT, RT, PX, PQ, KPV, (KPV == 32 ? 4 : 2) * KPV, W>(X, rowscale, mask, Qt, G, N, B, n_qblocks, n_steps, \
-                                                              n_wg, spw, cs, ci, gthr, gslots, st);
-#define VDB_SCAN_ALL(M)                                                                                  \
-    VDB_SCAN(M, 2, 32, 0, 2, 4, 4, 2) VDB_SCAN(M, 2, 64, 0, 2, 4, 4, 2) VDB_SCAN(M, 2, 128, 0, 2, 4, 4, 1) \
-    VDB_SCAN(M, 1, 256, 0, 2, 4, 4, 1)                                                                   \
-    VDB_SCAN(M, 2, 32, 1, 4, 4, 2, 2) VDB_SCAN(M, 2, 64, 1, 4, 4, 2, 2)                                   \
-    VDB_SCAN(M, 2, 32, 2, 4, 8, 2, 1) VDB_SCAN(M, 2, 64, 2, 4, 8, 2, 1)
+    if (!scan_variant_ok(prec, variant, G)) return hipErrorInvalidValue;
+#define VDB_SCAN(P, M, QT, KPV, V, RT, PX, PQ, W)                                                               \
+    if (prec == P && metric == M && KP == KPV && variant == V)                                                 \
+        return scan_dispatch<P, M, QT, RT, PX, PQ, KPV, (KPV == 32 ? 4 : 2) * KPV, W>(                          \
+            X, rowscale, mask, Qt, G, N, B, n_qblocks, n_steps, n_wg, spw, cs, ci, gthr, gslots, st);
+#define VDB_SCAN_ALL(M)                                                                                        \
+    VDB_SCAN(0, M, 2, 32, 0, 2, 4, 4, 2) VDB_SCAN(0, M, 2, 64, 0, 2, 4, 4, 2)                                  \
+    VDB_SCAN(0, M, 2, 128, 0, 2, 4, 4, 1) VDB_SCAN(0, M, 1, 256, 0, 2, 4, 4, 1)                                \
+    VDB_SCAN(0, M, 2, 32, 1, 4, 4, 2, 2) VDB_SCAN(0, M, 2, 64, 1, 4, 4, 2, 2)                                  \
+    VDB_SCAN(0, M, 2, 32, 2, 4, 8, 2, 1) VDB_SCAN(0, M, 2, 64, 2, 4, 8, 2, 1)                                  \
+    VDB_SCAN(1, M, 2, 32, 0, 2, 4, 2, 1) VDB_SCAN(1, M, 2, 64, 0, 2, 4, 2, 1)                                  \
+    VDB_SCAN(1, M, 2, 128, 0, 2, 4, 2, 1) VDB_SCAN(1, M, 1, 256, 0, 2, 4, 2, 1)                                \
+    VDB_SCAN(1, M, 2, 32, 1, 4, 4, 2, 1) VDB_SCAN(1, M, 2, 64, 1, 4, 4, 2, 1)                                  \
+    VDB_SCAN(1, M, 2, 128, 1, 4, 4, 2, 1)                                                                      \
+    VDB_SCAN(1, M, 2, 32, 2, 2, 8, 2, 1) VDB_SCAN(1, M, 2, 64, 2, 2, 8, 2, 1)
     VDB_SCAN_ALL(0)
     VDB_SCAN_ALL(1)
 #undef VDB_SCAN_ALL

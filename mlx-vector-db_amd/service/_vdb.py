@@ -27,6 +27,8 @@ VDB_ERR_UNSUPPORTED = -5
 VDB_ERR_NODEVICE = -6
 
 METRIC_IDS = {"cosine": 0, "euclidean": 1}
+# candidate-pass arithmetic (include/vdb.h VDB_PREC_*); results are identical, speed differs
+PRECISION_IDS = {"fp32": 0, "bf16x3": 1}
 MEM_HOST = 0
 MEM_DEVICE = 1
 
@@ -123,7 +125,7 @@ def _ptr(a: np.ndarray) -> int:
 class NativeIndex:
     """One device-resident corpus (tiled fp32 + norms) on one GPU."""
 
-    def __init__(self, dim: int, metric: str = "cosine", device: int = 0):
+    def __init__(self, dim: int, metric: str = "cosine", device: int = 0, precision: Optional[str] = None):
         if metric not in METRIC_IDS:
             raise ValueError(f"unsupported metric {metric!r}; the vdb core implements {sorted(METRIC_IDS)}")
         self._lib = load_library()
@@ -133,6 +135,8 @@ class NativeIndex:
         h = ctypes.c_void_p()
         _check(self._lib.vdb_index_create(self.dim, METRIC_IDS[metric], self.device, ctypes.byref(h)))
         self._h = h
+        if precision is not None:
+            self.set_precision(precision)
 
     # -- lifecycle -------------------------------------------------------------
     def close(self) -> None:
@@ -151,6 +155,16 @@ class NativeIndex:
 
     def set_param(self, name: str, value: int) -> None:
         _check(self._lib.vdb_index_set_param(self._h, name.encode(), int(value)))
+
+    def set_precision(self, precision: str) -> None:
+        if precision not in PRECISION_IDS:
+            raise ValueError(f"precision must be one of {sorted(PRECISION_IDS)}, got {precision!r}")
+        self.set_param("precision", PRECISION_IDS[precision])
+
+    @property
+    def precision(self) -> str:
+        v = self.stat("precision")
+        return next(k for k, i in PRECISION_IDS.items() if i == v)
 
     def stat(self, name: str) -> int:
         v = ctypes.c_int64(0)

@@ -55,7 +55,8 @@ def main():
              "| kernel | calls | avg µs | share % |", "|---|---|---|---|"]
     for r in stats:
         lines.append(f"| `{r['Name'][:110]}` | {r['Calls']} | {float(r['AverageNs']) / 1e3:.1f} | {r['Percentage']} |")
-    out = {"tag": tag, "config": bench["config"]["workload"].split(":")[0], "n_gpus": bench["n_gpus"]}
+    out = {"tag": tag, "config": bench["config"]["workload"].split(":")[0], "n_gpus": bench["n_gpus"],
+           "precision": bench["roofline"].get("precision", "fp32")}
     for name, cs in counters.items():
         if kern not in name:
             continue

@@ -31,8 +31,11 @@ def _mask_words(mask_bool):
     return np.packbits(bits, bitorder="little").view("<u4").astype(np.uint32)
 
 
-def _check(vdb, V, Q, k, metric, mask=None, force_exact=False, margin=None, chunked_add=False):
-    ix = vdb.NativeIndex(V.shape[1], metric)
+PRECISIONS = ["bf16x3", "fp32"]
+
+
+def _check(vdb, V, Q, k, metric, mask=None, force_exact=False, margin=None, chunked_add=False, precision="bf16x3"):
+    ix = vdb.NativeIndex(V.shape[1], metric, precision=precision)
     if force_exact:
         ix.set_param("force_exact", 1)
     if margin is not None:
@@ -54,12 +57,13 @@ def _check(vdb, V, Q, k, metric, mask=None, force_exact=False, margin=None, chun
     return ix, s, i
 
 
+@pytest.mark.parametrize("precision", PRECISIONS)
 @pytest.mark.parametrize("path", GOLDEN, ids=[os.path.basename(p) for p in GOLDEN])
-def test_golden_fixtures(vdb, path):
+def test_golden_fixtures(vdb, path, precision):
     z = np.load(path, allow_pickle=False)
     V, Q, k, metric = z["vectors"], z["queries"], int(z["k"]), str(z["metric"])
     mask = z["mask"] if z["mask"].size else None
-    ix = vdb.NativeIndex(V.shape[1], metric)
+    ix = vdb.NativeIndex(V.shape[1], metric, precision=precision)
     ix.add(V)
     s, i, kk = ix.search(Q, k, row_mask=_mask_words(mask) if mask is not None else None, with_keys=True)
     np.testing.assert_array_equal(i, z["exact_idx"])
@@ -69,23 +73,46 @@ def test_golden_fixtures(vdb, path):
     np.testing.assert_allclose(s[valid], z["ref_scores"][valid], atol=1e-4, rtol=0)
 
 
+@pytest.mark.parametrize("precision", PRECISIONS)
 @pytest.mark.parametrize("metric", ["cosine", "euclidean"])
 @pytest.mark.parametrize("N,D,B,k", [(5000, 384, 7, 10), (3000, 100, 3, 5), (4096, 128, 64, 100),
-                                     (1234, 33, 65, 32), (700, 1536, 9, 10)])
-def test_random_uniform(vdb, metric, N, D, B, k):
+                                     (1234, 33, 65, 32), (700, 1536, 9, 10), (20000, 768, 130, 10),
+                                     (9000, 64, 40, 200)])
+def test_random_uniform(vdb, metric, N, D, B, k, precision):
     rng = np.random.default_rng(N + D)
     V = rng.random((N, D), dtype=np.float32)
     Q = rng.random((B, D), dtype=np.float32)
-    _check(vdb, V, Q, k, metric)
+    _check(vdb, V, Q, k, metric, precision=precision)
 
 
+@pytest.mark.parametrize("precision", PRECISIONS)
 @pytest.mark.parametrize("metric", ["cosine", "euclidean"])
-def test_normal_with_mask_and_chunked_add(vdb, metric):
+def test_normal_with_mask_and_chunked_add(vdb, metric, precision):
     rng = np.random.default_rng(7)
     V = rng.standard_normal((6000, 200)).astype(np.float32)
     Q = rng.standard_normal((5, 200)).astype(np.float32)
     mask = rng.random(6000) < 0.3
-    _check(vdb, V, Q, 10, metric, mask=mask, chunked_add=True)
+    _check(vdb, V, Q, 10, metric, mask=mask, chunked_add=True, precision=precision)
+
+
+def test_precision_switch_keeps_results(vdb):
+    """Switching the candidate-pass arithmetic after ingest builds / drops the split
+    copy; results stay identical (the exact rerank decides)."""
+    rng = np.random.default_rng(21)
+    V = rng.random((7000, 160), dtype=np.float32) * 100.0 - 30.0
+    Q = rng.random((9, 160), dtype=np.float32) * 100.0 - 30.0
+    ix = vdb.NativeIndex(160, "euclidean", precision="fp32")
+    ix.add(V[:3000])
+    ix.set_precision("bf16x3")
+    ix.add(V[3000:])
+    a = ix.search(Q, 17, with_keys=True)
+    ix.set_precision("fp32")
+    b = ix.search(Q, 17, with_keys=True)
+    es, ei, ek = ref_cpu.exact_search(Q, V, 17, "euclidean")
+    for s, i, kk in (a, b):
+        np.testing.assert_array_equal(i, ei)
+        np.testing.assert_array_equal(kk, ek)
+    assert ix.stat("fallback_queries") == 0
 
 
 def test_duplicates_force_certificate_fallback(vdb):
@@ -215,7 +242,8 @@ def test_similarity_matrix_operator_slot(vdb):
 
 
 @pytest.mark.slow
-def test_full_size_c2_subset(vdb):
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_full_size_c2_subset(vdb, precision):
     """BASELINE.json configs[1]: 1M x 768 fp32 cosine, B=64, k=10.  The oracle
     checks 8 of the 64 queries exactly; every query checks size-independent
     properties (sorted scores, planted self-queries on top)."""
@@ -224,9 +252,10 @@ def test_full_size_c2_subset(vdb):
     Q = np.random.default_rng(1).random((B, D), dtype=np.float32)
     Q[5] = V[777_777]
     Q[6] = V[3]
-    ix = vdb.NativeIndex(D, "cosine")
+    ix = vdb.NativeIndex(D, "cosine", precision=precision)
     ix.add(V)
     s, i = ix.search(Q, k)
+    assert ix.stat("fallback_queries") == 0  # the candidate pass certified every query
     assert (np.diff(s, axis=1) <= 0).all()
     assert i[5, 0] == 777_777 and i[6, 0] == 3
     sub = [0, 1, 2, 5, 6, 31, 32, 63]
