@@ -76,7 +76,7 @@ struct Workspace {
     size_t exact_bytes = 0;
     int* host_flag = nullptr;  // pinned
     hipEvent_t done = nullptr;
-    hipEvent_t tev[3] = {nullptr, nullptr, nullptr};  // timing: scan start / scan end / rerank end
+    hipEvent_t tev[4] = {nullptr, nullptr, nullptr, nullptr};  // timing: scan start / end / rerank end / pilot start
     bool busy = false;
     bool used = false;
 };
@@ -104,6 +104,7 @@ struct vdb_index {
     int64_t force_exact = 0;
     int64_t n_wg_override = 0;
     int64_t timing = 0;  // record HIP events around the candidate pass
+    int64_t pilot_tiles = 512;  // row tiles sampled by the pilot bound (0 = off)
     int64_t scan_variant = 0;     // fp32 candidate pass variant (vdb_scan.hip)
     int64_t scan_variant_b3 = 0;  // bf16x3 candidate pass variant
     // stats
@@ -316,7 +317,7 @@ int32_t vdb_index_destroy(vdb_index* ix) {
         if (w->exact) (void)hipFree(w->exact);
         if (w->host_flag) (void)hipHostFree(w->host_flag);
         if (w->done) (void)hipEventDestroy(w->done);
-        for (int e = 0; e < 3; ++e)
+        for (int e = 0; e < 4; ++e)
             if (w->tev[e]) (void)hipEventDestroy(w->tev[e]);
         delete w;
     }
@@ -371,8 +372,12 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
         if (value < 0 || value > 2) return set_error(VDB_ERR_INVALID, "scan_variant must be 0, 1 or 2");
         ix->scan_variant = value;
     } else if (n == "scan_variant_bf16x3") {
-        if (value < 0 || value > 2) return set_error(VDB_ERR_INVALID, "scan_variant_bf16x3 must be 0, 1 or 2");
+        if (value < 0 || !scan_variant_ok(PREC_BF16X3, (int)value, 8))
+            return set_error(VDB_ERR_INVALID, "scan_variant_bf16x3 must be 0, 1 or 2");
         ix->scan_variant_b3 = value;
+    } else if (n == "pilot_tiles") {
+        if (value < 0 || value > 4096) return set_error(VDB_ERR_INVALID, "pilot_tiles must be in [0, 4096]");
+        ix->pilot_tiles = value;
     } else if (n == "timing") {
         ix->timing = value != 0;
     } else {
@@ -541,7 +546,8 @@ int32_t vdb_index_search(vdb_index* ix, const float* queries, int32_t B, int32_t
     const int64_t n_steps = std::max<int64_t>(1, round_up(N, step_rows) / step_rows);
     // one 4-wave workgroup per CU (1 wave per SIMD, all of its 512 registers):
     // measured faster than two per CU, whose top-k epilogues then overlap (profiles/)
-    int target = ix->n_wg_override > 0 ? (int)ix->n_wg_override : std::max(1, ix->n_cu / n_qblocks);
+    int target = ix->n_wg_override > 0 ? (int)ix->n_wg_override
+                                       : std::max(1, ix->n_cu * scan_wgs_per_cu(prec, variant, KP) / n_qblocks);
     int spw = (int)std::max<int64_t>(1, (n_steps + target - 1) / target);
     int n_wg = (int)((n_steps + spw - 1) / spw);
     const int64_t mask_words = round_up(N, 32) / 32;
@@ -557,12 +563,17 @@ int32_t vdb_index_search(vdb_index* ix, const float* queries, int32_t B, int32_t
     bytes += (size_t)(mask_words + 64) * 4 + 256;           // mask (host mode)
     bytes += (size_t)Bp * (ix->Dp + 16 * QG_EXTRA) * 4 + 256;  // Qt (tiled fp32 or split, duplicated groups)
     bytes += (size_t)Bp * 8 + 256;                          // qn64
-    bytes += (size_t)Bp * n_wg * KP * 8 + 512;              // candidate lists
     bytes += (size_t)Bp * KP * 8 + 512;                     // merged approx lists
     bytes += (size_t)B * k * 20 + 768;                      // outputs (host mode)
     bytes += (size_t)(B + 64) * 4 + 256;                    // flags
     bytes += (size_t)Bp * 4 + 256;                          // shared thresholds
-    bytes += (size_t)Bp * KP_MAX * 4 + 256;                 // shared threshold slots
+    bytes += (size_t)Bp * (KP_MAX + PILOT_SLOTS) * 4 + 256;  // shared threshold slots + pilot slots
+    const bool priv = !exact_all && scan_priv(prec, variant, KP);
+    // global per-query candidate lists: at most 512 entries per workgroup and query
+    // (the largest LDS buffer of any variant; 4 x 64 for the wave-private one)
+    const int64_t gl_cap = exact_all ? 0 : (int64_t)n_wg * 512;
+    bytes += (size_t)B * gl_cap * 8 + (size_t)Bp * 4 + 768;
+    const int n_pilot = (int)std::min<int64_t>(ix->pilot_tiles, round_up(N, 32) / 32);
     int rc = ws_reserve(w, bytes, st);
     if (rc) return rc;
     Carver c{w->dev};
@@ -570,16 +581,16 @@ int32_t vdb_index_search(vdb_index* ix, const float* queries, int32_t B, int32_t
     uint32_t* maskd = c.take<uint32_t>(mask_words + 64);
     float* Qt = c.take<float>((size_t)Bp * (ix->Dp + 16 * QG_EXTRA));
     double* qn64 = c.take<double>(Bp);
-    float* cs = c.take<float>((size_t)Bp * n_wg * KP);
-    uint32_t* ci = c.take<uint32_t>((size_t)Bp * n_wg * KP);
-    float* as = c.take<float>((size_t)Bp * KP);
-    uint32_t* ai = c.take<uint32_t>((size_t)Bp * KP);
     float* os = c.take<float>((size_t)B * k);
     int64_t* oi = c.take<int64_t>((size_t)B * k);
     double* ok = c.take<double>((size_t)B * k);
     int* flags = c.take<int>(B + 64);
     uint32_t* gthr = c.take<uint32_t>(Bp);
-    uint32_t* gslots = c.take<uint32_t>((size_t)Bp * KP_MAX);
+    uint32_t* gslots = c.take<uint32_t>((size_t)Bp * (KP_MAX + PILOT_SLOTS));
+    uint32_t* pslots = gslots + (size_t)Bp * KP_MAX;
+    float* gl_s = c.take<float>((size_t)B * gl_cap);
+    uint32_t* gl_i = c.take<uint32_t>((size_t)B * gl_cap);
+    uint32_t* gl_cnt = c.take<uint32_t>(Bp);
 
     const float* Qd = queries;
     const uint32_t* md = row_mask;
@@ -605,35 +616,45 @@ int32_t vdb_index_search(vdb_index* ix, const float* queries, int32_t B, int32_t
         if (out_k) HIP_TRY(hipMemsetAsync(out_k, 0, (size_t)B * k * 8, st));
     } else {
         HIP_TRY(launch_prep_queries(Qd, B, Bp, D, ix->G, ix->metric, prec == PREC_FP32 ? Qt : nullptr,
-                                    prec == PREC_FP32 ? nullptr : Qt, qn64, flags, gthr, gslots, st));
+                                    prec == PREC_FP32 ? nullptr : Qt, qn64, flags, gthr, gslots, gl_cnt, st));
         int n_flag = 0;
         if (!exact_all) {
             const bool timed = ix->timing != 0;
             if (timed) {
-                for (int e = 0; e < 3; ++e)
+                for (int e = 0; e < 4; ++e)
                     if (!w->tev[e]) HIP_TRY(hipEventCreate(&w->tev[e]));
-                HIP_TRY(hipEventRecord(w->tev[0], st));
+                HIP_TRY(hipEventRecord(w->tev[3], st));
             }
-            HIP_TRY(launch_scan_topk(prec, ix->metric, KP, variant, prec == PREC_FP32 ? ix->X : ix->Xs,
-                                     ix->metric == 0 ? ix->inv32 : ix->sq32, md, Qt, Gs, N,
-                                     B, n_qblocks, n_steps, n_wg, spw, cs, ci, gthr, gslots, st));
+            const float* rowscale = ix->metric == 0 ? ix->inv32 : ix->sq32;
+            const float* Xscan = prec == PREC_FP32 ? ix->X : ix->Xs;
+            if (n_pilot > 0)
+                HIP_TRY(launch_pilot(prec, ix->metric, KP, Xscan, rowscale, md, Qt, Gs, N, B, n_qblocks, QB, n_pilot,
+                                     pslots, gthr, st));
+            // scan_ns times the scan kernel alone (the roofline's kernel); pipeline_ns
+            // everything from the pilot to the rerank
+            if (timed) HIP_TRY(hipEventRecord(w->tev[0], st));
+            if (priv)
+                HIP_TRY(launch_scan_topk_priv(prec, ix->metric, KP, Xscan, rowscale, md, Qt, Gs, N, B, n_qblocks,
+                                              n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, st));
+            else
+                HIP_TRY(launch_scan_topk(prec, ix->metric, KP, variant, Xscan, rowscale, md, Qt, Gs, N, B, n_qblocks,
+                                         n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, st));
             if (timed) HIP_TRY(hipEventRecord(w->tev[1], st));
-            HIP_TRY(launch_merge_f32(KP, cs, ci, n_wg, B, as, ai, st));
-            RerankArgs ra;
-            ra.Q = Qd; ra.qn64 = qn64; ra.X = ix->X; ra.G = ix->G; ra.D = D;
-            ra.nrm64 = ix->nrm64; ra.app_s = as; ra.app_i = ai; ra.k = k;
+            FinishArgs fa;
+            fa.gl_s = gl_s; fa.gl_i = gl_i; fa.gl_cnt = gl_cnt; fa.gl_cap = gl_cap;
+            fa.Q = Qd; fa.qn64 = qn64; fa.X = ix->X; fa.G = ix->G; fa.D = D; fa.nrm64 = ix->nrm64; fa.k = k;
             // |approx - exact| <= eps_rel * sum|q_i x_i| (relative to |q||x|):
             //   fp32:   D fp32 MFMA additions + ~8 roundings of the normalisation / scaling
             //   bf16x3: 3D additions (each counted at 2^-23 in case the bf16 MFMA adds
             //           truncate) + the dropped hi*lo-order terms (< 3.1 2^-16) + the same 8
-            ra.eps_rel = prec == PREC_FP32
+            fa.eps_rel = prec == PREC_FP32
                              ? 1.01 * (double)(D + 8) * std::ldexp(1.0, -24)
                              : 1.01 * (3.0 * D * std::ldexp(1.0, -23) + 3.1 * std::ldexp(1.0, -16) +
                                        8.0 * std::ldexp(1.0, -24));
-            ra.xmax = ix->xmax;
-            ra.out_s = out_s; ra.out_i = out_i; ra.out_k = out_k; ra.index_offset = index_offset;
-            ra.flag_count = flags; ra.flag_list = flags + 1;
-            HIP_TRY(launch_rerank(ix->metric, KP, ra, B, st));
+            fa.xmax = ix->xmax;
+            fa.out_s = out_s; fa.out_i = out_i; fa.out_k = out_k; fa.index_offset = index_offset;
+            fa.flag_count = flags; fa.flag_list = flags + 1; fa.gthr = gthr;
+            HIP_TRY(launch_finish(ix->metric, KP, fa, B, st));
             if (timed) HIP_TRY(hipEventRecord(w->tev[2], st));
             HIP_TRY(hipMemcpyAsync(w->host_flag, flags, sizeof(int), hipMemcpyDeviceToHost, st));
             HIP_TRY(hipStreamSynchronize(st));
@@ -641,7 +662,7 @@ int32_t vdb_index_search(vdb_index* ix, const float* queries, int32_t B, int32_t
             if (timed) {
                 float ms_scan = 0.f, ms_pipe = 0.f;
                 HIP_TRY(hipEventElapsedTime(&ms_scan, w->tev[0], w->tev[1]));
-                HIP_TRY(hipEventElapsedTime(&ms_pipe, w->tev[0], w->tev[2]));
+                HIP_TRY(hipEventElapsedTime(&ms_pipe, w->tev[3], w->tev[2]));
                 ix->scan_ns += (int64_t)(ms_scan * 1e6);
                 ix->pipe_ns += (int64_t)(ms_pipe * 1e6);
                 ix->n_timed++;

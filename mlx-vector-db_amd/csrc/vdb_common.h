@@ -77,6 +77,17 @@ __device__ __forceinline__ void split8(const f32x4 a, const f32x4 b, f32x4& hi, 
     }
 }
 
+// Order-preserving float <-> uint32 keys (0 = "no bound" = -inf): the shared
+// per-query bounds are maintained with integer atomicMax.
+__device__ __forceinline__ uint32_t order_key(float f) {
+    const uint32_t u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float key_to_float(uint32_t k) {
+    if (k == 0) return -INFINITY;
+    return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
+}
+
 // ---- ordering ----------------------------------------------------------------
 // Keys are "higher is better"; ties go to the LOWER row index.  Index types are
 // compared unsigned so that the sentinel (UINT32_MAX / int64 -1) sorts last.

@@ -100,17 +100,25 @@ __global__ void __launch_bounds__(64 * RERANK_WAVES) rerank_kernel(RerankArgs a)
         }
     }
     if (lane == 0) {
+        // Rows never in a candidate list scored (approx) <= max(a_KP, T): a_KP for rows a
+        // workgroup dropped against its own KP-th best (the merged KP-th is >= it), T (the
+        // final shared bound; every bound used during the scan was <= it) for rows dropped
+        // against the shared bound.  Empty list tail and no bound = fewer eligible rows.
+        const bool full = a.app_i[(size_t)b * KP + KP - 1] != 0xFFFFFFFFu;
+        const double T = a.gthr ? (double)key_to_float(a.gthr[b]) : -INFINITY;
         bool ok = true;
-        if (a.app_i[(size_t)b * KP + KP - 1] != 0xFFFFFFFFu) {  // >= KP eligible rows: need the bound
-            const double ak = (double)a.app_s[(size_t)b * KP + a.k - 1];
-            const double akp = (double)a.app_s[(size_t)b * KP + KP - 1];
+        if (full || T > -INFINITY) {
+            const bool have_k = a.app_i[(size_t)b * KP + a.k - 1] != 0xFFFFFFFFu;
+            const double ak = have_k ? (double)a.app_s[(size_t)b * KP + a.k - 1] : -INFINITY;
+            const double akp = full ? (double)a.app_s[(size_t)b * KP + KP - 1] : -INFINITY;
+            const double acut = fmax(akp, T);
             double eps;
             if (METRIC == 0) {
                 eps = a.eps_rel;
             } else {
-                eps = a.eps_rel * (2.0 * qn * a.xmax + a.xmax * a.xmax) + 2.4e-7 * fmax(fabs(ak), fabs(akp));
+                eps = a.eps_rel * (2.0 * qn * a.xmax + a.xmax * a.xmax) + 2.4e-7 * fmax(fabs(ak), fabs(acut));
             }
-            ok = akp + eps < ak - eps;
+            ok = have_k && acut + eps < ak - eps;
         }
         if (!ok) {
             const int pos = atomicAdd(a.flag_count, 1);
@@ -128,6 +136,233 @@ hipError_t launch_rerank(int metric, int KP, const RerankArgs& a, int B, hipStre
     VDB_RR(0, 32) VDB_RR(0, 64) VDB_RR(0, 128) VDB_RR(0, 256)
     VDB_RR(1, 32) VDB_RR(1, 64) VDB_RR(1, 128) VDB_RR(1, 256)
 #undef VDB_RR
+    return hipErrorInvalidValue;
+}
+
+// =============================================================================
+// finish: select + exact rerank + certificate, one workgroup per query
+// =============================================================================
+// Input: the query's global candidate list (entries the candidate pass appended
+// above its shared bound; typically tens to a few hundred).  Wave 0 selects the
+// best min(KP, c) by (approx score desc, row asc) with ballot bisection (no sort
+// network: a dependent ds_bpermute costs ~140 cycles, a ballot a few); all four
+// waves compute exact fp64 keys, batched NB candidates per wave so the corpus
+// loads of a batch are in flight together; ranks come from counting (no sort);
+// thread 0 checks the certificate.  A list longer than FIN_CAP goes to the exact
+// scan.
+constexpr int FIN_CAP = 4096;
+constexpr int FIN_NB = 8;
+
+template <int METRIC, int NB>
+__device__ __forceinline__ void exact_keys_batch(const float* __restrict__ q, double qn, const float* __restrict__ X,
+                                                 int G, int D, const uint32_t* rows, const double* xn, int nb,
+                                                 double* out) {
+    const int lane = threadIdx.x & 63;
+    const int Dp = G * GROUP_DIMS;
+    const int np = (D + 255) / 256;
+    double acc[NB];
+#pragma unroll
+    for (int u = 0; u < NB; ++u) acc[u] = 0.0;
+    for (int m = 0; m < np; ++m) {
+        const int p = m * 64 + lane;
+        float qv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) qv[j] = 4 * p + j < D ? q[4 * p + j] : 0.0f;
+        f32x4 xv[NB];
+#pragma unroll
+        for (int u = 0; u < NB; ++u)
+            xv[u] = (u < nb && 4 * p < Dp) ? *(const f32x4*)(X + tiled_piece_offset(rows[u], p, G)) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int u = 0; u < NB; ++u)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const double qd = (double)qv[j];
+                const double xd = (double)xv[u][j];
+                if (METRIC == 0) {
+                    acc[u] = acc[u] + qd * xd;
+                } else {
+                    const double df = xd - qd;
+                    acc[u] = acc[u] + df * df;
+                }
+            }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1)
+#pragma unroll
+        for (int u = 0; u < NB; ++u) acc[u] = acc[u] + __shfl_xor(acc[u], off, 64);
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+        if (u < nb) out[u] = METRIC == 0 ? acc[u] / (fmax(qn, 1e-8) * fmax(xn[u], 1e-8)) : -acc[u];
+    }
+}
+
+template <int METRIC, int KP>
+__global__ void __launch_bounds__(256) finish_kernel(FinishArgs a) {
+    __shared__ uint32_t s_key[FIN_CAP];
+    __shared__ uint32_t s_row[FIN_CAP];
+    __shared__ uint32_t s_ck[KP];
+    __shared__ uint32_t s_cr[KP];
+    __shared__ double s_ek[KP];
+    __shared__ int s_m;
+    __shared__ uint32_t s_ak, s_akp;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wv = tid >> 6;
+    const int b = blockIdx.x;
+    const int64_t c = min((int64_t)a.gl_cnt[b], a.gl_cap);
+    if (c > FIN_CAP) {
+        if (tid == 0) {
+            const int pos = atomicAdd(a.flag_count, 1);
+            a.flag_list[pos] = b;
+        }
+        return;
+    }
+    const float* ls = a.gl_s + (size_t)b * a.gl_cap;
+    const uint32_t* li = a.gl_i + (size_t)b * a.gl_cap;
+    for (int e = tid; e < c; e += 256) {
+        s_key[e] = order_key(ls[e]);
+        s_row[e] = li[e];
+    }
+    if (tid == 0) {
+        s_ak = 0;
+        s_akp = 0;
+    }
+    __syncthreads();
+    const int n = (int)c;
+    if (wv == 0) {
+        int m = n < KP ? n : KP;
+        uint32_t T = 0, I = 0xFFFFFFFFu;
+        if (n > KP) {
+            for (int bit = 31; bit >= 0; --bit) {
+                const uint32_t cand = T | (1u << bit);
+                int ge = 0;
+                for (int e0 = 0; e0 < n; e0 += 64) ge += __popcll(__ballot(e0 + lane < n && s_key[e0 + lane] >= cand));
+                if (ge >= KP) T = cand;
+            }
+            int gt = 0, eq = 0;
+            for (int e0 = 0; e0 < n; e0 += 64) {
+                const bool in = e0 + lane < n;
+                const uint32_t kk = in ? s_key[e0 + lane] : 0u;
+                gt += __popcll(__ballot(in && kk > T));
+                eq += __popcll(__ballot(in && kk == T));
+            }
+            const int need = KP - gt;
+            if (eq > need) {
+                I = 0;
+                for (int bit = 31; bit >= 0; --bit) {
+                    const uint32_t cand = I | (1u << bit);
+                    int lt = 0;
+                    for (int e0 = 0; e0 < n; e0 += 64) {
+                        const bool in = e0 + lane < n;
+                        lt += __popcll(__ballot(in && s_key[e0 + lane] == T && s_row[e0 + lane] < cand));
+                    }
+                    if (lt < need) I = cand;
+                }
+            }
+        }
+        int base = 0;
+        for (int e0 = 0; e0 < n; e0 += 64) {
+            const int e = e0 + lane;
+            const bool in = e < n;
+            const uint32_t kk = in ? s_key[e] : 0u;
+            const uint32_t rr = in ? s_row[e] : 0u;
+            const bool keep = in && (n <= KP || kk > T || (kk == T && rr <= I));
+            const unsigned long long bm = __ballot(keep);
+            const int pos = base + __popcll(bm & ((1ull << lane) - 1ull));
+            if (keep && pos < KP) {
+                s_ck[pos] = kk;
+                s_cr[pos] = rr;
+            }
+            base += __popcll(bm);
+        }
+        if (lane == 0) s_m = m;
+    }
+    __syncthreads();
+    const int m = s_m;
+    const float* q = a.Q + (int64_t)b * a.D;
+    const double qn = a.qn64[b];
+    // exact keys: wave wv takes candidates wv, wv + 4, ... in batches of FIN_NB
+    for (int j0 = wv * FIN_NB; j0 < m; j0 += 4 * FIN_NB) {
+        uint32_t rows[FIN_NB];
+        double xn[FIN_NB];
+        const int nb = min(FIN_NB, m - j0);
+#pragma unroll
+        for (int u = 0; u < FIN_NB; ++u) {
+            rows[u] = u < nb ? s_cr[j0 + u] : 0u;
+            xn[u] = (METRIC == 0 && u < nb) ? a.nrm64[rows[u]] : 1.0;
+        }
+        double keys[FIN_NB];
+        exact_keys_batch<METRIC, FIN_NB>(q, qn, a.X, a.G, a.D, rows, xn, nb, keys);
+        if (lane == 0) {
+#pragma unroll
+            for (int u = 0; u < FIN_NB; ++u)
+                if (u < nb) s_ek[j0 + u] = keys[u];
+        }
+    }
+    __syncthreads();
+    // ranks by counting: exact (output order) and approx (certificate)
+    for (int j = tid; j < KP; j += 256) {
+        if (j < m) {
+            const double ek = s_ek[j];
+            const uint32_t ck = s_ck[j], r = s_cr[j];
+            int er = 0, ar = 0;
+            for (int i = 0; i < m; ++i) {
+                const double ei = s_ek[i];
+                const uint32_t ci = s_ck[i], ri = s_cr[i];
+                er += (ei > ek || (ei == ek && ri < r)) ? 1 : 0;
+                ar += (ci > ck || (ci == ck && ri < r)) ? 1 : 0;
+            }
+            if (er < a.k) {
+                const size_t o = (size_t)b * a.k + er;
+                write_result(METRIC, ek, (uint64_t)r + a.index_offset, true, a.out_s + o, a.out_i + o,
+                             a.out_k ? a.out_k + o : nullptr);
+            }
+            if (ar == a.k - 1) s_ak = ck;
+            if (ar == KP - 1) s_akp = ck;
+        } else if (j < a.k) {
+            const size_t o = (size_t)b * a.k + j;
+            write_result(METRIC, -INFINITY, 0, false, a.out_s + o, a.out_i + o, a.out_k ? a.out_k + o : nullptr);
+        }
+    }
+    for (int j = KP + tid; j < a.k; j += 256) {  // k > KP cannot happen on this path; defensive
+        const size_t o = (size_t)b * a.k + j;
+        write_result(METRIC, -INFINITY, 0, false, a.out_s + o, a.out_i + o, a.out_k ? a.out_k + o : nullptr);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        // Rows outside the candidates scored (approx) <= max(a_KP, T).
+        const bool full = m == KP;
+        const double T = (double)key_to_float(a.gthr[b]);
+        bool ok = true;
+        if (full || T > -INFINITY) {
+            const bool have_k = m >= a.k;
+            const double ak = have_k ? (double)key_to_float(s_ak) : -INFINITY;
+            const double akp = full ? (double)key_to_float(s_akp) : -INFINITY;
+            const double acut = fmax(akp, T);
+            double eps;
+            if (METRIC == 0) {
+                eps = a.eps_rel;
+            } else {
+                eps = a.eps_rel * (2.0 * qn * a.xmax + a.xmax * a.xmax) + 2.4e-7 * fmax(fabs(ak), fabs(acut));
+            }
+            ok = have_k && acut + eps < ak - eps;
+        }
+        if (!ok) {
+            const int pos = atomicAdd(a.flag_count, 1);
+            a.flag_list[pos] = b;
+        }
+    }
+}
+
+hipError_t launch_finish(int metric, int KP, const FinishArgs& a, int B, hipStream_t st) {
+#define VDB_FIN(M, KPV)                                                                         \
+    if (metric == M && KP == KPV) {                                                             \
+        hipLaunchKernelGGL((finish_kernel<M, KPV>), dim3(B), dim3(256), 0, st, a);              \
+        return hipGetLastError();                                                               \
+    }
+    VDB_FIN(0, 32) VDB_FIN(0, 64) VDB_FIN(0, 128) VDB_FIN(0, 256)
+    VDB_FIN(1, 32) VDB_FIN(1, 64) VDB_FIN(1, 128) VDB_FIN(1, 256)
+#undef VDB_FIN
     return hipErrorInvalidValue;
 }
 

@@ -37,23 +37,44 @@ hipError_t launch_unpack_rows(const float* X, int G, int D, int64_t row0, int64_
 // gslots[B][KP_MAX]: per-query slots of published workgroup bests; both zeroed by
 // prep_queries (see the publish step of scan_topk_kernel).
 constexpr int KP_MAX = 256;
+constexpr int PILOT_SLOTS = 256;  // pilot bound slots per query (pslots [Bp][PILOT_SLOTS])
 // Queries: row-major [B][D] -> tiled Qt [Bp/32 tiles] with G + QG_EXTRA groups
 // (the first QG_EXTRA groups repeated at the end; cosine: pre-normalised in
 // fp32; zero padding written) and/or the split-bf16 tiles Qs (G/2 + QG_EXTRA
 // groups, same wrap), canonical fp64 norms [Bp]; resets *flag_count.
 hipError_t launch_prep_queries(const float* Q, int B, int Bp, int D, int G, int metric,
                                float* Qt, float* Qs, double* qn64, int* flag_count, uint32_t* gthr,
-                               uint32_t* gslots, hipStream_t st);
+                               uint32_t* gslots, uint32_t* gl_cnt, hipStream_t st);
 
 // Candidate pass: MFMA fp32 scores fused with a per-workgroup top-KP.
 // Output lists cand_[s|i][B][n_wg][KP], each sorted best first.
 // X / Qt are the fp32 tiles (prec 0, G = Dp/8 groups) or the split tiles (prec 1, G = Dp/16).
 int scan_rows_per_step(int prec, int variant);
+int scan_wgs_per_cu(int prec, int variant, int KP);  // resident workgroups per CU the variant is built for
 bool scan_variant_ok(int prec, int variant, int G);
 hipError_t launch_scan_topk(int prec, int metric, int KP, int variant, const float* X, const float* rowscale,
                             const uint32_t* mask, const float* Qt, int G, int64_t N, int B, int n_qblocks, int64_t n_steps,
-                            int n_wg, int steps_per_wg, float* cand_s, uint32_t* cand_i, uint32_t* gthr,
-                            uint32_t* gslots, hipStream_t st);
+                            int n_wg, int steps_per_wg, float* gl_s, uint32_t* gl_i, uint32_t* gl_cnt, int64_t gl_cap,
+                            uint32_t* gthr, uint32_t* gslots, hipStream_t st);
+
+// Wave-private candidate pass (scan_priv(prec, variant, KP)): entries above the
+// shared bound are appended to global per-query lists gl_[s|i][B][gl_cap] (gl_cnt
+// zeroed by prep_queries); select_topk takes the sorted top KP of each list.
+bool scan_priv(int prec, int variant, int KP);
+int scan_priv_capw();
+hipError_t launch_scan_topk_priv(int prec, int metric, int KP, const float* X, const float* rowscale,
+                                 const uint32_t* mask, const float* Qt, int G, int64_t N, int B, int n_qblocks,
+                                 int64_t n_steps, int n_wg, int spw, float* gl_s, uint32_t* gl_i, uint32_t* gl_cnt,
+                                 int64_t gl_cap, uint32_t* gthr, uint32_t* gslots, hipStream_t st);
+hipError_t launch_select_topk(const float* gl_s, const uint32_t* gl_i, const uint32_t* gl_cnt, int64_t gl_cap, int KP,
+                              int B, float* out_s, uint32_t* out_i, hipStream_t st);
+
+// Pilot bound: scan-identical scores of n_sample evenly spaced row tiles; tile i's
+// best score per query goes into pilot slot (i mod PILOT_SLOTS) (atomicMax), then
+// gthr[q] = max(gthr[q], KP-th largest slot).  pslots zeroed by prep_queries.
+hipError_t launch_pilot(int prec, int metric, int KP, const float* X, const float* rowscale, const uint32_t* mask,
+                        const float* Qt, int G, int64_t N, int B, int n_qblocks, int QB, int n_sample,
+                        uint32_t* pslots, uint32_t* gthr, hipStream_t st);
 
 // Merge sorted per-workgroup lists -> sorted top-KP per query (fp32 keys).
 hipError_t launch_merge_f32(int KP, const float* ls, const uint32_t* li, int n_lists, int B,
@@ -66,8 +87,19 @@ struct RerankArgs {
     int k; double eps_rel; double xmax;
     float* out_s; int64_t* out_i; double* out_k; int64_t index_offset;
     int* flag_count; int* flag_list;
+    const uint32_t* gthr;  // final shared bound per query (rows at or below it may have been discarded)
 };
 hipError_t launch_rerank(int metric, int KP, const RerankArgs& a, int B, hipStream_t st);
+
+// Fused select (top KP of each global candidate list) + exact rerank + certificate.
+struct FinishArgs {
+    const float* gl_s; const uint32_t* gl_i; const uint32_t* gl_cnt; int64_t gl_cap;
+    const float* Q; const double* qn64; const float* X; int G; int D; const double* nrm64;
+    int k; double eps_rel; double xmax;
+    float* out_s; int64_t* out_i; double* out_k; int64_t index_offset;
+    int* flag_count; int* flag_list; const uint32_t* gthr;
+};
+hipError_t launch_finish(int metric, int KP, const FinishArgs& a, int B, hipStream_t st);
 
 // Exact fp64 scan of the whole corpus for the queries in qlist[0..nq):
 // per-workgroup sorted top-KE lists [nq][n_wg][KE] (fp64 keys, local rows).

@@ -12,9 +12,9 @@ namespace vdb {
 //
 // Select path (the common one): T = the KP-th best list HEAD is a lower bound
 // on the KP-th best entry overall (those KP heads are distinct rows), so only
-// entries not worse than T can be in the result.  All threads stream every
-// entry once (coalesced) and append survivors to LDS; one wave sorts them.
-// Survivors are typically ~KP.  Stream path (heavy ties overflow the buffer, or
+// entries not worse than T can be in the result.  Each thread walks its lists
+// from the head until an entry is worse than T and appends survivors to LDS;
+// one wave sorts them.  Survivors are typically ~KP.  Stream path (heavy ties overflow the buffer, or
 // more than 512 lists): one wave streams every entry through WaveTopK.
 constexpr int MERGE_BUF = 1024;
 constexpr int MERGE_HEADS = 512;
@@ -113,16 +113,35 @@ merge_lists_kernel(const K* __restrict__ ls, const I* __restrict__ li, int n_lis
         __syncthreads();
         const K tk = s_tk;
         const I ti = s_ti;
-        for (int f = threadIdx.x; f < total; f += 256) {
-            const int j = f / Lk, e = f - j * Lk;
-            const K kv = Lq[j * sj + e];
-            const I iv = Iq[j * sj + e];
-            if (iv != sentinel_idx<I>() && !better(tk, ti, kv, iv)) {
-                const int pos = atomicAdd(&s_cnt, 1);
-                if (pos < MERGE_BUF) {
-                    s_k[pos] = kv;
-                    s_i[pos] = iv;
+        // Lists are sorted, so thread t walks lists t, t + 256 from the head and stops
+        // at the first entry worse than T: typically one 4-entry batch per list (one
+        // round trip), instead of streaming all n_lists * Lk entries.
+        for (int j = threadIdx.x; j < n_lists; j += 256) {
+            const K* Lj = Lq + j * sj;
+            const I* Ij = Iq + j * sj;
+            for (int e0 = 0; e0 < Lk; e0 += 4) {
+                K kv[4];
+                I iv[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const bool in = e0 + u < Lk;
+                    kv[u] = in ? Lj[e0 + u] : (K)-INFINITY;
+                    iv[u] = in ? Ij[e0 + u] : sentinel_idx<I>();
                 }
+                bool more = true;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const bool keep = more && iv[u] != sentinel_idx<I>() && !better(tk, ti, kv[u], iv[u]);
+                    if (keep) {
+                        const int pos = atomicAdd(&s_cnt, 1);
+                        if (pos < MERGE_BUF) {
+                            s_k[pos] = kv[u];
+                            s_i[pos] = iv[u];
+                        }
+                    }
+                    more = keep;
+                }
+                if (!more) break;
             }
         }
         __syncthreads();

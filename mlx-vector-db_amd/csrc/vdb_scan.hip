@@ -36,16 +36,12 @@ __device__ unsigned long long g_scan_stamps[1 << 16][8];
 // Accumulator lane l / register v holds query 32 qt + (l & 31) against corpus
 // row 32 t + (v & 3) + 8 (v >> 2) + 4 (l >> 5).
 //
-// Top-KP per query lives in LDS: an append buffer of CAP = 2 KP (4 KP for
-// KP = 32: fewer compaction rounds while the first step fills it) (score, row)
-// per query plus a threshold (the KP-th best after the last compaction).  A
+// Top-KP per query lives in LDS: an append buffer of CAP >= 2 KP entries
+// (score, row) per query (larger CAP = fewer compaction rounds while the first
+// steps fill it) plus a threshold (the KP-th best after the last compaction).  A
 // score enters only if it beats the threshold; when a buffer fills, one wave
 // selects the best KP by bisection (compact_query).  Invariant used by the certificate in
 // rerank: every row not in the final list scored <= the list's KP-th entry.
-__device__ __forceinline__ uint32_t order_key(float f) {
-    const uint32_t u = __float_as_uint(f);
-    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);  // float order -> unsigned order
-}
 
 // Compaction of one query's append buffer (one wave): keep the best KP entries
 // by (score desc, row asc), unsorted, in slots [0, KP); the threshold becomes the
@@ -117,41 +113,58 @@ __device__ __forceinline__ void compact_query(float* sc, uint32_t* ix, int* cnt,
     }
 }
 
-__device__ __forceinline__ float key_to_float(uint32_t k) {
-    if (k == 0) return -INFINITY;
-    return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
-}
 
-// Final per-query list: best min(n, KP) entries sorted, sentinel padded.
-template <int KP, int CAP>
-__device__ __forceinline__ void flush_query(float* sc, uint32_t* ix, int* cnt, float* thr, float* out_s,
-                                            uint32_t* out_i) {
-    constexpr int EK = KP >= 64 ? KP / 64 : 1;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+// Flush of one wave's queries q(i) = q0 + qstep i (i < nq <= 64): the entries of LDS
+// buffer q (CAPX slots, cnt[q] used) scoring above that query's bound T (order key in
+// lane i's `tkey`) are appended to the global list of query qb0 + q.  One returning
+// atomic per query, all issued together (lane i for query i), so the flush costs one
+// round trip, not nq of them.
+template <int CAPX>
+__device__ __forceinline__ void append_flush(const float* sc, const uint32_t* ix, const int* cnt, int q0, int qstep,
+                                             int nq, int qb0, int B, uint32_t tkey, float* __restrict__ gl_s,
+                                             uint32_t* __restrict__ gl_i, uint32_t* __restrict__ gl_cnt,
+                                             int64_t gl_cap) {
+    constexpr int EW = (CAPX + 63) / 64;
     const int lane = threadIdx.x & 63;
-    compact_query<KP, CAP>(sc, ix, cnt, thr, nullptr);
-    const int n = *cnt < KP ? *cnt : KP;
-    float sv[EK];
-    uint32_t iv[EK];
+    int myc = 0;
+    for (int i = 0; i < nq; ++i) {
+        const int q = q0 + qstep * i;
+        const float Tq = key_to_float((uint32_t)__shfl((int)tkey, i, 64));
+        const int n = min(cnt[q], CAPX);
+        int c = 0;
 #pragma unroll
-    for (int i = 0; i < EK; ++i) {
-        const int e = i * 64 + lane;
-        sv[i] = e < n ? sc[e] : -INFINITY;
-        iv[i] = e < n ? ix[e] : 0xFFFFFFFFu;
+        for (int j = 0; j < EW; ++j) {
+            const int e = j * 64 + lane;
+            c += __popcll(__ballot(e < n && sc[q * CAPX + e] > Tq));
+        }
+        if (lane == i) myc = c;
     }
-    wave_sort_desc<float, uint32_t, EK>(sv, iv);
-    if (out_s) {
+    int mybase = 0;
+    if (lane < nq && qb0 + q0 + qstep * lane < B && myc > 0)
+        mybase = (int)atomicAdd(gl_cnt + qb0 + q0 + qstep * lane, (uint32_t)myc);
+    for (int i = 0; i < nq; ++i) {
+        const int q = q0 + qstep * i;
+        const int qg = qb0 + q;
+        if (qg >= B) continue;
+        const float Tq = key_to_float((uint32_t)__shfl((int)tkey, i, 64));
+        const int n = min(cnt[q], CAPX);
+        int base = __shfl(mybase, i, 64);
 #pragma unroll
-        for (int i = 0; i < EK; ++i) {
-            const int e = i * 64 + lane;
-            if (e < KP) {
-                out_s[e] = sv[i];
-                out_i[e] = iv[i];
+        for (int j = 0; j < EW; ++j) {
+            const int e = j * 64 + lane;
+            const bool pass = e < n && sc[q * CAPX + e] > Tq;
+            const unsigned long long m = __ballot(pass);
+            const int64_t pos = (int64_t)base + __popcll(m & ((1ull << lane) - 1ull));
+            if (pass && pos < gl_cap) {
+                gl_s[(size_t)qg * gl_cap + pos] = sc[q * CAPX + e];
+                gl_i[(size_t)qg * gl_cap + pos] = ix[q * CAPX + e];
             }
+            base += __popcll(m);
         }
     }
 }
-
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 // Inner products of one 8-dim (fp32) or 16-dim (split-bf16) group of RT corpus
 // tiles against QT query tiles.  PREC_BF16X3: x.q ~ xh.qh + xh.ql + xl.qh, each
@@ -181,23 +194,22 @@ __device__ __forceinline__ void group_mfma(const f32x4 (&x)[RT][PREC + 1], const
     }
 }
 
-template <int PREC, int METRIC, int QT, int RT, int PX, int PQ, int KP, int CAP, int WPS>
+template <int PREC, int METRIC, int QT, int RT, int PX, int PQ, int KP, int CAP, int PUB, int WPS>
 __global__ void __launch_bounds__(256, WPS)
 scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale, const uint32_t* __restrict__ mask,
                  const float* __restrict__ Qt, int G, int64_t N, int B, int64_t n_steps, int steps_per_wg,
-                 float* __restrict__ cand_s, uint32_t* __restrict__ cand_i, uint32_t* __restrict__ gthr,
-                 uint32_t* __restrict__ gslots) {
+                 float* __restrict__ gl_s, uint32_t* __restrict__ gl_i, uint32_t* __restrict__ gl_cnt, int64_t gl_cap,
+                 uint32_t* __restrict__ gthr, uint32_t* __restrict__ gslots) {
     static_assert(PX % PQ == 0, "query prefetch depth must divide the corpus prefetch depth");
     static_assert(PQ <= QG_EXTRA, "query prefetch deeper than the duplicated groups");
     constexpr int QB = 32 * QT;
-    constexpr int SR = 4 * RT * 32;  // rows per step
     __shared__ float s_sc[QB * CAP];
     __shared__ uint32_t s_ix[QB * CAP];
     __shared__ int s_cnt[QB];
     __shared__ float s_thr[QB];
-    __shared__ uint32_t s_best[QB];  // order key of the best score appended so far
+    __shared__ uint32_t s_best[QB];  // order key of the best score appended so far (PUB)
     __shared__ uint32_t s_pub[QB];   // ... and of the last one published
-    __shared__ float s_rs[2][SR];  // row scales, double-buffered by step parity
+    __shared__ uint32_t s_sh[QB];    // shared bound from the slots (order key), this WG's view
 
     const int lane = threadIdx.x & 63;
     // wave index made provably uniform: every tile/group address below is then
@@ -212,8 +224,21 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
         s_cnt[i] = 0;
         s_best[i] = 0;
         s_pub[i] = 0;
+        s_sh[i] = 0;
         s_thr[i] = -INFINITY;
     }
+    __syncthreads();
+    // slot publishing: lane group pq_i (LPQ lanes) of wave wv serves query pq = wv + 4 pq_i
+    constexpr int QPW = QB / 4;
+    constexpr int LPQ = 64 / QPW;
+    constexpr int SL = KP / LPQ;
+    constexpr int SLV = SL / 4 > 0 ? SL / 4 : 1;
+    static_assert(!PUB || SL % 4 == 0, "slots per lane must be whole uint4 loads");
+    const int pq_r = lane % LPQ;
+    const int pq = wv + 4 * (lane / LPQ);
+    const int pqg = qb * QB + pq;
+    uint4 sv[SLV];
+    bool sv_pending = false;
 
     const int64_t s_begin = (int64_t)wg * steps_per_wg;
     const int64_t s_end = s_begin + steps_per_wg < n_steps ? s_begin + steps_per_wg : n_steps;
@@ -249,14 +274,6 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
                 for (int pl = 0; pl < NPL; ++pl)
                     qr[p][qt][pl] = *(const f32x4*)(Qbase + p * GSTEP + pl * PLANE + qt * BLOCK_FLOATS + lane4);
     }
-
-    // row scales of the first step; later steps' are loaded one step ahead (next
-    // to the shared-threshold load) so that no step starts with a load whose
-    // value is needed at once (that wait would drain the corpus prefetch)
-    static_assert(SR % 256 == 0, "row scales are staged SR/256 per thread");
-    constexpr int RSN = SR / 256;
-    if (s_begin < s_end)
-        for (int i = 0; i < RSN; ++i) s_rs[s_begin & 1][threadIdx.x + 256 * i] = rowscale[s_begin * SR + threadIdx.x + 256 * i];
 #ifdef VDB_STAMP
     unsigned long long st_k = 0, st_e = 0, st_e0 = 0, st_t0 = STAMP_NOW();
     unsigned long long st_bar = 0, st_sc = 0, st_ins = 0, st_rt = 0, st_rounds = 0, st_compacts = 0;
@@ -266,11 +283,6 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
 #ifdef VDB_STAMP
         const unsigned long long st_a = STAMP_NOW();
 #endif
-        // row scales of this step -> LDS, read in the epilogue after the K-loop's
-        // barrier; buffer s&1 was last read in step s-2's epilogue (before step
-        // s-1's barriers)
-        const float* rs_buf = s_rs[s & 1];
-
         const int64_t t0 = (s * 4 + wv) * RT;
         const float* xs = X + blk((uint64_t)t0, 0, G);
         const float* xn = (s + 1 < s_end) ? X + blk((uint64_t)(t0 + 4 * RT), 0, G) : xs;
@@ -282,10 +294,10 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
 #pragma unroll
                 for (int v = 0; v < 16; ++v) acc[rt][qt][v] = 0.0f;
 
-        // One group: 4 k-steps of MFMAs on slot p, then refill slot p with the group
-        // PX ahead (from this step, or the next step's first groups).  The refill is
-        // pinned right after the MFMAs; left to itself the scheduler sinks it and
-        // shortens the prefetch distance.
+        // One group: the MFMAs of slot p, then refill slot p with the group PX ahead
+        // (from this step, or the next step's first groups).  The refill is pinned
+        // right after the MFMAs; left to itself the scheduler sinks it and shortens
+        // the prefetch distance.
         auto group = [&](const int p, const float* xsrc, const float* qsrc) {
             const int pq = p % PQ;
             group_mfma<PREC, RT, QT>(xr[p], qr[pq], acc);
@@ -308,31 +320,33 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
             for (int p = 0; p < PX; ++p)
                 group(p, xs + (size_t)(gb + p + PX) * GSTEP, Qbase + (size_t)(gb + p + PQ) * GSTEP);
         }
-        // shared thresholds (max over workgroups of their KP-th best so far), read
-        // before the last PX groups so the load hides under them; any value read,
-        // however stale (even an L1 copy), is a valid lower bound
+        // Loads whose values the epilogue needs are issued before the last PX groups
+        // (and before the next step's prefetch), so waiting for them never drains
+        // the corpus stream: the shared thresholds (any value read, however stale,
+        // even an L1 copy, is a valid lower bound), the row scales of this wave's
+        // rows (lane l needs rows (v & 3) + 8 (v >> 2) + 4 (l >> 5) of each tile)
+        // and the tile masks.
         uint32_t gk[QT];
 #pragma unroll
         for (int qt = 0; qt < QT; ++qt) {
             const int qg = qb * QB + qt * 32 + (lane & 31);
             gk[qt] = qg < B ? gthr[qg] : 0u;
         }
-        float rsn[RSN];
-        const int64_t sn = s + 1 < s_end ? s + 1 : s;
+        f32x4 rs4[RT][4];
+        uint32_t mword[RT];
 #pragma unroll
-        for (int i = 0; i < RSN; ++i) rsn[i] = rowscale[sn * SR + threadIdx.x + 256 * i];
+        for (int rt = 0; rt < RT; ++rt) {
+            const float* rsp = rowscale + (t0 + rt) * 32 + 4 * (lane >> 5);
+#pragma unroll
+            for (int m = 0; m < 4; ++m) rs4[rt][m] = *(const f32x4*)(rsp + 8 * m);
+            mword[rt] = mask ? mask[t0 + rt] : 0xFFFFFFFFu;
+        }
 #pragma unroll
         for (int p = 0; p < PX; ++p) group(p, xn + (size_t)p * GSTEP, Qbase + (size_t)(gb + p + PQ) * GSTEP);
 #ifdef VDB_STAMP
         const unsigned long long st_b = STAMP_NOW();
         st_k += st_b - st_a;
-#endif
-        __syncthreads();  // s_rs visible
-#pragma unroll
-        for (int i = 0; i < RSN; ++i) s_rs[(s + 1) & 1][threadIdx.x + 256 * i] = rsn[i];
-#ifdef VDB_STAMP
-        const unsigned long long st_b2 = STAMP_NOW();
-        st_bar += st_b2 - st_b;
+        const unsigned long long st_b2 = st_b;
 #endif
 
         // ---- epilogue -----------------------------------------------------------
@@ -345,26 +359,26 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) {
             const int64_t t = t0 + rt;
-            const uint32_t mword = mask ? mask[t] : 0xFFFFFFFFu;
-            const float* rsp = rs_buf + (wv * RT + rt) * 32 + 4 * (lane >> 5);
-            f32x4 rs4[4];
-#pragma unroll
-            for (int m = 0; m < 4; ++m) rs4[m] = *(const f32x4*)(rsp + 8 * m);
             uint32_t okbits = 0;
 #pragma unroll
             for (int v = 0; v < 16; ++v) {
                 const int ro = (v & 3) + 8 * (v >> 2) + 4 * (lane >> 5);
-                okbits |= (((mword >> ro) & 1u) && (t * 32 + ro < N)) ? (1u << v) : 0u;
+                okbits |= (((mword[rt] >> ro) & 1u) && (t * 32 + ro < N)) ? (1u << v) : 0u;
             }
 #pragma unroll
             for (int qt = 0; qt < QT; ++qt) {
                 const int ql = qt * 32 + (lane & 31);
-                const float thr = fmaxf(s_thr[ql], key_to_float(gk[qt]));
+                float thr = fmaxf(s_thr[ql], key_to_float(PUB ? max(gk[qt], s_sh[ql]) : gk[qt]));
+#ifdef VDB_STAMP
+                // diagnostic bounds (stamp build only, wrong results): PUB 2 = no insertion
+                // after the first step, PUB 3 = no insertion at all
+                if ((PUB == 2 && s > s_begin) || PUB == 3) thr = INFINITY;
+#endif
                 uint32_t pm = 0;
 #pragma unroll
                 for (int v = 0; v < 16; ++v) {
                     const float a = acc[rt][qt][v];
-                    const float rs = rs4[v >> 2][v & 3];
+                    const float rs = rs4[rt][v >> 2][v & 3];
                     const float sc = METRIC == 0 ? a * rs : fmaf(2.0f, a, -rs);
                     acc[rt][qt][v] = sc;
                     pm |= sc > thr ? (1u << v) : 0u;
@@ -383,10 +397,12 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
             if (!__any(pm != 0)) return 0u;
             const int ql = qt * 32 + (lane & 31);
             const int base = pm ? atomicAdd(&s_cnt[ql], __popc(pm)) : 0;
-            float mx = -INFINITY;
+            if constexpr (PUB) {
+                float mx = -INFINITY;
 #pragma unroll
-            for (int v = 0; v < 16; ++v) mx = ((pm >> v) & 1u) ? fmaxf(mx, acc[rt][qt][v]) : mx;
-            if (pm) atomicMax(&s_best[ql], order_key(mx));
+                for (int v = 0; v < 16; ++v) mx = ((pm >> v) & 1u) ? fmaxf(mx, acc[rt][qt][v]) : mx;
+                if (pm) atomicMax(&s_best[ql], order_key(mx));
+            }
             uint32_t left = 0;
 #pragma unroll
             for (int v = 0; v < 16; ++v) {
@@ -433,7 +449,8 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
             for (int rt = 0; rt < RT; ++rt) {
 #pragma unroll
                 for (int qt = 0; qt < QT; ++qt) {
-                    const float thr = fmaxf(s_thr[qt * 32 + (lane & 31)], key_to_float(gk[qt]));
+                    const int ql = qt * 32 + (lane & 31);
+                    const float thr = fmaxf(s_thr[ql], key_to_float(PUB ? max(gk[qt], s_sh[ql]) : gk[qt]));
                     uint32_t keep = 0;
 #pragma unroll
                     for (int v = 0; v < 16; ++v) keep |= acc[rt][qt][v] > thr ? (1u << v) : 0u;
@@ -447,38 +464,45 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
         const unsigned long long st_b5 = STAMP_NOW();
         st_pub_start = st_b5;
 #endif
-        // ---- publish: slot (query, wg % KP) of gslots holds the max over a fixed set
-        // of workgroups of their best score, so the KP slots of a query are scores of
-        // KP distinct rows and their minimum is a lower bound of the global KP-th best
-        // (DESIGN.md §3.2).  Only queries whose best improved are republished.
-        // Published after this workgroup's steps 1, 2, 4, 8, ... (each costs a global
-        // round trip, and the bound moves little once every slot is filled).
-        const int64_t sd = s - s_begin + 1;
-        if ((sd & (sd - 1)) == 0 || s + 1 == s_end) {
-            constexpr int QPW = QB / 4;
-            bool improved = false;
-            uint32_t best = 0;
-            int qg = 0;
-            if (lane < QPW) {
-                const int q = wv + 4 * lane;
-                qg = qb * QB + q;
-                best = s_best[q];
-                improved = qg < B && best > s_pub[q];
-                if (improved) {
-                    s_pub[q] = best;
-                    atomicMax(gslots + (size_t)qg * KP + (wg % KP), best);
-                }
-            }
-            if (__any(improved) && improved) {
-                // all KP slot loads in flight at once (one round trip)
-                const uint32_t* sl = gslots + (size_t)qg * KP;
+        if constexpr (PUB) {
+            // ---- publish: slot (query, wg % KP) of gslots holds the max over a fixed set
+            // of workgroups of their best score, so the KP slots of a query are scores of
+            // KP distinct rows and their minimum is a lower bound of the global KP-th best
+            // (DESIGN.md §3.1).  A group of LPQ lanes serves one query: its leader
+            // publishes (no-return atomic), all of them load SL slots each.  The slot
+            // loads are consumed one step later (min over the group's lanes -> gthr and
+            // s_sh): by then the next step's corpus loads, which are younger, have been
+            // waited for, so reading the slots never drains the HBM stream.
+            if (sv_pending) {
                 uint32_t mn = 0xFFFFFFFFu;
 #pragma unroll
-                for (int j = 0; j < KP; j += 4) {
-                    const uint4 v4 = *(const uint4*)(sl + j);
-                    mn = min(min(mn, min(v4.x, v4.y)), min(v4.z, v4.w));
+                for (int j = 0; j < SLV; ++j) mn = min(min(mn, min(sv[j].x, sv[j].y)), min(sv[j].z, sv[j].w));
+#pragma unroll
+                for (int off = 1; off < LPQ; off <<= 1) mn = min(mn, (uint32_t)__shfl_xor((int)mn, off, 64));
+                if (pq_r == 0 && pqg < B) {
+                    atomicMax(gthr + pqg, mn);
+                    atomicMax(&s_sh[pq], mn);
                 }
-                atomicMax(gthr + qg, mn);
+                sv_pending = false;
+            }
+            const int64_t sd = s - s_begin + 1;
+            if ((sd & (sd - 1)) == 0 || s + 1 == s_end) {
+                bool improved = false;
+                if (pq_r == 0 && pqg < B) {
+                    const uint32_t best = s_best[pq];
+                    improved = best > s_pub[pq];
+                    if (improved) {
+                        s_pub[pq] = best;
+                        atomicMax(gslots + (size_t)pqg * KP_MAX + (wg % KP), best);
+                    }
+                }
+                improved = __shfl((int)improved, lane - pq_r, 64) != 0;
+                if (improved) {
+                    const uint32_t* sl = gslots + (size_t)pqg * KP_MAX + pq_r * SL;
+#pragma unroll
+                    for (int j = 0; j < SLV; ++j) sv[j] = *(const uint4*)(sl + 4 * j);
+                }
+                sv_pending = improved;
             }
         }
 #ifdef VDB_STAMP
@@ -503,66 +527,579 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
     }
 #endif
 
-    // ---- flush: sorted top-KP of every query of the block ------------------------
+    // ---- flush: entries above the shared bound -> global per-query lists ----------
+    // (wave wv flushes queries wv + 4 i; lane i holds query i's bound)
     __syncthreads();
-    for (int q = wv; q < QB; q += 4) {
-        const int qg = qb * QB + q;
-        const size_t base = ((size_t)(qg < B ? qg : 0) * n_wg + wg) * KP;
-        flush_query<KP, CAP>(s_sc + q * CAP, s_ix + q * CAP, s_cnt + q, s_thr + q, qg < B ? cand_s + base : nullptr,
-                             cand_i + base);
+    (void)n_wg;
+    uint32_t tkey = 0;
+    if (lane < QPW && qb * QB + wv + 4 * lane < B) tkey = max(gthr[qb * QB + wv + 4 * lane], PUB ? s_sh[wv + 4 * lane] : 0u);
+    if constexpr (PUB) {
+        if (sv_pending) {  // a slot read-back still in flight: fold it in
+            uint32_t mn = 0xFFFFFFFFu;
+#pragma unroll
+            for (int j = 0; j < SLV; ++j) mn = min(min(mn, min(sv[j].x, sv[j].y)), min(sv[j].z, sv[j].w));
+#pragma unroll
+            for (int off = 1; off < LPQ; off <<= 1) mn = min(mn, (uint32_t)__shfl_xor((int)mn, off, 64));
+            if (pq_r == 0 && pqg < B) atomicMax(gthr + pqg, mn);
+        }
+    }
+    append_flush<CAP>(s_sc, s_ix, s_cnt, wv, 4, QPW, qb * QB, B, tkey, gl_s, gl_i, gl_cnt, gl_cap);
+}
+
+// =============================================================================
+// Candidate pass, wave-private variant (KP <= 32, 64 queries per block)
+// =============================================================================
+// Same K-loop as scan_topk_kernel, but every wave keeps its own top-KP per query
+// (LDS append buffer of CAPW entries per query and wave), so the step loop has no
+// workgroup barrier: a wave's epilogue never stalls the other three waves' corpus
+// streams.  Shared bounds as before (gthr: compaction thresholds + the deferred
+// slot minimum; s_sh: this workgroup's view of the slot minimum).  At the end each
+// wave appends the entries above the shared bound T to a global per-query list
+// (one returning atomic per query per wave); select_topk then takes the top KP of
+// each list.  Certificate invariant: every row not in a list scored <= max(the
+// list's KP-th entry, final gthr).
+template <int PREC, int METRIC, int QT, int RT, int PX, int PQ, int KP, int CAPW>
+__global__ void __launch_bounds__(256, 1)
+scan_topk_priv_kernel(const float* __restrict__ X, const float* __restrict__ rowscale,
+                      const uint32_t* __restrict__ mask, const float* __restrict__ Qt, int G, int64_t N, int B,
+                      int64_t n_steps, int steps_per_wg, float* __restrict__ gl_s, uint32_t* __restrict__ gl_i,
+                      uint32_t* __restrict__ gl_cnt, int64_t gl_cap, uint32_t* __restrict__ gthr,
+                      uint32_t* __restrict__ gslots) {
+    static_assert(PX % PQ == 0, "query prefetch depth must divide the corpus prefetch depth");
+    static_assert(PQ <= QG_EXTRA, "query prefetch deeper than the duplicated groups");
+    constexpr int QB = 32 * QT;
+    static_assert(QB <= 64 && KP % 4 == 0 && CAPW % 64 == 0, "one lane per query; whole uint4 slot loads");
+    __shared__ float s_sc[4][QB * CAPW];
+    __shared__ uint32_t s_ix[4][QB * CAPW];
+    __shared__ int s_cnt[4][QB];
+    __shared__ float s_thr[4][QB];
+    __shared__ uint32_t s_best[4][QB];
+    __shared__ uint32_t s_sh[QB];
+
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wg = blockIdx.x;
+    const int qb = blockIdx.y;
+    const int lane4 = lane * 4;
+    float* bs = s_sc[wv];
+    uint32_t* bi = s_ix[wv];
+    int* bc = s_cnt[wv];
+    float* bt = s_thr[wv];
+    uint32_t* bb = s_best[wv];
+    if (lane < QB) {
+        bc[lane] = 0;
+        bt[lane] = -INFINITY;
+        bb[lane] = 0;
+        if (wv == 0) s_sh[lane] = 0;
+    }
+    __syncthreads();
+
+    const int64_t s_begin = (int64_t)wg * steps_per_wg;
+    const int64_t s_end = s_begin + steps_per_wg < n_steps ? s_begin + steps_per_wg : n_steps;
+    constexpr int NPL = PREC + 1;
+    constexpr int GBLK = 4 * NPL;
+    constexpr size_t GSTEP = GBLK * BLOCK_FLOATS;
+    constexpr size_t PLANE = 4 * BLOCK_FLOATS;
+    auto blk = [](uint64_t t, int g, int GG) -> size_t {
+        return (((size_t)(t >> 2) * GG + g) * GBLK + (t & 3)) * BLOCK_FLOATS;
+    };
+    const float* Qbase = Qt + blk((uint64_t)(qb * QT), 0, G + QG_EXTRA);
+    // slot publishing: lane q < QB serves query q of the block
+    const int pqg = qb * QB + lane;
+    const bool pq_ok = lane < QB && pqg < B;
+    const int slot = (wg * 4 + wv) % KP;
+    uint32_t pub = 0;  // this wave's last published best (order key)
+    uint4 sv[KP / 4];
+    bool sv_pending = false;
+
+    f32x4 xr[PX][RT][NPL], qr[PQ][QT][NPL];
+    if (s_begin < s_end) {
+        const float* xs = X + blk((uint64_t)((s_begin * 4 + wv) * RT), 0, G);
+#pragma unroll
+        for (int p = 0; p < PX; ++p)
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+                for (int pl = 0; pl < NPL; ++pl)
+                    xr[p][rt][pl] = *(const f32x4*)(xs + p * GSTEP + pl * PLANE + rt * BLOCK_FLOATS + lane4);
+#pragma unroll
+        for (int p = 0; p < PQ; ++p)
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+                for (int pl = 0; pl < NPL; ++pl)
+                    qr[p][qt][pl] = *(const f32x4*)(Qbase + p * GSTEP + pl * PLANE + qt * BLOCK_FLOATS + lane4);
+    }
+    uint32_t gk[QT];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) gk[qt] = 0;
+
+    for (int64_t s = s_begin; s < s_end; ++s) {
+        const int64_t t0 = (s * 4 + wv) * RT;
+        const float* xs = X + blk((uint64_t)t0, 0, G);
+        const float* xn = (s + 1 < s_end) ? X + blk((uint64_t)(t0 + 4 * RT), 0, G) : xs;
+        f32x16 acc[RT][QT];
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+                for (int v = 0; v < 16; ++v) acc[rt][qt][v] = 0.0f;
+        auto group = [&](const int p, const float* xsrc, const float* qsrc) {
+            const int pq = p % PQ;
+            group_mfma<PREC, RT, QT>(xr[p], qr[pq], acc);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+                for (int pl = 0; pl < NPL; ++pl)
+                    xr[p][rt][pl] = *(const f32x4*)(xsrc + pl * PLANE + rt * BLOCK_FLOATS + lane4);
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+                for (int pl = 0; pl < NPL; ++pl)
+                    qr[pq][qt][pl] = *(const f32x4*)(qsrc + pl * PLANE + qt * BLOCK_FLOATS + lane4);
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        int gb = 0;
+        for (; gb < G - PX; gb += PX) {
+#pragma unroll
+            for (int p = 0; p < PX; ++p)
+                group(p, xs + (size_t)(gb + p + PX) * GSTEP, Qbase + (size_t)(gb + p + PQ) * GSTEP);
+        }
+        // epilogue inputs, issued before the next step's prefetch (see scan_topk_kernel)
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) {
+            const int qg = qb * QB + qt * 32 + (lane & 31);
+            gk[qt] = qg < B ? gthr[qg] : 0u;
+        }
+        f32x4 rs4[RT][4];
+        uint32_t mword[RT];
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+            const float* rsp = rowscale + (t0 + rt) * 32 + 4 * (lane >> 5);
+#pragma unroll
+            for (int m = 0; m < 4; ++m) rs4[rt][m] = *(const f32x4*)(rsp + 8 * m);
+            mword[rt] = mask ? mask[t0 + rt] : 0xFFFFFFFFu;
+        }
+#pragma unroll
+        for (int p = 0; p < PX; ++p) group(p, xn + (size_t)p * GSTEP, Qbase + (size_t)(gb + p + PQ) * GSTEP);
+
+        // ---- epilogue (wave-local) ----------------------------------------------
+        uint32_t pend[RT][QT];
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+            const int64_t t = t0 + rt;
+            uint32_t okbits = 0;
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+                const int ro = (v & 3) + 8 * (v >> 2) + 4 * (lane >> 5);
+                okbits |= (((mword[rt] >> ro) & 1u) && (t * 32 + ro < N)) ? (1u << v) : 0u;
+            }
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt) {
+                const int ql = qt * 32 + (lane & 31);
+                const float thr = fmaxf(bt[ql], key_to_float(max(gk[qt], s_sh[ql])));
+                uint32_t pm = 0;
+#pragma unroll
+                for (int v = 0; v < 16; ++v) {
+                    const float a = acc[rt][qt][v];
+                    const float rs = rs4[rt][v >> 2][v & 3];
+                    const float sc = METRIC == 0 ? a * rs : fmaf(2.0f, a, -rs);
+                    acc[rt][qt][v] = sc;
+                    pm |= sc > thr ? (1u << v) : 0u;
+                }
+                pend[rt][qt] = (qb * QB + ql < B) ? (pm & okbits) : 0u;
+            }
+        }
+        auto insert_tile = [&](int rt, int qt) -> uint32_t {
+            const uint32_t pm = pend[rt][qt];
+            if (!__any(pm != 0)) return 0u;
+            const int ql = qt * 32 + (lane & 31);
+            const int base = pm ? atomicAdd(&bc[ql], __popc(pm)) : 0;
+            float mx = -INFINITY;
+#pragma unroll
+            for (int v = 0; v < 16; ++v) mx = ((pm >> v) & 1u) ? fmaxf(mx, acc[rt][qt][v]) : mx;
+            if (pm) atomicMax(&bb[ql], order_key(mx));
+            uint32_t left = 0;
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+                if ((pm >> v) & 1u) {
+                    const int pos = base + __popc(pm & ((1u << v) - 1u));
+                    if (pos < CAPW) {
+                        const int ro = (v & 3) + 8 * (v >> 2) + 4 * (lane >> 5);
+                        bs[ql * CAPW + pos] = acc[rt][qt][v];
+                        bi[ql * CAPW + pos] = (uint32_t)((t0 + rt) * 32 + ro);
+                    } else {
+                        left |= 1u << v;
+                    }
+                }
+            }
+            return left;
+        };
+        uint32_t any_left = 0;
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt) {
+                pend[rt][qt] = insert_tile(rt, qt);
+                any_left |= pend[rt][qt];
+            }
+        while (__any(any_left != 0)) {
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            unsigned long long full = __ballot(lane < QB && bc[lane < QB ? lane : 0] >= CAPW);
+            while (full) {
+                const int q = __builtin_ctzll(full);
+                full &= full - 1;
+                compact_query<KP, CAPW>(bs + q * CAPW, bi + q * CAPW, bc + q, bt + q,
+                                        qb * QB + q < B ? gthr + qb * QB + q : nullptr);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            any_left = 0;
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) {
+#pragma unroll
+                for (int qt = 0; qt < QT; ++qt) {
+                    const int ql = qt * 32 + (lane & 31);
+                    const float thr = fmaxf(bt[ql], key_to_float(max(gk[qt], s_sh[ql])));
+                    uint32_t keep = 0;
+#pragma unroll
+                    for (int v = 0; v < 16; ++v) keep |= acc[rt][qt][v] > thr ? (1u << v) : 0u;
+                    pend[rt][qt] &= keep;
+                    pend[rt][qt] = insert_tile(rt, qt);
+                    any_left |= pend[rt][qt];
+                }
+            }
+        }
+        // ---- publish (lane q = query q; the slot read-back is consumed one step later) --
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        if (sv_pending) {
+            uint32_t mn = 0xFFFFFFFFu;
+#pragma unroll
+            for (int j = 0; j < KP / 4; ++j) mn = min(min(mn, min(sv[j].x, sv[j].y)), min(sv[j].z, sv[j].w));
+            atomicMax(gthr + pqg, mn);
+            atomicMax(&s_sh[lane], mn);
+            sv_pending = false;
+        }
+        const int64_t sd = s - s_begin + 1;
+        if ((sd & (sd - 1)) == 0 || s + 1 == s_end) {
+            const uint32_t best = pq_ok ? bb[lane] : 0u;
+            if (pq_ok && best > pub) {
+                pub = best;
+                atomicMax(gslots + (size_t)pqg * KP_MAX + slot, best);
+                const uint32_t* sl = gslots + (size_t)pqg * KP_MAX;
+#pragma unroll
+                for (int j = 0; j < KP / 4; ++j) sv[j] = *(const uint4*)(sl + 4 * j);
+                sv_pending = true;
+            }
+        }
+    }
+
+    // ---- flush: entries above the shared bound -> global per-query lists ----------
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    uint32_t tkey = pq_ok ? max(gthr[pqg], s_sh[lane]) : 0u;
+    if (sv_pending) {
+        uint32_t mn = 0xFFFFFFFFu;
+#pragma unroll
+        for (int j = 0; j < KP / 4; ++j) mn = min(min(mn, min(sv[j].x, sv[j].y)), min(sv[j].z, sv[j].w));
+        atomicMax(gthr + pqg, mn);
+        tkey = max(tkey, mn);
+    }
+    append_flush<CAPW>(bs, bi, bc, 0, 1, QB, qb * QB, B, tkey, gl_s, gl_i, gl_cnt, gl_cap);
+}
+
+// Top KP (sorted by score desc, row asc; sentinel padded) of each query's global
+// append list.  One wave per query: <= 256 entries in registers (bitonic), more
+// through the LDS streaming top-k (only when the shared bound was weak).
+constexpr int SELECT_REG = 256;
+__global__ void __launch_bounds__(64) select_topk_kernel(const float* __restrict__ gl_s, const uint32_t* __restrict__ gl_i,
+                                                         const uint32_t* __restrict__ gl_cnt, int64_t gl_cap, int KP,
+                                                         float* __restrict__ out_s, uint32_t* __restrict__ out_i) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x;
+    const int q = blockIdx.x;
+    const int64_t c = min((int64_t)gl_cnt[q], gl_cap);
+    const float* ls = gl_s + (size_t)q * gl_cap;
+    const uint32_t* li = gl_i + (size_t)q * gl_cap;
+    float* os = out_s + (size_t)q * KP;
+    uint32_t* oi = out_i + (size_t)q * KP;
+    if (c <= SELECT_REG) {
+        constexpr int E = SELECT_REG / 64;
+        float v[E];
+        uint32_t x[E];
+#pragma unroll
+        for (int i = 0; i < E; ++i) {
+            const int e = i * 64 + lane;
+            v[i] = e < c ? ls[e] : -INFINITY;
+            x[i] = e < c ? li[e] : 0xFFFFFFFFu;
+        }
+        wave_sort_desc<float, uint32_t, E>(v, x);
+#pragma unroll
+        for (int i = 0; i < E; ++i) {
+            const int e = i * 64 + lane;
+            if (e < KP) {
+                os[e] = v[i];
+                oi[e] = x[i];
+            }
+        }
+        for (int e = SELECT_REG + lane; e < KP; e += 64) {
+            os[e] = -INFINITY;
+            oi[e] = 0xFFFFFFFFu;
+        }
+        return;
+    }
+    WaveTopK<float, uint32_t> tk;
+    tk.init(reinterpret_cast<float*>(smem),
+            reinterpret_cast<uint32_t*>(smem + (size_t)WaveTopK<float, uint32_t>::capacity(KP) * sizeof(float)), KP);
+    for (int64_t f0 = 0; f0 < c; f0 += 64) {
+        const int64_t f = f0 + lane;
+        const bool in = f < c;
+        tk.offer(in, in ? ls[f] : -INFINITY, in ? li[f] : 0xFFFFFFFFu);
+    }
+    tk.finish();
+    for (int e = lane; e < KP; e += 64) {
+        os[e] = tk.bk[e];
+        oi[e] = tk.bi[e];
     }
 }
 
-template <int PREC, int METRIC, int QT, int RT, int PX, int PQ, int KP, int CAP, int WPS>
-static hipError_t scan_dispatch(const float* X, const float* rowscale, const uint32_t* mask, const float* Qt, int G,
-                                int64_t N, int B, int n_qblocks, int64_t n_steps, int n_wg, int spw, float* cs,
-                                uint32_t* ci, uint32_t* gthr, uint32_t* gslots, hipStream_t st) {
-    hipLaunchKernelGGL((scan_topk_kernel<PREC, METRIC, QT, RT, PX, PQ, KP, CAP, WPS>), dim3(n_wg, n_qblocks), dim3(256),
-                       0, st, X, rowscale, mask, Qt, G, N, B, n_steps, spw, cs, ci, gthr, gslots);
+hipError_t launch_select_topk(const float* gl_s, const uint32_t* gl_i, const uint32_t* gl_cnt, int64_t gl_cap, int KP,
+                              int B, float* out_s, uint32_t* out_i, hipStream_t st) {
+    const size_t lds = (size_t)WaveTopK<float, uint32_t>::capacity(KP) * 8;
+    hipLaunchKernelGGL(select_topk_kernel, dim3(B), dim3(64), lds, st, gl_s, gl_i, gl_cnt, gl_cap, KP, out_s, out_i);
     return hipGetLastError();
 }
 
-// Variants (RT row tiles of 32 per wave, corpus PX groups ahead, queries PQ ahead):
-//   fp32  0: RT=2 PX=4 PQ=4, 2 waves/SIMD     1: RT=4 PX=4 PQ=2, 2 waves/SIMD
-//         2: RT=4 PX=8 PQ=2, 1 wave/SIMD (accumulators in AGPRs)
-//   bf16x3 0: RT=2 PX=4 PQ=2, 1 wave/SIMD     1: RT=4 PX=4 PQ=2, 1 wave/SIMD
-//         2: RT=2 PX=8 PQ=2, 1 wave/SIMD
+template <int PREC, int METRIC, int QT, int RT, int PX, int PQ, int KP, int CAPW>
+static hipError_t scan_priv_dispatch(const float* X, const float* rowscale, const uint32_t* mask, const float* Qt,
+                                     int G, int64_t N, int B, int n_qblocks, int64_t n_steps, int n_wg, int spw,
+                                     float* gl_s, uint32_t* gl_i, uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr,
+                                     uint32_t* gslots, hipStream_t st) {
+    hipLaunchKernelGGL((scan_topk_priv_kernel<PREC, METRIC, QT, RT, PX, PQ, KP, CAPW>), dim3(n_wg, n_qblocks),
+                       dim3(256), 0, st, X, rowscale, mask, Qt, G, N, B, n_steps, spw, gl_s, gl_i, gl_cnt, gl_cap,
+                       gthr, gslots);
+    return hipGetLastError();
+}
+
+// wave-private candidate pass: fp32 variant 0 (measured faster there), bf16x3 variant 1
+bool scan_priv(int prec, int variant, int KP) {
+    return KP == 32 && ((prec == PREC_FP32 && variant == 0) || (prec == PREC_BF16X3 && variant == 1));
+}
+
+int scan_priv_capw() { return 64; }
+
+hipError_t launch_scan_topk_priv(int prec, int metric, int KP, const float* X, const float* rowscale,
+                                 const uint32_t* mask, const float* Qt, int G, int64_t N, int B, int n_qblocks,
+                                 int64_t n_steps, int n_wg, int spw, float* gl_s, uint32_t* gl_i, uint32_t* gl_cnt,
+                                 int64_t gl_cap, uint32_t* gthr, uint32_t* gslots, hipStream_t st) {
+    if (KP != 32 || G % 4 != 0) return hipErrorInvalidValue;
+#define VDB_PRIV(P, M, PQV)                                                                                   \
+    if (prec == P && metric == M)                                                                             \
+        return scan_priv_dispatch<P, M, 2, 2, 4, PQV, 32, 64>(X, rowscale, mask, Qt, G, N, B, n_qblocks, n_steps, \
+                                                            n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, st);
+    VDB_PRIV(0, 0, 4) VDB_PRIV(0, 1, 4) VDB_PRIV(1, 0, 2) VDB_PRIV(1, 1, 2)
+#undef VDB_PRIV
+    return hipErrorInvalidValue;
+}
+
+// =============================================================================
+// Pilot bound: scores of a strided sample of row tiles, KP-th best per query
+// =============================================================================
+// A cold scan inserts almost every score of its first steps (no bound yet), which
+// costs more than the rest of the epilogue.  The pilot scores n_sample evenly
+// spaced row tiles with exactly the scan's arithmetic (same group order through
+// group_mfma, same row scale), so its KP-th best per query is the KP-th best of a
+// subset of the rows the scan will score identically: a valid lower bound of the
+// global KP-th best, written to gthr before the scan starts.
+template <int PREC, int METRIC, int QT>
+__global__ void __launch_bounds__(64) pilot_scores_kernel(const float* __restrict__ X, const float* __restrict__ rowscale,
+                                                          const uint32_t* __restrict__ mask, const float* __restrict__ Qt,
+                                                          int G, int64_t N, int B, int64_t n_tiles, int n_sample,
+                                                          uint32_t* __restrict__ pslots) {
+    constexpr int QB = 32 * QT;
+    constexpr int NPL = PREC + 1;
+    constexpr int GBLK = 4 * NPL;
+    constexpr size_t GSTEP = GBLK * BLOCK_FLOATS;
+    constexpr size_t PLANE = 4 * BLOCK_FLOATS;
+    auto blk = [](uint64_t t, int g, int GG) -> size_t {
+        return (((size_t)(t >> 2) * GG + g) * GBLK + (t & 3)) * BLOCK_FLOATS;
+    };
+    const int lane = threadIdx.x;
+    const int i = blockIdx.x;
+    const int qb = blockIdx.y;
+    const uint64_t t = (uint64_t)((int64_t)i * n_tiles / n_sample);
+    const float* xs = X + blk(t, 0, G) + lane * 4;
+    const float* qs = Qt + blk((uint64_t)(qb * QT), 0, G + QG_EXTRA) + lane * 4;
+    f32x16 acc[1][QT];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) acc[0][qt][v] = 0.0f;
+    // one wave, groups in the scan's order (bit-identical accumulators), loads PP
+    // groups ahead so the tile costs a few HBM round trips, not G of them
+    constexpr int PP = 12;
+    f32x4 xr[PP][1][NPL], qr[PP][QT][NPL];
+    auto load = [&](int slot, int g) {
+        if (g < G) {
+#pragma unroll
+            for (int pl = 0; pl < NPL; ++pl) xr[slot][0][pl] = *(const f32x4*)(xs + g * GSTEP + pl * PLANE);
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+                for (int pl = 0; pl < NPL; ++pl)
+                    qr[slot][qt][pl] = *(const f32x4*)(qs + g * GSTEP + pl * PLANE + qt * BLOCK_FLOATS);
+        }
+    };
+#pragma unroll
+    for (int p = 0; p < PP; ++p) load(p, p);
+    for (int g0 = 0; g0 < G; g0 += PP) {
+#pragma unroll
+        for (int p = 0; p < PP; ++p) {
+            if (g0 + p < G) {
+                group_mfma<PREC, 1, QT>(xr[p], qr[p], acc);
+                load(p, g0 + p + PP);
+            }
+        }
+    }
+    // the tile's best eligible score per query -> pilot slot (i mod PILOT_SLOTS): the
+    // slots hold scores of distinct rows, so the KP-th largest slot is a lower bound
+    // of the global KP-th best (pilot_bound_kernel)
+    const uint32_t mword = mask ? mask[t] : 0xFFFFFFFFu;
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+        const int q = qb * QB + qt * 32 + (lane & 31);
+        float best = -INFINITY;
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+            const int ro = (v & 3) + 8 * (v >> 2) + 4 * (lane >> 5);
+            const float rs = rowscale[t * 32 + ro];
+            const float a = acc[0][qt][v];
+            const float sc = METRIC == 0 ? a * rs : fmaf(2.0f, a, -rs);
+            const bool ok = ((mword >> ro) & 1u) && ((int64_t)t * 32 + ro < N);
+            best = ok ? fmaxf(best, sc) : best;
+        }
+        if (q < B && best != -INFINITY) atomicMax(pslots + (size_t)q * PILOT_SLOTS + (i % PILOT_SLOTS), order_key(best));
+    }
+}
+
+// gthr[q] = max(gthr[q], KP-th largest pilot slot) when at least KP slots are
+// filled: one wave per query, ballot bisection over the 256 slots (4 per lane).
+__global__ void __launch_bounds__(64) pilot_bound_kernel(const uint32_t* __restrict__ pslots, int B, int KP,
+                                                         uint32_t* __restrict__ gthr) {
+    const int q = blockIdx.x;
+    const int lane = threadIdx.x;
+    constexpr int E = PILOT_SLOTS / 64;
+    uint32_t v[E];
+#pragma unroll
+    for (int i = 0; i < E; ++i) v[i] = pslots[(size_t)q * PILOT_SLOTS + i * 64 + lane];
+    int filled = 0;
+#pragma unroll
+    for (int i = 0; i < E; ++i) filled += __popcll(__ballot(v[i] != 0u));
+    if (filled < KP) return;
+    uint32_t T = 0;
+    for (int bit = 31; bit >= 0; --bit) {
+        const uint32_t c = T | (1u << bit);
+        int n = 0;
+#pragma unroll
+        for (int i = 0; i < E; ++i) n += __popcll(__ballot(v[i] >= c));
+        if (n >= KP) T = c;
+    }
+    if (lane == 0 && T != 0) atomicMax(gthr + q, T);
+}
+
+hipError_t launch_pilot(int prec, int metric, int KP, const float* X, const float* rowscale, const uint32_t* mask,
+                        const float* Qt, int G, int64_t N, int B, int n_qblocks, int QB, int n_sample,
+                        uint32_t* pslots, uint32_t* gthr, hipStream_t st) {
+    const int64_t n_tiles = (N + 31) / 32;
+    if (n_sample > n_tiles) n_sample = (int)n_tiles;
+    if (n_sample <= 0 || KP > PILOT_SLOTS) return hipSuccess;
+    const dim3 grid(n_sample, n_qblocks);
+    bool launched = false;
+#define VDB_PILOT(P, M, QTV)                                                                                     \
+    if (!launched && prec == P && metric == M && QB == 32 * QTV) {                                               \
+        hipLaunchKernelGGL((pilot_scores_kernel<P, M, QTV>), grid, dim3(64), 0, st, X, rowscale, mask, Qt, G, N,   \
+                           B, n_tiles, n_sample, pslots);                                                        \
+        launched = true;                                                                                         \
+    }
+    VDB_PILOT(0, 0, 2) VDB_PILOT(0, 1, 2) VDB_PILOT(1, 0, 2) VDB_PILOT(1, 1, 2)
+    VDB_PILOT(0, 0, 1) VDB_PILOT(0, 1, 1) VDB_PILOT(1, 0, 1) VDB_PILOT(1, 1, 1)
+#undef VDB_PILOT
+    if (!launched) return hipErrorInvalidValue;
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(pilot_bound_kernel, dim3(B), dim3(64), 0, st, pslots, B, KP, gthr);
+    return hipGetLastError();
+}
+
+template <int PREC, int METRIC, int QT, int RT, int PX, int PQ, int KP, int CAP, int PUB, int WPS>
+static hipError_t scan_dispatch(const float* X, const float* rowscale, const uint32_t* mask, const float* Qt, int G,
+                                int64_t N, int B, int n_qblocks, int64_t n_steps, int n_wg, int spw, float* gl_s,
+                                uint32_t* gl_i, uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr, uint32_t* gslots,
+                                hipStream_t st) {
+    hipLaunchKernelGGL((scan_topk_kernel<PREC, METRIC, QT, RT, PX, PQ, KP, CAP, PUB, WPS>), dim3(n_wg, n_qblocks),
+                       dim3(256), 0, st, X, rowscale, mask, Qt, G, N, B, n_steps, spw, gl_s, gl_i, gl_cnt, gl_cap,
+                       gthr, gslots);
+    return hipGetLastError();
+}
+
+// Variants (RT row tiles of 32 per wave, corpus PX groups ahead, queries PQ ahead,
+// CAP append-buffer entries per query, PUB = slot publishing of workgroup bests):
+//   fp32   0: RT=2 PX=4 PQ=4 PUB, 2 waves/SIMD   1: RT=4 PX=4 PQ=2 PUB   2: RT=4 PX=8 PQ=2 PUB, 1 wave/SIMD
+//   bf16x3 0: RT=2 PX=PQ=4, CAP 4 KP, slot publishing, 1 wave/SIMD
+//          1: wave-private top-k for KP = 32 (scan_topk_priv_kernel), else as 0 with CAP 8 KP
+//          2: RT=2 PX=4 PQ=2, CAP 4 KP, 2 workgroups per CU (256 registers) for KP <= 64: one
+//             workgroup's epilogue overlaps the other's corpus stream
+// PQ = PX for bf16x3: loads retire in issue order (vmcnt), so a query load issued
+// PQ < PX groups ahead caps the usable corpus prefetch at PQ groups.
 static int variant_rt(int prec, int variant) {
     if (prec == PREC_FP32) return variant == 0 ? 2 : 4;
-    return variant == 1 ? 4 : 2;
+    return 2;
 }
-static int variant_px(int prec, int variant) {
-    if (prec == PREC_FP32) return variant == 2 ? 8 : 4;
-    return variant == 2 ? 8 : 4;
+static int variant_px(int prec, int variant) { return (prec == PREC_FP32 && variant == 2) ? 8 : 4; }
+
+int scan_wgs_per_cu(int prec, int variant, int KP) {
+    return (prec == PREC_BF16X3 && variant == 2 && KP <= 64) ? 2 : 1;
 }
 
 int scan_rows_per_step(int prec, int variant) { return 4 * 32 * variant_rt(prec, variant); }
 
+#ifdef VDB_STAMP
+constexpr int kMaxVariant = 3;  // 3: diagnostic, no insertion after the first step (wrong results)
+#else
+constexpr int kMaxVariant = 2;
+#endif
 bool scan_variant_ok(int prec, int variant, int G) {
-    return variant >= 0 && variant <= 2 && G % variant_px(prec, variant) == 0;
+    return variant >= 0 && variant <= kMaxVariant && G % variant_px(prec, variant) == 0;
 }
 
 hipError_t launch_scan_topk(int prec, int metric, int KP, int variant, const float* X, const float* rowscale,
                             const uint32_t* mask, const float* Qt, int G, int64_t N, int B, int n_qblocks,
-                            int64_t n_steps, int n_wg, int spw, float* cs, uint32_t* ci, uint32_t* gthr,
-                            uint32_t* gslots, hipStream_t st) {
+                            int64_t n_steps, int n_wg, int spw, float* gl_s, uint32_t* gl_i, uint32_t* gl_cnt,
+                            int64_t gl_cap, uint32_t* gthr, uint32_t* gslots, hipStream_t st) {
     if (!scan_variant_ok(prec, variant, G)) return hipErrorInvalidValue;
-#define VDB_SCAN(P, M, QT, KPV, V, RT, PX, PQ, W)                                                               \
+#define VDB_SCAN(P, M, QT, KPV, V, RT, PX, PQ, CAPV, PUB, W)                                                     \
     if (prec == P && metric == M && KP == KPV && variant == V)                                                 \
-        return scan_dispatch<P, M, QT, RT, PX, PQ, KPV, (KPV == 32 ? 4 : 2) * KPV, W>(                          \
-            X, rowscale, mask, Qt, G, N, B, n_qblocks, n_steps, n_wg, spw, cs, ci, gthr, gslots, st);
+        return scan_dispatch<P, M, QT, RT, PX, PQ, KPV, CAPV, PUB, W>(X, rowscale, mask, Qt, G, N, B, n_qblocks, \
+                                                                    n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, \
+                                                                    gthr, gslots, st);
 #define VDB_SCAN_ALL(M)                                                                                        \
-    VDB_SCAN(0, M, 2, 32, 0, 2, 4, 4, 2) VDB_SCAN(0, M, 2, 64, 0, 2, 4, 4, 2)                                  \
-    VDB_SCAN(0, M, 2, 128, 0, 2, 4, 4, 1) VDB_SCAN(0, M, 1, 256, 0, 2, 4, 4, 1)                                \
-    VDB_SCAN(0, M, 2, 32, 1, 4, 4, 2, 2) VDB_SCAN(0, M, 2, 64, 1, 4, 4, 2, 2)                                  \
-    VDB_SCAN(0, M, 2, 32, 2, 4, 8, 2, 1) VDB_SCAN(0, M, 2, 64, 2, 4, 8, 2, 1)                                  \
-    VDB_SCAN(1, M, 2, 32, 0, 2, 4, 2, 1) VDB_SCAN(1, M, 2, 64, 0, 2, 4, 2, 1)                                  \
-    VDB_SCAN(1, M, 2, 128, 0, 2, 4, 2, 1) VDB_SCAN(1, M, 1, 256, 0, 2, 4, 2, 1)                                \
-    VDB_SCAN(1, M, 2, 32, 1, 4, 4, 2, 1) VDB_SCAN(1, M, 2, 64, 1, 4, 4, 2, 1)                                  \
-    VDB_SCAN(1, M, 2, 128, 1, 4, 4, 2, 1)                                                                      \
-    VDB_SCAN(1, M, 2, 32, 2, 2, 8, 2, 1) VDB_SCAN(1, M, 2, 64, 2, 2, 8, 2, 1)
+    VDB_SCAN(0, M, 2, 32, 0, 2, 4, 4, 128, 1, 2) VDB_SCAN(0, M, 2, 64, 0, 2, 4, 4, 128, 1, 2)                  \
+    VDB_SCAN(0, M, 2, 128, 0, 2, 4, 4, 256, 1, 1) VDB_SCAN(0, M, 1, 256, 0, 2, 4, 4, 512, 1, 1)                \
+    VDB_SCAN(0, M, 2, 32, 1, 4, 4, 2, 128, 1, 2) VDB_SCAN(0, M, 2, 64, 1, 4, 4, 2, 128, 1, 2)                  \
+    VDB_SCAN(0, M, 2, 32, 2, 4, 8, 2, 128, 1, 1) VDB_SCAN(0, M, 2, 64, 2, 4, 8, 2, 128, 1, 1)                  \
+    VDB_SCAN(1, M, 2, 32, 0, 2, 4, 4, 128, 1, 1) VDB_SCAN(1, M, 2, 64, 0, 2, 4, 4, 128, 1, 1)                  \
+    VDB_SCAN(1, M, 2, 128, 0, 2, 4, 4, 256, 1, 1) VDB_SCAN(1, M, 1, 256, 0, 2, 4, 4, 512, 1, 1)                \
+    VDB_SCAN(1, M, 2, 32, 1, 2, 4, 4, 256, 1, 1) VDB_SCAN(1, M, 2, 64, 1, 2, 4, 4, 256, 1, 1)                  \
+    VDB_SCAN(1, M, 2, 128, 1, 2, 4, 4, 256, 1, 1) VDB_SCAN(1, M, 1, 256, 1, 2, 4, 4, 512, 1, 1)                \
+    VDB_SCAN(1, M, 2, 32, 2, 2, 4, 2, 128, 1, 2) VDB_SCAN(1, M, 2, 64, 2, 2, 4, 2, 128, 1, 2)                  \
+    VDB_SCAN(1, M, 2, 128, 2, 2, 4, 4, 256, 1, 1) VDB_SCAN(1, M, 1, 256, 2, 2, 4, 4, 512, 1, 1)
     VDB_SCAN_ALL(0)
     VDB_SCAN_ALL(1)
+#ifdef VDB_STAMP
+    VDB_SCAN(1, 0, 2, 32, 3, 2, 4, 4, 128, 2, 1)
+#endif
 #undef VDB_SCAN_ALL
 #undef VDB_SCAN
     return hipErrorInvalidValue;
