@@ -179,6 +179,7 @@ def main():
         p50 = float(np.median(lat))
 
     fallback = ix.stat("fallback_queries")
+    overflow = ix.stat("overflow_queries")
     if rank == 0:
         # algorithmic work of one scan launch on this rank: every corpus row read once
         # (fp32 tiles or the split hi/lo tiles: 4 B per element either way), its row
@@ -236,6 +237,7 @@ def main():
                              hbm_frac=achieved_gbs / HBM_PEAK_GBS, mfma_frac=achieved_tf / mfma_peak),
             "pipeline_ms": pipe_ms,
             "fallback_queries_total": fallback,
+            "fallback_list_overflow": overflow,
         }
         if world == 1 and not args.no_cpu_baseline:
             V = np.concatenate(host_parts) if len(host_parts) > 1 else host_parts[0]

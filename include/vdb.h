@@ -92,7 +92,7 @@ int32_t vdb_index_reserve(vdb_index* idx, int64_t rows);
  * "scan_variant" / "scan_variant_bf16x3" (0..2, kernel tiling variants),
  * "timing" (0/1: HIP events around the candidate pass; stats "scan_ns",
  * "pipeline_ns", "timed_searches").  Stats also: "searches", "queries",
- * "fallback_queries", "capacity", "count", "device_bytes", "precision". */
+ * "fallback_queries", "overflow_queries", "capacity", "count", "device_bytes", "precision". */
 int32_t vdb_index_set_param(vdb_index* idx, const char* name, int64_t value);
 int32_t vdb_index_get_stat(const vdb_index* idx, const char* name, int64_t* value);
 

@@ -108,7 +108,7 @@ struct vdb_index {
     int64_t scan_variant = 0;     // fp32 candidate pass variant (vdb_scan.hip)
     int64_t scan_variant_b3 = 0;  // bf16x3 candidate pass variant
     // stats
-    std::atomic<int64_t> n_searches{0}, n_queries{0}, n_fallback{0};
+    std::atomic<int64_t> n_searches{0}, n_queries{0}, n_fallback{0}, n_overflow{0};
     std::atomic<int64_t> scan_ns{0}, pipe_ns{0}, n_timed{0};
     std::shared_mutex mu;  // add/clear/reserve exclusive; search shared
     std::mutex ws_mu;
@@ -392,6 +392,7 @@ int32_t vdb_index_get_stat(const vdb_index* ix, const char* name, int64_t* value
     if (n == "searches") *value = ix->n_searches.load();
     else if (n == "queries") *value = ix->n_queries.load();
     else if (n == "fallback_queries") *value = ix->n_fallback.load();
+    else if (n == "overflow_queries") *value = ix->n_overflow.load();
     else if (n == "capacity") *value = ix->cap_rows;
     else if (n == "scan_ns") *value = ix->scan_ns.load();
     else if (n == "pipeline_ns") *value = ix->pipe_ns.load();
@@ -531,14 +532,20 @@ int32_t vdb_index_search(vdb_index* ix, const float* queries, int32_t B, int32_t
     ix->n_queries += B;
 
     // ---- sizes ----------------------------------------------------------------
-    const int margin = ix->margin >= 0 ? (int)ix->margin : std::max(16, k / 4);
+    // candidates beyond k: the certificate needs a gap of 2 eps between the k-th and the
+    // KP-th approximate score; bf16x3's bound grows with D (3D additions), so large D
+    // gets a wider margin (1M x 1536 uniform: KP = 32 left ~1.5% of queries uncertified)
+    const int prec_req = ix->Xs && ix->precision == VDB_PREC_BF16X3 ? PREC_BF16X3 : PREC_FP32;
+    int margin_def = std::max(16, k / 4);
+    if (prec_req == PREC_BF16X3 && D >= 1024) margin_def = std::max(margin_def, 48);
+    const int margin = ix->margin >= 0 ? (int)ix->margin : margin_def;
     int KP = std::max(32, next_pow2(k + margin));
     const bool exact_all = ix->force_exact || k > kMaxApproxK || KP > 256;
     if (KP > 256) KP = 256;
     const int QB = KP == 256 ? 32 : 64;
     const int Bp = (int)round_up(B, 128);  // whole query super tiles (tiled layout)
     const int n_qblocks = (B + QB - 1) / QB;
-    const int prec = ix->Xs && ix->precision == VDB_PREC_BF16X3 ? PREC_BF16X3 : PREC_FP32;
+    const int prec = prec_req;
     const int Gs = prec == PREC_FP32 ? ix->G : ix->G / 2;  // scan groups (8 or 16 dims)
     int variant = (int)(prec == PREC_FP32 ? ix->scan_variant : ix->scan_variant_b3);
     if (!scan_variant_ok(prec, variant, Gs)) variant = 0;  // e.g. PX=8 needs Dp % 128 == 0
@@ -571,7 +578,7 @@ int32_t vdb_index_search(vdb_index* ix, const float* queries, int32_t B, int32_t
     const bool priv = !exact_all && scan_priv(prec, variant, KP);
     // global per-query candidate lists: at most 512 entries per workgroup and query
     // (the largest LDS buffer of any variant; 4 x 64 for the wave-private one)
-    const int64_t gl_cap = exact_all ? 0 : (int64_t)n_wg * 512;
+    const int64_t gl_cap = exact_all ? 0 : (int64_t)((n_wg + 7) / 8 * 8) * 512;
     bytes += (size_t)B * gl_cap * 8 + (size_t)Bp * 4 + 768;
     const int n_pilot = (int)std::min<int64_t>(ix->pilot_tiles, round_up(N, 32) / 32);
     int rc = ws_reserve(w, bytes, st);
@@ -653,12 +660,14 @@ int32_t vdb_index_search(vdb_index* ix, const float* queries, int32_t B, int32_t
                                        8.0 * std::ldexp(1.0, -24));
             fa.xmax = ix->xmax;
             fa.out_s = out_s; fa.out_i = out_i; fa.out_k = out_k; fa.index_offset = index_offset;
-            fa.flag_count = flags; fa.flag_list = flags + 1; fa.gthr = gthr;
+            fa.flag_count = flags; fa.flag_list = flags + 1; fa.gthr = gthr; fa.overflow_count = flags + B + 1;
             HIP_TRY(launch_finish(ix->metric, KP, fa, B, st));
             if (timed) HIP_TRY(hipEventRecord(w->tev[2], st));
             HIP_TRY(hipMemcpyAsync(w->host_flag, flags, sizeof(int), hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipMemcpyAsync(w->host_flag + 1, flags + B + 1, sizeof(int), hipMemcpyDeviceToHost, st));
             HIP_TRY(hipStreamSynchronize(st));
             n_flag = w->host_flag[0];
+            ix->n_overflow += w->host_flag[1];
             if (timed) {
                 float ms_scan = 0.f, ms_pipe = 0.f;
                 HIP_TRY(hipEventElapsedTime(&ms_scan, w->tev[0], w->tev[1]));

@@ -150,8 +150,18 @@ hipError_t launch_rerank(int metric, int KP, const RerankArgs& a, int B, hipStre
 // loads of a batch are in flight together; ranks come from counting (no sort);
 // thread 0 checks the certificate.  A list longer than FIN_CAP goes to the exact
 // scan.
-constexpr int FIN_CAP = 4096;
-constexpr int FIN_NB = 8;
+constexpr int FIN_CAP = 16384;  // 128 KiB of (key, row) in LDS
+constexpr int FIN_NB = 2;        // candidates per wave per batch
+constexpr int FIN_WAVES = 16;
+constexpr int FIN_REG = 512;     // lists up to this length are selected from registers
+
+#ifdef VDB_STAMP
+// Diagnostic build only: per-query phase timestamps of finish_kernel + list length.
+__device__ unsigned long long g_fin_stamps[8192][8];
+#define FIN_STAMP(i) do { if (threadIdx.x == 0) g_fin_stamps[blockIdx.x][i] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define FIN_STAMP(i) do { } while (0)
+#endif
 
 template <int METRIC, int NB>
 __device__ __forceinline__ void exact_keys_batch(const float* __restrict__ q, double qn, const float* __restrict__ X,
@@ -197,7 +207,7 @@ __device__ __forceinline__ void exact_keys_batch(const float* __restrict__ q, do
 }
 
 template <int METRIC, int KP>
-__global__ void __launch_bounds__(256) finish_kernel(FinishArgs a) {
+__global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
     __shared__ uint32_t s_key[FIN_CAP];
     __shared__ uint32_t s_row[FIN_CAP];
     __shared__ uint32_t s_ck[KP];
@@ -209,17 +219,22 @@ __global__ void __launch_bounds__(256) finish_kernel(FinishArgs a) {
     const int lane = tid & 63;
     const int wv = tid >> 6;
     const int b = blockIdx.x;
+    FIN_STAMP(0);
     const int64_t c = min((int64_t)a.gl_cnt[b], a.gl_cap);
+#ifdef VDB_STAMP
+    if (threadIdx.x == 0) g_fin_stamps[b][7] = (unsigned long long)c;
+#endif
     if (c > FIN_CAP) {
         if (tid == 0) {
             const int pos = atomicAdd(a.flag_count, 1);
             a.flag_list[pos] = b;
+            if (a.overflow_count) atomicAdd(a.overflow_count, 1);
         }
         return;
     }
     const float* ls = a.gl_s + (size_t)b * a.gl_cap;
     const uint32_t* li = a.gl_i + (size_t)b * a.gl_cap;
-    for (int e = tid; e < c; e += 256) {
+    for (int e = tid; e < c; e += 64 * FIN_WAVES) {
         s_key[e] = order_key(ls[e]);
         s_row[e] = li[e];
     }
@@ -228,23 +243,73 @@ __global__ void __launch_bounds__(256) finish_kernel(FinishArgs a) {
         s_akp = 0;
     }
     __syncthreads();
+    FIN_STAMP(1);
     const int n = (int)c;
+    // long lists: all waves count for each bisection round (LDS counter per round)
+    __shared__ int s_cnt2[2];
+    __shared__ uint32_t s_T, s_I;
+    if (n > FIN_REG) {
+        auto count_all = [&](auto pred, int parity) -> int {
+            int cnt = 0;
+            for (int e0 = wv * 64; e0 < n; e0 += 64 * FIN_WAVES) {
+                const int e = e0 + lane;
+                cnt += __popcll(__ballot(e < n && pred(e)));
+            }
+            if (lane == 0 && cnt) atomicAdd(&s_cnt2[parity], cnt);
+            __syncthreads();
+            const int total = s_cnt2[parity];
+            __syncthreads();
+            if (tid == 0) s_cnt2[parity] = 0;
+            return total;
+        };
+        if (tid == 0) s_cnt2[0] = s_cnt2[1] = 0;
+        __syncthreads();
+        uint32_t T = 0;
+        for (int bit = 31; bit >= 0; --bit) {
+            const uint32_t cand = T | (1u << bit);
+            if (count_all([&](int e) { return s_key[e] >= cand; }, bit & 1) >= KP) T = cand;
+        }
+        const int gt = count_all([&](int e) { return s_key[e] > T; }, 0);
+        const int eq = count_all([&](int e) { return s_key[e] == T; }, 1);
+        const int need = KP - gt;
+        uint32_t I = 0xFFFFFFFFu;
+        if (eq > need) {
+            I = 0;
+            for (int bit = 31; bit >= 0; --bit) {
+                const uint32_t cand = I | (1u << bit);
+                if (count_all([&](int e) { return s_key[e] == T && s_row[e] < cand; }, bit & 1) < need) I = cand;
+            }
+        }
+        if (tid == 0) {
+            s_T = T;
+            s_I = I;
+        }
+        __syncthreads();
+    }
     if (wv == 0) {
         int m = n < KP ? n : KP;
-        uint32_t T = 0, I = 0xFFFFFFFFu;
-        if (n > KP) {
+        uint32_t T = n > FIN_REG ? s_T : 0u, I = n > FIN_REG ? s_I : 0xFFFFFFFFu;
+        if (n > KP && n <= FIN_REG) {
+            constexpr int E = FIN_REG / 64;
+            uint32_t kv[E], rv[E];
+#pragma unroll
+            for (int i = 0; i < E; ++i) {
+                const int e = i * 64 + lane;
+                kv[i] = e < n ? s_key[e] : 0u;  // 0 = below every real key (order keys of finite floats are > 0)
+                rv[i] = e < n ? s_row[e] : 0xFFFFFFFFu;
+            }
             for (int bit = 31; bit >= 0; --bit) {
                 const uint32_t cand = T | (1u << bit);
                 int ge = 0;
-                for (int e0 = 0; e0 < n; e0 += 64) ge += __popcll(__ballot(e0 + lane < n && s_key[e0 + lane] >= cand));
+#pragma unroll
+                for (int i = 0; i < E; ++i) ge += __popcll(__ballot(kv[i] >= cand));
                 if (ge >= KP) T = cand;
             }
             int gt = 0, eq = 0;
-            for (int e0 = 0; e0 < n; e0 += 64) {
-                const bool in = e0 + lane < n;
-                const uint32_t kk = in ? s_key[e0 + lane] : 0u;
-                gt += __popcll(__ballot(in && kk > T));
-                eq += __popcll(__ballot(in && kk == T));
+#pragma unroll
+            for (int i = 0; i < E; ++i) {
+                gt += __popcll(__ballot(kv[i] > T));
+                eq += __popcll(__ballot(kv[i] == T && rv[i] != 0xFFFFFFFFu));
             }
             const int need = KP - gt;
             if (eq > need) {
@@ -252,10 +317,8 @@ __global__ void __launch_bounds__(256) finish_kernel(FinishArgs a) {
                 for (int bit = 31; bit >= 0; --bit) {
                     const uint32_t cand = I | (1u << bit);
                     int lt = 0;
-                    for (int e0 = 0; e0 < n; e0 += 64) {
-                        const bool in = e0 + lane < n;
-                        lt += __popcll(__ballot(in && s_key[e0 + lane] == T && s_row[e0 + lane] < cand));
-                    }
+#pragma unroll
+                    for (int i = 0; i < E; ++i) lt += __popcll(__ballot(kv[i] == T && rv[i] < cand));
                     if (lt < need) I = cand;
                 }
             }
@@ -278,11 +341,12 @@ __global__ void __launch_bounds__(256) finish_kernel(FinishArgs a) {
         if (lane == 0) s_m = m;
     }
     __syncthreads();
+    FIN_STAMP(2);
     const int m = s_m;
     const float* q = a.Q + (int64_t)b * a.D;
     const double qn = a.qn64[b];
-    // exact keys: wave wv takes candidates wv, wv + 4, ... in batches of FIN_NB
-    for (int j0 = wv * FIN_NB; j0 < m; j0 += 4 * FIN_NB) {
+    // exact keys: wave wv takes candidates wv FIN_NB, ... in batches of FIN_NB
+    for (int j0 = wv * FIN_NB; j0 < m; j0 += FIN_WAVES * FIN_NB) {
         uint32_t rows[FIN_NB];
         double xn[FIN_NB];
         const int nb = min(FIN_NB, m - j0);
@@ -300,8 +364,9 @@ __global__ void __launch_bounds__(256) finish_kernel(FinishArgs a) {
         }
     }
     __syncthreads();
+    FIN_STAMP(3);
     // ranks by counting: exact (output order) and approx (certificate)
-    for (int j = tid; j < KP; j += 256) {
+    for (int j = tid; j < KP; j += 64 * FIN_WAVES) {
         if (j < m) {
             const double ek = s_ek[j];
             const uint32_t ck = s_ck[j], r = s_cr[j];
@@ -324,11 +389,12 @@ __global__ void __launch_bounds__(256) finish_kernel(FinishArgs a) {
             write_result(METRIC, -INFINITY, 0, false, a.out_s + o, a.out_i + o, a.out_k ? a.out_k + o : nullptr);
         }
     }
-    for (int j = KP + tid; j < a.k; j += 256) {  // k > KP cannot happen on this path; defensive
+    for (int j = KP + tid; j < a.k; j += 64 * FIN_WAVES) {  // k > KP cannot happen on this path; defensive
         const size_t o = (size_t)b * a.k + j;
         write_result(METRIC, -INFINITY, 0, false, a.out_s + o, a.out_i + o, a.out_k ? a.out_k + o : nullptr);
     }
     __syncthreads();
+    FIN_STAMP(4);
     if (tid == 0) {
         // Rows outside the candidates scored (approx) <= max(a_KP, T).
         const bool full = m == KP;
@@ -352,12 +418,13 @@ __global__ void __launch_bounds__(256) finish_kernel(FinishArgs a) {
             a.flag_list[pos] = b;
         }
     }
+    FIN_STAMP(5);
 }
 
 hipError_t launch_finish(int metric, int KP, const FinishArgs& a, int B, hipStream_t st) {
 #define VDB_FIN(M, KPV)                                                                         \
     if (metric == M && KP == KPV) {                                                             \
-        hipLaunchKernelGGL((finish_kernel<M, KPV>), dim3(B), dim3(256), 0, st, a);              \
+        hipLaunchKernelGGL((finish_kernel<M, KPV>), dim3(B), dim3(64 * FIN_WAVES), 0, st, a);   \
         return hipGetLastError();                                                               \
     }
     VDB_FIN(0, 32) VDB_FIN(0, 64) VDB_FIN(0, 128) VDB_FIN(0, 256)
@@ -430,3 +497,9 @@ hipError_t launch_exact_scan(int metric, int KE, const float* Q, const double* q
 }
 
 }  // namespace vdb
+
+#ifdef VDB_STAMP
+extern "C" int vdb_debug_finish_stamps(unsigned long long* out, int n) {
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(vdb::g_fin_stamps), (size_t)n * 8 * sizeof(unsigned long long));
+}
+#endif

@@ -117,7 +117,10 @@ __global__ void __launch_bounds__(256) prep_queries_kernel(const float* __restri
                                                            uint32_t* __restrict__ gslots, uint32_t* __restrict__ gl_cnt) {
     const int lane = threadIdx.x & 63;
     const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (b == 0 && lane == 0 && flag_count) *flag_count = 0;
+    if (b == 0 && lane == 0 && flag_count) {
+        flag_count[0] = 0;      // certificate failures (list follows)
+        flag_count[B + 1] = 0;  // of which: candidate-list overflows
+    }
     if (b >= Bp) return;
     if (lane == 0 && gthr) gthr[b] = 0u;
     if (lane == 0 && gl_cnt) gl_cnt[b] = 0u;

@@ -98,6 +98,7 @@ struct FinishArgs {
     int k; double eps_rel; double xmax;
     float* out_s; int64_t* out_i; double* out_k; int64_t index_offset;
     int* flag_count; int* flag_list; const uint32_t* gthr;
+    int* overflow_count;  // lists longer than the finish kernel holds (they take the exact path)
 };
 hipError_t launch_finish(int metric, int KP, const FinishArgs& a, int B, hipStream_t st);
 

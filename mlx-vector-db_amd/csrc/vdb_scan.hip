@@ -116,6 +116,56 @@ __device__ __forceinline__ void compact_query(float* sc, uint32_t* ix, int* cnt,
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
+// Epilogue scoring of one step: scores replace the accumulators (cosine a * inv|x|,
+// L2 2a - |x|^2) and pend[rt][qt] gets the bits of the scores above the query's
+// threshold.  The common case costs ~1.5 VALU per score: scale + max3, then one
+// compare per tile; the per-score bits (and the row mask / N checks) are built
+// only for tiles where some lane of the wave passes.
+template <int METRIC, int RT, int QT>
+__device__ __forceinline__ void score_tiles(f32x16 (&acc)[RT][QT], const f32x4 (&rs4)[RT][4], const float (&thr)[QT],
+                                            const uint32_t (&mword)[RT], const bool (&qok)[QT], int64_t t0, int64_t N,
+                                            uint32_t (&pend)[RT][QT]) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) {
+            float mx = -INFINITY;
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+                const float a = acc[rt][qt][v];
+                const float rs = rs4[rt][v >> 2][v & 3];
+                const float sc = METRIC == 0 ? a * rs : fmaf(2.0f, a, -rs);
+                acc[rt][qt][v] = sc;
+                mx = fmaxf(mx, sc);
+            }
+            pend[rt][qt] = 0u;
+            if (__any(qok[qt] && mx > thr[qt])) {
+                const int64_t t = t0 + rt;
+                uint32_t pm = 0;
+#pragma unroll
+                for (int v = 0; v < 16; ++v) {
+                    const int ro = (v & 3) + 8 * (v >> 2) + 4 * (lane >> 5);
+                    const bool ok = ((mword[rt] >> ro) & 1u) && (t * 32 + ro < N);
+                    pm |= (ok && acc[rt][qt][v] > thr[qt]) ? (1u << v) : 0u;
+                }
+                pend[rt][qt] = qok[qt] ? pm : 0u;
+            }
+        }
+    }
+}
+
+// 1-D grid of round_up(n_wg, 8) * n_qb workgroups -> (row range wg, query block qb):
+// block L sits on XCD L % 8; ranges wg = 8 (j / n_qb) + L % 8 with j = L / 8, so the
+// n_qb blocks of a range share an XCD and consecutive dispatch slots.  Ranges past
+// n_wg get no steps (s_begin >= n_steps) and only flush nothing.
+__device__ __forceinline__ void xcd_map(int n_qb, int& wg, int& qb) {
+    const int L = blockIdx.x;
+    const int j = L >> 3;
+    qb = j % n_qb;
+    wg = (j / n_qb) * 8 + (L & 7);
+}
+
 // Flush of one wave's queries q(i) = q0 + qstep i (i < nq <= 64): the entries of LDS
 // buffer q (CAPX slots, cnt[q] used) scoring above that query's bound T (order key in
 // lane i's `tkey`) are appended to the global list of query qb0 + q.  One returning
@@ -198,8 +248,9 @@ template <int PREC, int METRIC, int QT, int RT, int PX, int PQ, int KP, int CAP,
 __global__ void __launch_bounds__(256, WPS)
 scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale, const uint32_t* __restrict__ mask,
                  const float* __restrict__ Qt, int G, int64_t N, int B, int64_t n_steps, int steps_per_wg,
-                 float* __restrict__ gl_s, uint32_t* __restrict__ gl_i, uint32_t* __restrict__ gl_cnt, int64_t gl_cap,
-                 uint32_t* __restrict__ gthr, uint32_t* __restrict__ gslots) {
+                 int n_qb, int n_wg_all, float* __restrict__ gl_s, uint32_t* __restrict__ gl_i,
+                 uint32_t* __restrict__ gl_cnt, int64_t gl_cap, uint32_t* __restrict__ gthr,
+                 uint32_t* __restrict__ gslots) {
     static_assert(PX % PQ == 0, "query prefetch depth must divide the corpus prefetch depth");
     static_assert(PQ <= QG_EXTRA, "query prefetch deeper than the duplicated groups");
     constexpr int QB = 32 * QT;
@@ -207,23 +258,30 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
     __shared__ uint32_t s_ix[QB * CAP];
     __shared__ int s_cnt[QB];
     __shared__ float s_thr[QB];
-    __shared__ uint32_t s_best[QB];  // order key of the best score appended so far (PUB)
-    __shared__ uint32_t s_pub[QB];   // ... and of the last one published
+    __shared__ uint32_t s_best[4][QB];  // per wave: order key of the best score appended so far (PUB)
+    __shared__ uint32_t s_pub[4][QB];   // ... and of the last one published
     __shared__ uint32_t s_sh[QB];    // shared bound from the slots (order key), this WG's view
 
     const int lane = threadIdx.x & 63;
     // wave index made provably uniform: every tile/group address below is then
     // scalar (SGPR base) + lane*16 (one VGPR), keeping VGPRs for the pipeline.
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int n_wg = gridDim.x;
-    const int wg = blockIdx.x;
-    const int qb = blockIdx.y;
+    // XCD-aware placement (1-D grid): workgroups are dealt round-robin over the 8
+    // XCDs, so the n_qb query blocks of one row range get block ids with the same
+    // residue mod 8 and adjacent dispatch slots: they stream the same corpus rows
+    // together through one XCD's L2 instead of each pulling them from HBM.
+    int wg, qb;
+    xcd_map(n_qb, wg, qb);
+    const int n_wg = n_wg_all;
     const int lane4 = lane * 4;
 
     for (int i = threadIdx.x; i < QB; i += 256) {
         s_cnt[i] = 0;
-        s_best[i] = 0;
-        s_pub[i] = 0;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            s_best[w][i] = 0;
+            s_pub[w][i] = 0;
+        }
         s_sh[i] = 0;
         s_thr[i] = -INFINITY;
     }
@@ -274,6 +332,26 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
                 for (int pl = 0; pl < NPL; ++pl)
                     qr[p][qt][pl] = *(const f32x4*)(Qbase + p * GSTEP + pl * PLANE + qt * BLOCK_FLOATS + lane4);
     }
+    // epilogue inputs of step s (see the step loop)
+    auto load_epi = [&](int64_t st_, uint32_t (&g_)[QT], f32x4 (&r_)[RT][4], uint32_t (&m_)[RT]) {
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) {
+            const int qg = qb * QB + qt * 32 + (lane & 31);
+            g_[qt] = qg < B ? gthr[qg] : 0u;
+        }
+        const int64_t tt = (st_ * 4 + wv) * RT;
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+            const float* rsp = rowscale + (tt + rt) * 32 + 4 * (lane >> 5);
+#pragma unroll
+            for (int m = 0; m < 4; ++m) r_[rt][m] = *(const f32x4*)(rsp + 8 * m);
+            m_[rt] = mask ? mask[tt + rt] : 0xFFFFFFFFu;
+        }
+    };
+    uint32_t gkn[QT];
+    f32x4 rsn[RT][4];
+    uint32_t mwn[RT];
+    if (s_begin < s_end) load_epi(s_begin, gkn, rsn, mwn);
 #ifdef VDB_STAMP
     unsigned long long st_k = 0, st_e = 0, st_e0 = 0, st_t0 = STAMP_NOW();
     unsigned long long st_bar = 0, st_sc = 0, st_ins = 0, st_rt = 0, st_rounds = 0, st_compacts = 0;
@@ -320,27 +398,24 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
             for (int p = 0; p < PX; ++p)
                 group(p, xs + (size_t)(gb + p + PX) * GSTEP, Qbase + (size_t)(gb + p + PQ) * GSTEP);
         }
-        // Loads whose values the epilogue needs are issued before the last PX groups
-        // (and before the next step's prefetch), so waiting for them never drains
-        // the corpus stream: the shared thresholds (any value read, however stale,
-        // even an L1 copy, is a valid lower bound), the row scales of this wave's
-        // rows (lane l needs rows (v & 3) + 8 (v >> 2) + 4 (l >> 5) of each tile)
-        // and the tile masks.
+        // The epilogue's global inputs (shared thresholds -- any value read, however
+        // stale, even an L1 copy, is a valid lower bound --, the row scales of this
+        // wave's rows: lane l needs rows (v & 3) + 8 (v >> 2) + 4 (l >> 5) of each
+        // tile, and the tile masks) are loaded one step ahead, before the last PX
+        // groups: waiting for them never drains the corpus stream, and their latency
+        // is covered even when a step is only a few groups long (small D).
         uint32_t gk[QT];
-#pragma unroll
-        for (int qt = 0; qt < QT; ++qt) {
-            const int qg = qb * QB + qt * 32 + (lane & 31);
-            gk[qt] = qg < B ? gthr[qg] : 0u;
-        }
         f32x4 rs4[RT][4];
         uint32_t mword[RT];
 #pragma unroll
-        for (int rt = 0; rt < RT; ++rt) {
-            const float* rsp = rowscale + (t0 + rt) * 32 + 4 * (lane >> 5);
+        for (int qt = 0; qt < QT; ++qt) gk[qt] = gkn[qt];
 #pragma unroll
-            for (int m = 0; m < 4; ++m) rs4[rt][m] = *(const f32x4*)(rsp + 8 * m);
-            mword[rt] = mask ? mask[t0 + rt] : 0xFFFFFFFFu;
+        for (int rt = 0; rt < RT; ++rt) {
+            mword[rt] = mwn[rt];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) rs4[rt][m] = rsn[rt][m];
         }
+        if (s + 1 < s_end) load_epi(s + 1, gkn, rsn, mwn);
 #pragma unroll
         for (int p = 0; p < PX; ++p) group(p, xn + (size_t)p * GSTEP, Qbase + (size_t)(gb + p + PQ) * GSTEP);
 #ifdef VDB_STAMP
@@ -356,35 +431,21 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
         // costs ~2 VALU per score.  A full buffer leaves a score pending, to be
         // re-tested after the buffer is compacted (retry loop below).
         uint32_t pend[RT][QT];
-#pragma unroll
-        for (int rt = 0; rt < RT; ++rt) {
-            const int64_t t = t0 + rt;
-            uint32_t okbits = 0;
-#pragma unroll
-            for (int v = 0; v < 16; ++v) {
-                const int ro = (v & 3) + 8 * (v >> 2) + 4 * (lane >> 5);
-                okbits |= (((mword[rt] >> ro) & 1u) && (t * 32 + ro < N)) ? (1u << v) : 0u;
-            }
+        {
+            float thr[QT];
+            bool qok[QT];
 #pragma unroll
             for (int qt = 0; qt < QT; ++qt) {
                 const int ql = qt * 32 + (lane & 31);
-                float thr = fmaxf(s_thr[ql], key_to_float(PUB ? max(gk[qt], s_sh[ql]) : gk[qt]));
+                thr[qt] = fmaxf(s_thr[ql], key_to_float(PUB ? max(gk[qt], s_sh[ql]) : gk[qt]));
 #ifdef VDB_STAMP
                 // diagnostic bounds (stamp build only, wrong results): PUB 2 = no insertion
                 // after the first step, PUB 3 = no insertion at all
-                if ((PUB == 2 && s > s_begin) || PUB == 3) thr = INFINITY;
+                if ((PUB == 2 && s > s_begin) || PUB == 3) thr[qt] = INFINITY;
 #endif
-                uint32_t pm = 0;
-#pragma unroll
-                for (int v = 0; v < 16; ++v) {
-                    const float a = acc[rt][qt][v];
-                    const float rs = rs4[rt][v >> 2][v & 3];
-                    const float sc = METRIC == 0 ? a * rs : fmaf(2.0f, a, -rs);
-                    acc[rt][qt][v] = sc;
-                    pm |= sc > thr ? (1u << v) : 0u;
-                }
-                pend[rt][qt] = (qb * QB + ql < B) ? (pm & okbits) : 0u;
+                qok[qt] = qb * QB + ql < B;
             }
+            score_tiles<METRIC, RT, QT>(acc, rs4, thr, mword, qok, t0, N, pend);
         }
 #ifdef VDB_STAMP
         const unsigned long long st_b3 = STAMP_NOW();
@@ -401,7 +462,7 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
                 float mx = -INFINITY;
 #pragma unroll
                 for (int v = 0; v < 16; ++v) mx = ((pm >> v) & 1u) ? fmaxf(mx, acc[rt][qt][v]) : mx;
-                if (pm) atomicMax(&s_best[ql], order_key(mx));
+                if (pm) atomicMax(&s_best[wv][ql], order_key(mx));
             }
             uint32_t left = 0;
 #pragma unroll
@@ -465,10 +526,11 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
         st_pub_start = st_b5;
 #endif
         if constexpr (PUB) {
-            // ---- publish: slot (query, wg % KP) of gslots holds the max over a fixed set
-            // of workgroups of their best score, so the KP slots of a query are scores of
-            // KP distinct rows and their minimum is a lower bound of the global KP-th best
-            // (DESIGN.md §3.1).  A group of LPQ lanes serves one query: its leader
+            // ---- publish: slot (query, (4 wg + w) % KP) of gslots holds the max over a
+            // fixed set of waves (disjoint rows) of their best score, so the KP slots of a
+            // query are scores of KP distinct rows and their minimum is a lower bound of
+            // the global KP-th best; 4 slots per workgroup so that KP
+            // slots fill even when there are fewer than KP workgroups.  A group of LPQ lanes serves one query: its leader
             // publishes (no-return atomic), all of them load SL slots each.  The slot
             // loads are consumed one step later (min over the group's lanes -> gthr and
             // s_sh): by then the next step's corpus loads, which are younger, have been
@@ -487,16 +549,17 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
             }
             const int64_t sd = s - s_begin + 1;
             if ((sd & (sd - 1)) == 0 || s + 1 == s_end) {
-                bool improved = false;
-                if (pq_r == 0 && pqg < B) {
-                    const uint32_t best = s_best[pq];
-                    improved = best > s_pub[pq];
+                int improved = 0;
+                if (pq_r < 4 && pqg < B) {  // lane r of the group publishes wave r's best
+                    const uint32_t best = s_best[pq_r][pq];
+                    improved = best > s_pub[pq_r][pq];
                     if (improved) {
-                        s_pub[pq] = best;
-                        atomicMax(gslots + (size_t)pqg * KP_MAX + (wg % KP), best);
+                        s_pub[pq_r][pq] = best;
+                        atomicMax(gslots + (size_t)pqg * KP_MAX + ((wg * 4 + pq_r) % KP), best);
                     }
                 }
-                improved = __shfl((int)improved, lane - pq_r, 64) != 0;
+#pragma unroll
+                for (int off = 1; off < LPQ; off <<= 1) improved |= __shfl_xor(improved, off, 64);
                 if (improved) {
                     const uint32_t* sl = gslots + (size_t)pqg * KP_MAX + pq_r * SL;
 #pragma unroll
@@ -562,7 +625,8 @@ template <int PREC, int METRIC, int QT, int RT, int PX, int PQ, int KP, int CAPW
 __global__ void __launch_bounds__(256, 1)
 scan_topk_priv_kernel(const float* __restrict__ X, const float* __restrict__ rowscale,
                       const uint32_t* __restrict__ mask, const float* __restrict__ Qt, int G, int64_t N, int B,
-                      int64_t n_steps, int steps_per_wg, float* __restrict__ gl_s, uint32_t* __restrict__ gl_i,
+                      int64_t n_steps, int steps_per_wg, int n_qb, int n_wg_all, float* __restrict__ gl_s,
+                      uint32_t* __restrict__ gl_i,
                       uint32_t* __restrict__ gl_cnt, int64_t gl_cap, uint32_t* __restrict__ gthr,
                       uint32_t* __restrict__ gslots) {
     static_assert(PX % PQ == 0, "query prefetch depth must divide the corpus prefetch depth");
@@ -578,8 +642,9 @@ scan_topk_priv_kernel(const float* __restrict__ X, const float* __restrict__ row
 
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int wg = blockIdx.x;
-    const int qb = blockIdx.y;
+    int wg, qb;
+    xcd_map(n_qb, wg, qb);
+    (void)n_wg_all;
     const int lane4 = lane * 4;
     float* bs = s_sc[wv];
     uint32_t* bi = s_ix[wv];
@@ -630,6 +695,26 @@ scan_topk_priv_kernel(const float* __restrict__ X, const float* __restrict__ row
                 for (int pl = 0; pl < NPL; ++pl)
                     qr[p][qt][pl] = *(const f32x4*)(Qbase + p * GSTEP + pl * PLANE + qt * BLOCK_FLOATS + lane4);
     }
+    // epilogue inputs of step s (see the step loop)
+    auto load_epi = [&](int64_t st_, uint32_t (&g_)[QT], f32x4 (&r_)[RT][4], uint32_t (&m_)[RT]) {
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) {
+            const int qg = qb * QB + qt * 32 + (lane & 31);
+            g_[qt] = qg < B ? gthr[qg] : 0u;
+        }
+        const int64_t tt = (st_ * 4 + wv) * RT;
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+            const float* rsp = rowscale + (tt + rt) * 32 + 4 * (lane >> 5);
+#pragma unroll
+            for (int m = 0; m < 4; ++m) r_[rt][m] = *(const f32x4*)(rsp + 8 * m);
+            m_[rt] = mask ? mask[tt + rt] : 0xFFFFFFFFu;
+        }
+    };
+    uint32_t gkn[QT];
+    f32x4 rsn[RT][4];
+    uint32_t mwn[RT];
+    if (s_begin < s_end) load_epi(s_begin, gkn, rsn, mwn);
     uint32_t gk[QT];
 #pragma unroll
     for (int qt = 0; qt < QT; ++qt) gk[qt] = 0;
@@ -667,50 +752,34 @@ scan_topk_priv_kernel(const float* __restrict__ X, const float* __restrict__ row
             for (int p = 0; p < PX; ++p)
                 group(p, xs + (size_t)(gb + p + PX) * GSTEP, Qbase + (size_t)(gb + p + PQ) * GSTEP);
         }
-        // epilogue inputs, issued before the next step's prefetch (see scan_topk_kernel)
-#pragma unroll
-        for (int qt = 0; qt < QT; ++qt) {
-            const int qg = qb * QB + qt * 32 + (lane & 31);
-            gk[qt] = qg < B ? gthr[qg] : 0u;
-        }
+        // epilogue inputs: this step's (loaded a step ahead), then the next step's
+        // (see scan_topk_kernel)
         f32x4 rs4[RT][4];
         uint32_t mword[RT];
 #pragma unroll
-        for (int rt = 0; rt < RT; ++rt) {
-            const float* rsp = rowscale + (t0 + rt) * 32 + 4 * (lane >> 5);
+        for (int qt = 0; qt < QT; ++qt) gk[qt] = gkn[qt];
 #pragma unroll
-            for (int m = 0; m < 4; ++m) rs4[rt][m] = *(const f32x4*)(rsp + 8 * m);
-            mword[rt] = mask ? mask[t0 + rt] : 0xFFFFFFFFu;
+        for (int rt = 0; rt < RT; ++rt) {
+            mword[rt] = mwn[rt];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) rs4[rt][m] = rsn[rt][m];
         }
+        if (s + 1 < s_end) load_epi(s + 1, gkn, rsn, mwn);
 #pragma unroll
         for (int p = 0; p < PX; ++p) group(p, xn + (size_t)p * GSTEP, Qbase + (size_t)(gb + p + PQ) * GSTEP);
 
         // ---- epilogue (wave-local) ----------------------------------------------
         uint32_t pend[RT][QT];
-#pragma unroll
-        for (int rt = 0; rt < RT; ++rt) {
-            const int64_t t = t0 + rt;
-            uint32_t okbits = 0;
-#pragma unroll
-            for (int v = 0; v < 16; ++v) {
-                const int ro = (v & 3) + 8 * (v >> 2) + 4 * (lane >> 5);
-                okbits |= (((mword[rt] >> ro) & 1u) && (t * 32 + ro < N)) ? (1u << v) : 0u;
-            }
+        {
+            float thr[QT];
+            bool qok[QT];
 #pragma unroll
             for (int qt = 0; qt < QT; ++qt) {
                 const int ql = qt * 32 + (lane & 31);
-                const float thr = fmaxf(bt[ql], key_to_float(max(gk[qt], s_sh[ql])));
-                uint32_t pm = 0;
-#pragma unroll
-                for (int v = 0; v < 16; ++v) {
-                    const float a = acc[rt][qt][v];
-                    const float rs = rs4[rt][v >> 2][v & 3];
-                    const float sc = METRIC == 0 ? a * rs : fmaf(2.0f, a, -rs);
-                    acc[rt][qt][v] = sc;
-                    pm |= sc > thr ? (1u << v) : 0u;
-                }
-                pend[rt][qt] = (qb * QB + ql < B) ? (pm & okbits) : 0u;
+                thr[qt] = fmaxf(bt[ql], key_to_float(max(gk[qt], s_sh[ql])));
+                qok[qt] = qb * QB + ql < B;
             }
+            score_tiles<METRIC, RT, QT>(acc, rs4, thr, mword, qok, t0, N, pend);
         }
         auto insert_tile = [&](int rt, int qt) -> uint32_t {
             const uint32_t pm = pend[rt][qt];
@@ -877,9 +946,10 @@ static hipError_t scan_priv_dispatch(const float* X, const float* rowscale, cons
                                      int G, int64_t N, int B, int n_qblocks, int64_t n_steps, int n_wg, int spw,
                                      float* gl_s, uint32_t* gl_i, uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr,
                                      uint32_t* gslots, hipStream_t st) {
-    hipLaunchKernelGGL((scan_topk_priv_kernel<PREC, METRIC, QT, RT, PX, PQ, KP, CAPW>), dim3(n_wg, n_qblocks),
-                       dim3(256), 0, st, X, rowscale, mask, Qt, G, N, B, n_steps, spw, gl_s, gl_i, gl_cnt, gl_cap,
-                       gthr, gslots);
+    const int n_wg8 = (n_wg + 7) / 8 * 8;
+    hipLaunchKernelGGL((scan_topk_priv_kernel<PREC, METRIC, QT, RT, PX, PQ, KP, CAPW>), dim3(n_wg8 * n_qblocks),
+                       dim3(256), 0, st, X, rowscale, mask, Qt, G, N, B, n_steps, spw, n_qblocks, n_wg8, gl_s, gl_i,
+                       gl_cnt, gl_cap, gthr, gslots);
     return hipGetLastError();
 }
 
@@ -1038,9 +1108,10 @@ static hipError_t scan_dispatch(const float* X, const float* rowscale, const uin
                                 int64_t N, int B, int n_qblocks, int64_t n_steps, int n_wg, int spw, float* gl_s,
                                 uint32_t* gl_i, uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr, uint32_t* gslots,
                                 hipStream_t st) {
-    hipLaunchKernelGGL((scan_topk_kernel<PREC, METRIC, QT, RT, PX, PQ, KP, CAP, PUB, WPS>), dim3(n_wg, n_qblocks),
-                       dim3(256), 0, st, X, rowscale, mask, Qt, G, N, B, n_steps, spw, gl_s, gl_i, gl_cnt, gl_cap,
-                       gthr, gslots);
+    const int n_wg8 = (n_wg + 7) / 8 * 8;
+    hipLaunchKernelGGL((scan_topk_kernel<PREC, METRIC, QT, RT, PX, PQ, KP, CAP, PUB, WPS>), dim3(n_wg8 * n_qblocks),
+                       dim3(256), 0, st, X, rowscale, mask, Qt, G, N, B, n_steps, spw, n_qblocks, n_wg8, gl_s, gl_i,
+                       gl_cnt, gl_cap, gthr, gslots);
     return hipGetLastError();
 }
 

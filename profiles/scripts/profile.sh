@@ -5,7 +5,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 TAG=$1; shift
-ARGS="--steps 20 --warmup 3 --no-cpu-baseline $*"
+ARGS="--steps ${STEPS:-20} --warmup 3 --no-cpu-baseline $*"
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python bench.py $ARGS > $OUT/trace_bench.json 2> $OUT/trace.err || { echo "trace failed"; tail -20 $OUT/trace.err; exit 1; }

@@ -30,3 +30,13 @@ print(f"{prec} variant {variant} nwg {nwg}: waves {len(a)}")
 for i, name in enumerate(["k-loop", "epilogue", "publish", "total", "barrier after k-loop", "scoring", "first insert pass", "retry loop (+barrier,-pub)"]):
     print(f"  {name:22s} mean {a[:, i].mean():12.0f}  max {a[:, i].max():12.0f}  (ticks)")
 print("  k-loop share", a[:, 0].sum() / a[:, 3].sum(), "epilogue share", a[:, 1].sum() / a[:, 3].sum())
+
+# finish_kernel phases (per query): list length, load, select, exact keys, ranks/write, certificate
+m = 64
+fb = (ctypes.c_ulonglong * (m * 8))()
+lib.vdb_debug_finish_stamps(fb, m)
+f = np.array(fb, dtype=np.uint64).reshape(m, 8).astype(np.float64)
+print("finish: list length mean %.0f max %.0f" % (f[:, 7].mean(), f[:, 7].max()))
+for i, name in enumerate(["load list", "select", "exact keys", "ranks+write", "certificate"]):
+    d = f[:, i + 1] - f[:, i]
+    print(f"  {name:14s} mean {d.mean():9.0f}  max {d.max():9.0f} ticks")
