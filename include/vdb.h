@@ -155,6 +155,32 @@ int32_t vdb_similarity_matrix(const float* corpus, int64_t n, int32_t dim,
                               const float* queries, int32_t n_queries, int32_t metric,
                               float* out, void* stream);
 
+/* --- graph index (the HNSW path) -------------------------------------------------
+ * Replaces ProductionHNSWIndex (performance/hnsw_index.py:23-129: hnswlib
+ * build / knn_query / save / load), re-laid out for the GPU: one
+ * level of out-degree `degree` (hnswlib's level-0 degree 2M) as a [N][degree]
+ * int32 neighbour array, built from the exact kNN of every row (the brute-force
+ * path above, `knn` neighbours) as the degree/2 nearest out-edges plus the nearest
+ * reverse edges; searches start from the best of `n_entries` spread rows.  The
+ * graph refers to the index's rows; adding rows makes it stale (search errors). */
+typedef struct vdb_graph vdb_graph;
+
+int32_t vdb_graph_build(vdb_index* idx, int32_t degree, int32_t knn, int32_t n_entries, vdb_graph** out);
+/* Persistence: a graph exported by vdb_graph_export (neighbours [n][degree], -1 =
+ * none; entry rows) re-attached to an index holding the same rows. */
+int32_t vdb_graph_import(vdb_index* idx, int32_t degree, int64_t n, const int32_t* nbr, int32_t n_entries,
+                         const int32_t* entries, vdb_graph** out);
+int32_t vdb_graph_export(const vdb_graph* g, int32_t* nbr_host, int32_t* entries_host);
+int32_t vdb_graph_info(const vdb_graph* g, int64_t* n_rows, int32_t* degree, int32_t* n_entries);
+/* hnswlib knn_query semantics (hnsw_index.py:98-101): labels [n_queries, k] int64
+ * (-1 = none), distances [n_queries, k] fp32: cosine 1 - cos, euclidean squared L2;
+ * best first.  ef = beam width (search depth), k <= ef <= 256. */
+int32_t vdb_graph_search(vdb_graph* g, const float* queries, int32_t n_queries, int32_t k, int32_t ef, int32_t mem,
+                         int64_t* labels, float* distances, void* stream);
+/* stats: "queries", "iterations" (beam iterations, summed over queries) */
+int32_t vdb_graph_stat(const vdb_graph* g, const char* name, int64_t* value);
+int32_t vdb_graph_destroy(vdb_graph* g);
+
 #ifdef __cplusplus
 }
 #endif

@@ -727,3 +727,261 @@ int32_t vdb_similarity_matrix(const float* corpus, int64_t n, int32_t dim, const
 }
 
 }  // extern "C"
+
+// =============================================================================
+// Graph index (HNSW replacement, performance/hnsw_index.py:23-129)
+// =============================================================================
+struct vdb_graph {
+    vdb_index* ix = nullptr;
+    int R = 0;
+    int64_t n = 0;
+    int n_entries = 0;
+    int32_t* nbr = nullptr;      // device [n][R]
+    int32_t* entries = nullptr;  // device [n_entries]
+    unsigned long long* d_stats = nullptr;
+    std::atomic<int64_t> n_queries{0};
+};
+
+namespace {
+
+int graph_upload(vdb_index* ix, int R, int64_t n, const int32_t* nbr_host, const int32_t* ent_host, int n_ent,
+                 vdb_graph** out) {
+    vdb_graph* g = new vdb_graph();
+    g->ix = ix;
+    g->R = R;
+    g->n = n;
+    g->n_entries = n_ent;
+    hipError_t e = hipMalloc(&g->nbr, (size_t)std::max<int64_t>(n, 1) * R * sizeof(int32_t));
+    if (e == hipSuccess) e = hipMalloc(&g->entries, (size_t)std::max(n_ent, 1) * sizeof(int32_t));
+    if (e == hipSuccess) e = hipMalloc(&g->d_stats, 64);
+    if (e == hipSuccess) e = hipMemset(g->d_stats, 0, 64);
+    if (e == hipSuccess && n > 0) e = hipMemcpy(g->nbr, nbr_host, (size_t)n * R * sizeof(int32_t), hipMemcpyHostToDevice);
+    if (e == hipSuccess && n_ent > 0)
+        e = hipMemcpy(g->entries, ent_host, (size_t)n_ent * sizeof(int32_t), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        (void)hipFree(g->nbr);
+        (void)hipFree(g->entries);
+        (void)hipFree(g->d_stats);
+        delete g;
+        return set_error(e == hipErrorOutOfMemory ? VDB_ERR_OOM : VDB_ERR_HIP, "graph upload failed: %s",
+                         hipGetErrorString(e));
+    }
+    *out = g;
+    return VDB_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t vdb_graph_build(vdb_index* ix, int32_t degree, int32_t knn, int32_t n_entries, vdb_graph** out) {
+    if (!ix || !out) return set_error(VDB_ERR_INVALID, "NULL argument");
+    *out = nullptr;
+    if (degree < 2 || degree > 64 || (degree & 1)) return set_error(VDB_ERR_INVALID, "degree must be even in [2, 64]");
+    if (knn < degree / 2 || knn > 200) return set_error(VDB_ERR_INVALID, "knn must be in [degree/2, 200]");
+    if (n_entries < 1 || n_entries > 256) return set_error(VDB_ERR_INVALID, "n_entries must be in [1, 256]");
+    HIP_TRY(hipSetDevice(ix->device));
+    const int64_t N = ix->count;
+    if (N > 0x7FFFFFFF) return set_error(VDB_ERR_INVALID, "graph rows are int32");
+    const int R = degree, F = degree / 2;
+    const int kk = (int)std::min<int64_t>(knn + 1, std::max<int64_t>(N, 1));  // + the row itself
+    const int D = ix->dim;
+    std::vector<int32_t> nbr((size_t)N * R, -1);
+    if (N > 1) {
+        // 1. exact kNN of every row (the brute-force path, rows as queries)
+        const int Bq = 512;
+        std::vector<int64_t> kid((size_t)N * kk);
+        std::vector<float> ksc((size_t)N * kk);
+        float* qbuf = nullptr;
+        float* dsc = nullptr;
+        int64_t* did = nullptr;
+        hipStream_t st = ix->stream;
+        hipError_t e = hipMalloc(&qbuf, (size_t)Bq * D * sizeof(float));
+        if (e == hipSuccess) e = hipMalloc(&dsc, (size_t)Bq * kk * sizeof(float));
+        if (e == hipSuccess) e = hipMalloc(&did, (size_t)Bq * kk * sizeof(int64_t));
+        int rc = e == hipSuccess ? VDB_OK : set_error(VDB_ERR_OOM, "graph build buffers: %s", hipGetErrorString(e));
+        for (int64_t r0 = 0; rc == VDB_OK && r0 < N; r0 += Bq) {
+            const int m = (int)std::min<int64_t>(Bq, N - r0);
+            {
+                std::shared_lock<std::shared_mutex> g(ix->mu);
+                e = launch_unpack_rows(ix->X, ix->G, D, r0, m, qbuf, st);
+            }
+            if (e != hipSuccess) {
+                rc = set_error(VDB_ERR_HIP, "graph build: %s", hipGetErrorString(e));
+                break;
+            }
+            rc = vdb_index_search(ix, qbuf, m, kk, nullptr, VDB_MEM_DEVICE, dsc, did, nullptr, 0, st);
+            if (rc) break;
+            e = hipMemcpyAsync(kid.data() + (size_t)r0 * kk, did, (size_t)m * kk * sizeof(int64_t),
+                               hipMemcpyDeviceToHost, st);
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(ksc.data() + (size_t)r0 * kk, dsc, (size_t)m * kk * sizeof(float),
+                                   hipMemcpyDeviceToHost, st);
+            if (e == hipSuccess) e = hipStreamSynchronize(st);
+            if (e != hipSuccess) rc = set_error(VDB_ERR_HIP, "graph build: %s", hipGetErrorString(e));
+        }
+        (void)hipFree(qbuf);
+        (void)hipFree(dsc);
+        (void)hipFree(did);
+        if (rc) return rc;
+        // 2. out-edges: the F nearest; then the nearest reverse edges; then further kNN
+        const bool hi_better = ix->metric == VDB_METRIC_COSINE;
+        std::vector<int32_t> fwd((size_t)N * knn, -1);
+        std::vector<float> fsc((size_t)N * knn);
+        std::vector<int> fcnt(N, 0);
+        for (int64_t i = 0; i < N; ++i) {
+            int c = 0;
+            for (int j = 0; j < kk && c < knn; ++j) {
+                const int64_t v = kid[(size_t)i * kk + j];
+                if (v < 0 || v == i) continue;
+                fwd[(size_t)i * knn + c] = (int32_t)v;
+                fsc[(size_t)i * knn + c] = hi_better ? ksc[(size_t)i * kk + j] : -ksc[(size_t)i * kk + j];
+                ++c;
+            }
+            fcnt[i] = c;
+        }
+        std::vector<int64_t> roff(N + 1, 0);
+        for (int64_t i = 0; i < N; ++i)
+            for (int j = 0; j < std::min(F, fcnt[i]); ++j) roff[fwd[(size_t)i * knn + j] + 1]++;
+        for (int64_t i = 0; i < N; ++i) roff[i + 1] += roff[i];
+        std::vector<std::pair<float, int32_t>> rev(roff[N]);
+        std::vector<int64_t> rpos(roff.begin(), roff.end() - 1);
+        for (int64_t i = 0; i < N; ++i)
+            for (int j = 0; j < std::min(F, fcnt[i]); ++j) {
+                const int32_t t = fwd[(size_t)i * knn + j];
+                rev[rpos[t]++] = {fsc[(size_t)i * knn + j], (int32_t)i};
+            }
+        for (int64_t i = 0; i < N; ++i) {
+            int32_t* row = nbr.data() + (size_t)i * R;
+            int c = 0;
+            for (int j = 0; j < std::min(F, fcnt[i]); ++j) row[c++] = fwd[(size_t)i * knn + j];
+            auto b = rev.begin() + roff[i], en = rev.begin() + roff[i + 1];
+            std::sort(b, en, [](const std::pair<float, int32_t>& x, const std::pair<float, int32_t>& y) {
+                return x.first > y.first || (x.first == y.first && x.second < y.second);
+            });
+            auto has = [&](int32_t v) {
+                for (int q = 0; q < c; ++q)
+                    if (row[q] == v) return true;
+                return false;
+            };
+            for (auto it = b; it != en && c < R; ++it)
+                if (!has(it->second)) row[c++] = it->second;
+            for (int j = F; j < fcnt[i] && c < R; ++j)
+                if (!has(fwd[(size_t)i * knn + j])) row[c++] = fwd[(size_t)i * knn + j];
+        }
+    }
+    // 3. entry rows: evenly spread
+    const int E = (int)std::min<int64_t>(n_entries, std::max<int64_t>(N, 1));
+    std::vector<int32_t> ent(E);
+    for (int i = 0; i < E; ++i) ent[i] = (int32_t)((int64_t)i * N / E);
+    return graph_upload(ix, R, N, nbr.data(), ent.data(), N > 0 ? E : 0, out);
+}
+
+int32_t vdb_graph_import(vdb_index* ix, int32_t degree, int64_t n, const int32_t* nbr, int32_t n_entries,
+                         const int32_t* entries, vdb_graph** out) {
+    if (!ix || !out || (n > 0 && !nbr) || (n_entries > 0 && !entries)) return set_error(VDB_ERR_INVALID, "NULL argument");
+    *out = nullptr;
+    if (degree < 1 || degree > 64) return set_error(VDB_ERR_INVALID, "degree must be in [1, 64]");
+    if (n != ix->count) return set_error(VDB_ERR_INVALID, "graph has %lld rows, index %lld", (long long)n, (long long)ix->count);
+    if (n_entries < 0 || n_entries > 256) return set_error(VDB_ERR_INVALID, "n_entries must be in [0, 256]");
+    for (int64_t i = 0; i < n * degree; ++i)
+        if (nbr[i] < -1 || nbr[i] >= n) return set_error(VDB_ERR_INVALID, "neighbour id out of range at %lld", (long long)i);
+    for (int i = 0; i < n_entries; ++i)
+        if (entries[i] < 0 || entries[i] >= n) return set_error(VDB_ERR_INVALID, "entry id out of range");
+    HIP_TRY(hipSetDevice(ix->device));
+    return graph_upload(ix, degree, n, nbr, entries, n_entries, out);
+}
+
+int32_t vdb_graph_info(const vdb_graph* g, int64_t* n_rows, int32_t* degree, int32_t* n_entries) {
+    if (!g) return set_error(VDB_ERR_INVALID, "graph is NULL");
+    if (n_rows) *n_rows = g->n;
+    if (degree) *degree = g->R;
+    if (n_entries) *n_entries = g->n_entries;
+    return VDB_OK;
+}
+
+int32_t vdb_graph_export(const vdb_graph* g, int32_t* nbr_host, int32_t* entries_host) {
+    if (!g) return set_error(VDB_ERR_INVALID, "graph is NULL");
+    HIP_TRY(hipSetDevice(g->ix->device));
+    if (nbr_host && g->n > 0)
+        HIP_TRY(hipMemcpy(nbr_host, g->nbr, (size_t)g->n * g->R * sizeof(int32_t), hipMemcpyDeviceToHost));
+    if (entries_host && g->n_entries > 0)
+        HIP_TRY(hipMemcpy(entries_host, g->entries, (size_t)g->n_entries * sizeof(int32_t), hipMemcpyDeviceToHost));
+    return VDB_OK;
+}
+
+int32_t vdb_graph_search(vdb_graph* g, const float* queries, int32_t nq, int32_t k, int32_t ef, int32_t mem,
+                         int64_t* labels, float* distances, void* stream) {
+    if (!g || !queries || !labels || !distances) return set_error(VDB_ERR_INVALID, "NULL argument");
+    if (nq <= 0) return set_error(VDB_ERR_INVALID, "n_queries must be >= 1");
+    if (ef < 1 || ef > 256) return set_error(VDB_ERR_INVALID, "ef must be in [1, 256], got %d", ef);
+    if (k < 1 || k > ef) return set_error(VDB_ERR_INVALID, "k must be in [1, ef], got k=%d ef=%d", k, ef);
+    if (mem != VDB_MEM_HOST && mem != VDB_MEM_DEVICE) return set_error(VDB_ERR_INVALID, "bad mem kind %d", mem);
+    vdb_index* ix = g->ix;
+    const int D = ix->dim;
+    if (mem == VDB_MEM_HOST && !all_finite(queries, (int64_t)nq * D))
+        return set_error(VDB_ERR_NONFINITE, "query contains NaN or Inf");
+    HIP_TRY(hipSetDevice(ix->device));
+    std::shared_lock<std::shared_mutex> lk(ix->mu);
+    if (ix->count != g->n) return set_error(VDB_ERR_INVALID, "graph is stale: %lld rows, index %lld", (long long)g->n,
+                                            (long long)ix->count);
+    hipStream_t st = stream ? (hipStream_t)stream : ix->stream;
+    const float* Qd = queries;
+    int64_t* ol = labels;
+    float* od = distances;
+    void* tmp = nullptr;
+    if (mem == VDB_MEM_HOST) {
+        const size_t qb = (size_t)nq * D * 4, lb = (size_t)nq * k * 8, db = (size_t)nq * k * 4;
+        HIP_TRY(hipMallocAsync(&tmp, qb + lb + db + 512, st));
+        char* base = (char*)tmp;
+        HIP_TRY(hipMemcpyAsync(base, queries, qb, hipMemcpyHostToDevice, st));
+        Qd = (const float*)base;
+        ol = (int64_t*)(base + ((qb + 255) & ~size_t(255)));
+        od = (float*)((char*)ol + ((lb + 255) & ~size_t(255)));
+    }
+    GraphSearchArgs a;
+    a.X = ix->X; a.G = ix->G; a.D = D; a.rowscale = ix->metric == 0 ? ix->inv32 : ix->sq32; a.n_rows = g->n;
+    a.nbr = g->nbr; a.R = g->R; a.entries = g->entries; a.n_entries = g->n_entries;
+    a.Q = Qd; a.k = k; a.ef = ef; a.out_lab = ol; a.out_dist = od; a.stats = g->d_stats;
+    if (g->n == 0) {
+        HIP_TRY(hipMemsetAsync(ol, 0xFF, (size_t)nq * k * 8, st));
+    } else {
+        HIP_TRY(launch_graph_search(ix->metric, a, nq, st));
+    }
+    g->n_queries += nq;
+    if (mem == VDB_MEM_HOST) {
+        HIP_TRY(hipMemcpyAsync(labels, ol, (size_t)nq * k * 8, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(distances, od, (size_t)nq * k * 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipFreeAsync(tmp, st));
+        HIP_TRY(hipStreamSynchronize(st));
+    }
+    return VDB_OK;
+}
+
+int32_t vdb_graph_stat(const vdb_graph* g, const char* name, int64_t* value) {
+    if (!g || !name || !value) return set_error(VDB_ERR_INVALID, "NULL argument");
+    std::string n(name);
+    if (n == "queries") {
+        *value = g->n_queries.load();
+    } else if (n == "iterations") {
+        unsigned long long v = 0;
+        HIP_TRY(hipMemcpy(&v, g->d_stats, sizeof(v), hipMemcpyDeviceToHost));
+        *value = (int64_t)v;
+    } else {
+        return set_error(VDB_ERR_INVALID, "unknown graph stat '%s'", name);
+    }
+    return VDB_OK;
+}
+
+int32_t vdb_graph_destroy(vdb_graph* g) {
+    if (!g) return VDB_OK;
+    (void)hipSetDevice(g->ix->device);
+    (void)hipDeviceSynchronize();
+    (void)hipFree(g->nbr);
+    (void)hipFree(g->entries);
+    (void)hipFree(g->d_stats);
+    delete g;
+    return VDB_OK;
+}
+
+}  // extern "C"

@@ -124,6 +124,16 @@ hipError_t launch_finalize_u32(int metric, const double* sk, const uint32_t* si,
 hipError_t launch_finalize_i64(int metric, const double* sk, const int64_t* si, int KP, int nq, const int* qmap,
                                int k, float* out_s, int64_t* out_i, double* out_k, hipStream_t st);
 
+// Graph search (vdb_graph.hip): one workgroup per query, beam of ef over a [N][R]
+// int32 neighbour array (-1 = none), started from the best of n_entries entry rows.
+struct GraphSearchArgs {
+    const float* X; int G; int D; const float* rowscale; int64_t n_rows;
+    const int32_t* nbr; int R; const int32_t* entries; int n_entries;
+    const float* Q; int k; int ef;
+    int64_t* out_lab; float* out_dist; unsigned long long* stats;
+};
+hipError_t launch_graph_search(int metric, const GraphSearchArgs& a, int nq, hipStream_t st);
+
 // Operator slot: full score matrix out[B][N] (fp32 reference arithmetic).
 hipError_t launch_similarity_matrix(const float* X, int64_t N, int D, const float* Q, int B, int metric,
                                     float* out, hipStream_t st);

@@ -31,6 +31,8 @@ METRIC_IDS = {"cosine": 0, "euclidean": 1}
 PRECISION_IDS = {"fp32": 0, "bf16x3": 1}
 MEM_HOST = 0
 MEM_DEVICE = 1
+# largest beam (ef) vdb_graph_search accepts (csrc/vdb_graph.hip GS_EF_MAX)
+GRAPH_EF_MAX = 256
 
 # Every symbol include/vdb.h declares (tests/test_abi.py checks the .so exports them).
 EXPORTED_SYMBOLS = (
@@ -39,6 +41,8 @@ EXPORTED_SYMBOLS = (
     "vdb_index_set_param", "vdb_index_get_stat",
     "vdb_index_add", "vdb_index_count", "vdb_index_clear", "vdb_index_get_vectors",
     "vdb_index_search", "vdb_merge_topk", "vdb_similarity_matrix",
+    "vdb_graph_build", "vdb_graph_import", "vdb_graph_export", "vdb_graph_info", "vdb_graph_search",
+    "vdb_graph_stat", "vdb_graph_destroy",
 )
 
 _lib = None
@@ -93,6 +97,13 @@ def load_library():
             "vdb_index_search": (c_i32, [c_vp, c_vp, c_i32, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp, c_i64, c_vp]),
             "vdb_merge_topk": (c_i32, [c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp]),
             "vdb_similarity_matrix": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i32, c_i32, c_vp, c_vp]),
+            "vdb_graph_build": (c_i32, [c_vp, c_i32, c_i32, c_i32, ctypes.POINTER(c_vp)]),
+            "vdb_graph_import": (c_i32, [c_vp, c_i32, c_i64, c_vp, c_i32, c_vp, ctypes.POINTER(c_vp)]),
+            "vdb_graph_export": (c_i32, [c_vp, c_vp, c_vp]),
+            "vdb_graph_info": (c_i32, [c_vp, p_i64, ctypes.POINTER(c_i32), ctypes.POINTER(c_i32)]),
+            "vdb_graph_search": (c_i32, [c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp]),
+            "vdb_graph_stat": (c_i32, [c_vp, ctypes.c_char_p, p_i64]),
+            "vdb_graph_destroy": (c_i32, [c_vp]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)
@@ -231,6 +242,79 @@ class NativeIndex:
             self._h, ctypes.c_void_p(q_ptr), int(n_queries), int(k), ctypes.c_void_p(mask_ptr or None),
             MEM_DEVICE, ctypes.c_void_p(out_scores_ptr), ctypes.c_void_p(out_idx_ptr),
             ctypes.c_void_p(out_keys_ptr or None), int(index_offset), ctypes.c_void_p(stream or None)))
+
+
+class NativeGraph:
+    """The graph index over a NativeIndex's rows (include/vdb.h vdb_graph_*):
+    hnswlib-style search results (labels, distances: cosine 1 - cos, L2 squared)."""
+
+    def __init__(self, index: "NativeIndex", handle):
+        self.index = index  # keeps the corpus alive
+        self._lib = index._lib
+        self._h = handle
+
+    @classmethod
+    def build(cls, index: "NativeIndex", degree: int = 32, knn: int = 32, n_entries: int = 256) -> "NativeGraph":
+        h = ctypes.c_void_p()
+        _check(index._lib.vdb_graph_build(index._h, int(degree), int(knn), int(n_entries), ctypes.byref(h)))
+        return cls(index, h)
+
+    @classmethod
+    def from_arrays(cls, index: "NativeIndex", neighbors: np.ndarray, entries: np.ndarray) -> "NativeGraph":
+        nb = np.ascontiguousarray(neighbors, dtype=np.int32)
+        en = np.ascontiguousarray(entries, dtype=np.int32)
+        if nb.ndim != 2:
+            raise ValueError(f"neighbors must be [n, degree], got {nb.shape}")
+        h = ctypes.c_void_p()
+        _check(index._lib.vdb_graph_import(index._h, nb.shape[1], nb.shape[0], _ptr(nb) if nb.size else None,
+                                           en.size, _ptr(en) if en.size else None, ctypes.byref(h)))
+        return cls(index, h)
+
+    def info(self) -> Tuple[int, int, int]:
+        n, d, e = ctypes.c_int64(0), ctypes.c_int32(0), ctypes.c_int32(0)
+        _check(self._lib.vdb_graph_info(self._h, ctypes.byref(n), ctypes.byref(d), ctypes.byref(e)))
+        return int(n.value), int(d.value), int(e.value)
+
+    def to_arrays(self) -> Tuple[np.ndarray, np.ndarray]:
+        n, d, e = self.info()
+        nb = np.empty((n, d), np.int32)
+        en = np.empty(e, np.int32)
+        _check(self._lib.vdb_graph_export(self._h, _ptr(nb) if nb.size else None, _ptr(en) if en.size else None))
+        return nb, en
+
+    def search(self, queries: np.ndarray, k: int, ef: int = 100):
+        q = np.ascontiguousarray(queries, dtype=np.float32)
+        if q.ndim == 1:
+            q = q[None, :]
+        if q.ndim != 2 or q.shape[1] != self.index.dim:
+            raise ValueError(f"queries must have shape (n, {self.index.dim}), got {np.shape(queries)}")
+        labels = np.empty((q.shape[0], int(k)), np.int64)
+        dist = np.empty((q.shape[0], int(k)), np.float32)
+        _check(self._lib.vdb_graph_search(self._h, _ptr(q), q.shape[0], int(k), int(ef), MEM_HOST, _ptr(labels),
+                                          _ptr(dist), None))
+        return labels, dist
+
+    def search_device(self, q_ptr: int, n_queries: int, k: int, ef: int, labels_ptr: int, dist_ptr: int,
+                      stream: int = 0) -> None:
+        _check(self._lib.vdb_graph_search(self._h, ctypes.c_void_p(q_ptr), int(n_queries), int(k), int(ef), MEM_DEVICE,
+                                          ctypes.c_void_p(labels_ptr), ctypes.c_void_p(dist_ptr),
+                                          ctypes.c_void_p(stream or None)))
+
+    def stat(self, name: str) -> int:
+        v = ctypes.c_int64(0)
+        _check(self._lib.vdb_graph_stat(self._h, name.encode(), ctypes.byref(v)))
+        return int(v.value)
+
+    def close(self) -> None:
+        h, self._h = getattr(self, "_h", None), None
+        if h:
+            self._lib.vdb_graph_destroy(h)
+
+    def __del__(self):  # pragma: no cover - GC timing
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def merge_topk_device(keys_ptr: int, idx_ptr: int, n_lists: int, n_queries: int, k_in: int, k_out: int,

@@ -83,7 +83,11 @@ class MLXVectorStore:
         self._dim: Optional[int] = None
         self._metadata: List[Dict] = []
         self._vector_count = 0
-        self._hnsw_index = None  # the HNSW graph path is not built yet
+        self._hnsw_index = None
+        if self.config.enable_hnsw:  # service/optimized_vector_store.py:72-78
+            from performance.hnsw_index import ProductionHNSWIndex
+            self._hnsw_index = ProductionHNSWIndex(self.config.dimension, self.store_path, self.config.metric,
+                                                   device=self.config.device)
         self._initialize_store()
         if self.config.jit_compile:
             self._compile_critical_functions()
@@ -136,6 +140,9 @@ class MLXVectorStore:
             self._vector_count = self._index.count() if self._index is not None else 0
             self._is_dirty = True
             self._save_store()
+            if self.config.enable_hnsw and self._hnsw_index is not None and self._index is not None:
+                # the reference rebuilds the graph from scratch on every add (:110-112)
+                self._hnsw_index.build(None, native_index=self._index)
             return {"vectors_added": len(metadata), "total_vectors": self._vector_count}
 
     # ---- query ---------------------------------------------------------------------
@@ -150,6 +157,31 @@ class MLXVectorStore:
         if q.ndim != 1:
             raise ValueError(f"query takes one vector of shape (dim,) or (1, dim), got {q.shape}; "
                              "use batch_query for several")
+        h = self._hnsw_index
+        if use_hnsw and self.config.enable_hnsw and h is not None and h.is_loaded:
+            # service/optimized_vector_store.py:120-143: hnswlib distances, k*10 candidates
+            # when filtering, brute force on any failure
+            try:
+                candidate_k = k * 10 if filter_metadata else k
+                indices, distances = h.search(q[None, :], k=candidate_k)
+                indices, distances = indices[0], distances[0]
+                if not filter_metadata:
+                    return ([int(i) for i in indices], distances.tolist(),
+                            [self._metadata[int(i)] for i in indices])
+                hits = []
+                for i, idx in enumerate(indices):
+                    if idx < len(self._metadata):
+                        meta = self._metadata[int(idx)]
+                        if all(meta.get(key) == value for key, value in filter_metadata.items()):
+                            hits.append((int(idx), float(distances[i]), meta))
+                    if len(hits) == k:
+                        break
+                if not hits:
+                    return [], [], []
+                fi, fd, fm = zip(*hits)
+                return list(fi), list(fd), list(fm)
+            except Exception as e:
+                logger.warning("HNSW-Suche fehlgeschlagen, falle auf Brute-Force zurück: %s", e)
         return self._brute_force_search(q[None, :], k, filter_metadata)[0]
 
     def batch_query(self, query_vectors: Union[np.ndarray, Any], k: int = 10,
@@ -211,6 +243,10 @@ class MLXVectorStore:
                     shutil.rmtree(self.store_path)
                 self.store_path.mkdir(parents=True, exist_ok=True)
                 self._create_empty_store()
+                if self.config.enable_hnsw:  # :205-206
+                    from performance.hnsw_index import ProductionHNSWIndex
+                    self._hnsw_index = ProductionHNSWIndex(self.config.dimension, self.store_path,
+                                                           self.config.metric, device=self.config.device)
             except Exception as e:  # the reference logs and swallows (:208-209)
                 logger.error("clearing store %s failed: %s", self.store_path, e)
 
@@ -284,6 +320,9 @@ class MLXVectorStore:
                 self._ensure_index(vecs.shape[1]).add(vecs)
             self._metadata = meta
             self._vector_count = self._index.count() if self._index is not None else 0
+            if self._hnsw_index is not None and self._index is not None:
+                if not self._hnsw_index.attach(self._index):
+                    self._hnsw_index.build(None, native_index=self._index)
         except Exception as e:  # reference: log and start empty (:237-239)
             logger.error("loading store %s failed, starting empty: %s", self.store_path, e)
             self._create_empty_store()
