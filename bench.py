@@ -45,7 +45,10 @@ CONFIGS = {
     "c2": (1_000_000, 768, 64, 10, "cosine", "1M x 768 fp32 cosine top-10, batch 64"),
     "c3": (1_000_000, 1536, 256, 10, "cosine", "1M x 1536 cosine top-10, batch 256 (fp32 candidate pass)"),
     "c4": (10_000_000, 128, 512, 100, "euclidean", "10M x 128 L2 top-100, batch 512, row-sharded"),
+    # graph path (performance/hnsw_index.py): batch 1, hnswlib M=16 -> out-degree 2M, efSearch 128
+    "c5": (5_000_000, 384, 1, 10, "cosine", "5M x 384 graph index (HNSW M=16) cosine top-10, efSearch=128, batch 1"),
 }
+GRAPH_M, GRAPH_EF = 16, 128
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md, Peak FP32 (matrix)
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md, Peak BF16 MFMA, dense
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md, HBM3E peak (spec)
@@ -85,6 +88,150 @@ def cpu_baseline(V, Q, k):
                       f"{dt:.2f} s"}
 
 
+def cpu_graph_baseline(V, nbr, entries, Q, k, ef, metric, gt, budget_s=15.0):
+    """The graph search restated on the CPU (oracle/ref_cpu.graph_search, hnswlib's
+    searchBaseLayerST) over the same neighbour array: queries one at a time until
+    the time budget is spent."""
+    from oracle import ref_cpu
+    inv = 1.0 / np.maximum(np.linalg.norm(V, axis=1), 1e-8) if metric == "cosine" else None  # once per corpus
+    t0 = time.perf_counter()
+    n = hits = 0
+    for b in range(Q.shape[0]):
+        lab, _, _ = ref_cpu.graph_search(V, nbr, entries, Q[b], k, ef, metric, inv_norms=inv)
+        hits += len(set(lab.tolist()) & set(gt[b].tolist()))
+        n += 1
+        if time.perf_counter() - t0 > budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "queries/s", "cores": 1, "kind": "port",
+            "sample": f"{n} single queries, numpy/heapq restatement of hnswlib's level-0 search "
+                      f"(searchBaseLayerST) over the same graph, ef={ef}; {dt:.2f} s",
+            "recall_at_10": hits / float(n * k)}
+
+
+def main_graph(args, world, rank, local, dev):
+    """C5: the graph path at batch 1.  N>1 runs independent replicas (SURVEY.md §8e:
+    each GPU holds the whole graph and serves its own queries); value = all queries
+    served / the slowest rank's time."""
+    from performance.hnsw_index import N_ENTRIES
+    N, D, B, k, metric, desc = CONFIGS["c5"]
+    N = args.rows or N
+    R = 2 * GRAPH_M
+    knn = args.graph_knn or R
+    ix = _vdb.NativeIndex(D, metric, local)
+    ix.reserve(N)
+    keep_host = world == 1 and rank == 0 and not args.no_cpu_baseline
+    parts = []
+    for s0 in range(0, N, 8 * CHUNK_ROWS):
+        part = corpus_rows(N, D, s0, min(s0 + 8 * CHUNK_ROWS, N))
+        ix.add(part)
+        if keep_host:
+            parts.append(part)
+    t0 = time.perf_counter()
+    g = _vdb.NativeGraph.build(ix, degree=R, knn=knn, n_entries=N_ENTRIES)
+    build_s = time.perf_counter() - t0
+    nq = args.warmup + args.steps
+    Q = np.random.default_rng(1 + rank).random((nq, D), dtype=np.float32)
+    q_dev = torch.from_numpy(Q).to(dev)
+    lab = torch.empty((nq, k), dtype=torch.int64, device=dev)
+    dst = torch.empty((nq, k), dtype=torch.float32, device=dev)
+    stream = torch.cuda.Stream(dev)  # a real stream: events and the kernel on the same queue
+    sp = stream.cuda_stream
+    torch.cuda.synchronize()
+
+    def one(i):
+        g.search_device(q_dev[i].data_ptr(), 1, k, GRAPH_EF, lab[i].data_ptr(), dst[i].data_ptr(), stream=sp)
+
+    for i in range(args.warmup):
+        one(i)
+    torch.cuda.synchronize()
+    it0, vis0 = g.stat("iterations"), g.stat("visited")
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    lat = []
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for j in range(args.steps):
+        t1 = time.perf_counter()
+        ev[j][0].record(stream)
+        one(args.warmup + j)
+        ev[j][1].record(stream)
+        torch.cuda.synchronize()
+        lat.append(time.perf_counter() - t1)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    iters = (g.stat("iterations") - it0) / args.steps
+    visited = (g.stat("visited") - vis0) / args.steps
+    # recall@10 of the timed queries against the exact brute-force path
+    Qt = Q[args.warmup:]
+    _, gt = ix.search(Qt, k)
+    got = lab[args.warmup:].cpu().numpy()
+    recall = sum(len(set(a.tolist()) & set(b.tolist())) for a, b in zip(got, gt)) / float(gt.size)
+    # exact brute force at batch 1 for comparison (same queries, device resident)
+    os_, oi_ = torch.empty((1, k), device=dev), torch.empty((1, k), dtype=torch.int64, device=dev)
+    for i in range(3):
+        ix.search_device(q_dev[i].data_ptr(), 1, k, os_.data_ptr(), oi_.data_ptr(), 0, stream=sp)
+    torch.cuda.synchronize()
+    bl = []
+    for i in range(min(args.steps, 50)):
+        t1 = time.perf_counter()
+        ix.search_device(q_dev[i].data_ptr(), 1, k, os_.data_ptr(), oi_.data_ptr(), 0, stream=sp)
+        torch.cuda.synchronize()
+        bl.append(time.perf_counter() - t1)
+    p50 = float(np.median(lat))
+    if world > 1:
+        t = torch.tensor([elapsed, p50, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, p50, kern_ms = t.tolist()
+    if rank == 0:
+        # algorithmic bytes of one search: every scored row (D fp32 + its row scale)
+        # plus the neighbour list of every expanded node (<= 4 per iteration)
+        q_bytes = visited * (4 * D + 4) + iters * 4 * R * 4
+        achieved = q_bytes / (kern_ms * 1e-3) / 1e9
+        rec = {
+            "metric": METRIC,
+            "value": args.steps * world / elapsed,
+            "unit": "queries/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "p50_ms": p50 * 1e3,
+            "p99_ms": float(np.percentile(lat, 99)) * 1e3,
+            "recall_at_10": recall,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic uniform [0,1) fp32 (numpy PCG64, corpus seed 0 per 65536-row chunk, queries seed 1)",
+            "config": {"workload": f"c5: {desc}", "n_rows": N, "dim": D, "global_batch": 1, "k": k,
+                       "metric": metric, "ef": GRAPH_EF, "degree": R, "build_knn": knn, "entries": N_ENTRIES,
+                       "parallelism": f"replicas x{world}" if world > 1 else "single GPU"},
+            "build_s": build_s,
+            "iterations_per_query": iters,
+            "visited_per_query": visited,
+            "exact_b1_p50_ms": float(np.median(bl)) * 1e3,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "graph_search",
+                         "avg_launch_ms": kern_ms, "algorithmic_bytes": q_bytes,
+                         "note": "one workgroup per query: bound by dependent hops (latency), not bandwidth"},
+        }
+        if keep_host:
+            V = np.concatenate(parts) if len(parts) > 1 else parts[0]
+            del parts
+            nbr, ent = g.to_arrays()
+            rec["cpu_baseline"] = cpu_graph_baseline(V, nbr, ent, Qt, k, GRAPH_EF, metric, gt)
+        print(json.dumps(rec), flush=True)
+    g.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -98,6 +245,8 @@ def main():
                     help="candidate-pass arithmetic (results identical; DESIGN.md §3)")
     ap.add_argument("--scan-variant", type=int, default=None, help="candidate-pass kernel variant (tuning)")
     ap.add_argument("--n-wg", type=int, default=None, help="candidate-pass workgroups (tuning)")
+    ap.add_argument("--rows", type=int, default=None, help="override the corpus rows (exploration only)")
+    ap.add_argument("--graph-knn", type=int, default=None, help="c5: kNN candidates per row for the build")
     ap.add_argument("--pmc-json", default=None,
                     help="HBM traffic of the scan kernel from a separate rocprofv3 --pmc pass "
                          "(default: newest profiles/*/pmc.json for this config, see profiles/scripts/)")
@@ -113,6 +262,8 @@ def main():
     else:
         torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if args.config == "c5":
+        return main_graph(args, world, rank, local, dev)
 
     N, D, B, k, metric, desc = CONFIGS[args.config]
     lo, hi = shard_bounds(N, world, rank)

@@ -177,7 +177,7 @@ int32_t vdb_graph_info(const vdb_graph* g, int64_t* n_rows, int32_t* degree, int
  * best first.  ef = beam width (search depth), k <= ef <= 256. */
 int32_t vdb_graph_search(vdb_graph* g, const float* queries, int32_t n_queries, int32_t k, int32_t ef, int32_t mem,
                          int64_t* labels, float* distances, void* stream);
-/* stats: "queries", "iterations" (beam iterations, summed over queries) */
+/* stats: "queries", "iterations" (beam iterations, summed over queries), "visited" (rows scored, summed) */
 int32_t vdb_graph_stat(const vdb_graph* g, const char* name, int64_t* value);
 int32_t vdb_graph_destroy(vdb_graph* g);
 

@@ -105,6 +105,7 @@ struct vdb_index {
     int64_t n_wg_override = 0;
     int64_t timing = 0;  // record HIP events around the candidate pass
     int64_t pilot_tiles = 512;  // row tiles sampled by the pilot bound (0 = off)
+    int64_t graph_fill = 0;     // graph build: top up pruned neighbour lists (hnswlib keepPrunedConnections)
     int64_t scan_variant = 0;     // fp32 candidate pass variant (vdb_scan.hip)
     int64_t scan_variant_b3 = 0;  // bf16x3 candidate pass variant
     // stats
@@ -375,6 +376,9 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
         if (value < 0 || !scan_variant_ok(PREC_BF16X3, (int)value, 8))
             return set_error(VDB_ERR_INVALID, "scan_variant_bf16x3 must be 0, 1 or 2");
         ix->scan_variant_b3 = value;
+    } else if (n == "graph_fill") {
+        if (value < 0 || value > 1) return set_error(VDB_ERR_INVALID, "graph_fill must be 0 or 1");
+        ix->graph_fill = value;
     } else if (n == "pilot_tiles") {
         if (value < 0 || value > 4096) return set_error(VDB_ERR_INVALID, "pilot_tiles must be in [0, 4096]");
         ix->pilot_tiles = value;
@@ -738,6 +742,8 @@ struct vdb_graph {
     int n_entries = 0;
     int32_t* nbr = nullptr;      // device [n][R]
     int32_t* entries = nullptr;  // device [n_entries]
+    float* rows = nullptr;       // device [n][Dp] row-major copy of the corpus (gathers)
+    int Dp = 0;
     unsigned long long* d_stats = nullptr;
     std::atomic<int64_t> n_queries{0};
 };
@@ -754,6 +760,13 @@ int graph_upload(vdb_index* ix, int R, int64_t n, const int32_t* nbr_host, const
     hipError_t e = hipMalloc(&g->nbr, (size_t)std::max<int64_t>(n, 1) * R * sizeof(int32_t));
     if (e == hipSuccess) e = hipMalloc(&g->entries, (size_t)std::max(n_ent, 1) * sizeof(int32_t));
     if (e == hipSuccess) e = hipMalloc(&g->d_stats, 64);
+    g->Dp = (ix->dim + 31) / 32 * 32;
+    if (e == hipSuccess) e = hipMalloc(&g->rows, (size_t)std::max<int64_t>(n, 1) * g->Dp * sizeof(float));
+    if (e == hipSuccess) {
+        std::shared_lock<std::shared_mutex> lk(ix->mu);
+        e = launch_graph_rows(ix->X, ix->G, n, g->Dp, g->rows, ix->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(ix->stream);
+    }
     if (e == hipSuccess) e = hipMemset(g->d_stats, 0, 64);
     if (e == hipSuccess && n > 0) e = hipMemcpy(g->nbr, nbr_host, (size_t)n * R * sizeof(int32_t), hipMemcpyHostToDevice);
     if (e == hipSuccess && n_ent > 0)
@@ -762,6 +775,7 @@ int graph_upload(vdb_index* ix, int R, int64_t n, const int32_t* nbr_host, const
         (void)hipFree(g->nbr);
         (void)hipFree(g->entries);
         (void)hipFree(g->d_stats);
+        (void)hipFree(g->rows);
         delete g;
         return set_error(e == hipErrorOutOfMemory ? VDB_ERR_OOM : VDB_ERR_HIP, "graph upload failed: %s",
                          hipGetErrorString(e));
@@ -824,51 +838,85 @@ int32_t vdb_graph_build(vdb_index* ix, int32_t degree, int32_t knn, int32_t n_en
         (void)hipFree(dsc);
         (void)hipFree(did);
         if (rc) return rc;
-        // 2. out-edges: the F nearest; then the nearest reverse edges; then further kNN
-        const bool hi_better = ix->metric == VDB_METRIC_COSINE;
-        std::vector<int32_t> fwd((size_t)N * knn, -1);
-        std::vector<float> fsc((size_t)N * knn);
-        std::vector<int> fcnt(N, 0);
+        // 2. hnswlib-style selection: pass 1 keeps <= M = R/2 diverse
+        //    out-edges from the kNN; pass 2 re-selects <= R from out- plus in-edges
+        //    (hnswlib's level-0 lists: the node's own links plus the links of later
+        //    insertions that chose it, re-pruned when they exceed 2M).
+        const int CW = std::min(knn, 63);
+        std::vector<int32_t> cand((size_t)N * CW, -1);
         for (int64_t i = 0; i < N; ++i) {
             int c = 0;
-            for (int j = 0; j < kk && c < knn; ++j) {
+            for (int j = 0; j < kk && c < CW; ++j) {
                 const int64_t v = kid[(size_t)i * kk + j];
                 if (v < 0 || v == i) continue;
-                fwd[(size_t)i * knn + c] = (int32_t)v;
-                fsc[(size_t)i * knn + c] = hi_better ? ksc[(size_t)i * kk + j] : -ksc[(size_t)i * kk + j];
-                ++c;
+                cand[(size_t)i * CW + c++] = (int32_t)v;
             }
-            fcnt[i] = c;
         }
-        std::vector<int64_t> roff(N + 1, 0);
-        for (int64_t i = 0; i < N; ++i)
-            for (int j = 0; j < std::min(F, fcnt[i]); ++j) roff[fwd[(size_t)i * knn + j] + 1]++;
-        for (int64_t i = 0; i < N; ++i) roff[i + 1] += roff[i];
-        std::vector<std::pair<float, int32_t>> rev(roff[N]);
-        std::vector<int64_t> rpos(roff.begin(), roff.end() - 1);
-        for (int64_t i = 0; i < N; ++i)
-            for (int j = 0; j < std::min(F, fcnt[i]); ++j) {
-                const int32_t t = fwd[(size_t)i * knn + j];
-                rev[rpos[t]++] = {fsc[(size_t)i * knn + j], (int32_t)i};
+        kid.clear(); kid.shrink_to_fit();
+        ksc.clear(); ksc.shrink_to_fit();
+        int32_t* dcand = nullptr;
+        int32_t* dnbr = nullptr;
+        float* ddist = nullptr;
+        e = hipMalloc(&dcand, (size_t)N * 63 * sizeof(int32_t));
+        if (e == hipSuccess) e = hipMalloc(&dnbr, (size_t)N * R * sizeof(int32_t));
+        if (e == hipSuccess) e = hipMalloc(&ddist, (size_t)N * R * sizeof(float));
+        rc = e == hipSuccess ? VDB_OK : set_error(VDB_ERR_OOM, "graph build buffers: %s", hipGetErrorString(e));
+        auto prune = [&](const std::vector<int32_t>& cv, int cw, int limit, int fill, int32_t* hn, float* hd) -> int {
+            hipError_t pe = hipMemcpyAsync(dcand, cv.data(), (size_t)N * cw * sizeof(int32_t), hipMemcpyHostToDevice, st);
+            GraphPruneArgs pa;
+            {
+                std::shared_lock<std::shared_mutex> g(ix->mu);
+                pa.X = ix->X; pa.G = ix->G;
+                pa.rowscale = ix->metric == VDB_METRIC_COSINE ? ix->inv32 : ix->sq32;
+                pa.cand = dcand; pa.cw = cw; pa.n_nodes = N; pa.limit = limit; pa.rw = limit; pa.fill = fill;
+                pa.out_nbr = dnbr; pa.out_dist = ddist;
+                if (pe == hipSuccess) pe = launch_graph_prune(ix->metric, pa, st);
             }
-        for (int64_t i = 0; i < N; ++i) {
-            int32_t* row = nbr.data() + (size_t)i * R;
-            int c = 0;
-            for (int j = 0; j < std::min(F, fcnt[i]); ++j) row[c++] = fwd[(size_t)i * knn + j];
-            auto b = rev.begin() + roff[i], en = rev.begin() + roff[i + 1];
-            std::sort(b, en, [](const std::pair<float, int32_t>& x, const std::pair<float, int32_t>& y) {
-                return x.first > y.first || (x.first == y.first && x.second < y.second);
-            });
-            auto has = [&](int32_t v) {
-                for (int q = 0; q < c; ++q)
-                    if (row[q] == v) return true;
-                return false;
-            };
-            for (auto it = b; it != en && c < R; ++it)
-                if (!has(it->second)) row[c++] = it->second;
-            for (int j = F; j < fcnt[i] && c < R; ++j)
-                if (!has(fwd[(size_t)i * knn + j])) row[c++] = fwd[(size_t)i * knn + j];
+            if (pe == hipSuccess) pe = hipMemcpyAsync(hn, dnbr, (size_t)N * limit * sizeof(int32_t), hipMemcpyDeviceToHost, st);
+            if (pe == hipSuccess && hd) pe = hipMemcpyAsync(hd, ddist, (size_t)N * limit * sizeof(float), hipMemcpyDeviceToHost, st);
+            if (pe == hipSuccess) pe = hipStreamSynchronize(st);
+            return pe == hipSuccess ? VDB_OK : set_error(VDB_ERR_HIP, "graph prune: %s", hipGetErrorString(pe));
+        };
+        std::vector<int32_t> fwd((size_t)N * F);
+        std::vector<float> fdist((size_t)N * F);
+        if (rc == VDB_OK) rc = prune(cand, CW, F, 0, fwd.data(), fdist.data());
+        if (rc == VDB_OK) {
+            // pool of v: out-edges of v and in-edges u -> v, nearest first, <= 63
+            std::vector<int64_t> roff(N + 1, 0);
+            for (size_t t = 0; t < fwd.size(); ++t)
+                if (fwd[t] >= 0) roff[fwd[t] + 1]++;
+            for (int64_t i = 0; i < N; ++i) roff[i + 1] += roff[i];
+            std::vector<std::pair<float, int32_t>> rev(roff[N]);
+            std::vector<int64_t> rpos(roff.begin(), roff.end() - 1);
+            for (int64_t u = 0; u < N; ++u)
+                for (int j = 0; j < F; ++j) {
+                    const int32_t w = fwd[(size_t)u * F + j];
+                    if (w >= 0) rev[rpos[w]++] = {fdist[(size_t)u * F + j], (int32_t)u};
+                }
+            std::vector<int32_t> cand2((size_t)N * 63, -1);
+            std::vector<std::pair<float, int32_t>> pool;
+            for (int64_t v = 0; v < N; ++v) {
+                pool.clear();
+                for (int j = 0; j < F; ++j)
+                    if (fwd[(size_t)v * F + j] >= 0) pool.push_back({fdist[(size_t)v * F + j], fwd[(size_t)v * F + j]});
+                pool.insert(pool.end(), rev.begin() + roff[v], rev.begin() + roff[v + 1]);
+                std::sort(pool.begin(), pool.end(), [](const std::pair<float, int32_t>& x, const std::pair<float, int32_t>& y) {
+                    return x.first < y.first || (x.first == y.first && x.second < y.second);
+                });
+                int c = 0;
+                int32_t* row = cand2.data() + (size_t)v * 63;
+                for (size_t t = 0; t < pool.size() && c < 63; ++t) {
+                    bool dup = false;
+                    for (int q = c - 1; q >= 0 && !dup; --q) dup = row[q] == pool[t].second;
+                    if (!dup) row[c++] = pool[t].second;
+                }
+            }
+            rc = prune(cand2, 63, R, (int)ix->graph_fill, nbr.data(), nullptr);
         }
+        (void)hipFree(dcand);
+        (void)hipFree(dnbr);
+        (void)hipFree(ddist);
+        if (rc) return rc;
     }
     // 3. entry rows: evenly spread
     const int E = (int)std::min<int64_t>(n_entries, std::max<int64_t>(N, 1));
@@ -940,7 +988,7 @@ int32_t vdb_graph_search(vdb_graph* g, const float* queries, int32_t nq, int32_t
         od = (float*)((char*)ol + ((lb + 255) & ~size_t(255)));
     }
     GraphSearchArgs a;
-    a.X = ix->X; a.G = ix->G; a.D = D; a.rowscale = ix->metric == 0 ? ix->inv32 : ix->sq32; a.n_rows = g->n;
+    a.rows = g->rows; a.Dp = g->Dp; a.D = D; a.rowscale = ix->metric == 0 ? ix->inv32 : ix->sq32; a.n_rows = g->n;
     a.nbr = g->nbr; a.R = g->R; a.entries = g->entries; a.n_entries = g->n_entries;
     a.Q = Qd; a.k = k; a.ef = ef; a.out_lab = ol; a.out_dist = od; a.stats = g->d_stats;
     if (g->n == 0) {
@@ -963,10 +1011,10 @@ int32_t vdb_graph_stat(const vdb_graph* g, const char* name, int64_t* value) {
     std::string n(name);
     if (n == "queries") {
         *value = g->n_queries.load();
-    } else if (n == "iterations") {
-        unsigned long long v = 0;
-        HIP_TRY(hipMemcpy(&v, g->d_stats, sizeof(v), hipMemcpyDeviceToHost));
-        *value = (int64_t)v;
+    } else if (n == "iterations" || n == "visited") {
+        unsigned long long v[2] = {0, 0};
+        HIP_TRY(hipMemcpy(v, g->d_stats, sizeof(v), hipMemcpyDeviceToHost));
+        *value = (int64_t)v[n == "visited" ? 1 : 0];
     } else {
         return set_error(VDB_ERR_INVALID, "unknown graph stat '%s'", name);
     }
@@ -980,6 +1028,7 @@ int32_t vdb_graph_destroy(vdb_graph* g) {
     (void)hipFree(g->nbr);
     (void)hipFree(g->entries);
     (void)hipFree(g->d_stats);
+    (void)hipFree(g->rows);
     delete g;
     return VDB_OK;
 }

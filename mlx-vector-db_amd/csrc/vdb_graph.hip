@@ -22,40 +22,58 @@ constexpr int GS_VIS = 16384;       // visited hash slots (row + 1; 0 = empty)
 constexpr int GS_PROBE = 64;        // linear probes before a node is treated as visited
 constexpr int GS_ENT_MAX = 256;
 constexpr int GS_MAX_ITERS = 8192;  // hard stop: every wave leaves the loop
-constexpr int GS_NR = 4;            // rows scored together by one wave
+constexpr int GS_RG = 4;            // groups of 8 rows a wave scores per call (32 rows)
+constexpr int GS_PC = 12;           // 16-byte pieces per lane and row in flight (12 x 8 lanes = 384 dims)
 
-// Scores of up to NR rows against the query in LDS (fp32; higher = better):
-// cosine q_hat . x * inv|x| (q_hat normalised), L2 2 q . x - |x|^2.
+// Scores of n <= 32 rows (ids[0..n)) of the row-major copy Xr [rows][Dp] against
+// the query in LDS (fp32; higher = better): cosine q_hat . x * inv|x| (q_hat
+// normalised), L2 2 q . x - |x|^2; written to out[0..n).  Eight lanes per row, so
+// every load instruction reads eight whole 128-byte lines; all pieces of all 32
+// rows (and their row scales) are requested before the first FMA: one dependent
+// HBM round trip per call for D <= 384.
 template <int METRIC>
-__device__ __forceinline__ void wave_scores(const float* __restrict__ qs, const float* __restrict__ X, int G, int D,
-                                            const float* __restrict__ rowscale, const int32_t* rows, int nr,
-                                            float* out) {
-    const int lane = threadIdx.x & 63;
-    const int npieces = (D + 3) / 4;
-    float acc[GS_NR];
+__device__ __forceinline__ void wave_score_rows(const float* __restrict__ qs, const float* __restrict__ Xr, int Dp,
+                                                const float* __restrict__ rowscale, const int32_t* ids, int n,
+                                                float* out, int lane) {
+    const int sub = lane & 7, u0 = lane >> 3;
+    int32_t row[GS_RG];
+    float rs[GS_RG], acc[GS_RG];
+    bool ok[GS_RG];
 #pragma unroll
-    for (int u = 0; u < GS_NR; ++u) acc[u] = 0.0f;
-    for (int p = lane; p < npieces; p += 64) {
-        f32x4 xv[GS_NR];
+    for (int g = 0; g < GS_RG; ++g) {
+        ok[g] = u0 + 8 * g < n;
+        row[g] = ok[g] ? ids[u0 + 8 * g] : 0;
+        rs[g] = ok[g] ? rowscale[row[g]] : 0.0f;
+        acc[g] = 0.0f;
+    }
+    const int nper = Dp >> 5;
+    for (int i0 = 0; i0 < nper; i0 += GS_PC) {
+        f32x4 xv[GS_RG][GS_PC];
 #pragma unroll
-        for (int u = 0; u < GS_NR; ++u)
-            xv[u] = u < nr ? *(const f32x4*)(X + tiled_piece_offset((uint64_t)rows[u], p, G)) : f32x4{0.f, 0.f, 0.f, 0.f};
-        const f32x4 qv = *(const f32x4*)(qs + 4 * p);
+        for (int g = 0; g < GS_RG; ++g)
 #pragma unroll
-        for (int u = 0; u < GS_NR; ++u)
+            for (int c = 0; c < GS_PC; ++c)
+                xv[g][c] = ok[g] && i0 + c < nper ? *(const f32x4*)(Xr + (size_t)row[g] * Dp + 4 * (sub + 8 * (i0 + c)))
+                                                  : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc[u] = fmaf(qv[j], xv[u][j], acc[u]);
+        for (int c = 0; c < GS_PC; ++c) {
+            if (i0 + c < nper) {
+                const f32x4 qv = *(const f32x4*)(qs + 4 * (sub + 8 * (i0 + c)));
+#pragma unroll
+                for (int g = 0; g < GS_RG; ++g)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) acc[g] = fmaf(qv[j], xv[g][c][j], acc[g]);
+            }
+        }
     }
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1)
+    for (int off = 4; off >= 1; off >>= 1)
 #pragma unroll
-        for (int u = 0; u < GS_NR; ++u) acc[u] += __shfl_xor(acc[u], off, 64);
+        for (int g = 0; g < GS_RG; ++g) acc[g] += __shfl_xor(acc[g], off, 64);
+    if (sub == 0) {
 #pragma unroll
-    for (int u = 0; u < GS_NR; ++u) {
-        if (u < nr) {
-            const float rs = rowscale[rows[u]];
-            out[u] = METRIC == 0 ? acc[u] * rs : fmaf(2.0f, acc[u], -rs);
-        }
+        for (int g = 0; g < GS_RG; ++g)
+            if (ok[g]) out[u0 + 8 * g] = METRIC == 0 ? acc[g] * rs[g] : fmaf(2.0f, acc[g], -rs[g]);
     }
 }
 
@@ -79,9 +97,9 @@ __global__ void __launch_bounds__(64 * GS_WAVES) graph_search_kernel(GraphSearch
     const int lane = tid & 63;
     const int wv = tid >> 6;
     const int b = blockIdx.x;
-    const int Dp4 = (a.D + 3) / 4 * 4;
-    float* qs = reinterpret_cast<float*>(smem);                                  // [Dp4]
-    uint32_t* vis = reinterpret_cast<uint32_t*>(smem + (size_t)Dp4 * 4);         // [GS_VIS]
+    const int Dp = a.Dp;
+    float* qs = reinterpret_cast<float*>(smem);                                  // [Dp]
+    uint32_t* vis = reinterpret_cast<uint32_t*>(smem + (size_t)Dp * 4);          // [GS_VIS]
     __shared__ float s_bs[2][GS_EF_MAX];
     __shared__ int32_t s_bi[2][GS_EF_MAX];
     __shared__ int s_bx[2][GS_EF_MAX];  // expanded flag
@@ -91,10 +109,11 @@ __global__ void __launch_bounds__(64 * GS_WAVES) graph_search_kernel(GraphSearch
     __shared__ int s_pick[GS_WAVES];
     __shared__ int s_npick, s_bn, s_cur;
     __shared__ float s_qn2;
+    __shared__ unsigned s_scored;  // rows scored (entries + fresh neighbours): the "visited" statistic
 
     // query -> LDS (cosine: normalised in fp32), |q|^2 for the L2 distance
     const float* q = a.Q + (int64_t)b * a.D;
-    for (int d = tid; d < Dp4; d += 64 * GS_WAVES) qs[d] = d < a.D ? q[d] : 0.0f;
+    for (int d = tid; d < Dp; d += 64 * GS_WAVES) qs[d] = d < a.D ? q[d] : 0.0f;
     for (int i = tid; i < GS_VIS; i += 64 * GS_WAVES) vis[i] = 0u;
     __syncthreads();
     if (wv == 0) {
@@ -115,21 +134,10 @@ __global__ void __launch_bounds__(64 * GS_WAVES) graph_search_kernel(GraphSearch
     const int E = a.n_entries < GS_ENT_MAX ? a.n_entries : GS_ENT_MAX;
     __shared__ float s_es[GS_ENT_MAX];
     __shared__ int32_t s_ei[GS_ENT_MAX];
-    for (int e0 = wv * GS_NR; e0 < E; e0 += GS_WAVES * GS_NR) {
-        int32_t rows[GS_NR];
-        float sc[GS_NR];
-        const int nr = min(GS_NR, E - e0);
-#pragma unroll
-        for (int u = 0; u < GS_NR; ++u) rows[u] = u < nr ? a.entries[e0 + u] : 0;
-        wave_scores<METRIC>(qs, a.X, a.G, a.D, a.rowscale, rows, nr, sc);
-        if (lane == 0) {
-#pragma unroll
-            for (int u = 0; u < GS_NR; ++u)
-                if (u < nr) {
-                    s_es[e0 + u] = sc[u];
-                    s_ei[e0 + u] = rows[u];
-                }
-        }
+    for (int e0 = wv * 32; e0 < E; e0 += GS_WAVES * 32) {
+        const int n = min(32, E - e0);
+        wave_score_rows<METRIC>(qs, a.rows, Dp, a.rowscale, a.entries + e0, n, s_es + e0, lane);
+        if (lane < n) s_ei[e0 + lane] = a.entries[e0 + lane];
     }
     __syncthreads();
     const int ef = a.ef;
@@ -148,6 +156,7 @@ __global__ void __launch_bounds__(64 * GS_WAVES) graph_search_kernel(GraphSearch
     if (tid == 0) {
         s_bn = E < ef ? E : ef;
         s_cur = 0;
+        s_scored = (unsigned)E;
     }
     __syncthreads();
 
@@ -185,20 +194,28 @@ __global__ void __launch_bounds__(64 * GS_WAVES) graph_search_kernel(GraphSearch
             if (fresh) s_ci[wv][pos] = nb;
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             __builtin_amdgcn_wave_barrier();
-            for (int j0 = 0; j0 < cnt; j0 += GS_NR) {
-                int32_t rows[GS_NR];
-                float sc[GS_NR];
-                const int nr = min(GS_NR, cnt - j0);
-#pragma unroll
-                for (int u = 0; u < GS_NR; ++u) rows[u] = u < nr ? s_ci[wv][j0 + u] : 0;
-                wave_scores<METRIC>(qs, a.X, a.G, a.D, a.rowscale, rows, nr, sc);
-                if (lane == 0) {
-#pragma unroll
-                    for (int u = 0; u < GS_NR; ++u)
-                        if (u < nr) s_cs[wv][j0 + u] = sc[u];
-                }
+            for (int j0 = 0; j0 < cnt; j0 += 32) {
+                const int n = min(32, cnt - j0);
+                wave_score_rows<METRIC>(qs, a.rows, Dp, a.rowscale, s_ci[wv] + j0, n, s_cs[wv] + j0, lane);
             }
-            if (lane == 0) s_cc[wv] = cnt;
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            // keep only candidates that can enter a full beam (better than its worst)
+            const float cs = lane < cnt ? s_cs[wv][lane] : 0.0f;
+            const int32_t ci = lane < cnt ? s_ci[wv][lane] : 0;
+            const bool enter = lane < cnt && (bn < ef || better(cs, (uint32_t)ci, s_bs[cur][bn - 1], (uint32_t)s_bi[cur][bn - 1]));
+            const unsigned long long km = __ballot(enter);
+            __builtin_amdgcn_wave_barrier();
+            if (enter) {
+                const int kp = __popcll(km & ((1ull << lane) - 1ull));
+                s_cs[wv][kp] = cs;
+                s_ci[wv][kp] = ci;
+            }
+            const int kept = __popcll(km);
+            if (lane == 0) {
+                s_cc[wv] = kept;
+                atomicAdd(&s_scored, (unsigned)cnt);
+            }
         } else if (lane == 0) {
             s_cc[wv] = 0;
         }
@@ -208,7 +225,6 @@ __global__ void __launch_bounds__(64 * GS_WAVES) graph_search_kernel(GraphSearch
         int nnew = 0;
 #pragma unroll
         for (int w = 0; w < GS_WAVES; ++w) nnew += s_cc[w];
-        const float worst = bn >= ef ? s_bs[cur][bn - 1] : -INFINITY;
         // beam entries: rank = own position + new candidates that beat it
         for (int e = tid; e < bn; e += 64 * GS_WAVES) {
             const float sv = s_bs[cur][e];
@@ -228,7 +244,6 @@ __global__ void __launch_bounds__(64 * GS_WAVES) graph_search_kernel(GraphSearch
             if (j >= s_cc[w]) continue;
             const float sv = s_cs[w][j];
             const int32_t iv = s_ci[w][j];
-            if (bn >= ef && !(sv > worst)) continue;  // cannot enter
             int lo = 0, hi = bn;  // first beam position not better than (sv, iv)
             while (lo < hi) {
                 const int mid = (lo + hi) >> 1;
@@ -266,12 +281,146 @@ __global__ void __launch_bounds__(64 * GS_WAVES) graph_search_kernel(GraphSearch
             a.out_dist[o] = INFINITY;
         }
     }
-    if (tid == 0 && a.stats) atomicAdd(a.stats, (unsigned long long)iters);
+    if (tid == 0 && a.stats) {
+        atomicAdd(a.stats, (unsigned long long)iters);
+        atomicAdd(a.stats + 1, (unsigned long long)s_scored);
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// Build: neighbour selection by hnswlib's heuristic (getNeighborsByHeuristic2, the
+// selection hnsw_index.py:63-70's add_items runs for every insertion): walk the
+// candidates nearest first and keep c unless an already kept r is closer to c than
+// the node is (dist(c, r) < dist(c, node)).  One wave per node; the Gram matrix of
+// [node, c_1 .. c_63] comes from v_mfma_f32_32x32x2_f32 over the tiled rows (three
+// 32x32 tiles, the fourth is the transpose), so every distance the heuristic
+// compares is derived from the same fp32 dot products: deterministic, and
+// independent of how the candidates were found.
+// ---------------------------------------------------------------------------------
+constexpr int GP_WAVES = 4;
+constexpr int GP_LD = 65;  // Gram row stride in LDS (floats)
+
+template <int METRIC>
+__global__ void __launch_bounds__(64 * GP_WAVES) graph_prune_kernel(GraphPruneArgs a) {
+    __shared__ float s_gram[GP_WAVES][64 * GP_LD];
+    const int lane = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6;
+    const int64_t v = (int64_t)blockIdx.x * GP_WAVES + wv;
+    if (v >= a.n_nodes) return;  // wave-uniform; no block barrier below
+    float* gram = s_gram[wv];
+    const int32_t* cand = a.cand + v * a.cw;
+    // Gram index i: 0 = the node, i >= 1 = candidate i-1 (-1 padded at the tail)
+    const int h = lane >> 5, r = lane & 31;
+    const int32_t c0 = r == 0 ? -1 : (r - 1 < a.cw ? cand[r - 1] : -1);
+    const int32_t c1 = r + 31 < a.cw ? cand[r + 31] : -1;
+    const int32_t row0 = r == 0 ? (int32_t)v : (c0 >= 0 ? c0 : (int32_t)v);
+    const int32_t row1 = c1 >= 0 ? c1 : (int32_t)v;
+    f32x16 t00, t01, t11;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t00[i] = t01[i] = t11[i] = 0.0f;
+    f32x4 n0 = *(const f32x4*)(a.X + tiled_piece_offset((uint64_t)row0, h, a.G));
+    f32x4 n1 = *(const f32x4*)(a.X + tiled_piece_offset((uint64_t)row1, h, a.G));
+    for (int j = 0; j < a.G; ++j) {
+        const f32x4 x0 = n0, x1 = n1;
+        if (j + 1 < a.G) {  // next pieces in flight during this step's MFMAs
+            n0 = *(const f32x4*)(a.X + tiled_piece_offset((uint64_t)row0, 2 * j + 2 + h, a.G));
+            n1 = *(const f32x4*)(a.X + tiled_piece_offset((uint64_t)row1, 2 * j + 2 + h, a.G));
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            t00 = __builtin_amdgcn_mfma_f32_32x32x2f32(x0[s], x0[s], t00, 0, 0, 0);
+            t01 = __builtin_amdgcn_mfma_f32_32x32x2f32(x0[s], x1[s], t01, 0, 0, 0);
+            t11 = __builtin_amdgcn_mfma_f32_32x32x2f32(x1[s], x1[s], t11, 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int m = (i & 3) + 8 * (i >> 2) + 4 * h;  // C/D layout: row m, column r
+        gram[m * GP_LD + r] = t00[i];
+        gram[m * GP_LD + 32 + r] = t01[i];
+        gram[(32 + r) * GP_LD + m] = t01[i];
+        gram[(32 + m) * GP_LD + 32 + r] = t11[i];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    // this lane's Gram index is `lane`
+    const int32_t my_row = lane == 0 ? (int32_t)v : (lane < 32 ? c0 : c1);
+    const float sc = a.rowscale[my_row >= 0 ? my_row : (int32_t)v];
+    const float sc0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sc), 0));  // the node's
+    const unsigned long long valid = __ballot(my_row >= 0);
+    uint64_t kept = 0;
+    int nk = 0;
+    const float my_d0 = METRIC == 0 ? 1.0f - gram[lane] * sc * sc0 : fmaf(-2.0f, gram[lane], sc + sc0);
+    for (int c = 1; c < 64 && nk < a.limit; ++c) {
+        if (!((valid >> c) & 1ull)) break;
+        const float g = gram[c * GP_LD + lane];
+        const float scc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sc), c));
+        const float d0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_d0), c));
+        const float dcr = METRIC == 0 ? 1.0f - g * scc * sc : fmaf(-2.0f, g, scc + sc);
+        const bool bad = ((kept >> lane) & 1ull) && dcr < d0;
+        if (__ballot(bad) == 0ull) {
+            kept |= 1ull << c;
+            ++nk;
+        }
+    }
+    if (a.fill) {  // hnswlib keepPrunedConnections: top up with the nearest pruned ones
+        for (int c = 1; c < 64 && nk < a.limit; ++c) {
+            if (!((valid >> c) & 1ull)) break;
+            if (!((kept >> c) & 1ull)) {
+                kept |= 1ull << c;
+                ++nk;
+            }
+        }
+    }
+    const bool mine = (kept >> lane) & 1ull;
+    const int pos = __popcll(kept & ((1ull << lane) - 1ull));
+    int32_t* on = a.out_nbr + v * a.rw;
+    float* od = a.out_dist + v * a.rw;
+    if (mine) {
+        on[pos] = my_row;
+        od[pos] = my_d0;
+    }
+    for (int i = nk + lane; i < a.rw; i += 64) {
+        on[i] = -1;
+        od[i] = INFINITY;
+    }
+}
+
+hipError_t launch_graph_prune(int metric, const GraphPruneArgs& a, hipStream_t st) {
+    if (a.cw < 1 || a.cw > 63 || a.limit < 1 || a.limit > a.rw || a.rw > 64) return hipErrorInvalidValue;
+    if (a.n_nodes <= 0) return hipSuccess;
+    const dim3 grid((unsigned)((a.n_nodes + GP_WAVES - 1) / GP_WAVES));
+    if (metric == 0)
+        hipLaunchKernelGGL(graph_prune_kernel<0>, grid, dim3(64 * GP_WAVES), 0, st, a);
+    else
+        hipLaunchKernelGGL(graph_prune_kernel<1>, grid, dim3(64 * GP_WAVES), 0, st, a);
+    return hipGetLastError();
+}
+
+// The graph's row-major copy of the corpus, [n][Dp] fp32 (Dp = D rounded up to 32,
+// zero padded): a gathered row is Dp/32 whole 128-byte lines, where the tiled scan
+// layout scatters it over 16-byte pieces of 2 * G different lines.
+__global__ void graph_rows_kernel(const float* __restrict__ X, int G, int64_t n, int Dp, float* __restrict__ out) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int ppr = Dp >> 2;
+    if (t >= n * ppr) return;
+    const int64_t r = t / ppr;
+    const int p = (int)(t - r * ppr);
+    const f32x4 v = p < 2 * G ? *(const f32x4*)(X + tiled_piece_offset((uint64_t)r, p, G)) : f32x4{0.f, 0.f, 0.f, 0.f};
+    *(f32x4*)(out + r * Dp + 4 * p) = v;
+}
+
+hipError_t launch_graph_rows(const float* X, int G, int64_t n, int Dp, float* out, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    const int64_t total = n * (Dp >> 2);
+    hipLaunchKernelGGL(graph_rows_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, X, G, n, Dp, out);
+    return hipGetLastError();
 }
 
 hipError_t launch_graph_search(int metric, const GraphSearchArgs& a, int nq, hipStream_t st) {
     if (a.R > GS_R_MAX || a.ef > GS_EF_MAX || a.ef < 1 || a.k > a.ef) return hipErrorInvalidValue;
-    const size_t lds = (size_t)((a.D + 3) / 4 * 4) * 4 + (size_t)GS_VIS * 4;
+    if (a.Dp % 32 || a.Dp < a.D) return hipErrorInvalidValue;
+    const size_t lds = (size_t)a.Dp * 4 + (size_t)GS_VIS * 4;
     if (metric == 0)
         hipLaunchKernelGGL(graph_search_kernel<0>, dim3(nq), dim3(64 * GS_WAVES), lds, st, a);
     else

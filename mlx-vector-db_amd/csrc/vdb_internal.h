@@ -127,12 +127,25 @@ hipError_t launch_finalize_i64(int metric, const double* sk, const int64_t* si, 
 // Graph search (vdb_graph.hip): one workgroup per query, beam of ef over a [N][R]
 // int32 neighbour array (-1 = none), started from the best of n_entries entry rows.
 struct GraphSearchArgs {
-    const float* X; int G; int D; const float* rowscale; int64_t n_rows;
+    const float* rows; int Dp; int D; const float* rowscale; int64_t n_rows;  // rows: [n_rows][Dp] row-major
     const int32_t* nbr; int R; const int32_t* entries; int n_entries;
     const float* Q; int k; int ef;
     int64_t* out_lab; float* out_dist; unsigned long long* stats;
 };
 hipError_t launch_graph_search(int metric, const GraphSearchArgs& a, int nq, hipStream_t st);
+// row-major [n][Dp] copy of the tiled corpus for the graph's gathers (Dp % 32 == 0)
+hipError_t launch_graph_rows(const float* X, int G, int64_t n, int Dp, float* out, hipStream_t st);
+
+// Graph build: hnswlib's neighbour-selection heuristic per node over up to 63
+// candidates cand[v][0..cw) (nearest first, -1 padded at the tail); out_nbr /
+// out_dist [v][rw] get the kept rows (nearest first) and their distances
+// (cosine 1 - cos, L2 squared), -1 / +inf padded.  fill: top up with pruned ones.
+struct GraphPruneArgs {
+    const float* X; int G; const float* rowscale;
+    const int32_t* cand; int cw; int64_t n_nodes; int limit; int rw; int fill;
+    int32_t* out_nbr; float* out_dist;
+};
+hipError_t launch_graph_prune(int metric, const GraphPruneArgs& a, hipStream_t st);
 
 // Operator slot: full score matrix out[B][N] (fp32 reference arithmetic).
 hipError_t launch_similarity_matrix(const float* X, int64_t N, int D, const float* Q, int B, int metric,

@@ -273,3 +273,64 @@ def merge_topk(keys_lists: np.ndarray, idx_lists: np.ndarray, k: int):
         out_k[b, :order.size] = kb[order]
         out_i[b, :order.size] = ib[order]
     return out_k, out_i
+
+
+# ---------------------------------------------------------------------------------
+# Graph path (performance/hnsw_index.py:79-103 -> hnswlib knn_query).  hnswlib is
+# absent, so this restates its published level-0 search
+# (hnswalg.h searchBaseLayerST: a min-heap of candidates, a bounded max-heap of
+# the ef best results, a visited set; stop when the nearest unexpanded candidate
+# is farther than the worst result of a full set) over the same flat neighbour
+# array and entry rows the GPU path searches.  Parity for HNSW is unpinned: the
+# checks are recall against exact search and agreement with this restatement.
+# ---------------------------------------------------------------------------------
+def graph_search(vectors: np.ndarray, nbr: np.ndarray, entries: np.ndarray, query: np.ndarray, k: int, ef: int,
+                 metric: str = "cosine", inv_norms: np.ndarray | None = None):
+    """One query.  Returns (labels int64 [k] (-1 padded), distances fp32 [k] with
+    hnswlib conventions: cosine 1 - cos, l2 squared), plus the number of rows scored.
+    inv_norms: 1 / max(|x|, 1e-8) per row, precomputed once per corpus (cosine)."""
+    import heapq
+    V = np.asarray(vectors, np.float32)
+    q = np.asarray(query, np.float32).reshape(-1)
+    if metric == "cosine":
+        qn = q / max(float(np.linalg.norm(q)), 1e-8)
+        inv = inv_norms if inv_norms is not None else 1.0 / np.maximum(np.linalg.norm(V, axis=1), 1e-8)
+
+        def dist(rows):
+            return 1.0 - (V[rows] @ qn) * inv[rows]
+    else:
+        def dist(rows):
+            d = V[rows] - q
+            return np.einsum("ij,ij->i", d, d)
+    ent = np.asarray(entries, np.int64)
+    de = dist(ent)
+    visited = set(ent.tolist())
+    cand = [(float(d), int(r)) for d, r in zip(de, ent)]
+    heapq.heapify(cand)
+    res = [(-d, -r) for d, r in sorted(cand)[:ef]]  # max-heap on (dist, row)
+    heapq.heapify(res)
+    scored = len(ent)
+    while cand:
+        d, r = heapq.heappop(cand)
+        if len(res) >= ef and (d, r) > (-res[0][0], -res[0][1]):
+            break
+        nb = [int(x) for x in nbr[r] if x >= 0 and int(x) not in visited]
+        if not nb:
+            continue
+        visited.update(nb)
+        dn = dist(np.asarray(nb, np.int64))
+        scored += len(nb)
+        for dv, rv in zip(dn.tolist(), nb):
+            if len(res) < ef or (dv, rv) < (-res[0][0], -res[0][1]):
+                heapq.heappush(cand, (dv, rv))
+                heapq.heappush(res, (-dv, -rv))
+                if len(res) > ef:
+                    heapq.heappop(res)
+    best = sorted((-a, -b) for a, b in res)[:k]
+    labels = np.full(k, -1, np.int64)
+    dists = np.full(k, np.inf, np.float32)
+    for i, (dv, rv) in enumerate(best):
+        labels[i], dists[i] = rv, dv
+    if metric != "cosine":
+        dists = np.maximum(dists, 0.0)
+    return labels, dists, scored

@@ -14,7 +14,9 @@ ix = _vdb.NativeIndex(D, "cosine")
 ix.add(V)
 t = time.time()
 es, ei, ek = ix.search(Q, k, with_keys=True)
-for deg, knn in [(32, 32), (32, 64), (48, 48), (64, 64)]:
+cfgs = [tuple(map(int, c.split("/"))) for c in (sys.argv[3].split(",") if len(sys.argv) > 3 else ["32/32", "32/64", "48/48", "64/64"])]
+print(f"exact ground truth {time.time() - t:.2f}s", flush=True)
+for deg, knn in cfgs:
     t0 = time.time()
     g = _vdb.NativeGraph.build(ix, degree=deg, knn=knn)
     tb = time.time() - t0
