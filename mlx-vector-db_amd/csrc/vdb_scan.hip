@@ -116,11 +116,16 @@ __device__ __forceinline__ void compact_query(float* sc, uint32_t* ix, int* cnt,
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-// Corpus stream loads: every corpus byte is read once per launch, so they carry
-// the non-temporal policy (global_load_dwordx4 ... nt): C2 scan 587 -> 559 us,
-// measured A/B on MI355X.  Query tiles (re-read by every
-// workgroup from L2) keep the default policy.
-#define CORPUS_LD(p) __builtin_nontemporal_load((const f32x4*)(p))
+// Corpus stream loads.  With one query block (B <= 64) every corpus byte is read
+// once per launch: the non-temporal policy (global_load_dwordx4 ... nt) then gives
+// C2 587 -> 559 us.  With several query blocks the blocks of one row range share
+// its lines through the XCD's L2 (xcd_map), which nt defeats (C3 2.62 -> 3.12 ms,
+// C4 7.56 -> 8.89 ms): default policy there.  Measured A/B on MI355X.
+template <bool NT>
+__device__ __forceinline__ f32x4 corpus_ld(const float* p) {
+    if constexpr (NT) return __builtin_nontemporal_load((const f32x4*)p);
+    else return *(const f32x4*)p;
+}
 
 // Epilogue scoring of one step: scores replace the accumulators (cosine a * inv|x|,
 // L2 2a - |x|^2) and pend[rt][qt] gets the bits of the scores above the query's
@@ -250,7 +255,7 @@ __device__ __forceinline__ void group_mfma(const f32x4 (&x)[RT][PREC + 1], const
     }
 }
 
-template <int PREC, int METRIC, int QT, int RT, int PX, int PQ, int KP, int CAP, int PUB, int WPS>
+template <int PREC, int METRIC, int QT, int RT, int PX, int PQ, int KP, int CAP, int PUB, int WPS, bool NT>
 __global__ void __launch_bounds__(256, WPS)
 scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale, const uint32_t* __restrict__ mask,
                  const float* __restrict__ Qt, int G, int64_t N, int B, int64_t n_steps, int steps_per_wg,
@@ -329,7 +334,7 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
             for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
                 for (int pl = 0; pl < NPL; ++pl)
-                    xr[p][rt][pl] = CORPUS_LD(xs + p * GSTEP + pl * PLANE + rt * BLOCK_FLOATS + lane4);
+                    xr[p][rt][pl] = corpus_ld<NT>(xs + p * GSTEP + pl * PLANE + rt * BLOCK_FLOATS + lane4);
 #pragma unroll
         for (int p = 0; p < PQ; ++p)
 #pragma unroll
@@ -390,7 +395,7 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
             for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
                 for (int pl = 0; pl < NPL; ++pl)
-                    xr[p][rt][pl] = CORPUS_LD(xsrc + pl * PLANE + rt * BLOCK_FLOATS + lane4);
+                    xr[p][rt][pl] = corpus_ld<NT>(xsrc + pl * PLANE + rt * BLOCK_FLOATS + lane4);
 #pragma unroll
             for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
@@ -692,7 +697,7 @@ scan_topk_priv_kernel(const float* __restrict__ X, const float* __restrict__ row
             for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
                 for (int pl = 0; pl < NPL; ++pl)
-                    xr[p][rt][pl] = CORPUS_LD(xs + p * GSTEP + pl * PLANE + rt * BLOCK_FLOATS + lane4);
+                    xr[p][rt][pl] = corpus_ld<false>(xs + p * GSTEP + pl * PLANE + rt * BLOCK_FLOATS + lane4);
 #pragma unroll
         for (int p = 0; p < PQ; ++p)
 #pragma unroll
@@ -744,7 +749,7 @@ scan_topk_priv_kernel(const float* __restrict__ X, const float* __restrict__ row
             for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
                 for (int pl = 0; pl < NPL; ++pl)
-                    xr[p][rt][pl] = CORPUS_LD(xsrc + pl * PLANE + rt * BLOCK_FLOATS + lane4);
+                    xr[p][rt][pl] = corpus_ld<false>(xsrc + pl * PLANE + rt * BLOCK_FLOATS + lane4);
 #pragma unroll
             for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
@@ -1109,13 +1114,13 @@ hipError_t launch_pilot(int prec, int metric, int KP, const float* X, const floa
     return hipGetLastError();
 }
 
-template <int PREC, int METRIC, int QT, int RT, int PX, int PQ, int KP, int CAP, int PUB, int WPS>
+template <int PREC, int METRIC, int QT, int RT, int PX, int PQ, int KP, int CAP, int PUB, int WPS, bool NT>
 static hipError_t scan_dispatch(const float* X, const float* rowscale, const uint32_t* mask, const float* Qt, int G,
                                 int64_t N, int B, int n_qblocks, int64_t n_steps, int n_wg, int spw, float* gl_s,
                                 uint32_t* gl_i, uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr, uint32_t* gslots,
                                 hipStream_t st) {
     const int n_wg8 = (n_wg + 7) / 8 * 8;
-    hipLaunchKernelGGL((scan_topk_kernel<PREC, METRIC, QT, RT, PX, PQ, KP, CAP, PUB, WPS>), dim3(n_wg8 * n_qblocks),
+    hipLaunchKernelGGL((scan_topk_kernel<PREC, METRIC, QT, RT, PX, PQ, KP, CAP, PUB, WPS, NT>), dim3(n_wg8 * n_qblocks),
                        dim3(256), 0, st, X, rowscale, mask, Qt, G, N, B, n_steps, spw, n_qblocks, n_wg8, gl_s, gl_i,
                        gl_cnt, gl_cap, gthr, gslots);
     return hipGetLastError();
@@ -1128,13 +1133,17 @@ static hipError_t scan_dispatch(const float* X, const float* rowscale, const uin
 //          1: wave-private top-k for KP = 32 (scan_topk_priv_kernel), else as 0 with CAP 8 KP
 //          2: RT=2 PX=4 PQ=2, CAP 4 KP, 2 workgroups per CU (256 registers) for KP <= 64: one
 //             workgroup's epilogue overlaps the other's corpus stream
+// (PX = PQ = 6 or 8 for bf16x3 spill registers at 256 VGPRs: C2 -2% / -18%, C3 -7% / -12%.)
 // PQ = PX for bf16x3: loads retire in issue order (vmcnt), so a query load issued
 // PQ < PX groups ahead caps the usable corpus prefetch at PQ groups.
 static int variant_rt(int prec, int variant) {
     if (prec == PREC_FP32) return variant == 0 ? 2 : 4;
     return 2;
 }
-static int variant_px(int prec, int variant) { return (prec == PREC_FP32 && variant == 2) ? 8 : 4; }
+static int variant_px(int prec, int variant) {
+    if (prec == PREC_FP32) return variant == 2 ? 8 : 4;
+    return 4;
+}
 
 int scan_wgs_per_cu(int prec, int variant, int KP) {
     return (prec == PREC_BF16X3 && variant == 2 && KP <= 64) ? 2 : 1;
@@ -1143,12 +1152,13 @@ int scan_wgs_per_cu(int prec, int variant, int KP) {
 int scan_rows_per_step(int prec, int variant) { return 4 * 32 * variant_rt(prec, variant); }
 
 #ifdef VDB_STAMP
-constexpr int kMaxVariant = 3;  // 3: diagnostic, no insertion after the first step (wrong results)
+constexpr int kStampVariant = 9;  // diagnostic, no insertion after the first step (wrong results)
 #else
-constexpr int kMaxVariant = 2;
+constexpr int kStampVariant = -1;
 #endif
 bool scan_variant_ok(int prec, int variant, int G) {
-    return variant >= 0 && variant <= kMaxVariant && G % variant_px(prec, variant) == 0;
+    const int vmax = 2;
+    return ((variant >= 0 && variant <= vmax) || variant == kStampVariant) && G % variant_px(prec, variant) == 0;
 }
 
 hipError_t launch_scan_topk(int prec, int metric, int KP, int variant, const float* X, const float* rowscale,
@@ -1156,18 +1166,27 @@ hipError_t launch_scan_topk(int prec, int metric, int KP, int variant, const flo
                             int64_t n_steps, int n_wg, int spw, float* gl_s, uint32_t* gl_i, uint32_t* gl_cnt,
                             int64_t gl_cap, uint32_t* gthr, uint32_t* gslots, hipStream_t st) {
     if (!scan_variant_ok(prec, variant, G)) return hipErrorInvalidValue;
+#define VDB_SCAN_NT(P, M, QT, KPV, V, RT, PX, PQ, CAPV, PUB, W, NT)                                           \
+    if (prec == P && metric == M && KP == KPV && variant == V && (n_qblocks == 1) == NT)                       \
+        return scan_dispatch<P, M, QT, RT, PX, PQ, KPV, CAPV, PUB, W, NT>(X, rowscale, mask, Qt, G, N, B,         \
+                                                                        n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, \
+                                                                        gl_cnt, gl_cap, gthr, gslots, st);
+// VDB_SCAN: default load policy only; VDB_SCAN2: plus the non-temporal build for one query block
 #define VDB_SCAN(P, M, QT, KPV, V, RT, PX, PQ, CAPV, PUB, W)                                                     \
     if (prec == P && metric == M && KP == KPV && variant == V)                                                 \
-        return scan_dispatch<P, M, QT, RT, PX, PQ, KPV, CAPV, PUB, W>(X, rowscale, mask, Qt, G, N, B, n_qblocks, \
-                                                                    n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, \
-                                                                    gthr, gslots, st);
+        return scan_dispatch<P, M, QT, RT, PX, PQ, KPV, CAPV, PUB, W, false>(X, rowscale, mask, Qt, G, N, B,      \
+                                                                           n_qblocks, n_steps, n_wg, spw, gl_s,    \
+                                                                           gl_i, gl_cnt, gl_cap, gthr, gslots, st);
+#define VDB_SCAN2(P, M, QT, KPV, V, RT, PX, PQ, CAPV, PUB, W)                                                    \
+    VDB_SCAN_NT(P, M, QT, KPV, V, RT, PX, PQ, CAPV, PUB, W, true)                                              \
+    VDB_SCAN_NT(P, M, QT, KPV, V, RT, PX, PQ, CAPV, PUB, W, false)
 #define VDB_SCAN_ALL(M)                                                                                        \
-    VDB_SCAN(0, M, 2, 32, 0, 2, 4, 4, 128, 1, 2) VDB_SCAN(0, M, 2, 64, 0, 2, 4, 4, 128, 1, 2)                  \
+    VDB_SCAN2(0, M, 2, 32, 0, 2, 4, 4, 128, 1, 2) VDB_SCAN2(0, M, 2, 64, 0, 2, 4, 4, 128, 1, 2)                \
     VDB_SCAN(0, M, 2, 128, 0, 2, 4, 4, 256, 1, 1) VDB_SCAN(0, M, 1, 256, 0, 2, 4, 4, 512, 1, 1)                \
     VDB_SCAN(0, M, 2, 32, 1, 4, 4, 2, 128, 1, 2) VDB_SCAN(0, M, 2, 64, 1, 4, 4, 2, 128, 1, 2)                  \
     VDB_SCAN(0, M, 2, 32, 2, 4, 8, 2, 128, 1, 1) VDB_SCAN(0, M, 2, 64, 2, 4, 8, 2, 128, 1, 1)                  \
-    VDB_SCAN(1, M, 2, 32, 0, 2, 4, 4, 128, 1, 1) VDB_SCAN(1, M, 2, 64, 0, 2, 4, 4, 128, 1, 1)                  \
-    VDB_SCAN(1, M, 2, 128, 0, 2, 4, 4, 256, 1, 1) VDB_SCAN(1, M, 1, 256, 0, 2, 4, 4, 512, 1, 1)                \
+    VDB_SCAN2(1, M, 2, 32, 0, 2, 4, 4, 128, 1, 1) VDB_SCAN2(1, M, 2, 64, 0, 2, 4, 4, 128, 1, 1)                \
+    VDB_SCAN2(1, M, 2, 128, 0, 2, 4, 4, 256, 1, 1) VDB_SCAN(1, M, 1, 256, 0, 2, 4, 4, 512, 1, 1)               \
     VDB_SCAN(1, M, 2, 32, 1, 2, 4, 4, 256, 1, 1) VDB_SCAN(1, M, 2, 64, 1, 2, 4, 4, 256, 1, 1)                  \
     VDB_SCAN(1, M, 2, 128, 1, 2, 4, 4, 256, 1, 1) VDB_SCAN(1, M, 1, 256, 1, 2, 4, 4, 512, 1, 1)                \
     VDB_SCAN(1, M, 2, 32, 2, 2, 4, 2, 128, 1, 2) VDB_SCAN(1, M, 2, 64, 2, 2, 4, 2, 128, 1, 2)                  \
@@ -1175,9 +1194,11 @@ hipError_t launch_scan_topk(int prec, int metric, int KP, int variant, const flo
     VDB_SCAN_ALL(0)
     VDB_SCAN_ALL(1)
 #ifdef VDB_STAMP
-    VDB_SCAN(1, 0, 2, 32, 3, 2, 4, 4, 128, 2, 1)
+    VDB_SCAN(1, 0, 2, 32, 9, 2, 4, 4, 128, 2, 1)
 #endif
 #undef VDB_SCAN_ALL
+#undef VDB_SCAN2
+#undef VDB_SCAN_NT
 #undef VDB_SCAN
     return hipErrorInvalidValue;
 }
