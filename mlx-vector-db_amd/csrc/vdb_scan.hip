@@ -1,9 +1,10 @@
 // vdb_scan.hip — gfx950 kernels of the brute-force distance + top-k path.
 //
 // Pipeline for one search:
-//   prep_queries  -> scan_topk (fp32 MFMA candidate pass, fused per-WG top-KP)
-//   -> merge_lists (per-query top-KP over all WG lists)
-//   -> rerank (exact fp64 keys of the KP candidates, top-k, certificate)
+//   prep_queries -> pilot_scores + pilot_bound (seed the shared bound from sampled tiles)
+//   -> scan_topk (MFMA candidate pass, fp32 or bf16x3, fused per-WG top-KP, appended
+//      to global per-query candidate lists)
+//   -> finish (vdb_exact.hip: select top-KP, exact fp64 rerank, top-k, certificate)
 //   -> [rare] exact_scan + merge + finalize for queries whose certificate failed.
 //
 // Reference semantics restated here (file:line in /root/reference):
