@@ -13,6 +13,9 @@ on device, bit-identical to one GPU.  Default "weak" scaling keeps the work per
 GPU fixed: the global batch is B x N queries against the same corpus (each rank:
 B x N queries x N_rows/N rows); "strong" keeps the batch at B.
 
+Throughput (`value`): the K timed batches are queued back to back on the stream
+(device-memory searches return without a host wait) between two synchronises;
+latency (`p50_ms`) comes from a separate loop that waits for every batch.
 Rank 0 prints one JSON line: QPS (whole job), p50 batch latency, the roofline
 of the dominant kernel (the scan kernel, HIP-event timed inside the library on
 the stream it runs on) and, at N=1, the CPU baseline: the reference's batched
@@ -245,6 +248,7 @@ def main():
                     help="candidate-pass arithmetic (results identical; DESIGN.md §3)")
     ap.add_argument("--scan-variant", type=int, default=None, help="candidate-pass kernel variant (tuning)")
     ap.add_argument("--n-wg", type=int, default=None, help="candidate-pass workgroups (tuning)")
+    ap.add_argument("--pilot-tiles", type=int, default=None, help="row tiles sampled by the pilot bound (tuning)")
     ap.add_argument("--rows", type=int, default=None, help="override the corpus rows (exploration only)")
     ap.add_argument("--graph-knn", type=int, default=None, help="c5: kNN candidates per row for the build")
     ap.add_argument("--pmc-json", default=None,
@@ -276,6 +280,8 @@ def main():
         ix.set_param("scan_variant" if args.precision == "fp32" else "scan_variant_bf16x3", args.scan_variant)
     if args.n_wg is not None:
         ix.set_param("n_wg", args.n_wg)
+    if args.pilot_tiles is not None:
+        ix.set_param("pilot_tiles", args.pilot_tiles)
     ix.reserve(n_local)
     host_parts = []
     for s in range(lo, hi, 8 * CHUNK_ROWS):
@@ -302,18 +308,17 @@ def main():
         step()
     torch.cuda.synchronize()
 
+    # Throughput (value): K batches queued back to back on the stream, as a server
+    # keeps the device fed; device-memory searches return without a host wait
+    # (DESIGN.md §3), so the host runs ahead and no step waits for its launch.
     ix.set_param("timing", 1)
     scan0, pipe0, n0 = ix.stat("scan_ns"), ix.stat("pipeline_ns"), ix.stat("timed_searches")
-    lat = []
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     for _ in range(args.steps):
-        t0 = time.perf_counter()
         step()
-        torch.cuda.synchronize()
-        lat.append(time.perf_counter() - t0)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -322,6 +327,13 @@ def main():
     scan_ms = (ix.stat("scan_ns") - scan0) / 1e6 / max(n_t, 1)
     pipe_ms = (ix.stat("pipeline_ns") - pipe0) / 1e6 / max(n_t, 1)
     ix.set_param("timing", 0)
+    # Latency (p50_ms): one batch at a time, each waited for
+    lat = []
+    for _ in range(min(args.steps, 50)):
+        t0 = time.perf_counter()
+        step()
+        torch.cuda.synchronize()
+        lat.append(time.perf_counter() - t0)
     if world > 1:
         t = torch.tensor([elapsed, scan_ms, pipe_ms, float(np.median(lat))], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

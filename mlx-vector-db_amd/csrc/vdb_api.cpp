@@ -47,6 +47,7 @@ int set_error(int code, const char* fmt, ...) {
     } while (0)
 
 constexpr int64_t kRowAlign = ROW_ALIGN;   // capacity granule, a multiple of every scan step
+constexpr size_t kGatedExactBytes = 256u << 20;  // device-gated fallback lists sized for every query of a batch
 constexpr int kMaxApproxK = 200;          // k above this uses the exact path
 
 inline int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
@@ -76,7 +77,12 @@ struct Workspace {
     size_t exact_bytes = 0;
     int* host_flag = nullptr;  // pinned
     hipEvent_t done = nullptr;
-    hipEvent_t tev[4] = {nullptr, nullptr, nullptr, nullptr};  // timing: scan start / end / rerank end / pilot start
+    // timing (vdb_index_set_param "timing"): a ring of event sets, one per timed search
+    // (scan start / scan end / finish end / pilot start), read once complete, so timed
+    // device-memory searches can be queued back to back without a host wait
+    static constexpr int kTRing = 64;
+    hipEvent_t tring[kTRing][4] = {};
+    int t_head = 0, t_pending = 0;
     bool busy = false;
     bool used = false;
 };
@@ -111,6 +117,7 @@ struct vdb_index {
     // stats
     std::atomic<int64_t> n_searches{0}, n_queries{0}, n_fallback{0}, n_overflow{0};
     std::atomic<int64_t> scan_ns{0}, pipe_ns{0}, n_timed{0};
+    unsigned long long* d_totals = nullptr;  // device: flagged / overflowed queries of device-gated searches
     std::shared_mutex mu;  // add/clear/reserve exclusive; search shared
     std::mutex ws_mu;
     std::vector<Workspace*> pool;
@@ -195,6 +202,34 @@ void release_ws(vdb_index* ix, Workspace* w, hipStream_t st) {
     w->busy = false;
 }
 
+// Accumulate the timing events of a search whose host side returned without
+// waiting for the device (device-gated fallback).
+// Read the `n` oldest pending event sets of the ring (waiting for them if needed).
+int flush_timing(vdb_index* ix, Workspace* w, int n = Workspace::kTRing) {
+    while (w->t_pending > 0 && n-- > 0) {
+        hipEvent_t* ev = w->tring[(w->t_head - w->t_pending + Workspace::kTRing) % Workspace::kTRing];
+        HIP_TRY(hipEventSynchronize(ev[2]));
+        float ms_scan = 0.f, ms_pipe = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms_scan, ev[0], ev[1]));
+        HIP_TRY(hipEventElapsedTime(&ms_pipe, ev[3], ev[2]));
+        ix->scan_ns += (int64_t)(ms_scan * 1e6);
+        ix->pipe_ns += (int64_t)(ms_pipe * 1e6);
+        ix->n_timed++;
+        w->t_pending--;
+    }
+    return VDB_OK;
+}
+
+int flush_all_timing(vdb_index* ix) {
+    std::lock_guard<std::mutex> g(ix->ws_mu);
+    for (Workspace* w : ix->pool)
+        if (!w->busy) {
+            const int rc = flush_timing(ix, w);
+            if (rc) return rc;
+        }
+    return VDB_OK;
+}
+
 // Make the workspace at least `bytes` large and stream-ordered after its last use.
 int ws_reserve(Workspace* w, size_t bytes, hipStream_t st) {
     if (w->used && w->done) HIP_TRY(hipStreamWaitEvent(st, w->done, 0));
@@ -232,13 +267,25 @@ bool all_finite(const float* p, int64_t n) {
 }
 
 // Exact full scan for queries qlist[0..nq) (device list) -> writes outputs.
+// Bytes of the exact path's lists for nq queries (device-gated form: one list per CU).
+size_t exact_bytes(vdb_index* ix, int nq, int k, bool gated) {
+    const int KE = std::max(32, next_pow2(k));
+    const int64_t n_wg = std::min<int64_t>(std::max<int64_t>(1, ix->n_cu * (gated ? 1 : 2)),
+                                           std::max<int64_t>(1, ix->count / 256));
+    return (size_t)nq * n_wg * KE * (sizeof(double) + sizeof(uint32_t)) + (size_t)nq * KE * 12 + 4096;
+}
+
+// Exact scan of the queries qlist[0..nq) (or 0..nq).  Device-gated form (qcount_dev):
+// the flagged count is read on the device, nq is the capacity, and nothing runs
+// when no query was flagged.
 int run_exact(vdb_index* ix, Workspace* w, const float* Qd, const double* qn64, const int* qlist_dev, int nq, int k,
               const uint32_t* mask_dev, float* out_s, int64_t* out_i, double* out_k, int64_t index_offset,
-              hipStream_t st) {
+              hipStream_t st, const int* qcount_dev = nullptr, const int* ovf_dev = nullptr) {
     const int KE = std::max(32, next_pow2(k));
     const int64_t N = ix->count;
-    // ~8 workgroups per CU of rows, at least 64 rows per wave
-    int n_wg = (int)std::min<int64_t>(std::max<int64_t>(1, ix->n_cu * 2), std::max<int64_t>(1, N / 256));
+    const bool gated = qcount_dev != nullptr;
+    // ~2 workgroups per CU of rows (gated: 1), at least 64 rows per wave
+    int n_wg = (int)std::min<int64_t>(std::max<int64_t>(1, ix->n_cu * (gated ? 1 : 2)), std::max<int64_t>(1, N / 256));
     const int64_t rpw = (N + n_wg - 1) / n_wg;
     n_wg = (int)((N + rpw - 1) / rpw);
     const int n_lists = n_wg;
@@ -252,9 +299,10 @@ int run_exact(vdb_index* ix, Workspace* w, const float* Qd, const double* qn64, 
     double* mk = c.take<double>((size_t)nq * KE);
     uint32_t* mi = c.take<uint32_t>((size_t)nq * KE);
     HIP_TRY(launch_exact_scan(ix->metric, KE, Qd, qn64, qlist_dev, nq, ix->X, ix->G, ix->dim, ix->nrm64, mask_dev, N,
-                              n_wg, rpw, lk, li, st));
-    HIP_TRY(launch_merge_f64_u32(KE, lk, li, n_lists, KE, (int64_t)n_lists * KE, KE, nq, mk, mi, st));
-    HIP_TRY(launch_finalize_u32(ix->metric, mk, mi, KE, nq, qlist_dev, k, index_offset, out_s, out_i, out_k, st));
+                              n_wg, rpw, lk, li, st, qcount_dev, ovf_dev, gated ? ix->d_totals : nullptr));
+    HIP_TRY(launch_merge_f64_u32(KE, lk, li, n_lists, KE, (int64_t)n_lists * KE, KE, nq, mk, mi, st, qcount_dev));
+    HIP_TRY(launch_finalize_u32(ix->metric, mk, mi, KE, nq, qlist_dev, k, index_offset, out_s, out_i, out_k, st,
+                                qcount_dev));
     return VDB_OK;
 }
 
@@ -318,8 +366,9 @@ int32_t vdb_index_destroy(vdb_index* ix) {
         if (w->exact) (void)hipFree(w->exact);
         if (w->host_flag) (void)hipHostFree(w->host_flag);
         if (w->done) (void)hipEventDestroy(w->done);
-        for (int e = 0; e < 4; ++e)
-            if (w->tev[e]) (void)hipEventDestroy(w->tev[e]);
+        for (int r = 0; r < Workspace::kTRing; ++r)
+            for (int e = 0; e < 4; ++e)
+                if (w->tring[r][e]) (void)hipEventDestroy(w->tring[r][e]);
         delete w;
     }
     if (ix->X) (void)hipFree(ix->X);
@@ -328,6 +377,7 @@ int32_t vdb_index_destroy(vdb_index* ix) {
     if (ix->inv32) (void)hipFree(ix->inv32);
     if (ix->sq32) (void)hipFree(ix->sq32);
     if (ix->d_xmax) (void)hipFree(ix->d_xmax);
+    if (ix->d_totals) (void)hipFree(ix->d_totals);
     if (ix->stream) (void)hipStreamDestroy(ix->stream);
     delete ix;
     return VDB_OK;
@@ -390,13 +440,25 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
     return VDB_OK;
 }
 
-int32_t vdb_index_get_stat(const vdb_index* ix, const char* name, int64_t* value) {
-    if (!ix || !name || !value) return set_error(VDB_ERR_INVALID, "NULL argument");
+int32_t vdb_index_get_stat(const vdb_index* cix, const char* name, int64_t* value) {
+    if (!cix || !name || !value) return set_error(VDB_ERR_INVALID, "NULL argument");
+    vdb_index* ix = const_cast<vdb_index*>(cix);  // pending device-side counts are folded in
     std::string n(name);
+    unsigned long long dt[2] = {0, 0};
+    if ((n == "fallback_queries" || n == "overflow_queries") && ix->d_totals) {
+        HIP_TRY(hipSetDevice(ix->device));
+        HIP_TRY(hipDeviceSynchronize());
+        HIP_TRY(hipMemcpy(dt, ix->d_totals, sizeof(dt), hipMemcpyDeviceToHost));
+    }
+    if (n == "scan_ns" || n == "pipeline_ns" || n == "timed_searches") {
+        HIP_TRY(hipSetDevice(ix->device));
+        const int rc = flush_all_timing(ix);
+        if (rc) return rc;
+    }
     if (n == "searches") *value = ix->n_searches.load();
     else if (n == "queries") *value = ix->n_queries.load();
-    else if (n == "fallback_queries") *value = ix->n_fallback.load();
-    else if (n == "overflow_queries") *value = ix->n_overflow.load();
+    else if (n == "fallback_queries") *value = ix->n_fallback.load() + (int64_t)dt[0];
+    else if (n == "overflow_queries") *value = ix->n_overflow.load() + (int64_t)dt[1];
     else if (n == "capacity") *value = ix->cap_rows;
     else if (n == "scan_ns") *value = ix->scan_ns.load();
     else if (n == "pipeline_ns") *value = ix->pipe_ns.load();
@@ -631,10 +693,18 @@ int32_t vdb_index_search(vdb_index* ix, const float* queries, int32_t B, int32_t
         int n_flag = 0;
         if (!exact_all) {
             const bool timed = ix->timing != 0;
+            hipEvent_t* tev = nullptr;
             if (timed) {
+                if (w->t_pending == Workspace::kTRing) {  // ring full: read the oldest set
+                    const int frc = flush_timing(ix, w, 1);
+                    if (frc) return frc;
+                }
+                tev = w->tring[w->t_head];
+                w->t_head = (w->t_head + 1) % Workspace::kTRing;
+                w->t_pending++;
                 for (int e = 0; e < 4; ++e)
-                    if (!w->tev[e]) HIP_TRY(hipEventCreate(&w->tev[e]));
-                HIP_TRY(hipEventRecord(w->tev[3], st));
+                    if (!tev[e]) HIP_TRY(hipEventCreate(&tev[e]));
+                HIP_TRY(hipEventRecord(tev[3], st));
             }
             const float* rowscale = ix->metric == 0 ? ix->inv32 : ix->sq32;
             const float* Xscan = prec == PREC_FP32 ? ix->X : ix->Xs;
@@ -643,14 +713,14 @@ int32_t vdb_index_search(vdb_index* ix, const float* queries, int32_t B, int32_t
                                      pslots, gthr, st));
             // scan_ns times the scan kernel alone (the roofline's kernel); pipeline_ns
             // everything from the pilot to the rerank
-            if (timed) HIP_TRY(hipEventRecord(w->tev[0], st));
+            if (timed) HIP_TRY(hipEventRecord(tev[0], st));
             if (priv)
                 HIP_TRY(launch_scan_topk_priv(prec, ix->metric, KP, Xscan, rowscale, md, Qt, Gs, N, B, n_qblocks,
                                               n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, st));
             else
                 HIP_TRY(launch_scan_topk(prec, ix->metric, KP, variant, Xscan, rowscale, md, Qt, Gs, N, B, n_qblocks,
                                          n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, st));
-            if (timed) HIP_TRY(hipEventRecord(w->tev[1], st));
+            if (timed) HIP_TRY(hipEventRecord(tev[1], st));
             FinishArgs fa;
             fa.gl_s = gl_s; fa.gl_i = gl_i; fa.gl_cnt = gl_cnt; fa.gl_cap = gl_cap;
             fa.Q = Qd; fa.qn64 = qn64; fa.X = ix->X; fa.G = ix->G; fa.D = D; fa.nrm64 = ix->nrm64; fa.k = k;
@@ -666,19 +736,27 @@ int32_t vdb_index_search(vdb_index* ix, const float* queries, int32_t B, int32_t
             fa.out_s = out_s; fa.out_i = out_i; fa.out_k = out_k; fa.index_offset = index_offset;
             fa.flag_count = flags; fa.flag_list = flags + 1; fa.gthr = gthr; fa.overflow_count = flags + B + 1;
             HIP_TRY(launch_finish(ix->metric, KP, fa, B, st));
-            if (timed) HIP_TRY(hipEventRecord(w->tev[2], st));
+            if (timed) HIP_TRY(hipEventRecord(tev[2], st));
+            // Device-memory searches do not wait for the certificate: the exact path is
+            // launched gated on the device's flag count (nothing runs when no query was
+            // flagged), so the call returns with the whole search queued.
+            if (mem == VDB_MEM_DEVICE && exact_bytes(ix, B, k, true) <= kGatedExactBytes) {
+                if (!ix->d_totals) {
+                    HIP_TRY(hipMalloc(&ix->d_totals, 2 * sizeof(unsigned long long)));
+                    HIP_TRY(hipMemsetAsync(ix->d_totals, 0, 2 * sizeof(unsigned long long), st));
+                }
+                rc = run_exact(ix, w, Qd, qn64, flags + 1, B, k, md, out_s, out_i, out_k, index_offset, st, flags,
+                               flags + B + 1);
+                return rc;
+            }
             HIP_TRY(hipMemcpyAsync(w->host_flag, flags, sizeof(int), hipMemcpyDeviceToHost, st));
             HIP_TRY(hipMemcpyAsync(w->host_flag + 1, flags + B + 1, sizeof(int), hipMemcpyDeviceToHost, st));
             HIP_TRY(hipStreamSynchronize(st));
             n_flag = w->host_flag[0];
             ix->n_overflow += w->host_flag[1];
             if (timed) {
-                float ms_scan = 0.f, ms_pipe = 0.f;
-                HIP_TRY(hipEventElapsedTime(&ms_scan, w->tev[0], w->tev[1]));
-                HIP_TRY(hipEventElapsedTime(&ms_pipe, w->tev[3], w->tev[2]));
-                ix->scan_ns += (int64_t)(ms_scan * 1e6);
-                ix->pipe_ns += (int64_t)(ms_pipe * 1e6);
-                ix->n_timed++;
+                const int frc = flush_timing(ix, w);
+                if (frc) return frc;
             }
             if (n_flag > 0) {
                 ix->n_fallback += n_flag;

@@ -442,57 +442,75 @@ __global__ void __launch_bounds__(256)
 exact_scan_kernel(const float* __restrict__ Q, const double* __restrict__ qn64, const int* __restrict__ qlist,
                   const float* __restrict__ X, int G, int D, const double* __restrict__ nrm64,
                   const uint32_t* __restrict__ mask, int64_t N, int64_t rows_per_wg, int KE,
-                  double* __restrict__ lk, uint32_t* __restrict__ li) {
+                  double* __restrict__ lk, uint32_t* __restrict__ li, const int* __restrict__ qcount, int nq_max,
+                  const int* __restrict__ ovf, unsigned long long* __restrict__ totals) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int cap = WaveTopK<double, uint32_t>::capacity(KE);
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
     double* bk = reinterpret_cast<double*>(smem) + (size_t)wv * cap;
     uint32_t* bi = reinterpret_cast<uint32_t*>(smem + (size_t)4 * cap * sizeof(double)) + (size_t)wv * cap;
-    const int qi = blockIdx.y;
-    const int b = qlist ? qlist[qi] : qi;
-    const float* q = Q + (int64_t)b * D;
-    const double qn = qn64[b];
-    const int64_t r0 = (int64_t)blockIdx.x * rows_per_wg;
-    const int64_t r1 = r0 + rows_per_wg < N ? r0 + rows_per_wg : N;
-    WaveTopK<double, uint32_t> tk;
-    tk.init(bk, bi, KE);
-    for (int64_t r = r0 + wv; r < r1; r += 4) {
-        if (mask && !((mask[r >> 5] >> (r & 31)) & 1u)) continue;
-        const double key = exact_key<METRIC>(q, qn, X, G, D, (uint64_t)r, nrm64[r]);
-        tk.offer(lane == 0, key, (uint32_t)r);
-    }
-    tk.finish();
-    __syncthreads();
-    if (wv != 0) return;
-    for (int w = 1; w < 4; ++w) {
-        const double* ok = reinterpret_cast<double*>(smem) + (size_t)w * cap;
-        const uint32_t* oi = reinterpret_cast<uint32_t*>(smem + (size_t)4 * cap * sizeof(double)) + (size_t)w * cap;
-        for (int e0 = 0; e0 < KE; e0 += 64) {
-            const int e = e0 + lane;
-            const bool in = e < KE && oi[e] != 0xFFFFFFFFu;
-            tk.offer(in, in ? ok[e] : -INFINITY, in ? oi[e] : 0xFFFFFFFFu);
+    // device-gated launch (qcount): the flagged queries are known only on the device;
+    // query slots qi = blockIdx.y, + gridDim.y, ... below min(*qcount, nq_max)
+    int nq = (int)gridDim.y;
+    if (qcount) {
+        const int c = *qcount;
+        nq = c < nq_max ? c : nq_max;
+        if (totals && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+            if (c) atomicAdd(totals, (unsigned long long)c);
+            if (ovf && *ovf) atomicAdd(totals + 1, (unsigned long long)*ovf);
         }
     }
-    tk.finish();
-    const size_t base = ((size_t)qi * gridDim.x + blockIdx.x) * KE;
-    for (int e = lane; e < KE; e += 64) {
-        lk[base + e] = bk[e];
-        li[base + e] = bi[e];
+    const int64_t r0 = (int64_t)blockIdx.x * rows_per_wg;
+    const int64_t r1 = r0 + rows_per_wg < N ? r0 + rows_per_wg : N;
+    for (int qi = blockIdx.y; qi < nq; qi += gridDim.y) {
+        const int b = qlist ? qlist[qi] : qi;
+        const float* q = Q + (int64_t)b * D;
+        const double qn = qn64[b];
+        WaveTopK<double, uint32_t> tk;
+        tk.init(bk, bi, KE);
+        for (int64_t r = r0 + wv; r < r1; r += 4) {
+            if (mask && !((mask[r >> 5] >> (r & 31)) & 1u)) continue;
+            const double key = exact_key<METRIC>(q, qn, X, G, D, (uint64_t)r, nrm64[r]);
+            tk.offer(lane == 0, key, (uint32_t)r);
+        }
+        tk.finish();
+        __syncthreads();
+        if (wv == 0) {
+            for (int w = 1; w < 4; ++w) {
+                const double* ok = reinterpret_cast<double*>(smem) + (size_t)w * cap;
+                const uint32_t* oi = reinterpret_cast<uint32_t*>(smem + (size_t)4 * cap * sizeof(double)) + (size_t)w * cap;
+                for (int e0 = 0; e0 < KE; e0 += 64) {
+                    const int e = e0 + lane;
+                    const bool in = e < KE && oi[e] != 0xFFFFFFFFu;
+                    tk.offer(in, in ? ok[e] : -INFINITY, in ? oi[e] : 0xFFFFFFFFu);
+                }
+            }
+            tk.finish();
+            const size_t base = ((size_t)qi * gridDim.x + blockIdx.x) * KE;
+            for (int e = lane; e < KE; e += 64) {
+                lk[base + e] = bk[e];
+                li[base + e] = bi[e];
+            }
+        }
+        __syncthreads();  // the LDS buffers are reused by the next query slot
     }
 }
 
 hipError_t launch_exact_scan(int metric, int KE, const float* Q, const double* qn64, const int* qlist, int nq,
                              const float* X, int G, int D, const double* nrm64, const uint32_t* mask, int64_t N,
-                             int n_wg, int64_t rows_per_wg, double* lk, uint32_t* li, hipStream_t st) {
+                             int n_wg, int64_t rows_per_wg, double* lk, uint32_t* li, hipStream_t st,
+                             const int* qcount, const int* ovf, unsigned long long* totals) {
     const size_t lds = (size_t)4 * WaveTopK<double, uint32_t>::capacity(KE) * (sizeof(double) + sizeof(uint32_t));
     if (lds > 160 * 1024) return hipErrorInvalidValue;
+    // gated: a few query slots per row range, each looping over the flagged queries
+    const dim3 grid(n_wg, qcount ? (nq < 4 ? nq : 4) : nq);
     if (metric == 0)
-        hipLaunchKernelGGL((exact_scan_kernel<0>), dim3(n_wg, nq), dim3(256), lds, st, Q, qn64, qlist, X, G, D, nrm64,
-                           mask, N, rows_per_wg, KE, lk, li);
+        hipLaunchKernelGGL((exact_scan_kernel<0>), grid, dim3(256), lds, st, Q, qn64, qlist, X, G, D, nrm64, mask, N,
+                           rows_per_wg, KE, lk, li, qcount, nq, ovf, totals);
     else
-        hipLaunchKernelGGL((exact_scan_kernel<1>), dim3(n_wg, nq), dim3(256), lds, st, Q, qn64, qlist, X, G, D, nrm64,
-                           mask, N, rows_per_wg, KE, lk, li);
+        hipLaunchKernelGGL((exact_scan_kernel<1>), grid, dim3(256), lds, st, Q, qn64, qlist, X, G, D, nrm64, mask, N,
+                           rows_per_wg, KE, lk, li, qcount, nq, ovf, totals);
     return hipGetLastError();
 }
 

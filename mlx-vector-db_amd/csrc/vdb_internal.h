@@ -104,15 +104,20 @@ hipError_t launch_finish(int metric, int KP, const FinishArgs& a, int B, hipStre
 
 // Exact fp64 scan of the whole corpus for the queries in qlist[0..nq):
 // per-workgroup sorted top-KE lists [nq][n_wg][KE] (fp64 keys, local rows).
+// Device-gated form (qcount != nullptr): the flagged queries qlist[0 .. *qcount) are
+// only known on the device; nq is then the most the lists have room for, and block
+// (0, 0) adds *qcount / *ovf to the cumulative totals[0] / totals[1].
 hipError_t launch_exact_scan(int metric, int KE, const float* Q, const double* qn64, const int* qlist, int nq,
                              const float* X, int G, int D, const double* nrm64, const uint32_t* mask,
                              int64_t N, int n_wg, int64_t rows_per_wg,
-                             double* lk, uint32_t* li, hipStream_t st);
+                             double* lk, uint32_t* li, hipStream_t st, const int* qcount = nullptr,
+                             const int* ovf = nullptr, unsigned long long* totals = nullptr);
 
 // Merge sorted fp64-key lists.  Element (q, j, e) lives at q*sq + j*sj + e, lists
 // have Lk entries; output [nq][KP] sorted.
 hipError_t launch_merge_f64_u32(int KP, const double* lk, const uint32_t* li, int n_lists, int Lk,
-                                int64_t sq, int64_t sj, int nq, double* out_k, uint32_t* out_i, hipStream_t st);
+                                int64_t sq, int64_t sj, int nq, double* out_k, uint32_t* out_i, hipStream_t st,
+                                const int* qcount = nullptr);
 hipError_t launch_merge_f64_i64(int KP, const double* lk, const int64_t* li, int n_lists, int Lk,
                                 int64_t sq, int64_t sj, int nq, double* out_k, int64_t* out_i, hipStream_t st);
 
@@ -120,7 +125,7 @@ hipError_t launch_merge_f64_i64(int KP, const double* lk, const int64_t* li, int
 // sorted [nq][KP] fp64-key lists.
 hipError_t launch_finalize_u32(int metric, const double* sk, const uint32_t* si, int KP, int nq, const int* qmap,
                                int k, int64_t index_offset, float* out_s, int64_t* out_i, double* out_k,
-                               hipStream_t st);
+                               hipStream_t st, const int* qcount = nullptr);
 hipError_t launch_finalize_i64(int metric, const double* sk, const int64_t* si, int KP, int nq, const int* qmap,
                                int k, float* out_s, int64_t* out_i, double* out_k, hipStream_t st);
 

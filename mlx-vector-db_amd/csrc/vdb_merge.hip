@@ -81,7 +81,8 @@ __device__ __attribute__((noinline)) void sort_store_prefix(const K* bk, const I
 template <typename K, typename I>
 __global__ void __launch_bounds__(256)
 merge_lists_kernel(const K* __restrict__ ls, const I* __restrict__ li, int n_lists, int Lk, int64_t sq, int64_t sj,
-                   int KP, K* __restrict__ out_k, I* __restrict__ out_i) {
+                   int KP, K* __restrict__ out_k, I* __restrict__ out_i, const int* __restrict__ qcount) {
+    if (qcount && (int)blockIdx.x >= *qcount) return;  // device-gated launch: only the flagged queries
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // LDS: MERGE_BUF survivors (select path) or the WaveTopK buffer (stream path)
     K* s_k = reinterpret_cast<K*>(smem);
@@ -193,12 +194,12 @@ merge_lists_kernel(const K* __restrict__ ls, const I* __restrict__ li, int n_lis
 
 template <typename K, typename I>
 static hipError_t merge_launch(int KP, const K* lk, const I* li, int n_lists, int Lk, int64_t sq, int64_t sj, int nq,
-                               K* ok, I* oi, hipStream_t st) {
+                               K* ok, I* oi, hipStream_t st, const int* qcount = nullptr) {
     if (KP < 32 || KP > 4096 || (KP & (KP - 1))) return hipErrorInvalidValue;
     const int cap = std::max(WaveTopK<K, I>::capacity(KP), MERGE_BUF);
     const size_t lds = (size_t)cap * (sizeof(K) + sizeof(I));
     hipLaunchKernelGGL((merge_lists_kernel<K, I>), dim3(nq), dim3(256), lds, st, lk, li, n_lists, Lk, sq, sj, KP, ok,
-                       oi);
+                       oi, qcount);
     return hipGetLastError();
 }
 
@@ -208,8 +209,8 @@ hipError_t launch_merge_f32(int KP, const float* ls, const uint32_t* li, int n_l
 }
 
 hipError_t launch_merge_f64_u32(int KP, const double* lk, const uint32_t* li, int n_lists, int Lk, int64_t sq,
-                                int64_t sj, int nq, double* out_k, uint32_t* out_i, hipStream_t st) {
-    return merge_launch<double, uint32_t>(KP, lk, li, n_lists, Lk, sq, sj, nq, out_k, out_i, st);
+                                int64_t sj, int nq, double* out_k, uint32_t* out_i, hipStream_t st, const int* qcount) {
+    return merge_launch<double, uint32_t>(KP, lk, li, n_lists, Lk, sq, sj, nq, out_k, out_i, st, qcount);
 }
 
 hipError_t launch_merge_f64_i64(int KP, const double* lk, const int64_t* li, int n_lists, int Lk, int64_t sq,
@@ -223,10 +224,11 @@ __global__ void __launch_bounds__(256) finalize_kernel(int metric, const double*
                                                        const I* __restrict__ si, int KP, int nq,
                                                        const int* __restrict__ qmap, int k, int64_t index_offset,
                                                        float* __restrict__ out_s, int64_t* __restrict__ out_i,
-                                                       double* __restrict__ out_k) {
+                                                       double* __restrict__ out_k, const int* __restrict__ qcount) {
     const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (t >= (int64_t)nq * k) return;
     const int qi = (int)(t / k);
+    if (qcount && qi >= *qcount) return;  // device-gated launch
     const int e = (int)(t % k);
     const int b = qmap ? qmap[qi] : qi;
     const double key = sk[(size_t)qi * KP + e];
@@ -239,10 +241,10 @@ __global__ void __launch_bounds__(256) finalize_kernel(int metric, const double*
 
 hipError_t launch_finalize_u32(int metric, const double* sk, const uint32_t* si, int KP, int nq, const int* qmap,
                                int k, int64_t index_offset, float* out_s, int64_t* out_i, double* out_k,
-                               hipStream_t st) {
+                               hipStream_t st, const int* qcount) {
     const int64_t n = (int64_t)nq * k;
     hipLaunchKernelGGL(finalize_kernel<uint32_t>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, metric, sk, si,
-                       KP, nq, qmap, k, index_offset, out_s, out_i, out_k);
+                       KP, nq, qmap, k, index_offset, out_s, out_i, out_k, qcount);
     return hipGetLastError();
 }
 
@@ -250,7 +252,7 @@ hipError_t launch_finalize_i64(int metric, const double* sk, const int64_t* si, 
                                int k, float* out_s, int64_t* out_i, double* out_k, hipStream_t st) {
     const int64_t n = (int64_t)nq * k;
     hipLaunchKernelGGL(finalize_kernel<int64_t>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, metric, sk, si,
-                       KP, nq, qmap, k, (int64_t)0, out_s, out_i, out_k);
+                       KP, nq, qmap, k, (int64_t)0, out_s, out_i, out_k, (const int*)nullptr);
     return hipGetLastError();
 }
 

@@ -256,8 +256,8 @@ __device__ __forceinline__ void group_mfma(const f32x4 (&x)[RT][PREC + 1], const
     }
 }
 
-template <int PREC, int METRIC, int QT, int RT, int PX, int PQ, int KP, int CAP, int PUB, int WPS, bool NT>
-__global__ void __launch_bounds__(256, WPS)
+template <int PREC, int METRIC, int QT, int RT, int PX, int PQ, int KP, int CAP, int PUB, int WPS, bool NT, int NW>
+__global__ void __launch_bounds__(64 * NW, WPS)
 scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale, const uint32_t* __restrict__ mask,
                  const float* __restrict__ Qt, int G, int64_t N, int B, int64_t n_steps, int steps_per_wg,
                  int n_qb, int n_wg_all, float* __restrict__ gl_s, uint32_t* __restrict__ gl_i,
@@ -270,8 +270,8 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
     __shared__ uint32_t s_ix[QB * CAP];
     __shared__ int s_cnt[QB];
     __shared__ float s_thr[QB];
-    __shared__ uint32_t s_best[4][QB];  // per wave: order key of the best score appended so far (PUB)
-    __shared__ uint32_t s_pub[4][QB];   // ... and of the last one published
+    __shared__ uint32_t s_best[NW][QB];  // per wave: order key of the best score appended so far (PUB)
+    __shared__ uint32_t s_pub[NW][QB];   // ... and of the last one published
     __shared__ uint32_t s_sh[QB];    // shared bound from the slots (order key), this WG's view
 
     const int lane = threadIdx.x & 63;
@@ -287,10 +287,10 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
     const int n_wg = n_wg_all;
     const int lane4 = lane * 4;
 
-    for (int i = threadIdx.x; i < QB; i += 256) {
+    for (int i = threadIdx.x; i < QB; i += 64 * NW) {
         s_cnt[i] = 0;
 #pragma unroll
-        for (int w = 0; w < 4; ++w) {
+        for (int w = 0; w < NW; ++w) {
             s_best[w][i] = 0;
             s_pub[w][i] = 0;
         }
@@ -298,14 +298,15 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
         s_thr[i] = -INFINITY;
     }
     __syncthreads();
-    // slot publishing: lane group pq_i (LPQ lanes) of wave wv serves query pq = wv + 4 pq_i
-    constexpr int QPW = QB / 4;
+    // slot publishing: lane group pq_i (LPQ lanes) of wave wv serves query pq = wv + NW pq_i
+    constexpr int QPW = QB / NW;
     constexpr int LPQ = 64 / QPW;
     constexpr int SL = KP / LPQ;
     constexpr int SLV = SL / 4 > 0 ? SL / 4 : 1;
     static_assert(!PUB || SL % 4 == 0, "slots per lane must be whole uint4 loads");
+    static_assert(LPQ >= NW, "a lane group publishes one best per wave");
     const int pq_r = lane % LPQ;
-    const int pq = wv + 4 * (lane / LPQ);
+    const int pq = wv + NW * (lane / LPQ);
     const int pqg = qb * QB + pq;
     uint4 sv[SLV];
     bool sv_pending = false;
@@ -328,7 +329,7 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
 
     f32x4 xr[PX][RT][NPL], qr[PQ][QT][NPL];
     if (s_begin < s_end) {
-        const float* xs = X + blk((uint64_t)((s_begin * 4 + wv) * RT), 0, G);
+        const float* xs = X + blk((uint64_t)((s_begin * NW + wv) * RT), 0, G);
 #pragma unroll
         for (int p = 0; p < PX; ++p)
 #pragma unroll
@@ -351,7 +352,7 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
             const int qg = qb * QB + qt * 32 + (lane & 31);
             g_[qt] = qg < B ? gthr[qg] : 0u;
         }
-        const int64_t tt = (st_ * 4 + wv) * RT;
+        const int64_t tt = (st_ * NW + wv) * RT;
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) {
             const float* rsp = rowscale + (tt + rt) * 32 + 4 * (lane >> 5);
@@ -373,9 +374,9 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
 #ifdef VDB_STAMP
         const unsigned long long st_a = STAMP_NOW();
 #endif
-        const int64_t t0 = (s * 4 + wv) * RT;
+        const int64_t t0 = (s * NW + wv) * RT;
         const float* xs = X + blk((uint64_t)t0, 0, G);
-        const float* xn = (s + 1 < s_end) ? X + blk((uint64_t)(t0 + 4 * RT), 0, G) : xs;
+        const float* xn = (s + 1 < s_end) ? X + blk((uint64_t)(t0 + NW * RT), 0, G) : xs;
         f32x16 acc[RT][QT];
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt)
@@ -508,7 +509,7 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
 #ifdef VDB_STAMP
             ++st_rounds;
 #endif
-            for (int q = wv; q < QB; q += 4)
+            for (int q = wv; q < QB; q += NW)
                 if (s_cnt[q] >= CAP) {
 #ifdef VDB_STAMP
                     ++st_compacts;
@@ -538,10 +539,10 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
         st_pub_start = st_b5;
 #endif
         if constexpr (PUB) {
-            // ---- publish: slot (query, (4 wg + w) % KP) of gslots holds the max over a
+            // ---- publish: slot (query, (NW wg + w) % KP) of gslots holds the max over a
             // fixed set of waves (disjoint rows) of their best score, so the KP slots of a
             // query are scores of KP distinct rows and their minimum is a lower bound of
-            // the global KP-th best; 4 slots per workgroup so that KP
+            // the global KP-th best; NW slots per workgroup so that KP
             // slots fill even when there are fewer than KP workgroups.  A group of LPQ lanes serves one query: its leader
             // publishes (no-return atomic), all of them load SL slots each.  The slot
             // loads are consumed one step later (min over the group's lanes -> gthr and
@@ -562,12 +563,12 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
             const int64_t sd = s - s_begin + 1;
             if ((sd & (sd - 1)) == 0 || s + 1 == s_end) {
                 int improved = 0;
-                if (pq_r < 4 && pqg < B) {  // lane r of the group publishes wave r's best
+                if (pq_r < NW && pqg < B) {  // lane r of the group publishes wave r's best
                     const uint32_t best = s_best[pq_r][pq];
                     improved = best > s_pub[pq_r][pq];
                     if (improved) {
                         s_pub[pq_r][pq] = best;
-                        atomicMax(gslots + (size_t)pqg * KP_MAX + ((wg * 4 + pq_r) % KP), best);
+                        atomicMax(gslots + (size_t)pqg * KP_MAX + ((wg * NW + pq_r) % KP), best);
                     }
                 }
 #pragma unroll
@@ -590,7 +591,7 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
     }
 #ifdef VDB_STAMP
     if (lane == 0 && blockIdx.y == 0) {
-        const int w = wg * 4 + wv;
+        const int w = wg * NW + wv;
         g_scan_stamps[w][0] = st_k;
         g_scan_stamps[w][1] = st_e;
         g_scan_stamps[w][2] = st_pub;
@@ -603,11 +604,11 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
 #endif
 
     // ---- flush: entries above the shared bound -> global per-query lists ----------
-    // (wave wv flushes queries wv + 4 i; lane i holds query i's bound)
+    // (wave wv flushes queries wv + NW i; lane i holds query i's bound)
     __syncthreads();
     (void)n_wg;
     uint32_t tkey = 0;
-    if (lane < QPW && qb * QB + wv + 4 * lane < B) tkey = max(gthr[qb * QB + wv + 4 * lane], PUB ? s_sh[wv + 4 * lane] : 0u);
+    if (lane < QPW && qb * QB + wv + NW * lane < B) tkey = max(gthr[qb * QB + wv + NW * lane], PUB ? s_sh[wv + NW * lane] : 0u);
     if constexpr (PUB) {
         if (sv_pending) {  // a slot read-back still in flight: fold it in
             uint32_t mn = 0xFFFFFFFFu;
@@ -618,7 +619,7 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
             if (pq_r == 0 && pqg < B) atomicMax(gthr + pqg, mn);
         }
     }
-    append_flush<CAP>(s_sc, s_ix, s_cnt, wv, 4, QPW, qb * QB, B, tkey, gl_s, gl_i, gl_cnt, gl_cap);
+    append_flush<CAP>(s_sc, s_ix, s_cnt, wv, NW, QPW, qb * QB, B, tkey, gl_s, gl_i, gl_cnt, gl_cap);
 }
 
 // =============================================================================
@@ -1115,14 +1116,14 @@ hipError_t launch_pilot(int prec, int metric, int KP, const float* X, const floa
     return hipGetLastError();
 }
 
-template <int PREC, int METRIC, int QT, int RT, int PX, int PQ, int KP, int CAP, int PUB, int WPS, bool NT>
+template <int PREC, int METRIC, int QT, int RT, int PX, int PQ, int KP, int CAP, int PUB, int WPS, bool NT, int NW>
 static hipError_t scan_dispatch(const float* X, const float* rowscale, const uint32_t* mask, const float* Qt, int G,
                                 int64_t N, int B, int n_qblocks, int64_t n_steps, int n_wg, int spw, float* gl_s,
                                 uint32_t* gl_i, uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr, uint32_t* gslots,
                                 hipStream_t st) {
     const int n_wg8 = (n_wg + 7) / 8 * 8;
-    hipLaunchKernelGGL((scan_topk_kernel<PREC, METRIC, QT, RT, PX, PQ, KP, CAP, PUB, WPS, NT>), dim3(n_wg8 * n_qblocks),
-                       dim3(256), 0, st, X, rowscale, mask, Qt, G, N, B, n_steps, spw, n_qblocks, n_wg8, gl_s, gl_i,
+    hipLaunchKernelGGL((scan_topk_kernel<PREC, METRIC, QT, RT, PX, PQ, KP, CAP, PUB, WPS, NT, NW>),
+                       dim3(n_wg8 * n_qblocks), dim3(64 * NW), 0, st, X, rowscale, mask, Qt, G, N, B, n_steps, spw, n_qblocks, n_wg8, gl_s, gl_i,
                        gl_cnt, gl_cap, gthr, gslots);
     return hipGetLastError();
 }
@@ -1134,6 +1135,8 @@ static hipError_t scan_dispatch(const float* X, const float* rowscale, const uin
 //          1: wave-private top-k for KP = 32 (scan_topk_priv_kernel), else as 0 with CAP 8 KP
 //          2: RT=2 PX=4 PQ=2, CAP 4 KP, 2 workgroups per CU (256 registers) for KP <= 64: one
 //             workgroup's epilogue overlaps the other's corpus stream
+// (8 waves per workgroup, 2 per SIMD, would overlap one wave's epilogue with another's MFMAs, but
+// the kernel holds 256 VGPRs + 200 AGPRs per wave: at 256 it spills ~200.)
 // (PX = PQ = 6 or 8 for bf16x3 spill registers at 256 VGPRs: C2 -2% / -18%, C3 -7% / -12%.)
 // PQ = PX for bf16x3: loads retire in issue order (vmcnt), so a query load issued
 // PQ < PX groups ahead caps the usable corpus prefetch at PQ groups.
@@ -1150,7 +1153,9 @@ int scan_wgs_per_cu(int prec, int variant, int KP) {
     return (prec == PREC_BF16X3 && variant == 2 && KP <= 64) ? 2 : 1;
 }
 
-int scan_rows_per_step(int prec, int variant) { return 4 * 32 * variant_rt(prec, variant); }
+static int variant_nw(int, int) { return 4; }  // waves per workgroup (the kernel takes NW; 8 spills)
+
+int scan_rows_per_step(int prec, int variant) { return variant_nw(prec, variant) * 32 * variant_rt(prec, variant); }
 
 #ifdef VDB_STAMP
 constexpr int kStampVariant = 9;  // diagnostic, no insertion after the first step (wrong results)
@@ -1169,13 +1174,13 @@ hipError_t launch_scan_topk(int prec, int metric, int KP, int variant, const flo
     if (!scan_variant_ok(prec, variant, G)) return hipErrorInvalidValue;
 #define VDB_SCAN_NT(P, M, QT, KPV, V, RT, PX, PQ, CAPV, PUB, W, NT)                                           \
     if (prec == P && metric == M && KP == KPV && variant == V && (n_qblocks == 1) == NT)                       \
-        return scan_dispatch<P, M, QT, RT, PX, PQ, KPV, CAPV, PUB, W, NT>(X, rowscale, mask, Qt, G, N, B,         \
+        return scan_dispatch<P, M, QT, RT, PX, PQ, KPV, CAPV, PUB, W, NT, 4>(X, rowscale, mask, Qt, G, N, B,      \
                                                                         n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, \
                                                                         gl_cnt, gl_cap, gthr, gslots, st);
 // VDB_SCAN: default load policy only; VDB_SCAN2: plus the non-temporal build for one query block
 #define VDB_SCAN(P, M, QT, KPV, V, RT, PX, PQ, CAPV, PUB, W)                                                     \
     if (prec == P && metric == M && KP == KPV && variant == V)                                                 \
-        return scan_dispatch<P, M, QT, RT, PX, PQ, KPV, CAPV, PUB, W, false>(X, rowscale, mask, Qt, G, N, B,      \
+        return scan_dispatch<P, M, QT, RT, PX, PQ, KPV, CAPV, PUB, W, false, 4>(X, rowscale, mask, Qt, G, N, B,   \
                                                                            n_qblocks, n_steps, n_wg, spw, gl_s,    \
                                                                            gl_i, gl_cnt, gl_cap, gthr, gslots, st);
 #define VDB_SCAN2(P, M, QT, KPV, V, RT, PX, PQ, CAPV, PUB, W)                                                    \

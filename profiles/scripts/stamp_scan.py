@@ -7,11 +7,12 @@ sys.path.insert(0, os.path.join(ROOT, "mlx-vector-db_amd")); sys.path.insert(0, 
 import torch  # noqa
 from service import _vdb
 import bench
-N, D, B, k = 1_000_000, 768, 64, 10
 variant = int(sys.argv[1]) if len(sys.argv) > 1 else 0
 nwg = int(sys.argv[2]) if len(sys.argv) > 2 else 0
 prec = sys.argv[3] if len(sys.argv) > 3 else "bf16x3"
-ix = _vdb.NativeIndex(D, "cosine", precision=prec)
+cfg = sys.argv[4] if len(sys.argv) > 4 else "c2"
+N, D, B, k, metric, _ = bench.CONFIGS[cfg]
+ix = _vdb.NativeIndex(D, metric, precision=prec)
 ix.set_param("scan_variant" if prec == "fp32" else "scan_variant_bf16x3", variant)
 if nwg: ix.set_param("n_wg", nwg)
 ix.reserve(N)
@@ -21,12 +22,12 @@ Q = np.random.default_rng(1).random((B, D), dtype=np.float32)
 for _ in range(3):
     ix.search(Q, k)
 lib = _vdb.load_library()
-n = 8192
+n = 1 << 16
 buf = (ctypes.c_ulonglong * (n * 8))()
 lib.vdb_debug_scan_stamps(buf, n)
 a = np.array(buf, dtype=np.uint64).reshape(n, 8).astype(np.float64)
 a = a[a[:, 3] > 0]
-print(f"{prec} variant {variant} nwg {nwg}: waves {len(a)}")
+print(f"{cfg} {prec} variant {variant} nwg {nwg}: waves {len(a)}")
 for i, name in enumerate(["k-loop", "epilogue", "publish", "total", "barrier after k-loop", "scoring", "first insert pass", "retry loop (+barrier,-pub)"]):
     print(f"  {name:22s} mean {a[:, i].mean():12.0f}  max {a[:, i].max():12.0f}  (ticks)")
 print("  k-loop share", a[:, 0].sum() / a[:, 3].sum(), "epilogue share", a[:, 1].sum() / a[:, 3].sum())

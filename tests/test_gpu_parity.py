@@ -224,6 +224,37 @@ def test_device_pointer_search_matches_host(vdb):
     np.testing.assert_array_equal(sd.cpu().numpy(), s_h)
 
 
+@pytest.mark.parametrize("metric", ["cosine", "euclidean"])
+def test_device_search_gated_fallback(vdb, metric):
+    """Device-memory searches do not wait for the certificate: the exact path is
+    queued gated on the device's flag count.  Duplicates force some queries onto
+    it; several searches are queued back to back before one synchronise."""
+    import torch
+    rng = np.random.default_rng(23)
+    V = rng.random((30000, 96), dtype=np.float32)
+    V[2000:2060] = V[11]
+    V[9000:9040] = V[29]
+    Q = np.concatenate([V[[11, 29]], rng.random((14, 96), dtype=np.float32)])
+    ix = vdb.NativeIndex(96, metric)
+    ix.add(V)
+    es, ei, ek = ref_cpu.exact_search(Q, V, 12, metric)
+    qd = torch.from_numpy(Q).cuda()
+    outs = []
+    st = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    for _ in range(3):
+        sd = torch.empty((16, 12), dtype=torch.float32, device="cuda")
+        idd = torch.empty((16, 12), dtype=torch.int64, device="cuda")
+        kd = torch.empty((16, 12), dtype=torch.float64, device="cuda")
+        ix.search_device(qd.data_ptr(), 16, 12, sd.data_ptr(), idd.data_ptr(), kd.data_ptr(), stream=st.cuda_stream)
+        outs.append((sd, idd, kd))
+    torch.cuda.synchronize()
+    for sd, idd, kd in outs:
+        np.testing.assert_array_equal(idd.cpu().numpy(), ei)
+        np.testing.assert_array_equal(kd.cpu().numpy(), ek)
+    assert ix.stat("fallback_queries") >= 3 * 2  # the two duplicated queries, every search
+
+
 def test_similarity_matrix_operator_slot(vdb):
     import torch
     rng = np.random.default_rng(19)
