@@ -31,6 +31,7 @@ from typing import Any, Dict, List, Optional, Tuple, Union
 import numpy as np
 
 from . import _vdb
+from .persistence import StoreFiles
 
 logger = logging.getLogger("mlx_vector_db.optimized_store")
 
@@ -47,7 +48,7 @@ class MLXVectorStoreConfig:
     enable_hnsw: bool = False
     jit_compile: bool = True
     device: int = 0          # GPU ordinal holding this store's corpus
-    persist: bool = True     # write vectors.npz / metadata.jsonl on every add (reference behaviour)
+    persist: bool = True     # persist every add (append log + periodic compaction, service/persistence.py)
 
 
 def _as_matrix(vectors: Any) -> np.ndarray:
@@ -84,6 +85,7 @@ class MLXVectorStore:
         self._metadata: List[Dict] = []
         self._vector_count = 0
         self._hnsw_index = None
+        self._files = StoreFiles(self.store_path)
         if self.config.enable_hnsw:  # service/optimized_vector_store.py:72-78
             from performance.hnsw_index import ProductionHNSWIndex
             self._hnsw_index = ProductionHNSWIndex(self.config.dimension, self.store_path, self.config.metric,
@@ -139,7 +141,13 @@ class MLXVectorStore:
             self._metadata.extend(metadata)
             self._vector_count = self._index.count() if self._index is not None else 0
             self._is_dirty = True
-            self._save_store()
+            if self.config.persist and v.shape[0] > 0:
+                # O(new rows) append instead of the reference's full rewrite per add (:113, :218-223)
+                self._files.append(v, metadata)
+                if self._files.needs_compaction():
+                    self._save_store(force=True)
+                else:
+                    self._is_dirty = False
             if self.config.enable_hnsw and self._hnsw_index is not None and self._index is not None:
                 # the reference rebuilds the graph from scratch on every add (:110-112)
                 self._hnsw_index.build(None, native_index=self._index)
@@ -242,6 +250,7 @@ class MLXVectorStore:
                 if self.store_path.exists():
                     shutil.rmtree(self.store_path)
                 self.store_path.mkdir(parents=True, exist_ok=True)
+                self._files = StoreFiles(self.store_path)
                 self._create_empty_store()
                 if self.config.enable_hnsw:  # :205-206
                     from performance.hnsw_index import ProductionHNSWIndex
@@ -289,38 +298,26 @@ class MLXVectorStore:
                 "memory_usage_mb": mem}
 
     # ---- persistence: vectors.npz + metadata.jsonl (service/optimized_vector_store.py:218-239)
+    # plus an append log between compactions (service/persistence.py)
     def _save_store(self, force: bool = False):
+        """Compaction: the whole store as the reference's two files (log dropped)."""
         if not (self.config.persist or force):
             return
-        if self._vector_count == 0 or not self._is_dirty:
+        if self._vector_count == 0 or not (self._is_dirty or self._files.log_rows):
             return
-        vecs = self._index.get_vectors()
-        np.savez(str(self.store_path / "vectors.npz"), vectors=vecs)
-        with open(self.store_path / "metadata.jsonl", "w") as f:
-            for meta in self._metadata:
-                f.write(json.dumps(meta) + "\n")
+        self._files.compact(self._index.get_vectors(), self._metadata[: self._vector_count])
         self._is_dirty = False
 
     def _load_store(self):
-        vectors_path = self.store_path / "vectors.npz"
-        if not vectors_path.exists():
-            self._create_empty_store()
-            return
         try:
-            with np.load(str(vectors_path), allow_pickle=False) as z:
-                vecs = np.asarray(z["vectors"], dtype=np.float32)
-            meta: List[Dict] = []
-            metadata_path = self.store_path / "metadata.jsonl"
-            if metadata_path.exists():
-                with open(metadata_path, "r") as f:
-                    meta = [json.loads(line) for line in f]
-            if vecs.ndim != 2:
-                raise ValueError(f"vectors.npz holds shape {vecs.shape}")
-            if vecs.shape[0]:
-                self._ensure_index(vecs.shape[1]).add(vecs)
+            vecs, meta = self._files.load()
+            if vecs.shape[0] == 0:
+                self._create_empty_store()
+                return
+            self._ensure_index(vecs.shape[1]).add(vecs)
             self._metadata = meta
-            self._vector_count = self._index.count() if self._index is not None else 0
-            if self._hnsw_index is not None and self._index is not None:
+            self._vector_count = self._index.count()
+            if self._hnsw_index is not None:
                 if not self._hnsw_index.attach(self._index):
                     self._hnsw_index.build(None, native_index=self._index)
         except Exception as e:  # reference: log and start empty (:237-239)

@@ -1,0 +1,113 @@
+"""The drop-in boundary on the GPU: the store mirror (service/optimized_vector_store.py)
+against the oracle's restatement of the reference store (oracle/ref_cpu.py
+reference_store_search = service/optimized_vector_store.py:116-192) and the
+reference's own known-answer tests: P1 self-query (tests/test_integration.py:81-136),
+P2/P3 filters (test_integration.py:139-160, tests/demo.py:217-243), P4 counts and P5
+result length (tests/test_vector_store.py:20-43), P6 batch shape (demo.py:130-139),
+P7 empty store (optimized_vector_store.py:117)."""
+import numpy as np
+import pytest
+
+from oracle import ref_cpu
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def store_mod():
+    from service import _vdb, optimized_vector_store
+    assert _vdb.device_count() >= 1, "no GPU visible"
+    return optimized_vector_store
+
+
+def _mk(store_mod, path, dim, metric="cosine", **kw):
+    return store_mod.MLXVectorStore(str(path), store_mod.MLXVectorStoreConfig(dimension=dim, metric=metric, **kw))
+
+
+@pytest.mark.parametrize("metric", ["cosine", "euclidean"])
+def test_query_matches_reference_store(store_mod, tmp_path, metric):
+    rng = np.random.default_rng(41)
+    V = rng.random((3000, 48), dtype=np.float32)
+    meta = [{"id": f"doc_{i}", "hash": i % 10, "kind": "a" if i % 3 else "b"} for i in range(3000)]
+    st = _mk(store_mod, tmp_path / "s", 48, metric)
+    r = st.add_vectors(V, meta)
+    assert r == {"vectors_added": 3000, "total_vectors": 3000}
+    for q, filt in ((rng.random(48, dtype=np.float32), None), (V[5], None),
+                    (rng.random(48, dtype=np.float32), {"hash": 7}),
+                    (rng.random(48, dtype=np.float32), {"hash": 3, "kind": "b"})):
+        gi, gs, gm = st.query(q, k=10, filter_metadata=filt)
+        ri, rs, rm = ref_cpu.reference_store_search(q, V, 10, metric, meta, filt)
+        assert gi == ri and gm == rm
+        np.testing.assert_allclose(gs, rs, rtol=1e-4, atol=1e-5)
+        if filt:
+            assert all(all(m[a] == b for a, b in filt.items()) for m in gm)  # P2 / P3
+
+
+def test_self_query_count_length_batch_empty(store_mod, tmp_path):
+    rng = np.random.default_rng(42)
+    st = _mk(store_mod, tmp_path / "e", 384)
+    assert st.query(rng.random(384, dtype=np.float32), k=5) == ([], [], [])           # P7
+    assert st.batch_query(rng.random((3, 384), dtype=np.float32), k=5) == [([], [], [])] * 3
+    V = rng.random((500, 384), dtype=np.float32)
+    st.add_vectors(V, [{"id": i} for i in range(500)])
+    i, s, m = st.query(V[123], k=5)
+    assert i[0] == 123 and s[0] > 0.999 and m[0]["id"] == 123                         # P1
+    assert len(i) == 5                                                                 # P5
+    res = st.batch_query(V[:7], k=4)                                                   # P6
+    assert len(res) == 7 and all(len(r[0]) == 4 for r in res)
+    assert [r[0][0] for r in res] == list(range(7))
+    assert st.query(V[0], k=1000)[0][:1] == [0] and len(st.query(V[0], k=1000)[0]) == 500  # min(k, N)
+    assert st.query(V[0], k=0) == ([], [], [])
+    assert st.query(V[0], k=3, filter_metadata={"id": -1}) == ([], [], [])
+    with pytest.raises(ValueError):
+        st.add_vectors(rng.random((2, 10), dtype=np.float32), [{}, {}])  # dimension is enforced
+    stats = st.get_stats()
+    assert stats["vector_count"] == 500 and stats["memory_usage_mb"] > 0
+    assert st.health_check()["healthy"]
+
+
+def test_no_operator_raises_like_reference(store_mod, tmp_path):
+    st = _mk(store_mod, tmp_path / "d", 16, "dot_product")
+    st.add_vectors(np.ones((4, 16), np.float32), [{}] * 4)
+    with pytest.raises(RuntimeError, match="Keine kompilierte"):
+        st.query(np.ones(16, np.float32), k=2)
+
+
+def test_persistence_append_log_and_compaction(store_mod, tmp_path):
+    from service import persistence as P
+    rng = np.random.default_rng(43)
+    path = tmp_path / "p"
+    st = _mk(store_mod, path, 32)
+    A, B = rng.random((100, 32), dtype=np.float32), rng.random((50, 32), dtype=np.float32)
+    st.add_vectors(A, [{"i": i} for i in range(100)])
+    st.add_vectors(B, [{"i": i} for i in range(100, 150)])
+    assert (path / P.LOG_VECTORS).exists() and not (path / "vectors.npz").exists()  # no rewrite per add
+    q = rng.random(32, dtype=np.float32)
+    want = st.query(q, k=8)
+    st2 = _mk(store_mod, path, 32)                       # reopen: base + log
+    assert st2._vector_count == 150 and st2.query(q, k=8) == want
+    st2.optimize()                                       # compaction -> the reference's two files
+    assert (path / "vectors.npz").exists() and not (path / P.LOG_VECTORS).exists()
+    with np.load(str(path / "vectors.npz"), allow_pickle=False) as z:
+        np.testing.assert_array_equal(z["vectors"], np.concatenate([A, B]))
+    st3 = _mk(store_mod, path, 32)
+    assert st3.query(q, k=8) == want
+    st3.clear()
+    assert st3.query(q, k=8) == ([], [], []) and not (path / "vectors.npz").exists()
+
+
+def test_functional_api_lifecycle(store_mod, tmp_path, monkeypatch):
+    """tests/test_vector_store.py:20-43 of the reference, verbatim in behaviour."""
+    monkeypatch.setenv("VECTOR_STORE_BASE", str(tmp_path / "base"))
+    sm = store_mod
+    if sm.store_exists("test_user", "test_model"):
+        sm.delete_store("test_user", "test_model")
+    sm.create_store("test_user", "test_model")
+    assert sm.store_exists("test_user", "test_model")
+    vecs = np.random.rand(5, 384).astype(np.float32)
+    sm.add_vectors("test_user", "test_model", vecs, [{"id": f"v{i}", "source": "test"} for i in range(5)])
+    stats = sm.count_vectors("test_user", "test_model")
+    assert stats["vectors"] == 5 and stats["metadata"] == 5
+    assert len(sm.query_vectors("test_user", "test_model", vecs[0], k=3)) == 3
+    sm.delete_store("test_user", "test_model")
+    assert not sm.store_exists("test_user", "test_model")
