@@ -244,11 +244,12 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
                     help="N>1: weak = global batch B*N (fixed work per GPU), strong = global batch B")
-    ap.add_argument("--precision", default="bf16x3", choices=["bf16x3", "fp32"],
+    ap.add_argument("--precision", default="bf16x3", choices=["bf16x3", "bf16", "fp32"],
                     help="candidate-pass arithmetic (results identical; DESIGN.md §3)")
     ap.add_argument("--scan-variant", type=int, default=None, help="candidate-pass kernel variant (tuning)")
     ap.add_argument("--n-wg", type=int, default=None, help="candidate-pass workgroups (tuning)")
     ap.add_argument("--pilot-tiles", type=int, default=None, help="row tiles sampled by the pilot bound (tuning)")
+    ap.add_argument("--margin", type=int, default=None, help="candidates beyond k (tuning; default per precision)")
     ap.add_argument("--rows", type=int, default=None, help="override the corpus rows (exploration only)")
     ap.add_argument("--graph-knn", type=int, default=None, help="c5: kNN candidates per row for the build")
     ap.add_argument("--pmc-json", default=None,
@@ -282,6 +283,8 @@ def main():
         ix.set_param("n_wg", args.n_wg)
     if args.pilot_tiles is not None:
         ix.set_param("pilot_tiles", args.pilot_tiles)
+    if args.margin is not None:
+        ix.set_param("margin", args.margin)
     ix.reserve(n_local)
     host_parts = []
     for s in range(lo, hi, 8 * CHUNK_ROWS):
@@ -347,12 +350,14 @@ def main():
         # algorithmic work of one scan launch on this rank: every corpus row read once
         # (fp32 tiles or the split hi/lo tiles: 4 B per element either way), its row
         # scale, the queries; flops = 2 B N D (x3 bf16 MFMA flops for the split product)
+        # (bf16: the hi plane only, 2 B per element; 2 bf16 MFMA per product)
         Dp = (D + 63) // 64 * 64
-        hbm_bytes = n_local * Dp * 4 + n_local * 4 + Bg * Dp * 4
+        elem = 2 if args.precision == "bf16" else 4
+        hbm_bytes = n_local * Dp * elem + n_local * 4 + Bg * Dp * 4
         if args.precision == "fp32":
             mfma_flops, mfma_peak = 2.0 * Bg * n_local * D, FP32_MFMA_PEAK_TFLOPS
         else:
-            mfma_flops, mfma_peak = 3 * 2.0 * Bg * n_local * D, BF16_MFMA_PEAK_TFLOPS
+            mfma_flops, mfma_peak = (3 if args.precision == "bf16x3" else 2) * 2.0 * Bg * n_local * D, BF16_MFMA_PEAK_TFLOPS
         t_hbm = hbm_bytes / (HBM_PEAK_GBS * 1e9)
         t_mfma = mfma_flops / (mfma_peak * 1e12)
         achieved_gbs = hbm_bytes / (scan_ms * 1e-3) / 1e9
@@ -388,7 +393,8 @@ def main():
             "higher_is_better": True,
             "scaling": args.scaling if world > 1 else "weak",
             "vs_baseline": None,
-            "dtype": "f32" if args.precision == "fp32" else "f32 (bf16x3 split MFMA candidates, fp64 exact rerank)",
+            "dtype": {"fp32": "f32", "bf16x3": "f32 (bf16x3 split MFMA candidates, fp64 exact rerank)",
+                      "bf16": "f32 (bf16 corpus x split query MFMA candidates, fp64 exact rerank)"}[args.precision],
             "data": "synthetic uniform [0,1) fp32 (numpy PCG64, corpus seed 0 per 65536-row chunk, queries seed 1)",
             "config": {"workload": f"{args.config}: {desc}", "n_rows": N, "dim": D, "global_batch": Bg,
                        "batch_per_gpu_equiv": B, "k": k,

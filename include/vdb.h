@@ -59,15 +59,19 @@ enum { VDB_METRIC_COSINE = 0, VDB_METRIC_EUCLIDEAN = 1 };
 enum { VDB_MEM_HOST = 0, VDB_MEM_DEVICE = 1 };
 
 /* Candidate-pass arithmetic for an index (vdb_index_set_param "precision").
- * The returned results are identical for both (the exact fp64 rerank decides);
+ * The returned results are identical for all (the exact fp64 rerank decides);
  * only the speed of the candidate pass differs.
  *   VDB_PREC_FP32    fp32 v_mfma_f32_32x32x2_f32 (MFMA-bound, 157 TF peak)
  *   VDB_PREC_BF16X3  split-bf16 "x3": x = hi + lo, q = hi + lo,
  *                    x.q ~ xh.qh + xh.ql + xl.qh on v_mfma_f32_32x32x16_bf16,
  *                    fp32 accumulate; error bound of the same order as fp32
  *                    (HBM-bound).  Default.  Keeps a split copy of the corpus
- *                    (same bytes as the fp32 copy). */
-enum { VDB_PREC_FP32 = 0, VDB_PREC_BF16X3 = 1 };
+ *                    (same bytes as the fp32 copy).
+ *   VDB_PREC_BF16    the hi plane of the split copy only: x.q ~ xh.qh + xh.ql,
+ *                    half the corpus bytes per search; the certificate adds the
+ *                    largest row residual |x - bf16(x)| (measured at ingest), so
+ *                    it is wider and takes a larger candidate margin. */
+enum { VDB_PREC_FP32 = 0, VDB_PREC_BF16X3 = 1, VDB_PREC_BF16 = 2 };
 
 typedef struct vdb_index vdb_index;
 

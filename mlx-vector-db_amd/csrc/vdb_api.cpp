@@ -102,6 +102,7 @@ struct vdb_index {
     unsigned long long* d_xmax = nullptr;
     int* d_nonfinite = nullptr;
     double xmax = 0.0;
+    double xres_rel = 0.0, xres_abs = 0.0;  // max |x - bf16(x)| / |x| and max |x - bf16(x)| (PREC_BF16 bound)
     hipStream_t stream = nullptr;
     int n_cu = 256;
     // knobs
@@ -132,7 +133,7 @@ int ensure_capacity(vdb_index* ix, int64_t rows) {
     cap = round_up(cap, kRowAlign);
     const size_t tile_floats = (size_t)ix->G * BLOCK_FLOATS;
     const size_t x_bytes = (size_t)(cap / 32) * tile_floats * sizeof(float);
-    const bool split = ix->precision == VDB_PREC_BF16X3;
+    const bool split = ix->precision != VDB_PREC_FP32;
     float* X = nullptr;
     float* Xs = nullptr;
     double* n64 = nullptr;
@@ -395,17 +396,17 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
     if (!ix || !name) return set_error(VDB_ERR_INVALID, "NULL argument");
     std::string n(name);
     if (n == "precision") {
-        if (value != VDB_PREC_FP32 && value != VDB_PREC_BF16X3)
-            return set_error(VDB_ERR_INVALID, "precision must be %d (fp32) or %d (bf16x3), got %lld", VDB_PREC_FP32,
-                             VDB_PREC_BF16X3, (long long)value);
+        if (value != VDB_PREC_FP32 && value != VDB_PREC_BF16X3 && value != VDB_PREC_BF16)
+            return set_error(VDB_ERR_INVALID, "precision must be %d (fp32), %d (bf16x3) or %d (bf16), got %lld",
+                             VDB_PREC_FP32, VDB_PREC_BF16X3, VDB_PREC_BF16, (long long)value);
         HIP_TRY(hipSetDevice(ix->device));
         std::unique_lock<std::shared_mutex> g(ix->mu);
         if (value == ix->precision) return VDB_OK;
         HIP_TRY(hipDeviceSynchronize());
         if (value == VDB_PREC_FP32) {
-            if (ix->Xs) (void)hipFree(ix->Xs);  // the split copy is only read by the bf16x3 pass
+            if (ix->Xs) (void)hipFree(ix->Xs);  // the split copy is only read by the bf16 passes
             ix->Xs = nullptr;
-        } else if (ix->cap_rows > 0) {
+        } else if (ix->cap_rows > 0 && !ix->Xs) {
             const size_t x_bytes = (size_t)(ix->cap_rows / 32) * ix->G * BLOCK_FLOATS * sizeof(float);
             HIP_TRY(hipMalloc(&ix->Xs, x_bytes));
             HIP_TRY(hipMemsetAsync(ix->Xs, 0, x_bytes, ix->stream));
@@ -509,9 +510,9 @@ int32_t vdb_index_add(vdb_index* ix, const float* vectors, int64_t n, int32_t me
     if (staging) (void)hipFree(staging);
     (void)stream;  // ingest always runs on the index's own stream (serialised with growth)
     int nonfinite = 0;
-    unsigned long long xb = 0;
+    unsigned long long xb[3] = {0, 0, 0};
     HIP_TRY(hipMemcpyAsync(&nonfinite, ix->d_nonfinite, sizeof(int), hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipMemcpyAsync(&xb, ix->d_xmax, sizeof(xb), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(xb, ix->d_xmax, sizeof(xb), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     if (nonfinite) {
         // rows past `count` are never read; the next add overwrites them
@@ -519,9 +520,11 @@ int32_t vdb_index_add(vdb_index* ix, const float* vectors, int64_t n, int32_t me
         (void)used_tiles;
         return set_error(VDB_ERR_NONFINITE, "%d row(s) contain NaN or Inf; nothing was added", nonfinite);
     }
-    double xm;
-    std::memcpy(&xm, &xb, sizeof(xm));
-    ix->xmax = xm;
+    double xm[3];
+    std::memcpy(xm, xb, sizeof(xm));
+    ix->xmax = xm[0];
+    ix->xres_rel = xm[1];
+    ix->xres_abs = xm[2];
     ix->count += n;
     return VDB_OK;
 }
@@ -549,6 +552,7 @@ int32_t vdb_index_clear(vdb_index* ix) {
     HIP_TRY(hipStreamSynchronize(ix->stream));
     ix->count = 0;
     ix->xmax = 0.0;
+    ix->xres_rel = ix->xres_abs = 0.0;
     return VDB_OK;
 }
 
@@ -601,9 +605,15 @@ int32_t vdb_index_search(vdb_index* ix, const float* queries, int32_t B, int32_t
     // candidates beyond k: the certificate needs a gap of 2 eps between the k-th and the
     // KP-th approximate score; bf16x3's bound grows with D (3D additions), so large D
     // gets a wider margin (1M x 1536 uniform: KP = 32 left ~1.5% of queries uncertified)
-    const int prec_req = ix->Xs && ix->precision == VDB_PREC_BF16X3 ? PREC_BF16X3 : PREC_FP32;
+    const int prec_req = !ix->Xs ? PREC_FP32
+                         : ix->precision == VDB_PREC_BF16X3 ? PREC_BF16X3
+                         : ix->precision == VDB_PREC_BF16 ? PREC_BF16 : PREC_FP32;
     int margin_def = std::max(16, k / 4);
     if (prec_req == PREC_BF16X3 && D >= 1024) margin_def = std::max(margin_def, 48);
+    // bf16 (hi plane only): eps ~ the rows' bf16 residual (~1.5e-3 relative on uniform data),
+    // ~30x bf16x3's: 1M x 768 uniform needs KP = 128 for k = 10 (KP = 64 left 26% of the
+    // queries uncertified; KP = 128: none of 2560)
+    if (prec_req == PREC_BF16) margin_def = std::max(16, std::min(std::max(112, k / 2), 256 - k));
     const int margin = ix->margin >= 0 ? (int)ix->margin : margin_def;
     int KP = std::max(32, next_pow2(k + margin));
     const bool exact_all = ix->force_exact || k > kMaxApproxK || KP > 256;
@@ -613,7 +623,7 @@ int32_t vdb_index_search(vdb_index* ix, const float* queries, int32_t B, int32_t
     const int n_qblocks = (B + QB - 1) / QB;
     const int prec = prec_req;
     const int Gs = prec == PREC_FP32 ? ix->G : ix->G / 2;  // scan groups (8 or 16 dims)
-    int variant = (int)(prec == PREC_FP32 ? ix->scan_variant : ix->scan_variant_b3);
+    int variant = (int)(prec == PREC_FP32 ? ix->scan_variant : ix->scan_variant_b3);  // (bf16 knob: both split modes)
     if (!scan_variant_ok(prec, variant, Gs)) variant = 0;  // e.g. PX=8 needs Dp % 128 == 0
     const int64_t step_rows = scan_rows_per_step(prec, variant);
     const int64_t n_steps = std::max<int64_t>(1, round_up(N, step_rows) / step_rows);
@@ -728,11 +738,17 @@ int32_t vdb_index_search(vdb_index* ix, const float* queries, int32_t B, int32_t
             //   fp32:   D fp32 MFMA additions + ~8 roundings of the normalisation / scaling
             //   bf16x3: 3D additions (each counted at 2^-23 in case the bf16 MFMA adds
             //           truncate) + the dropped hi*lo-order terms (< 3.1 2^-16) + the same 8
-            fa.eps_rel = prec == PREC_FP32
-                             ? 1.01 * (double)(D + 8) * std::ldexp(1.0, -24)
-                             : 1.01 * (3.0 * D * std::ldexp(1.0, -23) + 3.1 * std::ldexp(1.0, -16) +
+            //   bf16:   2D additions + the query split (2^-16) + the same 8, plus xres: the
+            //           corpus rounding |q.(x - bf16(x))| <= |q| |x - bf16(x)|, bounded by the
+            //           largest row residual measured at ingest (relative for cosine)
+            fa.eps_rel = prec == PREC_FP32 ? 1.01 * (double)(D + 8) * std::ldexp(1.0, -24)
+                         : prec == PREC_BF16X3
+                             ? 1.01 * (3.0 * D * std::ldexp(1.0, -23) + 3.1 * std::ldexp(1.0, -16) +
+                                       8.0 * std::ldexp(1.0, -24))
+                             : 1.01 * (2.0 * D * std::ldexp(1.0, -23) + 1.1 * std::ldexp(1.0, -16) +
                                        8.0 * std::ldexp(1.0, -24));
             fa.xmax = ix->xmax;
+            fa.xres = prec != PREC_BF16 ? 0.0 : 1.01 * (ix->metric == 0 ? ix->xres_rel : ix->xres_abs);
             fa.out_s = out_s; fa.out_i = out_i; fa.out_k = out_k; fa.index_offset = index_offset;
             fa.flag_count = flags; fa.flag_list = flags + 1; fa.gthr = gthr; fa.overflow_count = flags + B + 1;
             HIP_TRY(launch_finish(ix->metric, KP, fa, B, st));

@@ -407,9 +407,10 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
             const double acut = fmax(akp, T);
             double eps;
             if (METRIC == 0) {
-                eps = a.eps_rel;
+                eps = a.eps_rel + a.xres;
             } else {
-                eps = a.eps_rel * (2.0 * qn * a.xmax + a.xmax * a.xmax) + 2.4e-7 * fmax(fabs(ak), fabs(acut));
+                eps = a.eps_rel * (2.0 * qn * a.xmax + a.xmax * a.xmax) + 2.0 * qn * a.xres +
+                      2.4e-7 * fmax(fabs(ak), fabs(acut));
             }
             ok = have_k && acut + eps < ak - eps;
         }

@@ -23,7 +23,7 @@ __global__ void __launch_bounds__(256) pack_rows_kernel(const float* __restrict_
     const int np = (D + 255) / 256;
     const float* s = src + row * (int64_t)D;
     const uint64_t r = (uint64_t)(row0 + row);
-    double acc = 0.0;
+    double acc = 0.0, res = 0.0;  // |x|^2 and |x - bf16(x)|^2 (the PREC_BF16 residual)
     int bad = 0;
     for (int m = 0; m < np; ++m) {
         const int p = m * 64 + lane;
@@ -35,18 +35,29 @@ __global__ void __launch_bounds__(256) pack_rows_kernel(const float* __restrict_
             bad |= !isfinite(v[j]);
             const double dv = (double)v[j];
             acc = acc + dv * dv;
+            const double rv = dv - (double)__uint_as_float(bf16_rne_bits(v[j]) << 16);
+            res = res + rv * rv;
         }
         if (4 * p < Dp) *(f32x4*)(X + tiled_piece_offset(r, p, G)) = v;
     }
     acc = wave_sum_butterfly(acc);
+    res = wave_sum_butterfly(res);
     const int anybad = __any(bad);
     if (lane == 0) {
         const double nr = sqrt(acc);
         nrm64[r] = nr;
         inv32[r] = (float)(1.0 / fmax(nr, 1e-8));
         sq32[r] = (float)acc;
-        if (anybad) atomicAdd(nonfinite, 1);
-        else atomicMax(xmax_bits, (unsigned long long)__double_as_longlong(nr));
+        if (anybad) {
+            atomicAdd(nonfinite, 1);
+        } else {
+            // xmax_bits[0] max |x|; [1] max |x - bf16(x)| / max(|x|, 1e-8); [2] max |x - bf16(x)|
+            // (non-negative doubles order like their bit patterns)
+            const double dr = sqrt(res);
+            atomicMax(xmax_bits, (unsigned long long)__double_as_longlong(nr));
+            atomicMax(xmax_bits + 1, (unsigned long long)__double_as_longlong(dr / fmax(nr, 1e-8)));
+            atomicMax(xmax_bits + 2, (unsigned long long)__double_as_longlong(dr));
+        }
     }
 }
 

@@ -18,10 +18,15 @@ constexpr int ROW_ALIGN = 1024;    // corpus capacity granule (>= rows per scan 
 //               16-dim group: hi*hi + hi*lo + lo*hi (8 KiB per super-tile group: [plane][sub tile])
 constexpr int PREC_FP32 = 0;
 constexpr int PREC_BF16X3 = 1;
+//   PREC_BF16   the hi plane of the split copy only (x ~ bf16(x), half the bytes), query split:
+//               x.q ~ xh.qh + xh.ql, two v_mfma_f32_32x32x16_bf16 per 16-dim group; bounded by the
+//               index's largest row residual |x - bf16(x)| (pack_rows)
+constexpr int PREC_BF16 = 2;
 
 // Ingest: row-major fp32 [n][D] (device) -> tiled corpus rows [row0, row0+n),
-// canonical fp64 norms, fp32 inverse norms and squared norms, running max norm
-// (as fp64 bits) and a non-finite counter.
+// canonical fp64 norms, fp32 inverse norms and squared norms, running maxima (as
+// fp64 bits) xmax_bits[0] = |x|, [1] = |x - bf16(x)| / |x|, [2] = |x - bf16(x)|,
+// and a non-finite counter.
 hipError_t launch_pack_rows(const float* src, int64_t n, int D, int G, float* X, int64_t row0,
                             double* nrm64, float* inv32, float* sq32,
                             unsigned long long* xmax_bits, int* nonfinite, hipStream_t st);
@@ -96,6 +101,7 @@ struct FinishArgs {
     const float* gl_s; const uint32_t* gl_i; const uint32_t* gl_cnt; int64_t gl_cap;
     const float* Q; const double* qn64; const float* X; int G; int D; const double* nrm64;
     int k; double eps_rel; double xmax;
+    double xres;  // PREC_BF16: bound of |q.(x - bf16(x))| per unit |q| (cosine: relative, L2: absolute)
     float* out_s; int64_t* out_i; double* out_k; int64_t index_offset;
     int* flag_count; int* flag_list; const uint32_t* gthr;
     int* overflow_count;  // lists longer than the finish kernel holds (they take the exact path)

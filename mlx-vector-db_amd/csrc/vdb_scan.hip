@@ -122,6 +122,18 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 // C2 587 -> 559 us.  With several query blocks the blocks of one row range share
 // its lines through the XCD's L2 (xcd_map), which nt defeats (C3 2.62 -> 3.12 ms,
 // C4 7.56 -> 8.89 ms): default policy there.  Measured A/B on MI355X.
+// Operand planes per precision: XPL corpus planes loaded per group, QPL query
+// planes, LPL planes in the corpus layout (the split layout holds hi and lo).
+//   PREC_FP32    fp32 x fp32                  XPL 1  QPL 1  LPL 1
+//   PREC_BF16X3  (xh + xl) x (qh + ql)        XPL 2  QPL 2  LPL 2
+//   PREC_BF16    xh x (qh + ql): half the corpus bytes of the other two
+template <int PREC>
+struct Planes {
+    static constexpr int XPL = PREC == PREC_BF16X3 ? 2 : 1;
+    static constexpr int QPL = PREC == PREC_FP32 ? 1 : 2;
+    static constexpr int LPL = PREC == PREC_FP32 ? 1 : 2;
+};
+
 template <bool NT>
 __device__ __forceinline__ f32x4 corpus_ld(const float* p) {
     if constexpr (NT) return __builtin_nontemporal_load((const f32x4*)p);
@@ -230,10 +242,11 @@ __device__ __forceinline__ void append_flush(const float* sc, const uint32_t* ix
 
 // Inner products of one 8-dim (fp32) or 16-dim (split-bf16) group of RT corpus
 // tiles against QT query tiles.  PREC_BF16X3: x.q ~ xh.qh + xh.ql + xl.qh, each
-// product exact in fp32, dropped terms <= ~3 2^-16 |x||q| per element.
+// product exact in fp32, dropped terms <= ~3 2^-16 |x||q| per element; PREC_BF16:
+// x.q ~ xh.qh + xh.ql, off by |x - xh| <= 2^-9 |x| per element.
 template <int PREC, int RT, int QT>
-__device__ __forceinline__ void group_mfma(const f32x4 (&x)[RT][PREC + 1], const f32x4 (&q)[QT][PREC + 1],
-                                           f32x16 (&acc)[RT][QT]) {
+__device__ __forceinline__ void group_mfma(const f32x4 (&x)[RT][Planes<PREC>::XPL],
+                                           const f32x4 (&q)[QT][Planes<PREC>::QPL], f32x16 (&acc)[RT][QT]) {
     if constexpr (PREC == PREC_FP32) {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -242,6 +255,16 @@ __device__ __forceinline__ void group_mfma(const f32x4 (&x)[RT][PREC + 1], const
 #pragma unroll
                 for (int qt = 0; qt < QT; ++qt)
                     acc[rt][qt] = __builtin_amdgcn_mfma_f32_32x32x2f32(x[rt][0][j], q[qt][0][j], acc[rt][qt], 0, 0, 0);
+    } else if constexpr (PREC == PREC_BF16) {
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt) {
+                const bf16x8 xh = __builtin_bit_cast(bf16x8, x[rt][0]);
+                const bf16x8 qh = __builtin_bit_cast(bf16x8, q[qt][0]), ql = __builtin_bit_cast(bf16x8, q[qt][1]);
+                acc[rt][qt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xh, ql, acc[rt][qt], 0, 0, 0);
+                acc[rt][qt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xh, qh, acc[rt][qt], 0, 0, 0);
+            }
     } else {
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt)
@@ -316,8 +339,8 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
     // super-tile addressing: group g of row tile t starts at blk(t, g); consecutive
     // groups are GBLK blocks apart (fp32: 4 sub tiles; split: 2 planes x 4 sub
     // tiles), sub tiles of one group adjacent, the lo plane 4 blocks after hi.
-    constexpr int NPL = PREC + 1;
-    constexpr int GBLK = 4 * NPL;
+    constexpr int XPL = Planes<PREC>::XPL, QPL = Planes<PREC>::QPL;
+    constexpr int GBLK = 4 * Planes<PREC>::LPL;
     constexpr size_t GSTEP = GBLK * BLOCK_FLOATS;
     constexpr size_t PLANE = 4 * BLOCK_FLOATS;
     auto blk = [](uint64_t t, int g, int GG) -> size_t {
@@ -327,7 +350,7 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
     // the query stream of a step runs through groups PQ .. G+PQ-1 without a wrap
     const float* Qbase = Qt + blk((uint64_t)(qb * QT), 0, G + QG_EXTRA);
 
-    f32x4 xr[PX][RT][NPL], qr[PQ][QT][NPL];
+    f32x4 xr[PX][RT][XPL], qr[PQ][QT][QPL];
     if (s_begin < s_end) {
         const float* xs = X + blk((uint64_t)((s_begin * NW + wv) * RT), 0, G);
 #pragma unroll
@@ -335,14 +358,14 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-                for (int pl = 0; pl < NPL; ++pl)
+                for (int pl = 0; pl < XPL; ++pl)
                     xr[p][rt][pl] = corpus_ld<NT>(xs + p * GSTEP + pl * PLANE + rt * BLOCK_FLOATS + lane4);
 #pragma unroll
         for (int p = 0; p < PQ; ++p)
 #pragma unroll
             for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
-                for (int pl = 0; pl < NPL; ++pl)
+                for (int pl = 0; pl < QPL; ++pl)
                     qr[p][qt][pl] = *(const f32x4*)(Qbase + p * GSTEP + pl * PLANE + qt * BLOCK_FLOATS + lane4);
     }
     // epilogue inputs of step s (see the step loop)
@@ -396,12 +419,12 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-                for (int pl = 0; pl < NPL; ++pl)
+                for (int pl = 0; pl < XPL; ++pl)
                     xr[p][rt][pl] = corpus_ld<NT>(xsrc + pl * PLANE + rt * BLOCK_FLOATS + lane4);
 #pragma unroll
             for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
-                for (int pl = 0; pl < NPL; ++pl)
+                for (int pl = 0; pl < QPL; ++pl)
                     qr[pq][qt][pl] = *(const f32x4*)(qsrc + pl * PLANE + qt * BLOCK_FLOATS + lane4);
             __builtin_amdgcn_sched_barrier(0);
         };
@@ -674,8 +697,8 @@ scan_topk_priv_kernel(const float* __restrict__ X, const float* __restrict__ row
 
     const int64_t s_begin = (int64_t)wg * steps_per_wg;
     const int64_t s_end = s_begin + steps_per_wg < n_steps ? s_begin + steps_per_wg : n_steps;
-    constexpr int NPL = PREC + 1;
-    constexpr int GBLK = 4 * NPL;
+    constexpr int XPL = Planes<PREC>::XPL, QPL = Planes<PREC>::QPL;
+    constexpr int GBLK = 4 * Planes<PREC>::LPL;
     constexpr size_t GSTEP = GBLK * BLOCK_FLOATS;
     constexpr size_t PLANE = 4 * BLOCK_FLOATS;
     auto blk = [](uint64_t t, int g, int GG) -> size_t {
@@ -690,7 +713,7 @@ scan_topk_priv_kernel(const float* __restrict__ X, const float* __restrict__ row
     uint4 sv[KP / 4];
     bool sv_pending = false;
 
-    f32x4 xr[PX][RT][NPL], qr[PQ][QT][NPL];
+    f32x4 xr[PX][RT][XPL], qr[PQ][QT][QPL];
     if (s_begin < s_end) {
         const float* xs = X + blk((uint64_t)((s_begin * 4 + wv) * RT), 0, G);
 #pragma unroll
@@ -698,14 +721,14 @@ scan_topk_priv_kernel(const float* __restrict__ X, const float* __restrict__ row
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-                for (int pl = 0; pl < NPL; ++pl)
+                for (int pl = 0; pl < XPL; ++pl)
                     xr[p][rt][pl] = corpus_ld<false>(xs + p * GSTEP + pl * PLANE + rt * BLOCK_FLOATS + lane4);
 #pragma unroll
         for (int p = 0; p < PQ; ++p)
 #pragma unroll
             for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
-                for (int pl = 0; pl < NPL; ++pl)
+                for (int pl = 0; pl < QPL; ++pl)
                     qr[p][qt][pl] = *(const f32x4*)(Qbase + p * GSTEP + pl * PLANE + qt * BLOCK_FLOATS + lane4);
     }
     // epilogue inputs of step s (see the step loop)
@@ -750,12 +773,12 @@ scan_topk_priv_kernel(const float* __restrict__ X, const float* __restrict__ row
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-                for (int pl = 0; pl < NPL; ++pl)
+                for (int pl = 0; pl < XPL; ++pl)
                     xr[p][rt][pl] = corpus_ld<false>(xsrc + pl * PLANE + rt * BLOCK_FLOATS + lane4);
 #pragma unroll
             for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
-                for (int pl = 0; pl < NPL; ++pl)
+                for (int pl = 0; pl < QPL; ++pl)
                     qr[pq][qt][pl] = *(const f32x4*)(qsrc + pl * PLANE + qt * BLOCK_FLOATS + lane4);
             __builtin_amdgcn_sched_barrier(0);
         };
@@ -1002,8 +1025,8 @@ __global__ void __launch_bounds__(64) pilot_scores_kernel(const float* __restric
                                                           int G, int64_t N, int B, int64_t n_tiles, int n_sample,
                                                           uint32_t* __restrict__ pslots) {
     constexpr int QB = 32 * QT;
-    constexpr int NPL = PREC + 1;
-    constexpr int GBLK = 4 * NPL;
+    constexpr int XPL = Planes<PREC>::XPL, QPL = Planes<PREC>::QPL;
+    constexpr int GBLK = 4 * Planes<PREC>::LPL;
     constexpr size_t GSTEP = GBLK * BLOCK_FLOATS;
     constexpr size_t PLANE = 4 * BLOCK_FLOATS;
     auto blk = [](uint64_t t, int g, int GG) -> size_t {
@@ -1023,15 +1046,15 @@ __global__ void __launch_bounds__(64) pilot_scores_kernel(const float* __restric
     // one wave, groups in the scan's order (bit-identical accumulators), loads PP
     // groups ahead so the tile costs a few HBM round trips, not G of them
     constexpr int PP = 12;
-    f32x4 xr[PP][1][NPL], qr[PP][QT][NPL];
+    f32x4 xr[PP][1][XPL], qr[PP][QT][QPL];
     auto load = [&](int slot, int g) {
         if (g < G) {
 #pragma unroll
-            for (int pl = 0; pl < NPL; ++pl) xr[slot][0][pl] = *(const f32x4*)(xs + g * GSTEP + pl * PLANE);
+            for (int pl = 0; pl < XPL; ++pl) xr[slot][0][pl] = *(const f32x4*)(xs + g * GSTEP + pl * PLANE);
 #pragma unroll
             for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
-                for (int pl = 0; pl < NPL; ++pl)
+                for (int pl = 0; pl < QPL; ++pl)
                     qr[slot][qt][pl] = *(const f32x4*)(qs + g * GSTEP + pl * PLANE + qt * BLOCK_FLOATS);
         }
     };
@@ -1108,6 +1131,7 @@ hipError_t launch_pilot(int prec, int metric, int KP, const float* X, const floa
     }
     VDB_PILOT(0, 0, 2) VDB_PILOT(0, 1, 2) VDB_PILOT(1, 0, 2) VDB_PILOT(1, 1, 2)
     VDB_PILOT(0, 0, 1) VDB_PILOT(0, 1, 1) VDB_PILOT(1, 0, 1) VDB_PILOT(1, 1, 1)
+    VDB_PILOT(2, 0, 2) VDB_PILOT(2, 1, 2) VDB_PILOT(2, 0, 1) VDB_PILOT(2, 1, 1)
 #undef VDB_PILOT
     if (!launched) return hipErrorInvalidValue;
     hipError_t e = hipGetLastError();
@@ -1142,6 +1166,7 @@ static hipError_t scan_dispatch(const float* X, const float* rowscale, const uin
 // PQ < PX groups ahead caps the usable corpus prefetch at PQ groups.
 static int variant_rt(int prec, int variant) {
     if (prec == PREC_FP32) return variant == 0 ? 2 : 4;
+    if (prec == PREC_BF16) return variant == 1 ? 4 : 2;  // bf16 1: 4 row tiles per wave (16 KiB in flight)
     return 2;
 }
 static int variant_px(int prec, int variant) {
@@ -1163,7 +1188,7 @@ constexpr int kStampVariant = 9;  // diagnostic, no insertion after the first st
 constexpr int kStampVariant = -1;
 #endif
 bool scan_variant_ok(int prec, int variant, int G) {
-    const int vmax = 2;
+    const int vmax = prec == PREC_BF16 ? 1 : 2;
     return ((variant >= 0 && variant <= vmax) || variant == kStampVariant) && G % variant_px(prec, variant) == 0;
 }
 
@@ -1196,7 +1221,11 @@ hipError_t launch_scan_topk(int prec, int metric, int KP, int variant, const flo
     VDB_SCAN(1, M, 2, 32, 1, 2, 4, 4, 256, 1, 1) VDB_SCAN(1, M, 2, 64, 1, 2, 4, 4, 256, 1, 1)                  \
     VDB_SCAN(1, M, 2, 128, 1, 2, 4, 4, 256, 1, 1) VDB_SCAN(1, M, 1, 256, 1, 2, 4, 4, 512, 1, 1)                \
     VDB_SCAN(1, M, 2, 32, 2, 2, 4, 2, 128, 1, 2) VDB_SCAN(1, M, 2, 64, 2, 2, 4, 2, 128, 1, 2)                  \
-    VDB_SCAN(1, M, 2, 128, 2, 2, 4, 4, 256, 1, 1) VDB_SCAN(1, M, 1, 256, 2, 2, 4, 4, 512, 1, 1)
+    VDB_SCAN(1, M, 2, 128, 2, 2, 4, 4, 256, 1, 1) VDB_SCAN(1, M, 1, 256, 2, 2, 4, 4, 512, 1, 1)                \
+    VDB_SCAN2(2, M, 2, 32, 0, 2, 4, 4, 128, 1, 1) VDB_SCAN2(2, M, 2, 64, 0, 2, 4, 4, 128, 1, 1)                \
+    VDB_SCAN2(2, M, 2, 128, 0, 2, 4, 4, 256, 1, 1) VDB_SCAN(2, M, 1, 256, 0, 2, 4, 4, 512, 1, 1)               \
+    VDB_SCAN2(2, M, 2, 32, 1, 4, 4, 4, 128, 1, 1) VDB_SCAN2(2, M, 2, 64, 1, 4, 4, 4, 128, 1, 1)                \
+    VDB_SCAN2(2, M, 2, 128, 1, 4, 4, 4, 256, 1, 1) VDB_SCAN(2, M, 1, 256, 1, 4, 4, 4, 512, 1, 1)
     VDB_SCAN_ALL(0)
     VDB_SCAN_ALL(1)
 #ifdef VDB_STAMP

@@ -31,7 +31,7 @@ def _mask_words(mask_bool):
     return np.packbits(bits, bitorder="little").view("<u4").astype(np.uint32)
 
 
-PRECISIONS = ["bf16x3", "fp32"]
+PRECISIONS = ["bf16x3", "bf16", "fp32"]
 
 
 def _check(vdb, V, Q, k, metric, mask=None, force_exact=False, margin=None, chunked_add=False, precision="bf16x3"):
@@ -108,8 +108,10 @@ def test_precision_switch_keeps_results(vdb):
     a = ix.search(Q, 17, with_keys=True)
     ix.set_precision("fp32")
     b = ix.search(Q, 17, with_keys=True)
+    ix.set_precision("bf16")
+    c = ix.search(Q, 17, with_keys=True)
     es, ei, ek = ref_cpu.exact_search(Q, V, 17, "euclidean")
-    for s, i, kk in (a, b):
+    for s, i, kk in (a, b, c):
         np.testing.assert_array_equal(i, ei)
         np.testing.assert_array_equal(kk, ek)
     assert ix.stat("fallback_queries") == 0
