@@ -424,7 +424,7 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
         if (value < 0 || value > 2) return set_error(VDB_ERR_INVALID, "scan_variant must be 0, 1 or 2");
         ix->scan_variant = value;
     } else if (n == "scan_variant_bf16x3") {
-        if (value < 0 || !scan_variant_ok(PREC_BF16X3, (int)value, 96))
+        if (value < 0 || (!scan_variant_ok(PREC_BF16X3, (int)value, 96) && !scan_variant_ok(PREC_BF16, (int)value, 96)))
             return set_error(VDB_ERR_INVALID, "scan_variant_bf16x3 must be 0, 1 or 2");
         ix->scan_variant_b3 = value;
     } else if (n == "graph_fill") {

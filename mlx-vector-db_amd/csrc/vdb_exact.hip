@@ -60,6 +60,58 @@ __device__ __forceinline__ double exact_key(const float* __restrict__ q, double 
 //   reach the top k.  A failed certificate queues the query for exact_scan.
 constexpr int RERANK_WAVES = 16;
 
+// Same keys (same canonical order) with the query pieces in registers and every
+// row piece of NB rows requested before the first FMA: one dependent round trip
+// per batch instead of np of them (D <= 256 MP).
+template <int METRIC, int NB, int MP>
+__device__ __forceinline__ void exact_keys_regs(const float (&qv)[MP][4], double qn, const float* __restrict__ X,
+                                                int G, int np, const uint32_t* rows, const double* xn, int nb,
+                                                double* out) {
+    const int lane = threadIdx.x & 63;
+    const int Dp = G * GROUP_DIMS;
+    f32x4 xv[MP][NB];
+#pragma unroll
+    for (int m = 0; m < MP; ++m) {
+        const int p = m * 64 + lane;
+#pragma unroll
+        for (int u = 0; u < NB; ++u)
+            xv[m][u] = (m < np && u < nb && 4 * p < Dp) ? *(const f32x4*)(X + tiled_piece_offset(rows[u], p, G))
+                                                       : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    double acc[NB];
+#pragma unroll
+    for (int u = 0; u < NB; ++u) acc[u] = 0.0;
+#pragma unroll
+    for (int m = 0; m < MP; ++m) {
+        if (m < np) {
+#pragma unroll
+            for (int u = 0; u < NB; ++u)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const double qd = (double)qv[m][j];
+                    const double xd = (double)xv[m][u][j];
+                    if (METRIC == 0) {
+                        acc[u] = acc[u] + qd * xd;
+                    } else {
+                        const double df = xd - qd;
+                        acc[u] = acc[u] + df * df;
+                    }
+                }
+        }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1)
+#pragma unroll
+        for (int u = 0; u < NB; ++u) acc[u] = acc[u] + __shfl_xor(acc[u], off, 64);
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+        if (u < nb) out[u] = METRIC == 0 ? acc[u] / (fmax(qn, 1e-8) * fmax(xn[u], 1e-8)) : -acc[u];
+    }
+}
+
+constexpr int FIN_MP = 4;   // fast path: D <= 1024
+constexpr int FIN_NB4 = 3;  // rows per wave per batch on the fast path (4 spills at 128 VGPRs)
+
 template <int METRIC, int KP>
 __global__ void __launch_bounds__(64 * RERANK_WAVES) rerank_kernel(RerankArgs a) {
     constexpr int E = KP >= 64 ? KP / 64 : 1;
@@ -345,7 +397,35 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
     const int m = s_m;
     const float* q = a.Q + (int64_t)b * a.D;
     const double qn = a.qn64[b];
-    // exact keys: wave wv takes candidates wv FIN_NB, ... in batches of FIN_NB
+    // exact keys: wave wv takes candidates wv NB, ... in batches of NB
+    const int np = (a.D + 255) / 256;
+    if (np <= FIN_MP) {
+        float qv[FIN_MP][4];
+#pragma unroll
+        for (int mm = 0; mm < FIN_MP; ++mm)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int d = 4 * (mm * 64 + lane) + j;
+                qv[mm][j] = (mm < np && d < a.D) ? q[d] : 0.0f;
+            }
+        for (int j0 = wv * FIN_NB4; j0 < m; j0 += FIN_WAVES * FIN_NB4) {
+            uint32_t rows[FIN_NB4];
+            double xn[FIN_NB4];
+            const int nb = min(FIN_NB4, m - j0);
+#pragma unroll
+            for (int u = 0; u < FIN_NB4; ++u) {
+                rows[u] = u < nb ? s_cr[j0 + u] : 0u;
+                xn[u] = (METRIC == 0 && u < nb) ? a.nrm64[rows[u]] : 1.0;
+            }
+            double keys[FIN_NB4];
+            exact_keys_regs<METRIC, FIN_NB4, FIN_MP>(qv, qn, a.X, a.G, np, rows, xn, nb, keys);
+            if (lane == 0) {
+#pragma unroll
+                for (int u = 0; u < FIN_NB4; ++u)
+                    if (u < nb) s_ek[j0 + u] = keys[u];
+            }
+        }
+    } else
     for (int j0 = wv * FIN_NB; j0 < m; j0 += FIN_WAVES * FIN_NB) {
         uint32_t rows[FIN_NB];
         double xn[FIN_NB];
