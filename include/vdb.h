@@ -17,11 +17,13 @@
  *     failing call on the calling thread.
  *   - Plain pointers and sizes only.  `mem` says whether the query / output
  *     pointers of a call are host (VDB_MEM_HOST) or device (VDB_MEM_DEVICE)
- *     memory.  Work is stream-ordered on `stream` (a hipStream_t, or NULL for
- *     the index's own stream).  Host-memory calls return when the results are
- *     in host memory; a device-memory search synchronises `stream` once (to
- *     read the exactness certificate, see vdb_index_search) and returns with
- *     the results in device memory.
+ *     memory.  Device-memory calls are stream-ordered on `stream` (a
+ *     hipStream_t; NULL = the null stream, which orders with PyTorch's default
+ *     stream) and return without waiting: the results are in device memory
+ *     once the stream reaches that point (the exactness certificate is
+ *     checked and any fallback queued on the device, see vdb_index_search).
+ *     Host-memory calls run on `stream` or, if NULL, the index's own stream
+ *     and return when the results are in host memory.
  *   - The library never frees caller memory.  An index owns its device-resident
  *     corpus (tiled fp32 layout) and a per-call workspace pool.
  *   - All entry points are thread-safe; searches on one index may run from

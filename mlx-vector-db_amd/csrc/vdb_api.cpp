@@ -596,7 +596,9 @@ int32_t vdb_index_search(vdb_index* ix, const float* queries, int32_t B, int32_t
         return set_error(VDB_ERR_NONFINITE, "query contains NaN or Inf");
     HIP_TRY(hipSetDevice(ix->device));
     std::shared_lock<std::shared_mutex> g(ix->mu);
-    hipStream_t st = stream ? (hipStream_t)stream : ix->stream;
+    // device memory: the caller's stream, NULL = the null stream (ordered with the caller's
+    // default-stream work, e.g. PyTorch's); host memory: NULL = the index's own stream
+    hipStream_t st = (stream || mem == VDB_MEM_DEVICE) ? (hipStream_t)stream : ix->stream;
     const int64_t N = ix->count;
     ix->n_searches++;
     ix->n_queries += B;
@@ -1067,7 +1069,9 @@ int32_t vdb_graph_search(vdb_graph* g, const float* queries, int32_t nq, int32_t
     std::shared_lock<std::shared_mutex> lk(ix->mu);
     if (ix->count != g->n) return set_error(VDB_ERR_INVALID, "graph is stale: %lld rows, index %lld", (long long)g->n,
                                             (long long)ix->count);
-    hipStream_t st = stream ? (hipStream_t)stream : ix->stream;
+    // device memory: the caller's stream, NULL = the null stream (ordered with the caller's
+    // default-stream work, e.g. PyTorch's); host memory: NULL = the index's own stream
+    hipStream_t st = (stream || mem == VDB_MEM_DEVICE) ? (hipStream_t)stream : ix->stream;
     const float* Qd = queries;
     int64_t* ol = labels;
     float* od = distances;

@@ -226,6 +226,25 @@ def test_device_pointer_search_matches_host(vdb):
     np.testing.assert_array_equal(sd.cpu().numpy(), s_h)
 
 
+def test_device_search_orders_with_torch_default_stream(vdb):
+    """stream=0 (PyTorch's default stream) must order the search with the torch work
+    around it: no explicit synchronise between the search and the copy that reads it."""
+    import torch
+    rng = np.random.default_rng(24)
+    V = rng.random((50000, 128), dtype=np.float32)
+    Q = rng.random((64, 128), dtype=np.float32)
+    ix = vdb.NativeIndex(128, "cosine")
+    ix.add(V)
+    _, ei, _ = ref_cpu.exact_search(Q, V, 10, "cosine")
+    qd = torch.from_numpy(Q).cuda()
+    for _ in range(3):
+        idd = torch.full((64, 10), -7, dtype=torch.int64, device="cuda")
+        sd = torch.empty((64, 10), dtype=torch.float32, device="cuda")
+        ix.search_device(qd.data_ptr(), 64, 10, sd.data_ptr(), idd.data_ptr(), stream=0)
+        got = idd.clone().cpu().numpy()  # torch work on the default stream, no synchronise
+        np.testing.assert_array_equal(got, ei)
+
+
 @pytest.mark.parametrize("metric", ["cosine", "euclidean"])
 def test_device_search_gated_fallback(vdb, metric):
     """Device-memory searches do not wait for the certificate: the exact path is
