@@ -133,6 +133,7 @@ def main_graph(args, world, rank, local, dev):
     t0 = time.perf_counter()
     g = _vdb.NativeGraph.build(ix, degree=R, knn=knn, n_entries=N_ENTRIES)
     build_s = time.perf_counter() - t0
+    g.set_param("teams", args.teams)
     nq = args.warmup + args.steps
     Q = np.random.default_rng(1 + rank).random((nq, D), dtype=np.float32)
     q_dev = torch.from_numpy(Q).to(dev)
@@ -185,6 +186,22 @@ def main_graph(args, world, rank, local, dev):
         ix.search_device(q_dev[i].data_ptr(), 1, k, os_.data_ptr(), oi_.data_ptr(), 0, stream=sp)
         torch.cuda.synchronize()
         bl.append(time.perf_counter() - t1)
+    # the same queries at other team counts (p50 over <= 100 single queries, recall)
+    sweep = []
+    for tm in [int(x) for x in args.teams_sweep.split(",") if x.strip()]:
+        if tm == args.teams:
+            continue
+        g.set_param("teams", tm)
+        tl = []
+        for j in range(min(args.steps, 100)):
+            t1 = time.perf_counter()
+            one(args.warmup + j)
+            torch.cuda.synchronize()
+            tl.append(time.perf_counter() - t1)
+        gl = lab[args.warmup:args.warmup + len(tl)].cpu().numpy()
+        rc = sum(len(set(a.tolist()) & set(b.tolist())) for a, b in zip(gl, gt[:len(tl)])) / float(len(tl) * k)
+        sweep.append({"teams": tm, "p50_ms": float(np.median(tl)) * 1e3, "recall_at_10": rc})
+    g.set_param("teams", args.teams)
     p50 = float(np.median(lat))
     if world > 1:
         t = torch.tensor([elapsed, p50, kern_ms], dtype=torch.float64, device=dev)
@@ -193,7 +210,7 @@ def main_graph(args, world, rank, local, dev):
     if rank == 0:
         # algorithmic bytes of one search: every scored row (D fp32 + its row scale)
         # plus the neighbour list of every expanded node (<= 4 per iteration)
-        q_bytes = visited * (4 * D + 4) + iters * 4 * R * 4
+        q_bytes = visited * (4 * D + 4) + iters * 4 * R * 4  # (visited / iterations summed over the teams)
         achieved = q_bytes / (kern_ms * 1e-3) / 1e9
         rec = {
             "metric": METRIC,
@@ -213,15 +230,18 @@ def main_graph(args, world, rank, local, dev):
             "data": "synthetic uniform [0,1) fp32 (numpy PCG64, corpus seed 0 per 65536-row chunk, queries seed 1)",
             "config": {"workload": f"c5: {desc}", "n_rows": N, "dim": D, "global_batch": 1, "k": k,
                        "metric": metric, "ef": GRAPH_EF, "degree": R, "build_knn": knn, "entries": N_ENTRIES,
+                       "teams": args.teams,
                        "parallelism": f"replicas x{world}" if world > 1 else "single GPU"},
             "build_s": build_s,
             "iterations_per_query": iters,
             "visited_per_query": visited,
             "exact_b1_p50_ms": float(np.median(bl)) * 1e3,
+            "teams_sweep": sweep,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "graph_search",
                          "avg_launch_ms": kern_ms, "algorithmic_bytes": q_bytes,
-                         "note": "one workgroup per query: bound by dependent hops (latency), not bandwidth"},
+                         "note": f"{args.teams} workgroups per query, each a chain of dependent beam steps: "
+                                 "latency-bound, not bandwidth-bound"},
         }
         if keep_host:
             V = np.concatenate(parts) if len(parts) > 1 else parts[0]
@@ -252,6 +272,8 @@ def main():
     ap.add_argument("--margin", type=int, default=None, help="candidates beyond k (tuning; default per precision)")
     ap.add_argument("--rows", type=int, default=None, help="override the corpus rows (exploration only)")
     ap.add_argument("--graph-knn", type=int, default=None, help="c5: kNN candidates per row for the build")
+    ap.add_argument("--teams", type=int, default=64, help="c5: workgroups per query (vdb_graph_set_param teams)")
+    ap.add_argument("--teams-sweep", default="1,16,256", help="c5: extra teams settings reported beside the line")
     ap.add_argument("--pmc-json", default=None,
                     help="HBM traffic of the scan kernel from a separate rocprofv3 --pmc pass "
                          "(default: newest profiles/*/pmc.json for this config, see profiles/scripts/)")

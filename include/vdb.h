@@ -183,8 +183,17 @@ int32_t vdb_graph_info(const vdb_graph* g, int64_t* n_rows, int32_t* degree, int
  * best first.  ef = beam width (search depth), k <= ef <= 256. */
 int32_t vdb_graph_search(vdb_graph* g, const float* queries, int32_t n_queries, int32_t k, int32_t ef, int32_t mem,
                          int64_t* labels, float* distances, void* stream);
-/* stats: "queries", "iterations" (beam iterations, summed over queries), "visited" (rows scored, summed) */
+/* stats: "queries", "iterations" (beam iterations, summed over queries and teams),
+ * "visited" (rows scored, summed) */
 int32_t vdb_graph_stat(const vdb_graph* g, const char* name, int64_t* value);
+/* Graph search knobs: "teams" (1..256, at most the entry rows; default 1): workgroups per query, each
+ * searching from a disjoint slice of the entry rows (entry rank r -> team r mod
+ * teams) with its own beam of `ef`, merged into the top k distinct rows.  At
+ * batch 1 it puts several CUs on the query: more of the graph explored (higher
+ * recall) in about the same latency.  Replaces: nothing in hnswlib (its search
+ * is single-threaded per query). */
+int32_t vdb_graph_set_param(vdb_graph* g, const char* name, int64_t value);
+
 int32_t vdb_graph_destroy(vdb_graph* g);
 
 #ifdef __cplusplus

@@ -840,6 +840,7 @@ struct vdb_graph {
     int32_t* entries = nullptr;  // device [n_entries]
     float* rows = nullptr;       // device [n][Dp] row-major copy of the corpus (gathers)
     int Dp = 0;
+    int teams = 1;               // workgroups per query (vdb_graph_set_param "teams")
     unsigned long long* d_stats = nullptr;
     std::atomic<int64_t> n_queries{0};
 };
@@ -1076,19 +1077,29 @@ int32_t vdb_graph_search(vdb_graph* g, const float* queries, int32_t nq, int32_t
     int64_t* ol = labels;
     float* od = distances;
     void* tmp = nullptr;
-    if (mem == VDB_MEM_HOST) {
-        const size_t qb = (size_t)nq * D * 4, lb = (size_t)nq * k * 8, db = (size_t)nq * k * 4;
-        HIP_TRY(hipMallocAsync(&tmp, qb + lb + db + 512, st));
+    const int T = (int)std::min<int64_t>(g->teams, std::max(g->n_entries, 1));
+    const size_t qb = mem == VDB_MEM_HOST ? (size_t)nq * D * 4 : 0, lb = (size_t)nq * k * 8, db = (size_t)nq * k * 4;
+    const size_t tb = T > 1 ? (size_t)nq * T * k * 12 + 512 : 0;
+    if (mem == VDB_MEM_HOST || T > 1) {
+        HIP_TRY(hipMallocAsync(&tmp, qb + lb + db + tb + 1024, st));
         char* base = (char*)tmp;
-        HIP_TRY(hipMemcpyAsync(base, queries, qb, hipMemcpyHostToDevice, st));
-        Qd = (const float*)base;
-        ol = (int64_t*)(base + ((qb + 255) & ~size_t(255)));
-        od = (float*)((char*)ol + ((lb + 255) & ~size_t(255)));
+        if (mem == VDB_MEM_HOST) {
+            HIP_TRY(hipMemcpyAsync(base, queries, qb, hipMemcpyHostToDevice, st));
+            Qd = (const float*)base;
+            ol = (int64_t*)(base + ((qb + 255) & ~size_t(255)));
+            od = (float*)((char*)ol + ((lb + 255) & ~size_t(255)));
+        }
     }
     GraphSearchArgs a;
     a.rows = g->rows; a.Dp = g->Dp; a.D = D; a.rowscale = ix->metric == 0 ? ix->inv32 : ix->sq32; a.n_rows = g->n;
     a.nbr = g->nbr; a.R = g->R; a.entries = g->entries; a.n_entries = g->n_entries;
     a.Q = Qd; a.k = k; a.ef = ef; a.out_lab = ol; a.out_dist = od; a.stats = g->d_stats;
+    a.teams = T;
+    if (T > 1) {
+        char* tbase = (char*)tmp + ((qb + 255) & ~size_t(255)) + ((lb + 255) & ~size_t(255)) + ((db + 255) & ~size_t(255));
+        a.tmp_lab = (int64_t*)tbase;
+        a.tmp_dist = (float*)(tbase + (((size_t)nq * T * k * 8 + 255) & ~size_t(255)));
+    }
     if (g->n == 0) {
         HIP_TRY(hipMemsetAsync(ol, 0xFF, (size_t)nq * k * 8, st));
     } else {
@@ -1098,8 +1109,20 @@ int32_t vdb_graph_search(vdb_graph* g, const float* queries, int32_t nq, int32_t
     if (mem == VDB_MEM_HOST) {
         HIP_TRY(hipMemcpyAsync(labels, ol, (size_t)nq * k * 8, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipMemcpyAsync(distances, od, (size_t)nq * k * 4, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipFreeAsync(tmp, st));
-        HIP_TRY(hipStreamSynchronize(st));
+    }
+    if (tmp) HIP_TRY(hipFreeAsync(tmp, st));
+    if (mem == VDB_MEM_HOST) HIP_TRY(hipStreamSynchronize(st));
+    return VDB_OK;
+}
+
+int32_t vdb_graph_set_param(vdb_graph* g, const char* name, int64_t value) {
+    if (!g || !name) return set_error(VDB_ERR_INVALID, "NULL argument");
+    const std::string n(name);
+    if (n == "teams") {
+        if (value < 1 || value > 256) return set_error(VDB_ERR_INVALID, "teams must be in [1, 256]");
+        g->teams = (int)value;
+    } else {
+        return set_error(VDB_ERR_INVALID, "unknown graph parameter '%s'", name);
     }
     return VDB_OK;
 }

@@ -96,7 +96,13 @@ __global__ void __launch_bounds__(64 * GS_WAVES) graph_search_kernel(GraphSearch
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wv = tid >> 6;
-    const int b = blockIdx.x;
+    // teams > 1: a.teams workgroups search one query from disjoint entry slices
+    // (entry rank r goes to team r mod teams), each with its own beam and visited
+    // set; their top-k lists are merged by graph_merge_kernel.  At batch 1 this
+    // puts a.teams CUs on the query instead of one.
+    const int T = a.teams;
+    const int b = blockIdx.x / T;
+    const int team = blockIdx.x % T;
     const int Dp = a.Dp;
     float* qs = reinterpret_cast<float*>(smem);                                  // [Dp]
     uint32_t* vis = reinterpret_cast<uint32_t*>(smem + (size_t)Dp * 4);          // [GS_VIS]
@@ -146,15 +152,19 @@ __global__ void __launch_bounds__(64 * GS_WAVES) graph_search_kernel(GraphSearch
         const int32_t iv = s_ei[e];
         int rank = 0;
         for (int j = 0; j < E; ++j) rank += better(s_es[j], (uint32_t)s_ei[j], sv, (uint32_t)iv) ? 1 : 0;
-        if (rank < ef) {
-            s_bs[0][rank] = sv;
-            s_bi[0][rank] = iv;
-            s_bx[0][rank] = 0;
+        if (rank % T == team) {
+            const int pos = rank / T;
+            if (pos < ef) {
+                s_bs[0][pos] = sv;
+                s_bi[0][pos] = iv;
+                s_bx[0][pos] = 0;
+            }
+            visit(vis, iv);
         }
-        visit(vis, iv);
     }
     if (tid == 0) {
-        s_bn = E < ef ? E : ef;
+        const int mine = (E - team + T - 1) / T;
+        s_bn = mine < ef ? mine : ef;
         s_cur = 0;
         s_scored = (unsigned)E;
     }
@@ -270,15 +280,17 @@ __global__ void __launch_bounds__(64 * GS_WAVES) graph_search_kernel(GraphSearch
     // ---- results: top k of the beam, hnswlib distance conventions
     const int cur = s_cur;
     const int bn = s_bn;
+    int64_t* out_lab = T > 1 ? a.tmp_lab + (size_t)team * a.k : a.out_lab;  // teams: [b][team][k]
+    float* out_dist = T > 1 ? a.tmp_dist + (size_t)team * a.k : a.out_dist;
     for (int e = tid; e < a.k; e += 64 * GS_WAVES) {
-        const size_t o = (size_t)b * a.k + e;
+        const size_t o = (size_t)b * T * a.k + e;
         if (e < bn) {
             const float sv = s_bs[cur][e];
-            a.out_lab[o] = (int64_t)s_bi[cur][e];
-            a.out_dist[o] = METRIC == 0 ? 1.0f - sv : fmaxf(s_qn2 - sv, 0.0f);
+            out_lab[o] = (int64_t)s_bi[cur][e];
+            out_dist[o] = METRIC == 0 ? 1.0f - sv : fmaxf(s_qn2 - sv, 0.0f);
         } else {
-            a.out_lab[o] = -1;
-            a.out_dist[o] = INFINITY;
+            out_lab[o] = -1;
+            out_dist[o] = INFINITY;
         }
     }
     if (tid == 0 && a.stats) {
@@ -417,14 +429,69 @@ hipError_t launch_graph_rows(const float* X, int G, int64_t n, int Dp, float* ou
     return hipGetLastError();
 }
 
+// Teams' lists [b][T][k] (distance ascending) -> top k distinct rows by (distance,
+// row).  A row found by several teams carries the same distance in each (same
+// arithmetic), so "the next pair strictly after the last one taken" skips copies.
+constexpr int64_t kNoLabel = 0x7FFFFFFFFFFFFFFFll;
+
+__global__ void __launch_bounds__(64) graph_merge_kernel(const int64_t* __restrict__ tl, const float* __restrict__ td,
+                                                         int T, int k, int64_t* __restrict__ out_lab,
+                                                         float* __restrict__ out_dist) {
+    const int b = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int n = T * k;
+    const int64_t* L = tl + (size_t)b * n;
+    const float* Dd = td + (size_t)b * n;
+    float last_d = -INFINITY;
+    int64_t last_l = -1;  // labels are >= 0
+    for (int e = 0; e < k; ++e) {
+        float bd = INFINITY;
+        int64_t bl = kNoLabel;
+        for (int i = lane; i < n; i += 64) {
+            const float d = Dd[i];
+            const int64_t l = L[i];
+            if (l < 0) continue;
+            const bool after = d > last_d || (d == last_d && l > last_l);
+            const bool before = d < bd || (d == bd && l < bl);
+            if (after && before) {
+                bd = d;
+                bl = l;
+            }
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const float od = __shfl_xor(bd, off, 64);
+            const int64_t ol = __shfl_xor(bl, off, 64);
+            if (od < bd || (od == bd && ol < bl)) {
+                bd = od;
+                bl = ol;
+            }
+        }
+        if (lane == 0) {
+            out_lab[(size_t)b * k + e] = bl == kNoLabel ? -1 : bl;
+            out_dist[(size_t)b * k + e] = bl == kNoLabel ? INFINITY : bd;
+        }
+        last_d = bd;
+        last_l = bl;
+    }
+}
+
 hipError_t launch_graph_search(int metric, const GraphSearchArgs& a, int nq, hipStream_t st) {
     if (a.R > GS_R_MAX || a.ef > GS_EF_MAX || a.ef < 1 || a.k > a.ef) return hipErrorInvalidValue;
+    if (a.teams < 1 || a.teams > GS_ENT_MAX || (a.teams > 1 && (!a.tmp_lab || !a.tmp_dist))) return hipErrorInvalidValue;
     if (a.Dp % 32 || a.Dp < a.D) return hipErrorInvalidValue;
     const size_t lds = (size_t)a.Dp * 4 + (size_t)GS_VIS * 4;
+    const dim3 grid((unsigned)nq * a.teams);
     if (metric == 0)
-        hipLaunchKernelGGL(graph_search_kernel<0>, dim3(nq), dim3(64 * GS_WAVES), lds, st, a);
+        hipLaunchKernelGGL(graph_search_kernel<0>, grid, dim3(64 * GS_WAVES), lds, st, a);
     else
-        hipLaunchKernelGGL(graph_search_kernel<1>, dim3(nq), dim3(64 * GS_WAVES), lds, st, a);
+        hipLaunchKernelGGL(graph_search_kernel<1>, grid, dim3(64 * GS_WAVES), lds, st, a);
+    if (a.teams > 1) {
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(graph_merge_kernel, dim3(nq), dim3(64), 0, st, a.tmp_lab, a.tmp_dist, a.teams, a.k,
+                           a.out_lab, a.out_dist);
+    }
     return hipGetLastError();
 }
 

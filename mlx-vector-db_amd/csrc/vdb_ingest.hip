@@ -53,10 +53,15 @@ __global__ void __launch_bounds__(256) pack_rows_kernel(const float* __restrict_
         } else {
             // xmax_bits[0] max |x|; [1] max |x - bf16(x)| / max(|x|, 1e-8); [2] max |x - bf16(x)|
             // (non-negative doubles order like their bit patterns)
+            // (a plain read first: the maxima are monotone, so a stale value only lets an
+            // atomic through; one atomic per row on three shared words serialised ingest)
             const double dr = sqrt(res);
-            atomicMax(xmax_bits, (unsigned long long)__double_as_longlong(nr));
-            atomicMax(xmax_bits + 1, (unsigned long long)__double_as_longlong(dr / fmax(nr, 1e-8)));
-            atomicMax(xmax_bits + 2, (unsigned long long)__double_as_longlong(dr));
+            const unsigned long long v[3] = {(unsigned long long)__double_as_longlong(nr),
+                                             (unsigned long long)__double_as_longlong(dr / fmax(nr, 1e-8)),
+                                             (unsigned long long)__double_as_longlong(dr)};
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+                if (v[i] > __atomic_load_n(xmax_bits + i, __ATOMIC_RELAXED)) atomicMax(xmax_bits + i, v[i]);
         }
     }
 }

@@ -142,6 +142,8 @@ struct GraphSearchArgs {
     const int32_t* nbr; int R; const int32_t* entries; int n_entries;
     const float* Q; int k; int ef;
     int64_t* out_lab; float* out_dist; unsigned long long* stats;
+    int teams = 1;                                          // workgroups per query (disjoint entry slices)
+    int64_t* tmp_lab = nullptr; float* tmp_dist = nullptr;  // teams > 1: per-team lists [nq][teams][k]
 };
 hipError_t launch_graph_search(int metric, const GraphSearchArgs& a, int nq, hipStream_t st);
 // row-major [n][Dp] copy of the tiled corpus for the graph's gathers (Dp % 32 == 0)

@@ -42,7 +42,7 @@ EXPORTED_SYMBOLS = (
     "vdb_index_add", "vdb_index_count", "vdb_index_clear", "vdb_index_get_vectors",
     "vdb_index_search", "vdb_merge_topk", "vdb_similarity_matrix",
     "vdb_graph_build", "vdb_graph_import", "vdb_graph_export", "vdb_graph_info", "vdb_graph_search",
-    "vdb_graph_stat", "vdb_graph_destroy",
+    "vdb_graph_stat", "vdb_graph_set_param", "vdb_graph_destroy",
 )
 
 _lib = None
@@ -103,6 +103,7 @@ def load_library():
             "vdb_graph_info": (c_i32, [c_vp, p_i64, ctypes.POINTER(c_i32), ctypes.POINTER(c_i32)]),
             "vdb_graph_search": (c_i32, [c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp]),
             "vdb_graph_stat": (c_i32, [c_vp, ctypes.c_char_p, p_i64]),
+            "vdb_graph_set_param": (c_i32, [c_vp, ctypes.c_char_p, c_i64]),
             "vdb_graph_destroy": (c_i32, [c_vp]),
         }
         for name, (res, args) in sig.items():
@@ -304,6 +305,10 @@ class NativeGraph:
         v = ctypes.c_int64(0)
         _check(self._lib.vdb_graph_stat(self._h, name.encode(), ctypes.byref(v)))
         return int(v.value)
+
+    def set_param(self, name: str, value: int) -> None:
+        """include/vdb.h vdb_graph_set_param ("teams": workgroups per query)."""
+        _check(self._lib.vdb_graph_set_param(self._h, name.encode(), int(value)))
 
     def close(self) -> None:
         h, self._h = getattr(self, "_h", None), None

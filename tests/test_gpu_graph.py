@@ -163,3 +163,31 @@ def test_graph_search_agrees_with_cpu_restatement(vdb, metric):
     v0 = g.stat("visited")
     g.search(Q[:1], k, ef=ef)
     assert g.stat("visited") > v0
+
+
+@pytest.mark.parametrize("metric", ["cosine", "euclidean"])
+def test_graph_teams_explore_more(vdb, metric):
+    """teams > 1: several workgroups per query from disjoint entry slices, merged
+    into distinct rows; at least the recall of one team, same conventions."""
+    rng = np.random.default_rng(37)
+    N, D, nq, k = 30000, 96, 64, 10
+    V = rng.random((N, D), dtype=np.float32)
+    Q = rng.random((nq, D), dtype=np.float32)
+    ix = vdb.NativeIndex(D, metric)
+    ix.add(V)
+    g = vdb.NativeGraph.build(ix, degree=32, knn=32)
+    _, ei, _ = ref_cpu.exact_search(Q, V, k, metric)
+    one, _ = g.search(Q, k, ef=32)
+    g.set_param("teams", 16)
+    lab, dist = g.search(Q, k, ef=32)
+    assert all(len(set(r.tolist())) == k for r in lab) and (lab >= 0).all()
+    assert (np.diff(dist, axis=1) >= 0).all()
+    for b in range(nq):
+        keys = ref_cpu.exact_keys(Q[b], V[lab[b]], metric)
+        want = 1.0 - keys if metric == "cosine" else -keys
+        np.testing.assert_allclose(dist[b], want, rtol=1e-4, atol=1e-5)
+    assert _recall(lab, ei) >= _recall(one, ei)
+    single = np.stack([g.search(Q[b], k, ef=32)[0][0] for b in range(4)])
+    np.testing.assert_array_equal(single, lab[:4])  # deterministic, batch-independent
+    with pytest.raises(ValueError):
+        g.set_param("teams", 0)
