@@ -34,6 +34,10 @@ logger = logging.getLogger("mlx_hnsw_lib")
 
 GRAPH_FILE = "hnsw_graph.npz"
 N_ENTRIES = 256
+# workgroups per query (include/vdb.h vdb_graph_set_param "teams"): at batch 1 the
+# query gets 64 CUs, each searching from its own slice of the entry rows
+# (5M x 384, ef 128: recall@10 0.06 -> 0.39 for p50 0.54 -> 0.66 ms)
+TEAMS = 64
 
 
 class ProductionHNSWIndex:
@@ -75,6 +79,7 @@ class ProductionHNSWIndex:
             self.index.close()
         degree = 2 * int(M)
         self.index = _vdb.NativeGraph.build(native_index, degree=degree, knn=degree, n_entries=N_ENTRIES)
+        self.index.set_param("teams", TEAMS)
         self._native = native_index
         self.max_elements = max(self.max_elements, n)
         self.is_loaded = True
@@ -133,6 +138,7 @@ class ProductionHNSWIndex:
             logger.warning("saved graph has %d rows, corpus %d: rebuild needed", nbr.shape[0], native_index.count())
             return False
         self.index = _vdb.NativeGraph.from_arrays(native_index, nbr, ent)
+        self.index.set_param("teams", TEAMS)
         self._native = native_index
         self.is_loaded = True
         self._pending = None
