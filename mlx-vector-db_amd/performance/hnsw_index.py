@@ -9,10 +9,12 @@ l2 -> squared L2, hnsw_index.py:35,101), ``save_index`` / ``_load_index``,
 ``is_loaded``, ``RuntimeError`` when searched before it is built (:91-92).
 
 What differs: the graph is one level of out-degree 2M (hnswlib's
-level-0 degree) built on the GPU from the exact kNN of every row — the nearest M
-out-edges plus the nearest reverse edges — instead of hnswlib's incremental
-insertion, so ``ef_construction`` and ``num_threads`` have nothing to control;
-the upper levels' job (a good start) is done by scoring 256 spread entry rows.
+level-0 degree) built on the GPU from the exact kNN of every row — hnswlib's
+neighbour heuristic selects <= M out-edges, then <= 2M of out- and in-edges —
+instead of hnswlib's incremental insertion, so ``ef_construction`` and
+``num_threads`` have nothing to control; the upper levels' job (a good start) is
+done by scoring 256 spread entry rows, and each query is searched by TEAMS
+workgroups from disjoint slices of them.
 The file is ``hnsw_graph.npz`` (neighbour array + entry rows); hnswlib's
 ``hnsw_index.bin`` format is not produced (its compatibility is unpinned,
 SURVEY.md §8f).  The graph refers to the corpus rows of a device index: ``build``
