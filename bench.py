@@ -268,6 +268,8 @@ def main():
                     help="candidate-pass arithmetic (results identical; DESIGN.md §3)")
     ap.add_argument("--scan-variant", type=int, default=None, help="candidate-pass kernel variant (tuning)")
     ap.add_argument("--n-wg", type=int, default=None, help="candidate-pass workgroups (tuning)")
+    ap.add_argument("--scan-sync", type=int, default=None,
+                    help="candidate-pass step end: 1 lockstep barrier, 2 flag-gated rounds (tuning; default by D)")
     ap.add_argument("--pilot-tiles", type=int, default=None, help="row tiles sampled by the pilot bound (tuning)")
     ap.add_argument("--margin", type=int, default=None, help="candidates beyond k (tuning; default per precision)")
     ap.add_argument("--rows", type=int, default=None, help="override the corpus rows (exploration only)")
@@ -303,6 +305,8 @@ def main():
         ix.set_param("scan_variant" if args.precision == "fp32" else "scan_variant_bf16x3", args.scan_variant)
     if args.n_wg is not None:
         ix.set_param("n_wg", args.n_wg)
+    if args.scan_sync is not None:
+        ix.set_param("scan_sync", args.scan_sync)
     if args.pilot_tiles is not None:
         ix.set_param("pilot_tiles", args.pilot_tiles)
     if args.margin is not None:

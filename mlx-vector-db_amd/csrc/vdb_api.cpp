@@ -115,6 +115,7 @@ struct vdb_index {
     int64_t graph_fill = 0;     // graph build: top up pruned neighbour lists (hnswlib keepPrunedConnections)
     int64_t scan_variant = 0;     // fp32 candidate pass variant (vdb_scan.hip)
     int64_t scan_variant_b3 = 0;  // bf16x3 candidate pass variant
+    int64_t scan_sync = 0;        // scan step end: 0 auto, 1 lockstep barrier, 2 flag-gated rounds
     // stats
     std::atomic<int64_t> n_searches{0}, n_queries{0}, n_fallback{0}, n_overflow{0};
     std::atomic<int64_t> scan_ns{0}, pipe_ns{0}, n_timed{0};
@@ -420,6 +421,9 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
         ix->force_exact = value != 0;
     } else if (n == "n_wg") {
         ix->n_wg_override = value;
+    } else if (n == "scan_sync") {
+        if (value < 0 || value > 2) return set_error(VDB_ERR_INVALID, "scan_sync must be 0, 1 or 2");
+        ix->scan_sync = value;
     } else if (n == "scan_variant") {
         if (value < 0 || value > 2) return set_error(VDB_ERR_INVALID, "scan_variant must be 0, 1 or 2");
         ix->scan_variant = value;
@@ -636,6 +640,10 @@ int32_t vdb_index_search(vdb_index* ix, const float* queries, int32_t B, int32_t
     int spw = (int)std::max<int64_t>(1, (n_steps + target - 1) / target);
     int n_wg = (int)((n_steps + spw - 1) / spw);
     const int64_t mask_words = round_up(N, 32) / 32;
+    // Step end of the scan (vdb_scan.hip): short steps (Dp <= 128: C4's 10M x 128 runs 8 split
+    // groups per step, the epilogue ~half of it) gain from dropping the per-step workgroup barrier
+    // (C4 scan 7.58 -> 6.22 ms); long steps lose (C2 0.57 -> 0.65 ms, C3 2.62 -> 2.90 ms), measured.
+    const int lockstep = ix->scan_sync == 0 ? (ix->Dp > 128) : ix->scan_sync == 1;
 
     Workspace* w = acquire_ws(ix);
     struct Releaser {
@@ -731,7 +739,7 @@ int32_t vdb_index_search(vdb_index* ix, const float* queries, int32_t B, int32_t
                                               n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, st));
             else
                 HIP_TRY(launch_scan_topk(prec, ix->metric, KP, variant, Xscan, rowscale, md, Qt, Gs, N, B, n_qblocks,
-                                         n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, st));
+                                         n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, lockstep, st));
             if (timed) HIP_TRY(hipEventRecord(tev[1], st));
             FinishArgs fa;
             fa.gl_s = gl_s; fa.gl_i = gl_i; fa.gl_cnt = gl_cnt; fa.gl_cap = gl_cap;

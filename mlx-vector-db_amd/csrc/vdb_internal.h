@@ -60,7 +60,7 @@ bool scan_variant_ok(int prec, int variant, int G);
 hipError_t launch_scan_topk(int prec, int metric, int KP, int variant, const float* X, const float* rowscale,
                             const uint32_t* mask, const float* Qt, int G, int64_t N, int B, int n_qblocks, int64_t n_steps,
                             int n_wg, int steps_per_wg, float* gl_s, uint32_t* gl_i, uint32_t* gl_cnt, int64_t gl_cap,
-                            uint32_t* gthr, uint32_t* gslots, hipStream_t st);
+                            uint32_t* gthr, uint32_t* gslots, int lockstep, hipStream_t st);
 
 // Wave-private candidate pass (scan_priv(prec, variant, KP)): entries above the
 // shared bound are appended to global per-query lists gl_[s|i][B][gl_cap] (gl_cnt

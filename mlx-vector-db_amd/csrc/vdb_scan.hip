@@ -279,7 +279,8 @@ __device__ __forceinline__ void group_mfma(const f32x4 (&x)[RT][Planes<PREC>::XP
     }
 }
 
-template <int PREC, int METRIC, int QT, int RT, int PX, int PQ, int KP, int CAP, int PUB, int WPS, bool NT, int NW>
+template <int PREC, int METRIC, int QT, int RT, int PX, int PQ, int KP, int CAP, int PUB, int WPS, bool NT, int NW,
+          bool FLAGSYNC>
 __global__ void __launch_bounds__(64 * NW, WPS)
 scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale, const uint32_t* __restrict__ mask,
                  const float* __restrict__ Qt, int G, int64_t N, int B, int64_t n_steps, int steps_per_wg,
@@ -296,8 +297,14 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
     __shared__ uint32_t s_best[NW][QB];  // per wave: order key of the best score appended so far (PUB)
     __shared__ uint32_t s_pub[NW][QB];   // ... and of the last one published
     __shared__ uint32_t s_sh[QB];    // shared bound from the slots (order key), this WG's view
+    __shared__ int s_need;           // some wave holds scores that did not fit: compaction round wanted
+    __shared__ int s_done;           // waves past their last step
 
     const int lane = threadIdx.x & 63;
+    if (FLAGSYNC && threadIdx.x == 0) {
+        s_need = 0;
+        s_done = 0;
+    }
     // wave index made provably uniform: every tile/group address below is then
     // scalar (SGPR base) + lane*16 (one VGPR), keeping VGPRs for the pipeline.
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -528,7 +535,25 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
         const unsigned long long st_b4 = STAMP_NOW();
         st_ins += st_b4 - st_b3;
 #endif
-        while (__syncthreads_or(any_left != 0)) {
+        // Compaction rounds without a per-step barrier: a wave left with scores that
+        // did not fit raises s_need and waits at B1; every other wave looks at s_need
+        // at the end of each of its steps (and once more after its last one, below)
+        // and joins.  In the common step (nothing left anywhere) no wave waits for
+        // another, so the four corpus streams of a workgroup never realign.  The flag
+        // is looked at once per step: after a round a wave stays only while it still
+        // holds leftovers (else waves past their last step, which raise the flag every
+        // round, would keep it here forever).
+        // Without FLAGSYNC (measured better for long steps) every step
+        // ends in one workgroup barrier instead, which doubles as B1.
+        for (bool joined = false;; joined = true) {
+            if constexpr (!FLAGSYNC) {
+                if (!__syncthreads_or(any_left != 0)) break;
+            } else {
+                const bool mine = __any(any_left != 0);
+                if (mine && lane == 0) *(volatile int*)&s_need = 1;
+                if (!mine && (joined || !__builtin_amdgcn_readfirstlane(*(volatile int*)&s_need))) break;
+                __syncthreads();  // B1: all waves here, each with leftovers or having seen the flag
+            }
 #ifdef VDB_STAMP
             ++st_rounds;
 #endif
@@ -540,7 +565,8 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
                     compact_query<KP, CAP>(s_sc + q * CAP, s_ix + q * CAP, s_cnt + q, s_thr + q,
                                            qb * QB + q < B ? gthr + qb * QB + q : nullptr);
                 }
-            __syncthreads();
+            if (FLAGSYNC && threadIdx.x == 0) *(volatile int*)&s_need = 0;  // nobody reads it between B1 and B2
+            __syncthreads();  // B2
             any_left = 0;
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt) {
@@ -625,6 +651,23 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
         g_scan_stamps[w][7] = st_rt;
     }
 #endif
+
+    // Past the last step: keep answering compaction rounds (B1 / B2 as in the step
+    // loop) until every wave of the workgroup is here; a wave still stepping sees
+    // s_need (raised by this wave every round) at its next step end.  All waves
+    // read s_done == NW after the same B1, so they leave together.
+    if (FLAGSYNC && lane == 0) atomicAdd(&s_done, 1);
+    for (; FLAGSYNC;) {
+        if (lane == 0) *(volatile int*)&s_need = 1;
+        __syncthreads();  // B1
+        if (__builtin_amdgcn_readfirstlane(*(volatile int*)&s_done) == NW) break;
+        for (int q = wv; q < QB; q += NW)
+            if (s_cnt[q] >= CAP)
+                compact_query<KP, CAP>(s_sc + q * CAP, s_ix + q * CAP, s_cnt + q, s_thr + q,
+                                       qb * QB + q < B ? gthr + qb * QB + q : nullptr);
+        if (threadIdx.x == 0) *(volatile int*)&s_need = 0;
+        __syncthreads();  // B2
+    }
 
     // ---- flush: entries above the shared bound -> global per-query lists ----------
     // (wave wv flushes queries wv + NW i; lane i holds query i's bound)
@@ -1140,15 +1183,24 @@ hipError_t launch_pilot(int prec, int metric, int KP, const float* X, const floa
     return hipGetLastError();
 }
 
-template <int PREC, int METRIC, int QT, int RT, int PX, int PQ, int KP, int CAP, int PUB, int WPS, bool NT, int NW>
+template <int V, int PREC, int METRIC, int QT, int RT, int PX, int PQ, int KP, int CAP, int PUB, int WPS, bool NT, int NW>
 static hipError_t scan_dispatch(const float* X, const float* rowscale, const uint32_t* mask, const float* Qt, int G,
                                 int64_t N, int B, int n_qblocks, int64_t n_steps, int n_wg, int spw, float* gl_s,
                                 uint32_t* gl_i, uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr, uint32_t* gslots,
-                                hipStream_t st) {
+                                int lockstep, hipStream_t st) {
     const int n_wg8 = (n_wg + 7) / 8 * 8;
-    hipLaunchKernelGGL((scan_topk_kernel<PREC, METRIC, QT, RT, PX, PQ, KP, CAP, PUB, WPS, NT, NW>),
-                       dim3(n_wg8 * n_qblocks), dim3(64 * NW), 0, st, X, rowscale, mask, Qt, G, N, B, n_steps, spw, n_qblocks, n_wg8, gl_s, gl_i,
-                       gl_cnt, gl_cap, gthr, gslots);
+    // flag-gated step ends are built for the default variants only (others run lockstep)
+    if constexpr (V == 0) {
+        if (!lockstep) {
+            hipLaunchKernelGGL((scan_topk_kernel<PREC, METRIC, QT, RT, PX, PQ, KP, CAP, PUB, WPS, NT, NW, true>),
+                               dim3(n_wg8 * n_qblocks), dim3(64 * NW), 0, st, X, rowscale, mask, Qt, G, N, B, n_steps,
+                               spw, n_qblocks, n_wg8, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots);
+            return hipGetLastError();
+        }
+    }
+    hipLaunchKernelGGL((scan_topk_kernel<PREC, METRIC, QT, RT, PX, PQ, KP, CAP, PUB, WPS, NT, NW, false>),
+                       dim3(n_wg8 * n_qblocks), dim3(64 * NW), 0, st, X, rowscale, mask, Qt, G, N, B, n_steps, spw,
+                       n_qblocks, n_wg8, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots);
     return hipGetLastError();
 }
 
@@ -1195,19 +1247,19 @@ bool scan_variant_ok(int prec, int variant, int G) {
 hipError_t launch_scan_topk(int prec, int metric, int KP, int variant, const float* X, const float* rowscale,
                             const uint32_t* mask, const float* Qt, int G, int64_t N, int B, int n_qblocks,
                             int64_t n_steps, int n_wg, int spw, float* gl_s, uint32_t* gl_i, uint32_t* gl_cnt,
-                            int64_t gl_cap, uint32_t* gthr, uint32_t* gslots, hipStream_t st) {
+                            int64_t gl_cap, uint32_t* gthr, uint32_t* gslots, int lockstep, hipStream_t st) {
     if (!scan_variant_ok(prec, variant, G)) return hipErrorInvalidValue;
 #define VDB_SCAN_NT(P, M, QT, KPV, V, RT, PX, PQ, CAPV, PUB, W, NT)                                           \
     if (prec == P && metric == M && KP == KPV && variant == V && (n_qblocks == 1) == NT)                       \
-        return scan_dispatch<P, M, QT, RT, PX, PQ, KPV, CAPV, PUB, W, NT, 4>(X, rowscale, mask, Qt, G, N, B,      \
+        return scan_dispatch<V, P, M, QT, RT, PX, PQ, KPV, CAPV, PUB, W, NT, 4>(X, rowscale, mask, Qt, G, N, B,      \
                                                                         n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, \
-                                                                        gl_cnt, gl_cap, gthr, gslots, st);
+                                                                        gl_cnt, gl_cap, gthr, gslots, lockstep, st);
 // VDB_SCAN: default load policy only; VDB_SCAN2: plus the non-temporal build for one query block
 #define VDB_SCAN(P, M, QT, KPV, V, RT, PX, PQ, CAPV, PUB, W)                                                     \
     if (prec == P && metric == M && KP == KPV && variant == V)                                                 \
-        return scan_dispatch<P, M, QT, RT, PX, PQ, KPV, CAPV, PUB, W, false, 4>(X, rowscale, mask, Qt, G, N, B,   \
+        return scan_dispatch<V, P, M, QT, RT, PX, PQ, KPV, CAPV, PUB, W, false, 4>(X, rowscale, mask, Qt, G, N, B,   \
                                                                            n_qblocks, n_steps, n_wg, spw, gl_s,    \
-                                                                           gl_i, gl_cnt, gl_cap, gthr, gslots, st);
+                                                                           gl_i, gl_cnt, gl_cap, gthr, gslots, lockstep, st);
 #define VDB_SCAN2(P, M, QT, KPV, V, RT, PX, PQ, CAPV, PUB, W)                                                    \
     VDB_SCAN_NT(P, M, QT, KPV, V, RT, PX, PQ, CAPV, PUB, W, true)                                              \
     VDB_SCAN_NT(P, M, QT, KPV, V, RT, PX, PQ, CAPV, PUB, W, false)

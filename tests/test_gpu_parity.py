@@ -34,8 +34,11 @@ def _mask_words(mask_bool):
 PRECISIONS = ["bf16x3", "bf16", "fp32"]
 
 
-def _check(vdb, V, Q, k, metric, mask=None, force_exact=False, margin=None, chunked_add=False, precision="bf16x3"):
+def _check(vdb, V, Q, k, metric, mask=None, force_exact=False, margin=None, chunked_add=False, precision="bf16x3",
+           params=None):
     ix = vdb.NativeIndex(V.shape[1], metric, precision=precision)
+    for name, value in (params or {}).items():
+        ix.set_param(name, value)
     if force_exact:
         ix.set_param("force_exact", 1)
     if margin is not None:
@@ -93,6 +96,24 @@ def test_normal_with_mask_and_chunked_add(vdb, metric, precision):
     Q = rng.standard_normal((5, 200)).astype(np.float32)
     mask = rng.random(6000) < 0.3
     _check(vdb, V, Q, 10, metric, mask=mask, chunked_add=True, precision=precision)
+
+
+@pytest.mark.parametrize("sync", [1, 2])
+@pytest.mark.parametrize("metric", ["cosine", "euclidean"])
+@pytest.mark.parametrize("D,B,k", [(128, 150, 100), (384, 70, 10)])
+def test_scan_step_sync_modes(vdb, sync, metric, D, B, k):
+    """Both step ends of the scan (lockstep barrier / flag-gated compaction rounds,
+    vdb_scan.hip) on data that keeps every workgroup's buffers overflowing: rows
+    approach the queries' direction as the row index grows, so each step beats the
+    last and compaction rounds run all the way to the end of the row range."""
+    rng = np.random.default_rng(D + sync)
+    N = 60000
+    Q = rng.random((B, D), dtype=np.float32)
+    t = (np.arange(N, dtype=np.float32) / N)[:, None]
+    V = (Q[rng.integers(0, B, N)] * t + rng.random((N, D), dtype=np.float32) * (1.0 - t)).astype(np.float32)
+    ix, _, _ = _check(vdb, V, Q, k, metric, params={"scan_sync": sync})
+    with pytest.raises(Exception):
+        ix.set_param("scan_sync", 3)
 
 
 def test_precision_switch_keeps_results(vdb):
