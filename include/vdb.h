@@ -96,6 +96,8 @@ int32_t vdb_index_reserve(vdb_index* idx, int64_t rows);
 /* Tuning / test knobs: "precision" (VDB_PREC_*), "margin" (extra candidates
  * per query), "force_exact" (0/1), "n_wg" (candidate-pass workgroups),
  * "scan_variant" / "scan_variant_bf16x3" (0..2, kernel tiling variants),
+ * "scan_sync" (candidate-pass step end: 0 auto by dimension, 1 per-step barrier,
+ * 2 flag-gated compaction rounds; results identical, speed differs),
  * "timing" (0/1: HIP events around the candidate pass; stats "scan_ns",
  * "pipeline_ns", "timed_searches").  Stats also: "searches", "queries",
  * "fallback_queries", "overflow_queries", "capacity", "count", "device_bytes", "precision". */
