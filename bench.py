@@ -255,6 +255,36 @@ def main_graph(args, world, rank, local, dev):
         dist.destroy_process_group()
 
 
+def _rank_entry(local_rank, world, port, argv):
+    os.environ.update(RANK=str(local_rank), LOCAL_RANK=str(local_rank), WORLD_SIZE=str(world),
+                      LOCAL_WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    sys.argv = [sys.argv[0]] + argv
+    main()
+
+
+def spawn_ranks(n):
+    """`bench.py --gpus N` without torchrun: start N fresh rank processes (one per GPU,
+    torch.multiprocessing spawn) from this parent, which never touches the GPU itself
+    (torch.cuda.device_count() does not initialise it), and return their exit status."""
+    import socket
+    import torch.multiprocessing as mp
+    have = torch.cuda.device_count()
+    if have < n:
+        print(f"bench.py: --gpus {n} but only {have} GPU(s) visible", file=sys.stderr)
+        return 2
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    try:
+        mp.start_processes(_rank_entry, args=(n, port, sys.argv[1:]), nprocs=n, join=True, start_method="spawn")
+    except Exception as e:  # a rank failed: its traceback is already on stderr
+        print(f"bench.py: rank process failed: {e}", file=sys.stderr)
+        return 1
+    return 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -282,6 +312,11 @@ def main():
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus != world:
+        if "WORLD_SIZE" in os.environ or args.gpus < 1:
+            sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU "
+                     f"(torchrun --nproc-per-node {args.gpus}) or run without torchrun")
+        sys.exit(spawn_ranks(args.gpus))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:

@@ -198,6 +198,38 @@ int32_t vdb_graph_set_param(vdb_graph* g, const char* name, int64_t value);
 
 int32_t vdb_graph_destroy(vdb_graph* g);
 
+/* --- multi-device corpus (one process, several GPUs) ------------------------------
+ * The store's corpus row-sharded over `n_devices` GPUs of this process (SURVEY.md §8e;
+ * the reference serves from one process, main.py:395, with the corpus on one device,
+ * service/optimized_vector_store.py:59-114).  Rows keep their global ids (insertion
+ * order); each add is cut into contiguous pieces that level the shard sizes.  A search
+ * runs on every shard at once (one stream each, device-resident top-k with exact fp64
+ * keys and global ids), gathers the G lists to devices[0] by peer copies over xGMI and
+ * merges them there by (key desc, row asc): results identical to vdb_index_search on
+ * one index holding every row.  Host memory in and out.  A device may repeat. */
+typedef struct vdb_shards vdb_shards;
+int32_t vdb_shards_create(int32_t dim, int32_t metric, const int32_t* devices, int32_t n_devices, vdb_shards** out);
+int32_t vdb_shards_destroy(vdb_shards* s);
+int32_t vdb_shards_add(vdb_shards* s, const float* vectors_host, int64_t n);
+int32_t vdb_shards_count(const vdb_shards* s, int64_t* n);
+int32_t vdb_shards_shard_count(const vdb_shards* s, int32_t shard, int64_t* n);
+/* row_mask: NULL or ceil(count/32) host words over GLOBAL rows (as vdb_index_search) */
+int32_t vdb_shards_search(vdb_shards* s, const float* queries_host, int32_t n_queries, int32_t k,
+                          const uint32_t* row_mask, float* out_scores, int64_t* out_indices, double* out_keys);
+int32_t vdb_shards_get_vectors(vdb_shards* s, int64_t start, int64_t n, float* out_host);
+int32_t vdb_shards_clear(vdb_shards* s);
+int32_t vdb_shards_reserve(vdb_shards* s, int64_t rows);
+/* applied to every shard's index (vdb_index_set_param names) */
+int32_t vdb_shards_set_param(vdb_shards* s, const char* name, int64_t value);
+/* "count", "shards", else the vdb_index_get_stat name summed over the shards */
+int32_t vdb_shards_get_stat(const vdb_shards* s, const char* name, int64_t* value);
+
+/* --- lifecycle ------------------------------------------------------------------------
+ * Waits for every queued search of every live index, releases their idle per-search
+ * workspaces and trims the devices' stream-ordered pools back to the driver.  Indexes
+ * stay valid; the next search re-allocates what it needs. */
+int32_t vdb_shutdown(void);
+
 #ifdef __cplusplus
 }
 #endif

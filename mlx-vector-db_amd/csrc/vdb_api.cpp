@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <cstring>
 #include <mutex>
+#include <set>
 #include <shared_mutex>
 #include <string>
 #include <vector>
@@ -127,6 +128,20 @@ struct vdb_index {
 
 namespace {
 
+// Live indexes, for vdb_shutdown().
+std::mutex g_reg_mu;
+std::set<vdb_index*> g_indices;
+
+void free_workspace_memory(Workspace* w) {
+    if (w->dev) (void)hipFree(w->dev);
+    if (w->exact) (void)hipFree(w->exact);
+    if (w->host_flag) (void)hipHostFree(w->host_flag);
+    w->dev = nullptr;
+    w->exact = nullptr;
+    w->host_flag = nullptr;
+    w->dev_bytes = w->exact_bytes = 0;
+}
+
 int ensure_capacity(vdb_index* ix, int64_t rows) {
     if (rows <= ix->cap_rows) return VDB_OK;
     int64_t cap = std::max<int64_t>(ix->cap_rows * 2, kRowAlign);
@@ -139,33 +154,51 @@ int ensure_capacity(vdb_index* ix, int64_t rows) {
     float* Xs = nullptr;
     double* n64 = nullptr;
     float *i32 = nullptr, *s32 = nullptr;
-    HIP_TRY(hipMalloc(&X, x_bytes));
+    // All new buffers are allocated and filled before the index switches to them; on
+    // any failure (typically out of memory while doubling at large N) they are freed
+    // and the index keeps its current buffers, so a later retry sees the same HBM.
+    auto fail = [&](hipError_t e, const char* what) {
+        (void)hipStreamSynchronize(ix->stream);
+        for (void* p : {(void*)X, (void*)Xs, (void*)n64, (void*)i32, (void*)s32})
+            if (p) (void)hipFree(p);
+        return set_error(e == hipErrorOutOfMemory ? VDB_ERR_OOM : VDB_ERR_HIP,
+                         "growing the index to %lld rows: %s failed: %s", (long long)cap, what, hipGetErrorString(e));
+    };
+#define CAP_TRY(expr)                          \
+    do {                                       \
+        hipError_t _e = (expr);                \
+        if (_e != hipSuccess) return fail(_e, #expr); \
+    } while (0)
+    CAP_TRY(hipMalloc(&X, x_bytes));
     if (split) {
-        HIP_TRY(hipMalloc(&Xs, x_bytes));
-        HIP_TRY(hipMemsetAsync(Xs, 0, x_bytes, ix->stream));
+        CAP_TRY(hipMalloc(&Xs, x_bytes));
+        CAP_TRY(hipMemsetAsync(Xs, 0, x_bytes, ix->stream));
     }
-    HIP_TRY(hipMalloc(&n64, cap * sizeof(double)));
-    HIP_TRY(hipMalloc(&i32, cap * sizeof(float)));
-    HIP_TRY(hipMalloc(&s32, cap * sizeof(float)));
-    HIP_TRY(hipMemsetAsync(X, 0, (size_t)(cap / 32) * tile_floats * sizeof(float), ix->stream));
-    HIP_TRY(hipMemsetAsync(n64, 0, cap * sizeof(double), ix->stream));
-    HIP_TRY(hipMemsetAsync(i32, 0, cap * sizeof(float), ix->stream));
-    HIP_TRY(hipMemsetAsync(s32, 0, cap * sizeof(float), ix->stream));
+    CAP_TRY(hipMalloc(&n64, cap * sizeof(double)));
+    CAP_TRY(hipMalloc(&i32, cap * sizeof(float)));
+    CAP_TRY(hipMalloc(&s32, cap * sizeof(float)));
+    CAP_TRY(hipMemsetAsync(X, 0, x_bytes, ix->stream));
+    CAP_TRY(hipMemsetAsync(n64, 0, cap * sizeof(double), ix->stream));
+    CAP_TRY(hipMemsetAsync(i32, 0, cap * sizeof(float), ix->stream));
+    CAP_TRY(hipMemsetAsync(s32, 0, cap * sizeof(float), ix->stream));
     if (ix->X) {
         // all searches that might read the old buffers must be finished
-        HIP_TRY(hipDeviceSynchronize());
+        CAP_TRY(hipDeviceSynchronize());
         const int64_t used_tiles = round_up(ix->count, 128) / 32;  // whole super tiles (prefix of the layout)
-        HIP_TRY(hipMemcpyAsync(X, ix->X, (size_t)used_tiles * tile_floats * sizeof(float), hipMemcpyDeviceToDevice,
+        CAP_TRY(hipMemcpyAsync(X, ix->X, (size_t)used_tiles * tile_floats * sizeof(float), hipMemcpyDeviceToDevice,
                                ix->stream));
         if (split && ix->Xs)
-            HIP_TRY(hipMemcpyAsync(Xs, ix->Xs, (size_t)used_tiles * tile_floats * sizeof(float),
+            CAP_TRY(hipMemcpyAsync(Xs, ix->Xs, (size_t)used_tiles * tile_floats * sizeof(float),
                                    hipMemcpyDeviceToDevice, ix->stream));
         else if (split)
-            HIP_TRY(launch_split_rows(X, ix->G, 0, ix->count, Xs, ix->stream));
-        HIP_TRY(hipMemcpyAsync(n64, ix->nrm64, ix->count * sizeof(double), hipMemcpyDeviceToDevice, ix->stream));
-        HIP_TRY(hipMemcpyAsync(i32, ix->inv32, ix->count * sizeof(float), hipMemcpyDeviceToDevice, ix->stream));
-        HIP_TRY(hipMemcpyAsync(s32, ix->sq32, ix->count * sizeof(float), hipMemcpyDeviceToDevice, ix->stream));
-        HIP_TRY(hipStreamSynchronize(ix->stream));
+            CAP_TRY(launch_split_rows(X, ix->G, 0, ix->count, Xs, ix->stream));
+        CAP_TRY(hipMemcpyAsync(n64, ix->nrm64, ix->count * sizeof(double), hipMemcpyDeviceToDevice, ix->stream));
+        CAP_TRY(hipMemcpyAsync(i32, ix->inv32, ix->count * sizeof(float), hipMemcpyDeviceToDevice, ix->stream));
+        CAP_TRY(hipMemcpyAsync(s32, ix->sq32, ix->count * sizeof(float), hipMemcpyDeviceToDevice, ix->stream));
+    }
+    CAP_TRY(hipStreamSynchronize(ix->stream));
+#undef CAP_TRY
+    if (ix->X) {
         (void)hipFree(ix->X);
         if (ix->Xs) (void)hipFree(ix->Xs);
         (void)hipFree(ix->nrm64);
@@ -178,7 +211,6 @@ int ensure_capacity(vdb_index* ix, int64_t rows) {
     ix->inv32 = i32;
     ix->sq32 = s32;
     ix->cap_rows = cap;
-    HIP_TRY(hipStreamSynchronize(ix->stream));
     return VDB_OK;
 }
 
@@ -282,7 +314,7 @@ size_t exact_bytes(vdb_index* ix, int nq, int k, bool gated) {
 // when no query was flagged.
 int run_exact(vdb_index* ix, Workspace* w, const float* Qd, const double* qn64, const int* qlist_dev, int nq, int k,
               const uint32_t* mask_dev, float* out_s, int64_t* out_i, double* out_k, int64_t index_offset,
-              hipStream_t st, const int* qcount_dev = nullptr, const int* ovf_dev = nullptr) {
+              const int64_t* row_ids, hipStream_t st, const int* qcount_dev = nullptr, const int* ovf_dev = nullptr) {
     const int KE = std::max(32, next_pow2(k));
     const int64_t N = ix->count;
     const bool gated = qcount_dev != nullptr;
@@ -304,7 +336,7 @@ int run_exact(vdb_index* ix, Workspace* w, const float* Qd, const double* qn64, 
                               n_wg, rpw, lk, li, st, qcount_dev, ovf_dev, gated ? ix->d_totals : nullptr));
     HIP_TRY(launch_merge_f64_u32(KE, lk, li, n_lists, KE, (int64_t)n_lists * KE, KE, nq, mk, mi, st, qcount_dev));
     HIP_TRY(launch_finalize_u32(ix->metric, mk, mi, KE, nq, qlist_dev, k, index_offset, out_s, out_i, out_k, st,
-                                qcount_dev));
+                                qcount_dev, row_ids));
     return VDB_OK;
 }
 
@@ -355,18 +387,24 @@ int32_t vdb_index_create(int32_t dim, int32_t metric, int32_t device, vdb_index*
         return set_error(VDB_ERR_HIP, "index setup failed: %s", hipGetErrorString(e));
     }
     ix->d_nonfinite = reinterpret_cast<int*>(reinterpret_cast<char*>(ix->d_xmax) + 32);
+    {
+        std::lock_guard<std::mutex> rg(g_reg_mu);
+        g_indices.insert(ix);
+    }
     *out = ix;
     return VDB_OK;
 }
 
 int32_t vdb_index_destroy(vdb_index* ix) {
     if (!ix) return VDB_OK;
+    {
+        std::lock_guard<std::mutex> rg(g_reg_mu);
+        g_indices.erase(ix);
+    }
     (void)hipSetDevice(ix->device);
     (void)hipDeviceSynchronize();
     for (Workspace* w : ix->pool) {
-        if (w->dev) (void)hipFree(w->dev);
-        if (w->exact) (void)hipFree(w->exact);
-        if (w->host_flag) (void)hipHostFree(w->host_flag);
+        free_workspace_memory(w);
         if (w->done) (void)hipEventDestroy(w->done);
         for (int r = 0; r < Workspace::kTRing; ++r)
             for (int e = 0; e < 4; ++e)
@@ -587,9 +625,12 @@ int32_t vdb_index_get_vectors(vdb_index* ix, int64_t start, int64_t n, float* ou
     return VDB_OK;
 }
 
-int32_t vdb_index_search(vdb_index* ix, const float* queries, int32_t B, int32_t k, const uint32_t* row_mask,
-                         int32_t mem, float* out_scores, int64_t* out_indices, double* out_keys,
-                         int64_t index_offset, void* stream) {
+// vdb_index_search with an optional global id per row (row_ids, device memory, read by
+// the result write-out): a shard of a multi-device set holds pieces of the global
+// insertion order (vdb_shards_*).
+static int32_t search_impl(vdb_index* ix, const float* queries, int32_t B, int32_t k, const uint32_t* row_mask,
+                           int32_t mem, float* out_scores, int64_t* out_indices, double* out_keys,
+                           int64_t index_offset, void* stream, const int64_t* row_ids) {
     if (!ix) return set_error(VDB_ERR_INVALID, "index is NULL");
     if (B <= 0) return set_error(VDB_ERR_INVALID, "n_queries must be >= 1, got %d", B);
     if (k <= 0 || k > 1024) return set_error(VDB_ERR_INVALID, "k must be in [1, 1024], got %d", k);
@@ -760,6 +801,7 @@ int32_t vdb_index_search(vdb_index* ix, const float* queries, int32_t B, int32_t
             fa.xmax = ix->xmax;
             fa.xres = prec != PREC_BF16 ? 0.0 : 1.01 * (ix->metric == 0 ? ix->xres_rel : ix->xres_abs);
             fa.out_s = out_s; fa.out_i = out_i; fa.out_k = out_k; fa.index_offset = index_offset;
+            fa.row_ids = row_ids;
             fa.flag_count = flags; fa.flag_list = flags + 1; fa.gthr = gthr; fa.overflow_count = flags + B + 1;
             HIP_TRY(launch_finish(ix->metric, KP, fa, B, st));
             if (timed) HIP_TRY(hipEventRecord(tev[2], st));
@@ -771,8 +813,8 @@ int32_t vdb_index_search(vdb_index* ix, const float* queries, int32_t B, int32_t
                     HIP_TRY(hipMalloc(&ix->d_totals, 2 * sizeof(unsigned long long)));
                     HIP_TRY(hipMemsetAsync(ix->d_totals, 0, 2 * sizeof(unsigned long long), st));
                 }
-                rc = run_exact(ix, w, Qd, qn64, flags + 1, B, k, md, out_s, out_i, out_k, index_offset, st, flags,
-                               flags + B + 1);
+                rc = run_exact(ix, w, Qd, qn64, flags + 1, B, k, md, out_s, out_i, out_k, index_offset, row_ids, st,
+                               flags, flags + B + 1);
                 return rc;
             }
             HIP_TRY(hipMemcpyAsync(w->host_flag, flags, sizeof(int), hipMemcpyDeviceToHost, st));
@@ -786,12 +828,13 @@ int32_t vdb_index_search(vdb_index* ix, const float* queries, int32_t B, int32_t
             }
             if (n_flag > 0) {
                 ix->n_fallback += n_flag;
-                rc = run_exact(ix, w, Qd, qn64, flags + 1, n_flag, k, md, out_s, out_i, out_k, index_offset, st);
+                rc = run_exact(ix, w, Qd, qn64, flags + 1, n_flag, k, md, out_s, out_i, out_k, index_offset, row_ids,
+                               st);
                 if (rc) return rc;
             }
         } else {
             ix->n_fallback += B;
-            rc = run_exact(ix, w, Qd, qn64, nullptr, B, k, md, out_s, out_i, out_k, index_offset, st);
+            rc = run_exact(ix, w, Qd, qn64, nullptr, B, k, md, out_s, out_i, out_k, index_offset, row_ids, st);
             if (rc) return rc;
         }
     }
@@ -803,6 +846,60 @@ int32_t vdb_index_search(vdb_index* ix, const float* queries, int32_t B, int32_t
     }
     return VDB_OK;
 }
+
+int32_t vdb_shutdown(void) {
+    std::vector<vdb_index*> live;
+    {
+        std::lock_guard<std::mutex> rg(g_reg_mu);
+        live.assign(g_indices.begin(), g_indices.end());
+    }
+    std::set<int> devices;
+    for (vdb_index* ix : live) {
+        HIP_TRY(hipSetDevice(ix->device));
+        devices.insert(ix->device);
+        HIP_TRY(hipDeviceSynchronize());  // every queued search of this device is done
+        const int frc = flush_all_timing(ix);
+        if (frc) return frc;
+        std::lock_guard<std::mutex> g(ix->ws_mu);
+        for (Workspace* w : ix->pool)
+            if (!w->busy) free_workspace_memory(w);
+    }
+    for (int d : devices) {  // stream-ordered allocations (merge / graph scratch) back to the driver
+        HIP_TRY(hipSetDevice(d));
+        hipMemPool_t pool = nullptr;
+        if (hipDeviceGetDefaultMemPool(&pool, d) == hipSuccess && pool) (void)hipMemPoolTrimTo(pool, 0);
+    }
+    return VDB_OK;
+}
+
+int32_t vdb_index_search(vdb_index* ix, const float* queries, int32_t B, int32_t k, const uint32_t* row_mask,
+                         int32_t mem, float* out_scores, int64_t* out_indices, double* out_keys,
+                         int64_t index_offset, void* stream) {
+    return search_impl(ix, queries, B, k, row_mask, mem, out_scores, out_indices, out_keys, index_offset, stream,
+                       nullptr);
+}
+
+}  // extern "C"
+
+// ---- internal hooks for the multi-device set (vdb_shards.cpp) ----------------------------
+namespace vdb {
+int32_t index_search_rows(vdb_index* ix, const float* queries, int32_t B, int32_t k, const uint32_t* row_mask,
+                          float* out_scores, int64_t* out_indices, double* out_keys, void* stream,
+                          const int64_t* row_ids) {
+    return search_impl(ix, queries, B, k, row_mask, VDB_MEM_DEVICE, out_scores, out_indices, out_keys, 0, stream,
+                       row_ids);
+}
+// Drop rows past `rows` (undo of a partial multi-shard add; rows past count are never read).
+int32_t index_truncate(vdb_index* ix, int64_t rows) {
+    std::unique_lock<std::shared_mutex> g(ix->mu);
+    if (rows < ix->count) ix->count = rows;
+    return VDB_OK;
+}
+int index_device(const vdb_index* ix) { return ix->device; }
+int32_t set_error_msg(int code, const char* msg) { return set_error(code, "%s", msg); }
+}  // namespace vdb
+
+extern "C" {
 
 int32_t vdb_merge_topk(const double* keys, const int64_t* idx, int32_t n_lists, int32_t nq, int32_t k_in,
                        int32_t k_out, int32_t metric, float* out_scores, int64_t* out_indices, double* out_keys,

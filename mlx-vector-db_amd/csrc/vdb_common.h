@@ -184,6 +184,12 @@ __device__ __forceinline__ size_t tiled_piece_offset(uint64_t r, int p, int G) {
     return tiled_block(r >> 5, p >> 1, G) + (size_t)(r & 31) * 4 + (size_t)(p & 1) * 128;
 }
 
+// Global id of local row r: row_ids[r] (a shard of a multi-device set, whose rows are
+// pieces of the global insertion order), else r + offset.
+__device__ __forceinline__ uint64_t global_row(const int64_t* row_ids, uint64_t r, int64_t offset) {
+    return row_ids ? (uint64_t)row_ids[r] : r + (uint64_t)offset;
+}
+
 // Write one result slot (fp32 score, int64 row, optional fp64 key).
 __device__ __forceinline__ void write_result(int metric, double key, uint64_t row_plus_off, bool valid, float* os,
                                              int64_t* oi, double* ok) {

@@ -459,7 +459,7 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
             }
             if (er < a.k) {
                 const size_t o = (size_t)b * a.k + er;
-                write_result(METRIC, ek, (uint64_t)r + a.index_offset, true, a.out_s + o, a.out_i + o,
+                write_result(METRIC, ek, global_row(a.row_ids, r, a.index_offset), true, a.out_s + o, a.out_i + o,
                              a.out_k ? a.out_k + o : nullptr);
             }
             if (ar == a.k - 1) s_ak = ck;

@@ -105,6 +105,7 @@ struct FinishArgs {
     float* out_s; int64_t* out_i; double* out_k; int64_t index_offset;
     int* flag_count; int* flag_list; const uint32_t* gthr;
     int* overflow_count;  // lists longer than the finish kernel holds (they take the exact path)
+    const int64_t* row_ids = nullptr;  // global id per row (multi-device shard), else row + index_offset
 };
 hipError_t launch_finish(int metric, int KP, const FinishArgs& a, int B, hipStream_t st);
 
@@ -131,7 +132,7 @@ hipError_t launch_merge_f64_i64(int KP, const double* lk, const int64_t* li, int
 // sorted [nq][KP] fp64-key lists.
 hipError_t launch_finalize_u32(int metric, const double* sk, const uint32_t* si, int KP, int nq, const int* qmap,
                                int k, int64_t index_offset, float* out_s, int64_t* out_i, double* out_k,
-                               hipStream_t st, const int* qcount = nullptr);
+                               hipStream_t st, const int* qcount = nullptr, const int64_t* row_ids = nullptr);
 hipError_t launch_finalize_i64(int metric, const double* sk, const int64_t* si, int KP, int nq, const int* qmap,
                                int k, float* out_s, int64_t* out_i, double* out_k, hipStream_t st);
 

@@ -224,7 +224,8 @@ __global__ void __launch_bounds__(256) finalize_kernel(int metric, const double*
                                                        const I* __restrict__ si, int KP, int nq,
                                                        const int* __restrict__ qmap, int k, int64_t index_offset,
                                                        float* __restrict__ out_s, int64_t* __restrict__ out_i,
-                                                       double* __restrict__ out_k, const int* __restrict__ qcount) {
+                                                       double* __restrict__ out_k, const int* __restrict__ qcount,
+                                                       const int64_t* __restrict__ row_ids) {
     const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (t >= (int64_t)nq * k) return;
     const int qi = (int)(t / k);
@@ -235,16 +236,16 @@ __global__ void __launch_bounds__(256) finalize_kernel(int metric, const double*
     const I ix = si[(size_t)qi * KP + e];
     const bool valid = sizeof(I) == 8 ? (int64_t)ix >= 0 : (uint32_t)ix != 0xFFFFFFFFu;
     const size_t o = (size_t)b * k + e;
-    write_result(metric, key, (uint64_t)ix + (uint64_t)index_offset, valid && key != -INFINITY, out_s + o, out_i + o,
-                 out_k ? out_k + o : nullptr);
+    write_result(metric, key, valid ? global_row(row_ids, (uint64_t)ix, index_offset) : 0, valid && key != -INFINITY,
+                 out_s + o, out_i + o, out_k ? out_k + o : nullptr);
 }
 
 hipError_t launch_finalize_u32(int metric, const double* sk, const uint32_t* si, int KP, int nq, const int* qmap,
                                int k, int64_t index_offset, float* out_s, int64_t* out_i, double* out_k,
-                               hipStream_t st, const int* qcount) {
+                               hipStream_t st, const int* qcount, const int64_t* row_ids) {
     const int64_t n = (int64_t)nq * k;
     hipLaunchKernelGGL(finalize_kernel<uint32_t>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, metric, sk, si,
-                       KP, nq, qmap, k, index_offset, out_s, out_i, out_k, qcount);
+                       KP, nq, qmap, k, index_offset, out_s, out_i, out_k, qcount, row_ids);
     return hipGetLastError();
 }
 
@@ -252,7 +253,7 @@ hipError_t launch_finalize_i64(int metric, const double* sk, const int64_t* si, 
                                int k, float* out_s, int64_t* out_i, double* out_k, hipStream_t st) {
     const int64_t n = (int64_t)nq * k;
     hipLaunchKernelGGL(finalize_kernel<int64_t>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, metric, sk, si,
-                       KP, nq, qmap, k, (int64_t)0, out_s, out_i, out_k, (const int*)nullptr);
+                       KP, nq, qmap, k, (int64_t)0, out_s, out_i, out_k, (const int*)nullptr, (const int64_t*)nullptr);
     return hipGetLastError();
 }
 

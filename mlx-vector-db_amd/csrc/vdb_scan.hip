@@ -388,7 +388,8 @@ scan_topk_kernel(const float* __restrict__ X, const float* __restrict__ rowscale
             const float* rsp = rowscale + (tt + rt) * 32 + 4 * (lane >> 5);
 #pragma unroll
             for (int m = 0; m < 4; ++m) r_[rt][m] = *(const f32x4*)(rsp + 8 * m);
-            m_[rt] = mask ? mask[tt + rt] : 0xFFFFFFFFu;
+            // the caller's bitmap holds ceil(N/32) words (vdb.h): tiles past it are rows >= N
+            m_[rt] = !mask ? 0xFFFFFFFFu : (tt + rt < ((N + 31) >> 5) ? mask[tt + rt] : 0u);
         }
     };
     uint32_t gkn[QT];
@@ -787,7 +788,8 @@ scan_topk_priv_kernel(const float* __restrict__ X, const float* __restrict__ row
             const float* rsp = rowscale + (tt + rt) * 32 + 4 * (lane >> 5);
 #pragma unroll
             for (int m = 0; m < 4; ++m) r_[rt][m] = *(const f32x4*)(rsp + 8 * m);
-            m_[rt] = mask ? mask[tt + rt] : 0xFFFFFFFFu;
+            // the caller's bitmap holds ceil(N/32) words (vdb.h): tiles past it are rows >= N
+            m_[rt] = !mask ? 0xFFFFFFFFu : (tt + rt < ((N + 31) >> 5) ? mask[tt + rt] : 0u);
         }
     };
     uint32_t gkn[QT];

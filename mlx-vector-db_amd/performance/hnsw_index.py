@@ -88,6 +88,12 @@ class ProductionHNSWIndex:
         logger.info("graph index over %d vectors built in %.2f s (degree %d)", n, time.time() - t0, degree)
         self.save_index()
 
+    def add_rows(self, native_index: _vdb.NativeIndex, first_new_row: int):
+        """The store appended rows [first_new_row, count) to `native_index`: bring the graph
+        up to date (the reference rebuilds hnswlib from scratch on every add,
+        service/optimized_vector_store.py:110-112)."""
+        self.build(None, native_index=native_index)
+
     def search(self, query_data: np.ndarray, k: int, ef_search: int = 100) -> Tuple[np.ndarray, np.ndarray]:
         """hnsw_index.py:79-103: (labels uint64 [n, k], distances fp32 [n, k])."""
         if not self.is_loaded or self.index is None:

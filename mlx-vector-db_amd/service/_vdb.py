@@ -43,6 +43,9 @@ EXPORTED_SYMBOLS = (
     "vdb_index_search", "vdb_merge_topk", "vdb_similarity_matrix",
     "vdb_graph_build", "vdb_graph_import", "vdb_graph_export", "vdb_graph_info", "vdb_graph_search",
     "vdb_graph_stat", "vdb_graph_set_param", "vdb_graph_destroy",
+    "vdb_shards_create", "vdb_shards_destroy", "vdb_shards_add", "vdb_shards_count", "vdb_shards_shard_count",
+    "vdb_shards_search", "vdb_shards_get_vectors", "vdb_shards_clear", "vdb_shards_reserve",
+    "vdb_shards_set_param", "vdb_shards_get_stat", "vdb_shutdown",
 )
 
 _lib = None
@@ -105,6 +108,18 @@ def load_library():
             "vdb_graph_stat": (c_i32, [c_vp, ctypes.c_char_p, p_i64]),
             "vdb_graph_set_param": (c_i32, [c_vp, ctypes.c_char_p, c_i64]),
             "vdb_graph_destroy": (c_i32, [c_vp]),
+            "vdb_shards_create": (c_i32, [c_i32, c_i32, c_vp, c_i32, ctypes.POINTER(c_vp)]),
+            "vdb_shards_destroy": (c_i32, [c_vp]),
+            "vdb_shards_add": (c_i32, [c_vp, c_vp, c_i64]),
+            "vdb_shards_count": (c_i32, [c_vp, p_i64]),
+            "vdb_shards_shard_count": (c_i32, [c_vp, c_i32, p_i64]),
+            "vdb_shards_search": (c_i32, [c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp]),
+            "vdb_shards_get_vectors": (c_i32, [c_vp, c_i64, c_i64, c_vp]),
+            "vdb_shards_clear": (c_i32, [c_vp]),
+            "vdb_shards_reserve": (c_i32, [c_vp, c_i64]),
+            "vdb_shards_set_param": (c_i32, [c_vp, ctypes.c_char_p, c_i64]),
+            "vdb_shards_get_stat": (c_i32, [c_vp, ctypes.c_char_p, p_i64]),
+            "vdb_shutdown": (c_i32, []),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)
@@ -243,6 +258,107 @@ class NativeIndex:
             self._h, ctypes.c_void_p(q_ptr), int(n_queries), int(k), ctypes.c_void_p(mask_ptr or None),
             MEM_DEVICE, ctypes.c_void_p(out_scores_ptr), ctypes.c_void_p(out_idx_ptr),
             ctypes.c_void_p(out_keys_ptr or None), int(index_offset), ctypes.c_void_p(stream or None)))
+
+
+class NativeShards:
+    """One corpus row-sharded over several GPUs of this process (include/vdb.h vdb_shards_*):
+    the same interface as NativeIndex for the store; results identical to one index."""
+
+    def __init__(self, dim: int, metric: str = "cosine", devices=(0,), precision: Optional[str] = None):
+        if metric not in METRIC_IDS:
+            raise ValueError(f"unsupported metric {metric!r}; the vdb core implements {sorted(METRIC_IDS)}")
+        devices = [int(d) for d in devices]
+        if not devices:
+            raise ValueError("devices must name at least one GPU")
+        self._lib = load_library()
+        self.dim = int(dim)
+        self.metric = metric
+        self.devices = devices
+        dv = (ctypes.c_int32 * len(devices))(*devices)
+        h = ctypes.c_void_p()
+        _check(self._lib.vdb_shards_create(self.dim, METRIC_IDS[metric], dv, len(devices), ctypes.byref(h)))
+        self._h = h
+        if precision is not None:
+            self.set_param("precision", PRECISION_IDS[precision])
+
+    def close(self) -> None:
+        h, self._h = getattr(self, "_h", None), None
+        if h:
+            self._lib.vdb_shards_destroy(h)
+
+    def __del__(self):  # pragma: no cover - GC timing
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def reserve(self, rows: int) -> None:
+        _check(self._lib.vdb_shards_reserve(self._h, int(rows)))
+
+    def set_param(self, name: str, value: int) -> None:
+        _check(self._lib.vdb_shards_set_param(self._h, name.encode(), int(value)))
+
+    def stat(self, name: str) -> int:
+        v = ctypes.c_int64(0)
+        _check(self._lib.vdb_shards_get_stat(self._h, name.encode(), ctypes.byref(v)))
+        return int(v.value)
+
+    def shard_counts(self):
+        out = []
+        for g in range(len(self.devices)):
+            v = ctypes.c_int64(0)
+            _check(self._lib.vdb_shards_shard_count(self._h, g, ctypes.byref(v)))
+            out.append(int(v.value))
+        return out
+
+    def add(self, vectors: np.ndarray) -> None:
+        v = np.ascontiguousarray(vectors, dtype=np.float32)
+        if v.ndim != 2 or v.shape[1] != self.dim:
+            raise ValueError(f"vectors must have shape (n, {self.dim}), got {v.shape}")
+        if v.shape[0]:
+            _check(self._lib.vdb_shards_add(self._h, _ptr(v), v.shape[0]))
+
+    def count(self) -> int:
+        n = ctypes.c_int64(0)
+        _check(self._lib.vdb_shards_count(self._h, ctypes.byref(n)))
+        return int(n.value)
+
+    def clear(self) -> None:
+        _check(self._lib.vdb_shards_clear(self._h))
+
+    def get_vectors(self, start: int = 0, n: Optional[int] = None) -> np.ndarray:
+        total = self.count()
+        n = total - start if n is None else n
+        out = np.empty((max(n, 0), self.dim), dtype=np.float32)
+        if n > 0:
+            _check(self._lib.vdb_shards_get_vectors(self._h, int(start), int(n), _ptr(out)))
+        return out
+
+    def search(self, queries: np.ndarray, k: int, row_mask: Optional[np.ndarray] = None, with_keys: bool = False):
+        q = np.ascontiguousarray(queries, dtype=np.float32)
+        if q.ndim == 1:
+            q = q[None, :]
+        if q.ndim != 2 or q.shape[1] != self.dim:
+            raise ValueError(f"queries must have shape (B, {self.dim}), got {np.shape(queries)}")
+        B, k = q.shape[0], int(k)
+        scores = np.empty((B, k), dtype=np.float32)
+        idx = np.empty((B, k), dtype=np.int64)
+        keys = np.empty((B, k), dtype=np.float64) if with_keys else None
+        mask_p = None
+        if row_mask is not None:
+            m = np.ascontiguousarray(row_mask, dtype=np.uint32)
+            need = (self.count() + 31) // 32
+            if m.size < need:
+                raise ValueError(f"row_mask needs {need} uint32 words, got {m.size}")
+            mask_p = _ptr(m)
+        _check(self._lib.vdb_shards_search(self._h, _ptr(q), B, k, mask_p, _ptr(scores), _ptr(idx),
+                                           _ptr(keys) if keys is not None else None))
+        return (scores, idx, keys) if with_keys else (scores, idx)
+
+
+def shutdown() -> None:
+    """include/vdb.h vdb_shutdown: release idle workspaces of every live index."""
+    _check(load_library().vdb_shutdown())
 
 
 class NativeGraph:

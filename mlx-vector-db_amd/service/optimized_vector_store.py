@@ -31,6 +31,7 @@ from typing import Any, Dict, List, Optional, Tuple, Union
 import numpy as np
 
 from . import _vdb
+from .metadata_index import MetadataIndex
 from .persistence import StoreFiles
 
 logger = logging.getLogger("mlx_vector_db.optimized_store")
@@ -49,6 +50,10 @@ class MLXVectorStoreConfig:
     jit_compile: bool = True
     device: int = 0          # GPU ordinal holding this store's corpus
     persist: bool = True     # persist every add (append log + periodic compaction, service/persistence.py)
+    # several GPUs of this process: the corpus is row-sharded over them, each query batch is
+    # searched on every shard at once and the per-shard top-k lists are gathered and merged
+    # on the first device (service/_vdb.py NativeShards); None = the single `device`
+    devices: Optional[List[int]] = None
 
 
 def _as_matrix(vectors: Any) -> np.ndarray:
@@ -59,15 +64,63 @@ def _as_matrix(vectors: Any) -> np.ndarray:
     return a
 
 
-def _filter_mask(metadata: List[Dict], filt: Dict, n: int) -> Tuple[np.ndarray, int]:
-    """AND of exact `meta.get(key) == value` (service/optimized_vector_store.py:159-165),
-    as a row bitmap for the device top-k.  Returns (uint32 words, matches)."""
-    hits = np.fromiter((all(m.get(k) == v for k, v in filt.items()) for m in metadata[:n]),
-                       dtype=bool, count=n)
-    bits = np.zeros(((n + 31) // 32) * 32, dtype=bool)
-    bits[:n] = hits
-    words = np.packbits(bits, bitorder="little").view("<u4").astype(np.uint32)
-    return words, int(hits.sum())
+class _RWLock:
+    """Many readers (queries) or one writer (add / clear / optimize).  The reference
+    takes an RLock in add_vectors and clear but none in query
+    (service/optimized_vector_store.py:97,116,199) and is served from a 4-thread
+    executor (api/routes/vectors.py:43); here queries still run concurrently with each
+    other (ctypes releases the GIL inside the C-ABI), but always see a consistent
+    (rows, metadata) snapshot instead of a half-applied add."""
+
+    def __init__(self):
+        self._cond = threading.Condition(threading.Lock())
+        self._readers = 0
+        self._writer = False
+        self._waiting_writers = 0
+
+    def acquire_read(self):
+        with self._cond:
+            while self._writer or self._waiting_writers:
+                self._cond.wait()
+            self._readers += 1
+
+    def release_read(self):
+        with self._cond:
+            self._readers -= 1
+            if self._readers == 0:
+                self._cond.notify_all()
+
+    def acquire_write(self):
+        with self._cond:
+            self._waiting_writers += 1
+            while self._writer or self._readers:
+                self._cond.wait()
+            self._waiting_writers -= 1
+            self._writer = True
+
+    def release_write(self):
+        with self._cond:
+            self._writer = False
+            self._cond.notify_all()
+
+
+class _Read:
+    def __init__(self, lk: _RWLock):
+        self.lk = lk
+
+    def __enter__(self):
+        self.lk.acquire_read()
+
+    def __exit__(self, *a):
+        self.lk.release_read()
+
+
+class _Write(_Read):
+    def __enter__(self):
+        self.lk.acquire_write()
+
+    def __exit__(self, *a):
+        self.lk.release_write()
 
 
 class MLXVectorStore:
@@ -76,30 +129,36 @@ class MLXVectorStore:
     def __init__(self, store_path: str, config: Optional[MLXVectorStoreConfig] = None):
         self.store_path = Path(store_path).expanduser()
         self.config = config or MLXVectorStoreConfig()
-        self._lock = threading.RLock()
+        self._lock = threading.RLock()  # serialises writers (the reference's lock, :97, :199)
+        self._rw = _RWLock()            # queries (shared) vs adds / clear (exclusive)
         self.store_path.mkdir(parents=True, exist_ok=True)
         self._is_dirty = False
         self._compiled_similarity_fn = None
-        self._index: Optional[_vdb.NativeIndex] = None
+        self._index = None  # _vdb.NativeIndex, or _vdb.NativeShards over config.devices
         self._dim: Optional[int] = None
         self._metadata: List[Dict] = []
+        self._meta_index = MetadataIndex()
         self._vector_count = 0
         self._hnsw_index = None
         self._files = StoreFiles(self.store_path)
         if self.config.enable_hnsw:  # service/optimized_vector_store.py:72-78
             from performance.hnsw_index import ProductionHNSWIndex
             self._hnsw_index = ProductionHNSWIndex(self.config.dimension, self.store_path, self.config.metric,
-                                                   device=self.config.device)
+                                                   device=self._devices()[0])
         self._initialize_store()
         if self.config.jit_compile:
             self._compile_critical_functions()
         logger.info("vdb store initialised: %s | HNSW: %s", self.store_path, self.config.enable_hnsw)
 
     # ---- state -----------------------------------------------------------------
+    def _devices(self) -> List[int]:
+        return list(self.config.devices) if self.config.devices else [self.config.device]
+
     def _create_empty_store(self):
         if self._index is not None:
             self._index.clear()
         self._metadata = []
+        self._meta_index.clear()
         self._vector_count = 0
         self._is_dirty = False
 
@@ -111,10 +170,15 @@ class MLXVectorStore:
         if self.config.metric in _vdb.METRIC_IDS:
             self._compiled_similarity_fn = self.config.metric
 
-    def _ensure_index(self, dim: int) -> _vdb.NativeIndex:
+    def _ensure_index(self, dim: int):
         if self._index is None:
             metric = self.config.metric if self.config.metric in _vdb.METRIC_IDS else "cosine"
-            self._index = _vdb.NativeIndex(dim, metric, self.config.device)
+            devs = self._devices()
+            if len(devs) > 1:
+                # row shards over several GPUs of this process (service/_vdb.py NativeShards)
+                self._index = _vdb.NativeShards(dim, metric, devs)
+            else:
+                self._index = _vdb.NativeIndex(dim, metric, devs[0])
             self._dim = dim
         elif dim != self._dim:
             raise ValueError(f"Dimension mismatch: store holds {self._dim}-d vectors, got {dim}-d")
@@ -130,15 +194,18 @@ class MLXVectorStore:
     # ---- ingest ------------------------------------------------------------------
     def add_vectors(self, vectors: Union[np.ndarray, Any], metadata: List[Dict]):
         """service/optimized_vector_store.py:96-114."""
-        with self._lock:
+        with self._lock, _Write(self._rw):
             v = _as_matrix(vectors)
             if v.ndim == 1:
                 v = v[None, :]
             if v.ndim != 2:
                 raise ValueError(f"vectors must be 2-D (n, dim), got shape {v.shape}")
+            n0 = self._vector_count
             if v.shape[0] > 0:
                 self._ensure_index(v.shape[1]).add(v)
             self._metadata.extend(metadata)
+            # the filter postings index exactly the rows' metadata (row r <-> metadata[r])
+            self._meta_index.extend(self._metadata[len(self._meta_index):])
             self._vector_count = self._index.count() if self._index is not None else 0
             self._is_dirty = True
             if self.config.persist and v.shape[0] > 0:
@@ -149,65 +216,78 @@ class MLXVectorStore:
                 else:
                     self._is_dirty = False
             if self.config.enable_hnsw and self._hnsw_index is not None and self._index is not None:
-                # the reference rebuilds the graph from scratch on every add (:110-112)
-                self._hnsw_index.build(None, native_index=self._index)
+                # the reference rebuilds the graph from scratch on every add (:110-112); the graph
+                # path inserts the new rows into the existing graph instead (performance/hnsw_index.py)
+                self._hnsw_index.add_rows(self._index, n0)
             return {"vectors_added": len(metadata), "total_vectors": self._vector_count}
 
     # ---- query ---------------------------------------------------------------------
     def query(self, query_vector: Union[np.ndarray, Any], k: int = 10,
               filter_metadata: Optional[Dict] = None, use_hnsw: bool = True) -> Tuple:
         """service/optimized_vector_store.py:116-145 -> (indices, scores, metadata)."""
-        if self._vector_count == 0:
-            return [], [], []
-        q = _as_matrix(query_vector)
-        if q.ndim == 2 and q.shape[0] == 1:
-            q = q[0]
-        if q.ndim != 1:
-            raise ValueError(f"query takes one vector of shape (dim,) or (1, dim), got {q.shape}; "
-                             "use batch_query for several")
-        h = self._hnsw_index
-        if use_hnsw and self.config.enable_hnsw and h is not None and h.is_loaded:
-            # service/optimized_vector_store.py:120-143: hnswlib distances, k*10 candidates
-            # when filtering, brute force on any failure
-            try:
-                candidate_k = k * 10 if filter_metadata else k
-                indices, distances = h.search(q[None, :], k=candidate_k)
-                indices, distances = indices[0], distances[0]
-                if not filter_metadata:
-                    return ([int(i) for i in indices], distances.tolist(),
-                            [self._metadata[int(i)] for i in indices])
-                hits = []
-                for i, idx in enumerate(indices):
-                    if idx < len(self._metadata):
-                        meta = self._metadata[int(idx)]
-                        if all(meta.get(key) == value for key, value in filter_metadata.items()):
-                            hits.append((int(idx), float(distances[i]), meta))
-                    if len(hits) == k:
-                        break
-                if not hits:
-                    return [], [], []
-                fi, fd, fm = zip(*hits)
-                return list(fi), list(fd), list(fm)
-            except Exception as e:
-                logger.warning("HNSW-Suche fehlgeschlagen, falle auf Brute-Force zurück: %s", e)
-        return self._brute_force_search(q[None, :], k, filter_metadata)[0]
+        with _Read(self._rw):
+            if self._vector_count == 0:
+                return [], [], []
+            q = _as_matrix(query_vector)
+            if q.ndim == 2 and q.shape[0] == 1:
+                q = q[0]
+            if q.ndim != 1:
+                raise ValueError(f"query takes one vector of shape (dim,) or (1, dim), got {q.shape}; "
+                                 "use batch_query for several")
+            h = self._hnsw_index
+            if use_hnsw and self.config.enable_hnsw and h is not None and h.is_loaded:
+                # service/optimized_vector_store.py:120-143: hnswlib distances, k*10 candidates
+                # when filtering, brute force on any failure
+                try:
+                    candidate_k = k * 10 if filter_metadata else k
+                    indices, distances = h.search(q[None, :], k=candidate_k)
+                    indices, distances = indices[0], distances[0]
+                    if not filter_metadata:
+                        return ([int(i) for i in indices], distances.tolist(),
+                                [self._metadata[int(i)] for i in indices])
+                    hits = []
+                    for i, idx in enumerate(indices):
+                        if idx < len(self._metadata):
+                            meta = self._metadata[int(idx)]
+                            if all(meta.get(key) == value for key, value in filter_metadata.items()):
+                                hits.append((int(idx), float(distances[i]), meta))
+                        if len(hits) == k:
+                            break
+                    if not hits:
+                        return [], [], []
+                    fi, fd, fm = zip(*hits)
+                    return list(fi), list(fd), list(fm)
+                except Exception as e:
+                    logger.warning("HNSW-Suche fehlgeschlagen, falle auf Brute-Force zurück: %s", e)
+            return self._brute_force_search(q[None, :], k, filter_metadata)[0]
 
     def batch_query(self, query_vectors: Union[np.ndarray, Any], k: int = 10,
                     filter_metadata: Optional[Dict] = None) -> List[Tuple]:
         """The batched path (performance/mlx_optimized.py:217-248) behind the store API that
-        api/routes/vectors.py:291 and tests/demo.py:134 call: one (indices, scores, metadata)
-        tuple per query, each exactly what ``query`` returns for that row."""
+        api/routes/vectors.py:291 and tests/demo.py:134-137 call: one (indices, distances,
+        metadata) tuple per query, same rows and order as ``query`` for that vector.
+
+        The second element is a DISTANCE, because that is how its only caller reads it:
+        /vectors/batch_query unpacks ``indices, distances, metadata_list`` and scores cosine
+        as ``max(0, 1.0 - dist)`` and euclidean as ``1 / (1 + dist)``
+        (api/routes/vectors.py:300-306).  So cosine returns ``1 - cos`` and euclidean the
+        sqrt-L2 distance (which is what ``query`` already returns for euclidean)."""
         q = _as_matrix(query_vectors)
         if q.ndim == 1:
             q = q[None, :]
         if q.ndim != 2:
             raise ValueError(f"query_vectors must be 2-D (B, dim), got {q.shape}")
-        if self._vector_count == 0 or q.shape[0] == 0:
-            return [([], [], []) for _ in range(q.shape[0])]
-        return self._brute_force_search(q, k, filter_metadata)
+        with _Read(self._rw):
+            if self._vector_count == 0 or q.shape[0] == 0:
+                return [([], [], []) for _ in range(q.shape[0])]
+            res = self._brute_force_search(q, k, filter_metadata)
+        if self.config.metric == "cosine":
+            res = [(i, [1.0 - s for s in sc], m) for i, sc, m in res]
+        return res
 
     def _brute_force_search(self, Q: np.ndarray, k: int, filter_metadata: Optional[Dict] = None):
-        """service/optimized_vector_store.py:149-192 for a [B, D] block of queries."""
+        """service/optimized_vector_store.py:149-192 for a [B, D] block of queries
+        (called with the read lock held)."""
         if not self._compiled_similarity_fn:
             raise RuntimeError(_NO_OPERATOR_MSG)
         B = Q.shape[0]
@@ -221,7 +301,8 @@ class MLXVectorStore:
         mask = None
         eligible = n
         if filter_metadata:
-            mask, eligible = _filter_mask(self._metadata, filter_metadata, n)
+            # posting lists maintained at add time, not the reference's O(N) scan (:159-165)
+            mask, eligible = self._meta_index.bitmap(filter_metadata, n)
             if eligible == 0:
                 return empty
         kk = min(k, eligible)
@@ -245,7 +326,7 @@ class MLXVectorStore:
 
     def clear(self):
         """service/optimized_vector_store.py:198-209."""
-        with self._lock:
+        with self._lock, _Write(self._rw):
             try:
                 if self.store_path.exists():
                     shutil.rmtree(self.store_path)
@@ -255,7 +336,7 @@ class MLXVectorStore:
                 if self.config.enable_hnsw:  # :205-206
                     from performance.hnsw_index import ProductionHNSWIndex
                     self._hnsw_index = ProductionHNSWIndex(self.config.dimension, self.store_path,
-                                                           self.config.metric, device=self.config.device)
+                                                           self.config.metric, device=self._devices()[0])
             except Exception as e:  # the reference logs and swallows (:208-209)
                 logger.error("clearing store %s failed: %s", self.store_path, e)
 
@@ -263,11 +344,12 @@ class MLXVectorStore:
         """Callers: api/routes/admin.py:230, api/routes/performance.py:188, tests/demo.py:248.
         Flushes persistence and pre-sizes the device corpus to a 256-row multiple."""
         t0 = time.time()
-        with self._lock:
+        with self._lock, _Write(self._rw):
             if self._index is not None:
                 self._index.reserve(self._vector_count)
             self._is_dirty = True
             self._save_store(force=True)
+        with _Read(self._rw):
             self._warmup_kernels()
         return {"optimized": True, "vector_count": self._vector_count,
                 "optimization_time_ms": (time.time() - t0) * 1000.0}
@@ -284,7 +366,7 @@ class MLXVectorStore:
         if not self._compiled_similarity_fn:
             issues.append(_NO_OPERATOR_MSG)
         return {"healthy": not issues, "issues": issues, "vector_count": self._vector_count,
-                "metric": self.config.metric, "device": self.config.device}
+                "metric": self.config.metric, "devices": self._devices()}
 
     def get_stats(self):
         """service/optimized_vector_store.py:241-242 (+ memory_usage_mb, read by
@@ -316,6 +398,8 @@ class MLXVectorStore:
                 return
             self._ensure_index(vecs.shape[1]).add(vecs)
             self._metadata = meta
+            self._meta_index.clear()
+            self._meta_index.extend(meta)
             self._vector_count = self._index.count()
             if self._hnsw_index is not None:
                 if not self._hnsw_index.attach(self._index):

@@ -84,6 +84,11 @@ class StoreFiles:
         info = self._read_info()
         if info is None:
             return vecs, meta
+        if info.get("base_rows") == self.base_rows and len(meta) != self.base_rows:
+            # a compaction stopped between its two renames (metadata.jsonl is renamed first,
+            # see compact): the new metadata already covers the log's rows; or the base was
+            # written with a different metadata count.  Row r's metadata is line r either way.
+            meta = (meta + [{}] * self.base_rows)[: self.base_rows]
         if info.get("base_rows") != self.base_rows:
             logger.warning("append log continues %s base rows, base holds %d: already compacted, dropped",
                            info.get("base_rows"), self.base_rows)
@@ -143,12 +148,19 @@ class StoreFiles:
         return self.log_rows > max(self.base_rows // 4, MIN_COMPACT_ROWS)
 
     def compact(self, vectors: np.ndarray, metadata: List[Dict]) -> None:
-        """Write `vectors` / `metadata` (the whole store) as the new base, drop the log."""
+        """Write `vectors` / `metadata` (the whole store) as the new base, drop the log.
+
+        Crash safety: both files are written to temporaries first; metadata.jsonl is renamed
+        before vectors.npz.  Stopped between the renames, the directory holds the old
+        vectors.npz, the new (longer) metadata.jsonl and the log, whose base_rows still
+        matches the old base: load() keeps the first base_rows metadata lines and appends the
+        log's, which is the same store.  Stopped after the vectors rename, the log's
+        base_rows no longer matches and load() drops it (the new base holds its rows)."""
         v = np.ascontiguousarray(vectors, dtype=np.float32)
         self.path.mkdir(parents=True, exist_ok=True)
-        _write_atomic(self.path / BASE_VECTORS, lambda f: np.savez(f, vectors=v))
         _write_atomic(self.path / BASE_META,
                       lambda f: f.write("".join(json.dumps(m) + "\n" for m in metadata).encode()))
+        _write_atomic(self.path / BASE_VECTORS, lambda f: np.savez(f, vectors=v))
         self.base_rows = v.shape[0]
         self.dim = v.shape[1] if v.ndim == 2 and v.shape[0] else self.dim
         self._remove_log()

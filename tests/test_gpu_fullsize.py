@@ -1,0 +1,174 @@
+"""BASELINE.json's configurations at their full sizes on one GPU, through the C-ABI.
+
+Every query of every batch is checked for the size-independent properties (sorted
+output, planted self-queries on top, no invalid slots, fallbacks counted); a spread of
+queries across all query blocks is checked exactly (indices and fp64 keys) against the
+oracle (oracle/ref_cpu.exact_search, which keys only a prefiltered candidate set, so it
+finishes in seconds at these sizes).
+
+  C2  1M x 768 cosine, B=64, k=10 (bf16x3 default): the exact-vs-MLX-fp32 question
+      (north_star: indices "bit-exact" with the fp32 reference): the numpy restatement of
+      the reference's fp32 batched path (reference_batch_search = performance/mlx_optimized.py:217-248)
+      is run on the same queries, and every place its order differs from the returned one
+      must be a near tie -- exact keys closer than the fp32 error bound of the reference's
+      own arithmetic.  The count goes to $VDB_TEST_REPORT_DIR/c2_fp32_ref.json.
+  C3  1M x 1536 cosine, B=256, k=10 (4 query blocks).
+  C4  10M x 128 L2, B=512, k=100 (8 query blocks), both step-end modes of the scan.
+  C5  5M x 384 graph (M=16 -> degree 32, efSearch=128), batch 1: hnswlib's distance
+      conventions (performance/hnsw_index.py:35,101) checked against exact keys of the
+      returned rows, recall@10 against the exact path on 100 queries.
+"""
+import json
+import os
+import time
+
+import numpy as np
+import pytest
+
+from oracle import ref_cpu
+
+pytestmark = [pytest.mark.gpu, pytest.mark.slow]
+
+
+@pytest.fixture(scope="module")
+def vdb():
+    from service import _vdb
+    assert _vdb.device_count() >= 1, "no GPU visible"
+    return _vdb
+
+
+def _report(name, obj):
+    d = os.environ.get("VDB_TEST_REPORT_DIR")
+    if d:
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, name), "w") as f:
+            json.dump(obj, f, indent=1)
+    print(name, json.dumps(obj))
+
+
+def _properties(s, i, metric, N):
+    assert (i >= 0).all() and (i < N).all()
+    if metric == "cosine":
+        assert (np.diff(s, axis=1) <= 0).all()
+    else:
+        assert (np.diff(s, axis=1) >= 0).all()
+    for row in i:  # no row twice in one list
+        assert np.unique(row).size == row.size
+
+
+def test_c2_exact_vs_reference_fp32_order(vdb):
+    N, D, B, k = 1_000_000, 768, 64, 10
+    V = np.random.default_rng(0).random((N, D), dtype=np.float32)
+    Q = np.random.default_rng(1).random((B, D), dtype=np.float32)
+    Q[5], Q[40] = V[777_777], V[3]
+    ix = vdb.NativeIndex(D, "cosine")
+    ix.add(V)
+    s, i, kk = ix.search(Q, k, with_keys=True)
+    _properties(s, i, "cosine", N)
+    assert i[5, 0] == 777_777 and i[40, 0] == 3
+    sub = [0, 1, 5, 17, 31, 40, 50, 63]
+    es, ei, ek = ref_cpu.exact_search(Q[sub], V, k, "cosine")
+    np.testing.assert_array_equal(i[sub], ei)
+    np.testing.assert_array_equal(kk[sub], ek)
+    # the reference's own fp32 arithmetic (normalise, fp32 matmul, stable argsort)
+    ri, rs = ref_cpu.reference_batch_search(Q[sub], V, k)
+    # rigorous bound of one fp32 cosine: D additions + normalisation roundings, relative to |q||x| = 1
+    eps32 = 1.01 * (D + 8) * 2.0 ** -24
+    pos_diff, set_diff, worst = 0, 0, 0.0
+    for r, b in enumerate(sub):
+        ours, ref = i[b].tolist(), ri[r].tolist()
+        pairs = [(a, c) for a, c in zip(ours, ref) if a != c]
+        pos_diff += len(pairs)
+        set_diff += len(set(ref) - set(ours))
+        rows = sorted(set(ours) | set(ref))
+        key = dict(zip(rows, ref_cpu.exact_keys(Q[b], V[rows], "cosine")))
+        for a, c in pairs:
+            gap = abs(key[a] - key[c])
+            worst = max(worst, gap)
+            assert gap < 2 * eps32, (b, a, c, gap)
+        for c in set(ref) - set(ours):  # a reference row we left out ties with our k-th
+            assert key[ours[-1]] - key[c] < 2 * eps32
+    np.testing.assert_allclose(s[sub], rs, atol=1e-4, rtol=0)
+    assert ix.stat("fallback_queries") == 0
+    _report("c2_fp32_ref.json", {"queries": len(sub), "k": k, "positions_differing": pos_diff,
+                                 "rows_differing": set_diff, "max_exact_key_gap_of_a_swap": worst,
+                                 "fp32_bound_2eps": 2 * eps32})
+
+
+def test_c3_1m_x_1536_b256(vdb):
+    N, D, B, k = 1_000_000, 1536, 256, 10
+    V = np.random.default_rng(3).random((N, D), dtype=np.float32)
+    Q = np.random.default_rng(4).random((B, D), dtype=np.float32)
+    plant = {0: 12, 100: 999_999, 200: 500_000, 255: 77}
+    for b, r in plant.items():
+        Q[b] = V[r]
+    ix = vdb.NativeIndex(D, "cosine")
+    ix.add(V)
+    t0 = time.perf_counter()
+    s, i, kk = ix.search(Q, k, with_keys=True)
+    dt = time.perf_counter() - t0
+    _properties(s, i, "cosine", N)
+    for b, r in plant.items():
+        assert i[b, 0] == r and s[b, 0] > 0.9999
+    sub = [0, 1, 63, 64, 100, 127, 128, 191, 200, 255]  # all 4 query blocks
+    es, ei, ek = ref_cpu.exact_search(Q[sub], V, k, "cosine")
+    np.testing.assert_array_equal(i[sub], ei)
+    np.testing.assert_array_equal(kk[sub], ek)
+    fb = ix.stat("fallback_queries")
+    _report("c3.json", {"fallback_queries": fb, "host_search_s": dt})
+    assert fb <= B // 50  # certified by the candidate pass (a fallback is still exact, only slower)
+
+
+@pytest.mark.parametrize("sync", [0, 1])
+def test_c4_10m_x_128_l2_b512_top100(vdb, sync):
+    N, D, B, k = 10_000_000, 128, 512, 100
+    V = np.random.default_rng(5).random((N, D), dtype=np.float32)
+    Q = np.random.default_rng(6).random((B, D), dtype=np.float32)
+    plant = {3: 9_999_999, 70: 0, 300: 4_242_424, 511: 1_234_567}
+    for b, r in plant.items():
+        Q[b] = V[r]
+    ix = vdb.NativeIndex(D, "euclidean")
+    ix.set_param("scan_sync", sync)  # 0 = auto (flag-gated at Dp = 128), 1 = lockstep
+    ix.reserve(N)
+    for s0 in range(0, N, 1 << 21):
+        ix.add(V[s0:s0 + (1 << 21)])
+    s, i, kk = ix.search(Q, k, with_keys=True)
+    _properties(s, i, "euclidean", N)
+    for b, r in plant.items():
+        assert i[b, 0] == r and s[b, 0] == 0.0
+    sub = [0, 3, 70, 130, 200, 290, 300, 350, 450, 511]  # all 8 query blocks
+    es, ei, ek = ref_cpu.exact_search(Q[sub], V, k, "euclidean")
+    np.testing.assert_array_equal(i[sub], ei)
+    np.testing.assert_array_equal(kk[sub], ek)
+    fb = ix.stat("fallback_queries")
+    _report(f"c4_sync{sync}.json", {"fallback_queries": fb})
+    assert fb <= B // 50
+
+
+@pytest.mark.timeout(600)
+def test_c5_graph_5m_x_384(vdb):
+    from performance.hnsw_index import N_ENTRIES, TEAMS
+    N, D, k, ef = 5_000_000, 384, 10, 128
+    V = np.random.default_rng(7).random((N, D), dtype=np.float32)
+    Q = np.random.default_rng(8).random((100, D), dtype=np.float32)
+    Q[0] = V[4_999_999]
+    ix = vdb.NativeIndex(D, "cosine")
+    ix.reserve(N)
+    for s0 in range(0, N, 1 << 20):
+        ix.add(V[s0:s0 + (1 << 20)])
+    t0 = time.perf_counter()
+    g = vdb.NativeGraph.build(ix, degree=32, knn=32, n_entries=N_ENTRIES)
+    build_s = time.perf_counter() - t0
+    g.set_param("teams", TEAMS)
+    lab, dist = g.search(Q, k, ef)
+    assert (lab >= 0).all() and (lab < N).all()
+    assert (np.diff(dist, axis=1) >= 0).all()
+    # hnswlib cosine convention: distance = 1 - cos of the returned row (fp32 of the same products)
+    for b in range(0, 100, 10):
+        ex = ref_cpu.exact_keys(Q[b], V[lab[b]], "cosine")
+        np.testing.assert_allclose(dist[b], 1.0 - ex, atol=2e-6, rtol=0)
+    assert lab[0, 0] == 4_999_999 and abs(dist[0, 0]) < 1e-5
+    _, ei, _ = ref_cpu.exact_search(Q, V, k, "cosine")
+    recall = np.mean([len(set(a) & set(b)) / k for a, b in zip(lab.tolist(), ei.tolist())])
+    _report("c5.json", {"recall_at_10": recall, "build_s": build_s, "teams": TEAMS, "ef": ef})
+    assert recall >= 0.2  # parity for the graph is recall, not equality

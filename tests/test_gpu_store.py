@@ -111,3 +111,59 @@ def test_functional_api_lifecycle(store_mod, tmp_path, monkeypatch):
     assert len(sm.query_vectors("test_user", "test_model", vecs[0], k=3)) == 3
     sm.delete_store("test_user", "test_model")
     assert not sm.store_exists("test_user", "test_model")
+
+
+@pytest.mark.parametrize("metric", ["cosine", "euclidean"])
+def test_multi_device_shards_equal_one_index(store_mod, metric):
+    """vdb_shards_* (include/vdb.h): rows dealt to shards in pieces over several adds, two
+    and three shards on the one GPU of the box (the code path of distinct devices, with
+    device-local peer copies); results, fp64 keys and ties bit-identical to one index."""
+    from service import _vdb
+    rng = np.random.default_rng(44)
+    V = rng.random((30011, 72), dtype=np.float32)
+    V[29000:29010] = V[17]          # ties straddling pieces / shards
+    V[5:8] = V[20000]
+    Q = np.concatenate([V[[17, 20000]], rng.random((20, 72), dtype=np.float32)])
+    mask = rng.random(V.shape[0]) < 0.6
+    mask[[17, 29003, 20000, 6]] = True
+    bits = np.zeros(((V.shape[0] + 31) // 32) * 32, bool)
+    bits[:V.shape[0]] = mask
+    words = np.packbits(bits, bitorder="little").view("<u4").astype(np.uint32)
+    for devs in ([0, 0], [0, 0, 0]):
+        sh = _vdb.NativeShards(72, metric, devs)
+        for a, b in ((0, 7), (7, 10007), (10007, 10008), (10008, 30011)):
+            sh.add(V[a:b])
+        assert sh.count() == V.shape[0] and sum(sh.shard_counts()) == V.shape[0]
+        assert max(sh.shard_counts()) - min(sh.shard_counts()) <= 10007
+        np.testing.assert_array_equal(sh.get_vectors(), V)
+        np.testing.assert_array_equal(sh.get_vectors(29990, 21), V[29990:])
+        for k, m in ((10, None), (37, words)):
+            s, i, kk = sh.search(Q, k, row_mask=m, with_keys=True)
+            es, ei, ek = ref_cpu.exact_search(Q, V, k, metric, row_mask=None if m is None else mask)
+            np.testing.assert_array_equal(i, ei)
+            np.testing.assert_array_equal(kk, ek)
+            np.testing.assert_array_equal(s, es)
+        sh.clear()
+        assert sh.count() == 0
+        sh.close()
+
+
+def test_store_over_devices_list(store_mod, tmp_path):
+    """MLXVectorStoreConfig(devices=[0, 0]): the store API over the shard set."""
+    rng = np.random.default_rng(45)
+    V = rng.random((5000, 40), dtype=np.float32)
+    meta = [{"id": i, "g": i % 3} for i in range(5000)]
+    st = _mk(store_mod, tmp_path / "m", 40, devices=[0, 0])
+    st.add_vectors(V[:1234], meta[:1234])
+    st.add_vectors(V[1234:], meta[1234:])
+    for q, filt in ((V[4321], None), (rng.random(40, dtype=np.float32), {"g": 1})):
+        gi, gs, gm = st.query(q, k=10, filter_metadata=filt)
+        ri, rs, rm = ref_cpu.reference_store_search(q, V, 10, "cosine", meta, filt)
+        assert gi == ri and gm == rm
+        np.testing.assert_allclose(gs, rs, rtol=1e-4, atol=1e-5)
+    assert st.batch_query(V[:3], k=2)[1][0][0] == 1
+    st2 = _mk(store_mod, tmp_path / "m", 40, devices=[0, 0])  # reload from the append log
+    assert st2._vector_count == 5000 and st2.query(V[4321], k=3)[0][0] == 4321
+    from service import _vdb
+    _vdb.shutdown()  # idle workspaces released; the stores keep working
+    assert st.query(V[10], k=1)[0] == [10]

@@ -97,3 +97,40 @@ def test_dimension_mismatch_rejected(tmp_path):
         pass
     else:
         raise AssertionError("expected ValueError")
+
+
+def test_compaction_stopped_between_its_two_renames(tmp_path, monkeypatch):
+    """a crash after metadata.jsonl is renamed but before vectors.npz is must not
+    lose or shift metadata (compact renames metadata first; load keeps base_rows lines)."""
+    import os
+    rng = np.random.default_rng(4)
+    f = P.StoreFiles(tmp_path)
+    A, B = _rows(rng, 5), _rows(rng, 3)
+    f.compact(A, [{"i": i} for i in range(5)])
+    f.append(B, [{"i": i} for i in range(5, 8)])
+    v, m = P.StoreFiles(tmp_path).load()
+    real_replace = os.replace
+    calls = []
+
+    def crash_on_second(src, dst):
+        calls.append(dst)
+        if len(calls) == 2:
+            raise OSError("simulated crash between the two renames")
+        return real_replace(src, dst)
+
+    monkeypatch.setattr(P.os, "replace", crash_on_second)
+    try:
+        P.StoreFiles(tmp_path).compact(v, m)
+    except OSError:
+        pass
+    monkeypatch.setattr(P.os, "replace", real_replace)
+    assert str(calls[0]).endswith(P.BASE_META)
+    g = P.StoreFiles(tmp_path)
+    v2, m2 = g.load()
+    np.testing.assert_array_equal(v2, np.concatenate([A, B]))
+    assert [x["i"] for x in m2] == list(range(8))
+    C = _rows(rng, 1)
+    g.append(C, [{"i": 8}])  # later adds keep row r <-> metadata line r
+    v3, m3 = P.StoreFiles(tmp_path).load()
+    np.testing.assert_array_equal(v3, np.concatenate([A, B, C]))
+    assert [x["i"] for x in m3] == list(range(9))
