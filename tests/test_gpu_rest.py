@@ -6,6 +6,7 @@ with the reference route's S12 formatting (api/routes/vectors.py:236-258, :296-3
 here; and the store under the reference's concurrency (4 executor threads, api/routes/vectors.py:43)
 while a fifth thread adds rows."""
 import threading
+import time
 
 import numpy as np
 import pytest
@@ -113,11 +114,18 @@ def test_concurrent_queries_during_adds(store_mod, tmp_path):
         except Exception as e:  # pragma: no cover - reported below
             errors.append(repr(e))
 
+    def wait_answers(n, limit=60.0):
+        t0 = time.time()
+        while len(answers) < n and time.time() - t0 < limit and not errors:
+            time.sleep(0.002)
+
     def writer():
         try:
             for j in range(n_chunks):
+                wait_answers(len(answers) + 8)  # some answers between every two adds
                 s = N0 + chunk * j
                 st.add_vectors(V[s:s + chunk], [{"i": i} for i in range(s, s + chunk)])
+            wait_answers(len(answers) + 8)
         except Exception as e:  # pragma: no cover
             errors.append(repr(e))
 
