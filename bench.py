@@ -74,21 +74,46 @@ def corpus_rows(N, D, start, stop, seed=0):
     return out
 
 
-def cpu_baseline(V, Q, k):
-    """The reference's batched path restated in numpy (oracle/ref_cpu.py), one full batch."""
+def cpu_baseline(V, Q, k, metric="cosine", budget_s=10.0):
+    """BASELINE.md §2, both reference paths restated in numpy (oracle/ref_cpu.py), each
+    timed for at least `budget_s` on this host's cores:
+      (ii) batched  `optimized_batch_similarity_search` (performance/mlx_optimized.py:217-248):
+           whole batches of B queries (normalise + fp32 BLAS matmul + stable argsort);
+      (i)  per-query store path `_brute_force_search` (service/optimized_vector_store.py:149-192):
+           one query at a time (re-normalise the corpus, matvec, full stable argsort, [:k]).
+    `value` is the faster of the two (the batched path); p50 is per batch / per query."""
     from oracle import ref_cpu
     try:
         from threadpoolctl import threadpool_info
         threads = max([p.get("num_threads", 1) for p in threadpool_info() if p.get("user_api") == "blas"] or [1])
     except Exception:
         threads = int(os.environ.get("OMP_NUM_THREADS", "1"))
+    bt = []
     t0 = time.perf_counter()
-    ref_cpu.reference_batch_search(Q, V, k)
-    dt = time.perf_counter() - t0
-    return {"value": Q.shape[0] / dt, "unit": "queries/s", "cores": threads, "kind": "port",
-            "sample": f"1 batch of {Q.shape[0]} queries x full {V.shape[0]}x{V.shape[1]} corpus, numpy restatement "
-                      f"of optimized_batch_similarity_search (normalise + fp32 BLAS matmul + stable argsort); "
-                      f"{dt:.2f} s"}
+    while not bt or (time.perf_counter() - t0 < budget_s and len(bt) < 50):
+        t1 = time.perf_counter()
+        if metric == "cosine":
+            ref_cpu.reference_batch_search(Q, V, k)
+        else:  # the store's euclidean operator, per query of the batch (the batched module has none)
+            for q in Q:
+                ref_cpu.reference_topk_indices(ref_cpu.reference_euclidean_distances(q, V), k, metric)
+        bt.append(time.perf_counter() - t1)
+    qt = []
+    t0 = time.perf_counter()
+    i = 0
+    while not qt or (time.perf_counter() - t0 < budget_s and len(qt) < 50):
+        t1 = time.perf_counter()
+        ref_cpu.reference_store_search(Q[i % Q.shape[0]], V, k, metric)
+        qt.append(time.perf_counter() - t1)
+        i += 1
+    batched_qps = Q.shape[0] / float(np.mean(bt))
+    single_qps = 1.0 / float(np.mean(qt))
+    return {"value": max(batched_qps, single_qps), "unit": "queries/s", "cores": threads, "kind": "port",
+            "sample": f"numpy restatement on this host: (ii) {len(bt)} batch(es) of {Q.shape[0]} queries x the full "
+                      f"{V.shape[0]}x{V.shape[1]} corpus ({sum(bt):.1f} s) and (i) {len(qt)} single queries through "
+                      f"the store path ({sum(qt):.1f} s); value = the faster path",
+            "batched": {"qps": batched_qps, "p50_ms_per_batch": float(np.median(bt)) * 1e3, "batches": len(bt)},
+            "per_query": {"qps": single_qps, "p50_ms": float(np.median(qt)) * 1e3, "queries": len(qt)}}
 
 
 def cpu_graph_baseline(V, nbr, entries, Q, k, ef, metric, gt, budget_s=15.0):
@@ -472,7 +497,7 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             V = np.concatenate(host_parts) if len(host_parts) > 1 else host_parts[0]
             del host_parts
-            rec["cpu_baseline"] = cpu_baseline(V, Q, k)
+            rec["cpu_baseline"] = cpu_baseline(V, Q, k, metric)
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.barrier()

@@ -57,7 +57,7 @@ enum {
     VDB_ERR_NODEVICE = -6     /* no gfx950 device visible                    */
 };
 
-enum { VDB_METRIC_COSINE = 0, VDB_METRIC_EUCLIDEAN = 1 };
+enum { VDB_METRIC_COSINE = 0, VDB_METRIC_EUCLIDEAN = 1, VDB_METRIC_DOT = 2 /* operator slot only */ };
 enum { VDB_MEM_HOST = 0, VDB_MEM_DEVICE = 1 };
 
 /* Candidate-pass arithmetic for an index (vdb_index_set_param "precision").
@@ -154,14 +154,27 @@ int32_t vdb_merge_topk(const double* keys, const int64_t* idx, int32_t n_lists, 
 /* --- stateless operator slot ---------------------------------------------------
  * The reference's similarity functions themselves, returning every score
  * (no top-k): `_compiled_cosine_similarity` / `_compiled_euclidean_distance`
- * (service/optimized_vector_store.py:31-48) for n_queries = 1 and
+ * (service/optimized_vector_store.py:31-48) for n_queries = 1,
  * `compute_cosine_similarity_batch` (performance/mlx_optimized.py:59-88) for
- * n_queries > 1.  All pointers are device memory: corpus [n, dim] row-major
- * fp32, queries [n_queries, dim], out [n_queries, n] fp32.  fp32 arithmetic
- * (normalise, then MFMA dot), within 1e-4 of the reference. */
+ * n_queries > 1, and `compute_dot_product` (mlx_optimized.py:150-156, metric
+ * VDB_METRIC_DOT).  All pointers are device memory: corpus [n, dim] row-major
+ * fp32, queries [n_queries, dim], out [n_queries, n] fp32.  cosine / dot: an fp32
+ * MFMA GEMM over LDS-staged tiles with the norms applied in the epilogue;
+ * euclidean: direct differences (the reference's form).  Within 1e-4 of the
+ * reference's fp32 arithmetic. */
 int32_t vdb_similarity_matrix(const float* corpus, int64_t n, int32_t dim,
                               const float* queries, int32_t n_queries, int32_t metric,
                               float* out, void* stream);
+/* `normalize_vectors` (performance/mlx_optimized.py:110-125): out = x / max(|x|, 1e-8)
+ * per row; device memory, in == out allowed. */
+int32_t vdb_normalize_rows(const float* in, int64_t n, int32_t dim, float* out, void* stream);
+/* `fast_top_k_indices` / `mx.argsort(-scores)[:k]` (mlx_optimized.py:90-108,
+ * optimized_vector_store.py:176-183) over `rows` score rows of length n (device
+ * memory): the k best per row, largest first (largest = 1) or smallest first, ties to
+ * the lower index, NaN last.  out_indices [rows, k] int64, out_values NULL or
+ * [rows, k] fp32.  1 <= k <= min(n, 1024). */
+int32_t vdb_topk_scores(const float* scores, int32_t rows, int64_t n, int32_t k, int32_t largest,
+                        int64_t* out_indices, float* out_values, void* stream);
 
 /* --- graph index (the HNSW path) -------------------------------------------------
  * Replaces ProductionHNSWIndex (performance/hnsw_index.py:23-129: hnswlib

@@ -926,8 +926,30 @@ int32_t vdb_similarity_matrix(const float* corpus, int64_t n, int32_t dim, const
                               int32_t metric, float* out, void* stream) {
     if (!corpus || !queries || !out) return set_error(VDB_ERR_INVALID, "NULL argument");
     if (n < 0 || dim <= 0 || nq <= 0) return set_error(VDB_ERR_INVALID, "bad sizes");
-    if (metric != 0 && metric != 1) return set_error(VDB_ERR_UNSUPPORTED, "metric %d", metric);
+    if (metric < 0 || metric > 2) return set_error(VDB_ERR_UNSUPPORTED, "metric %d", metric);
     HIP_TRY(launch_similarity_matrix(corpus, n, dim, queries, nq, metric, out, (hipStream_t)stream));
+    return VDB_OK;
+}
+
+int32_t vdb_normalize_rows(const float* in, int64_t n, int32_t dim, float* out, void* stream) {
+    if ((!in || !out) && n > 0) return set_error(VDB_ERR_INVALID, "NULL argument");
+    if (n < 0 || dim <= 0) return set_error(VDB_ERR_INVALID, "bad sizes");
+    HIP_TRY(launch_normalize_rows(in, n, dim, out, (hipStream_t)stream));
+    return VDB_OK;
+}
+
+int32_t vdb_topk_scores(const float* scores, int32_t rows, int64_t n, int32_t k, int32_t largest, int64_t* out_indices,
+                        float* out_values, void* stream) {
+    if (!scores || !out_indices) return set_error(VDB_ERR_INVALID, "NULL argument");
+    if (rows <= 0 || n <= 0 || n > 0xFFFFFFFEll) return set_error(VDB_ERR_INVALID, "bad sizes rows=%d n=%lld", rows,
+                                                                   (long long)n);
+    if (k <= 0 || k > 1024 || k > n) return set_error(VDB_ERR_INVALID, "k must be in [1, min(n, 1024)], got %d", k);
+    hipStream_t st = (hipStream_t)stream;
+    void* ws = nullptr;
+    HIP_TRY(hipMallocAsync(&ws, topk_workspace_bytes(n, rows, k), st));
+    const hipError_t e = launch_topk_scores(scores, rows, n, k, largest, out_indices, out_values, ws, st);
+    HIP_TRY(hipFreeAsync(ws, st));
+    HIP_TRY(e);
     return VDB_OK;
 }
 

@@ -1,4 +1,4 @@
-// vdb_ingest.hip: ingest (pack/unpack), query preparation and the operator-slot score matrix — part of the gfx950 kernels of the brute-force distance + top-k path
+// vdb_ingest.hip: ingest (pack/unpack) and query preparation — part of the gfx950 kernels of the brute-force distance + top-k path
 // (pipeline overview: vdb_scan.hip).  Built with -ffp-contract=off.
 #include "vdb_common.h"
 #include "vdb_internal.h"
@@ -203,52 +203,4 @@ hipError_t launch_prep_queries(const float* Q, int B, int Bp, int D, int G, int 
                        qn64, flag_count, gthr, gslots, gl_cnt);
     return hipGetLastError();
 }
-// =============================================================================
-// Operator slot: the full score matrix, reference fp32 arithmetic
-// =============================================================================
-// cosine: x/max(|x|,1e-8) and q/max(|q|,1e-8) in fp32, then the dot product;
-// euclidean: sqrt(sum((x-q)^2)).  One wave per corpus row, looping queries; not
-// the hot path (service/optimized_vector_store.py:31-48 materialise [N] per
-// query, performance/mlx_optimized.py:59-88 [B,N]).
-__global__ void __launch_bounds__(256) similarity_matrix_kernel(const float* __restrict__ X, int64_t N, int D,
-                                                                const float* __restrict__ Q, int B, int metric,
-                                                                float* __restrict__ out) {
-    const int lane = threadIdx.x & 63;
-    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (r >= N) return;
-    const float* x = X + r * D;
-    float xs = 0.0f;
-    for (int d = lane; d < D; d += 64) xs = fmaf(x[d], x[d], xs);
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) xs += __shfl_xor(xs, off, 64);
-    const float xinv = 1.0f / fmaxf(sqrtf(xs), 1e-8f);
-    for (int b = 0; b < B; ++b) {
-        const float* q = Q + (int64_t)b * D;
-        float acc = 0.0f, qs = 0.0f;
-        for (int d = lane; d < D; d += 64) {
-            if (metric == 0) {
-                acc = fmaf(q[d], x[d] * xinv, acc);
-                qs = fmaf(q[d], q[d], qs);
-            } else {
-                const float df = x[d] - q[d];
-                acc = fmaf(df, df, acc);
-            }
-        }
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {
-            acc += __shfl_xor(acc, off, 64);
-            qs += __shfl_xor(qs, off, 64);
-        }
-        if (lane == 0) out[(int64_t)b * N + r] = metric == 0 ? acc / fmaxf(sqrtf(qs), 1e-8f) : sqrtf(acc);
-    }
-}
-
-hipError_t launch_similarity_matrix(const float* X, int64_t N, int D, const float* Q, int B, int metric, float* out,
-                                    hipStream_t st) {
-    if (N <= 0 || B <= 0) return hipSuccess;
-    hipLaunchKernelGGL(similarity_matrix_kernel, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, st, X, N, D, Q, B,
-                       metric, out);
-    return hipGetLastError();
-}
-
 }  // namespace vdb

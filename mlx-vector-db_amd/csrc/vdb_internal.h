@@ -161,8 +161,16 @@ struct GraphPruneArgs {
 };
 hipError_t launch_graph_prune(int metric, const GraphPruneArgs& a, hipStream_t st);
 
-// Operator slot: full score matrix out[B][N] (fp32 reference arithmetic).
+// Operator slot (vdb_ops.hip): full score matrix out[B][N] of row-major X [N][D], Q [B][D]:
+// metric 0 cosine / 2 dot product (fp32 MFMA GEMM), 1 euclidean (direct differences).
 hipError_t launch_similarity_matrix(const float* X, int64_t N, int D, const float* Q, int B, int metric,
                                     float* out, hipStream_t st);
+// x / max(|x|, 1e-8) per row
+hipError_t launch_normalize_rows(const float* in, int64_t n, int D, float* out, hipStream_t st);
+// top-k of each of `rows` score rows of length n (largest or smallest first, ties to the
+// lower index, NaN last); ws: topk_workspace_bytes(n, rows, k) bytes of device memory
+size_t topk_workspace_bytes(int64_t n, int rows, int k);
+hipError_t launch_topk_scores(const float* S, int rows, int64_t n, int k, int largest, int64_t* out_idx,
+                              float* out_val, void* ws, hipStream_t st);
 
 }  // namespace vdb

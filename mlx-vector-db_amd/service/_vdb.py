@@ -40,7 +40,7 @@ EXPORTED_SYMBOLS = (
     "vdb_index_create", "vdb_index_destroy", "vdb_index_reserve",
     "vdb_index_set_param", "vdb_index_get_stat",
     "vdb_index_add", "vdb_index_count", "vdb_index_clear", "vdb_index_get_vectors",
-    "vdb_index_search", "vdb_merge_topk", "vdb_similarity_matrix",
+    "vdb_index_search", "vdb_merge_topk", "vdb_similarity_matrix", "vdb_normalize_rows", "vdb_topk_scores",
     "vdb_graph_build", "vdb_graph_import", "vdb_graph_export", "vdb_graph_info", "vdb_graph_search",
     "vdb_graph_stat", "vdb_graph_set_param", "vdb_graph_destroy",
     "vdb_shards_create", "vdb_shards_destroy", "vdb_shards_add", "vdb_shards_count", "vdb_shards_shard_count",
@@ -100,6 +100,8 @@ def load_library():
             "vdb_index_search": (c_i32, [c_vp, c_vp, c_i32, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp, c_i64, c_vp]),
             "vdb_merge_topk": (c_i32, [c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp]),
             "vdb_similarity_matrix": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i32, c_i32, c_vp, c_vp]),
+            "vdb_normalize_rows": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp]),
+            "vdb_topk_scores": (c_i32, [c_vp, c_i32, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp]),
             "vdb_graph_build": (c_i32, [c_vp, c_i32, c_i32, c_i32, ctypes.POINTER(c_vp)]),
             "vdb_graph_import": (c_i32, [c_vp, c_i32, c_i64, c_vp, c_i32, c_vp, ctypes.POINTER(c_vp)]),
             "vdb_graph_export": (c_i32, [c_vp, c_vp, c_vp]),
@@ -448,9 +450,25 @@ def merge_topk_device(keys_ptr: int, idx_ptr: int, n_lists: int, n_queries: int,
                               ctypes.c_void_p(stream or None)))
 
 
+# the operator slot also serves the dot product (performance/mlx_optimized.py:150-156)
+OP_METRIC_IDS = dict(METRIC_IDS, dot_product=2)
+
+
 def similarity_matrix_device(corpus_ptr: int, n: int, dim: int, q_ptr: int, n_queries: int, metric: str,
                              out_ptr: int, stream: int = 0) -> None:
     lib = load_library()
     _check(lib.vdb_similarity_matrix(ctypes.c_void_p(corpus_ptr), int(n), int(dim), ctypes.c_void_p(q_ptr),
-                                     int(n_queries), METRIC_IDS[metric], ctypes.c_void_p(out_ptr),
+                                     int(n_queries), OP_METRIC_IDS[metric], ctypes.c_void_p(out_ptr),
                                      ctypes.c_void_p(stream or None)))
+
+
+def normalize_rows_device(in_ptr: int, n: int, dim: int, out_ptr: int, stream: int = 0) -> None:
+    _check(load_library().vdb_normalize_rows(ctypes.c_void_p(in_ptr), int(n), int(dim), ctypes.c_void_p(out_ptr),
+                                             ctypes.c_void_p(stream or None)))
+
+
+def topk_scores_device(scores_ptr: int, rows: int, n: int, k: int, largest: bool, out_idx_ptr: int,
+                       out_val_ptr: int = 0, stream: int = 0) -> None:
+    _check(load_library().vdb_topk_scores(ctypes.c_void_p(scores_ptr), int(rows), int(n), int(k), int(bool(largest)),
+                                          ctypes.c_void_p(out_idx_ptr), ctypes.c_void_p(out_val_ptr or None),
+                                          ctypes.c_void_p(stream or None)))
