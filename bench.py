@@ -327,7 +327,10 @@ def main():
                     help="candidate-pass step end: 1 lockstep barrier, 2 flag-gated rounds (tuning; default by D)")
     ap.add_argument("--pilot-tiles", type=int, default=None, help="row tiles sampled by the pilot bound (tuning)")
     ap.add_argument("--margin", type=int, default=None, help="candidates beyond k (tuning; default per precision)")
+    ap.add_argument("--pilot-rank", type=int, default=None, help="rank of the pilot bound (tuning; default: Poisson rule)")
     ap.add_argument("--rows", type=int, default=None, help="override the corpus rows (exploration only)")
+    ap.add_argument("--no-fallback", action="store_true",
+                    help="diagnostics only (kernel-variant timing): skip the exact fallback; results may be wrong")
     ap.add_argument("--graph-knn", type=int, default=None, help="c5: kNN candidates per row for the build")
     ap.add_argument("--teams", type=int, default=64, help="c5: workgroups per query (vdb_graph_set_param teams)")
     ap.add_argument("--teams-sweep", default="1,16,256", help="c5: extra teams settings reported beside the line")
@@ -371,6 +374,10 @@ def main():
         ix.set_param("pilot_tiles", args.pilot_tiles)
     if args.margin is not None:
         ix.set_param("margin", args.margin)
+    if args.pilot_rank is not None:
+        ix.set_param("pilot_rank", args.pilot_rank)
+    if args.no_fallback:
+        ix.set_param("no_fallback", 1)
     ix.reserve(n_local)
     host_parts = []
     for s in range(lo, hi, 8 * CHUNK_ROWS):

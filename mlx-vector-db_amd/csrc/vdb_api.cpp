@@ -100,6 +100,7 @@ struct vdb_index {
     double* nrm64 = nullptr;
     float* inv32 = nullptr;
     float* sq32 = nullptr;
+    float* rinit32 = nullptr;  // -|x|^2 / 2: the split pass's L2 accumulator start (vdb_scan2.hip)
     unsigned long long* d_xmax = nullptr;
     int* d_nonfinite = nullptr;
     double xmax = 0.0;
@@ -117,6 +118,8 @@ struct vdb_index {
     int64_t scan_variant = 0;     // fp32 candidate pass variant (vdb_scan.hip)
     int64_t scan_variant_b3 = 0;  // bf16x3 candidate pass variant
     int64_t scan_sync = 0;        // scan step end: 0 auto, 1 lockstep barrier, 2 flag-gated rounds
+    int64_t no_fallback = 0;      // diagnostics only: skip the exact fallback (results may be wrong)
+    int64_t pilot_rank_override = 0;  // tuning: rank of the pilot bound (0 = the Poisson rule)
     // stats
     std::atomic<int64_t> n_searches{0}, n_queries{0}, n_fallback{0}, n_overflow{0};
     std::atomic<int64_t> scan_ns{0}, pipe_ns{0}, n_timed{0};
@@ -153,13 +156,13 @@ int ensure_capacity(vdb_index* ix, int64_t rows) {
     float* X = nullptr;
     float* Xs = nullptr;
     double* n64 = nullptr;
-    float *i32 = nullptr, *s32 = nullptr;
+    float *i32 = nullptr, *s32 = nullptr, *r32 = nullptr;
     // All new buffers are allocated and filled before the index switches to them; on
     // any failure (typically out of memory while doubling at large N) they are freed
     // and the index keeps its current buffers, so a later retry sees the same HBM.
     auto fail = [&](hipError_t e, const char* what) {
         (void)hipStreamSynchronize(ix->stream);
-        for (void* p : {(void*)X, (void*)Xs, (void*)n64, (void*)i32, (void*)s32})
+        for (void* p : {(void*)X, (void*)Xs, (void*)n64, (void*)i32, (void*)s32, (void*)r32})
             if (p) (void)hipFree(p);
         return set_error(e == hipErrorOutOfMemory ? VDB_ERR_OOM : VDB_ERR_HIP,
                          "growing the index to %lld rows: %s failed: %s", (long long)cap, what, hipGetErrorString(e));
@@ -177,6 +180,8 @@ int ensure_capacity(vdb_index* ix, int64_t rows) {
     CAP_TRY(hipMalloc(&n64, cap * sizeof(double)));
     CAP_TRY(hipMalloc(&i32, cap * sizeof(float)));
     CAP_TRY(hipMalloc(&s32, cap * sizeof(float)));
+    CAP_TRY(hipMalloc(&r32, cap * sizeof(float)));
+    CAP_TRY(hipMemsetAsync(r32, 0, cap * sizeof(float), ix->stream));
     CAP_TRY(hipMemsetAsync(X, 0, x_bytes, ix->stream));
     CAP_TRY(hipMemsetAsync(n64, 0, cap * sizeof(double), ix->stream));
     CAP_TRY(hipMemsetAsync(i32, 0, cap * sizeof(float), ix->stream));
@@ -191,10 +196,12 @@ int ensure_capacity(vdb_index* ix, int64_t rows) {
             CAP_TRY(hipMemcpyAsync(Xs, ix->Xs, (size_t)used_tiles * tile_floats * sizeof(float),
                                    hipMemcpyDeviceToDevice, ix->stream));
         else if (split)
-            CAP_TRY(launch_split_rows(X, ix->G, 0, ix->count, Xs, ix->stream));
+            CAP_TRY(launch_split_rows(X, ix->G, 0, ix->count, ix->metric == VDB_METRIC_COSINE ? i32 : nullptr, Xs,
+                                      ix->stream));
         CAP_TRY(hipMemcpyAsync(n64, ix->nrm64, ix->count * sizeof(double), hipMemcpyDeviceToDevice, ix->stream));
         CAP_TRY(hipMemcpyAsync(i32, ix->inv32, ix->count * sizeof(float), hipMemcpyDeviceToDevice, ix->stream));
         CAP_TRY(hipMemcpyAsync(s32, ix->sq32, ix->count * sizeof(float), hipMemcpyDeviceToDevice, ix->stream));
+        CAP_TRY(hipMemcpyAsync(r32, ix->rinit32, ix->count * sizeof(float), hipMemcpyDeviceToDevice, ix->stream));
     }
     CAP_TRY(hipStreamSynchronize(ix->stream));
 #undef CAP_TRY
@@ -204,12 +211,14 @@ int ensure_capacity(vdb_index* ix, int64_t rows) {
         (void)hipFree(ix->nrm64);
         (void)hipFree(ix->inv32);
         (void)hipFree(ix->sq32);
+        (void)hipFree(ix->rinit32);
     }
     ix->X = X;
     ix->Xs = Xs;
     ix->nrm64 = n64;
     ix->inv32 = i32;
     ix->sq32 = s32;
+    ix->rinit32 = r32;
     ix->cap_rows = cap;
     return VDB_OK;
 }
@@ -416,6 +425,7 @@ int32_t vdb_index_destroy(vdb_index* ix) {
     if (ix->nrm64) (void)hipFree(ix->nrm64);
     if (ix->inv32) (void)hipFree(ix->inv32);
     if (ix->sq32) (void)hipFree(ix->sq32);
+    if (ix->rinit32) (void)hipFree(ix->rinit32);
     if (ix->d_xmax) (void)hipFree(ix->d_xmax);
     if (ix->d_totals) (void)hipFree(ix->d_totals);
     if (ix->stream) (void)hipStreamDestroy(ix->stream);
@@ -449,7 +459,8 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
             const size_t x_bytes = (size_t)(ix->cap_rows / 32) * ix->G * BLOCK_FLOATS * sizeof(float);
             HIP_TRY(hipMalloc(&ix->Xs, x_bytes));
             HIP_TRY(hipMemsetAsync(ix->Xs, 0, x_bytes, ix->stream));
-            HIP_TRY(launch_split_rows(ix->X, ix->G, 0, ix->count, ix->Xs, ix->stream));
+            HIP_TRY(launch_split_rows(ix->X, ix->G, 0, ix->count, ix->metric == VDB_METRIC_COSINE ? ix->inv32 : nullptr,
+                                      ix->Xs, ix->stream));
             HIP_TRY(hipStreamSynchronize(ix->stream));
         }
         ix->precision = value;
@@ -466,8 +477,7 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
         if (value < 0 || value > 2) return set_error(VDB_ERR_INVALID, "scan_variant must be 0, 1 or 2");
         ix->scan_variant = value;
     } else if (n == "scan_variant_bf16x3") {
-        if (value < 0 || (!scan_variant_ok(PREC_BF16X3, (int)value, 96) && !scan_variant_ok(PREC_BF16, (int)value, 96)))
-            return set_error(VDB_ERR_INVALID, "scan_variant_bf16x3 must be 0, 1 or 2");
+        if (value != 0) return set_error(VDB_ERR_INVALID, "the split-bf16 pass has one variant (0)");
         ix->scan_variant_b3 = value;
     } else if (n == "graph_fill") {
         if (value < 0 || value > 1) return set_error(VDB_ERR_INVALID, "graph_fill must be 0 or 1");
@@ -477,6 +487,11 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
         ix->pilot_tiles = value;
     } else if (n == "timing") {
         ix->timing = value != 0;
+    } else if (n == "no_fallback") {
+        ix->no_fallback = value != 0;
+    } else if (n == "pilot_rank") {
+        if (value < 0 || value > 256) return set_error(VDB_ERR_INVALID, "pilot_rank must be in [0, 256]");
+        ix->pilot_rank_override = value;
     } else {
         return set_error(VDB_ERR_INVALID, "unknown parameter '%s'", name);
     }
@@ -509,7 +524,7 @@ int32_t vdb_index_get_stat(const vdb_index* cix, const char* name, int64_t* valu
     else if (n == "count") *value = ix->count;
     else if (n == "precision") *value = ix->precision;
     else if (n == "device_bytes")
-        *value = (int64_t)(ix->cap_rows / 32) * ix->G * BLOCK_FLOATS * 4 * (ix->Xs ? 2 : 1) + ix->cap_rows * 16;
+        *value = (int64_t)(ix->cap_rows / 32) * ix->G * BLOCK_FLOATS * 4 * (ix->Xs ? 2 : 1) + ix->cap_rows * 20;
     else return set_error(VDB_ERR_INVALID, "unknown stat '%s'", name);
     return VDB_OK;
 }
@@ -535,9 +550,12 @@ int32_t vdb_index_add(vdb_index* ix, const float* vectors, int64_t n, int32_t me
         const float* src = vectors + r * D;
         if (mem == VDB_MEM_HOST) {
             hipError_t e = hipMemcpyAsync(staging, src, (size_t)m * D * sizeof(float), hipMemcpyHostToDevice, st);
-            if (e == hipSuccess) e = launch_pack_rows(staging, m, D, ix->G, ix->X, ix->count + r, ix->nrm64,
-                                                      ix->inv32, ix->sq32, ix->d_xmax, ix->d_nonfinite, st);
-            if (e == hipSuccess && ix->Xs) e = launch_split_rows(ix->X, ix->G, ix->count + r, m, ix->Xs, st);
+            if (e == hipSuccess)
+                e = launch_pack_rows(staging, m, D, ix->G, ix->X, ix->count + r, ix->nrm64, ix->inv32, ix->sq32,
+                                     ix->rinit32, ix->metric == VDB_METRIC_COSINE, ix->d_xmax, ix->d_nonfinite, st);
+            if (e == hipSuccess && ix->Xs)
+                e = launch_split_rows(ix->X, ix->G, ix->count + r, m, ix->metric == VDB_METRIC_COSINE ? ix->inv32 : nullptr,
+                                      ix->Xs, st);
             if (e == hipSuccess) e = hipStreamSynchronize(st);  // staging reuse
             if (e != hipSuccess) {
                 (void)hipFree(staging);
@@ -545,8 +563,10 @@ int32_t vdb_index_add(vdb_index* ix, const float* vectors, int64_t n, int32_t me
             }
         } else {
             HIP_TRY(launch_pack_rows(src, m, D, ix->G, ix->X, ix->count + r, ix->nrm64, ix->inv32, ix->sq32,
-                                     ix->d_xmax, ix->d_nonfinite, st));
-            if (ix->Xs) HIP_TRY(launch_split_rows(ix->X, ix->G, ix->count + r, m, ix->Xs, st));
+                                     ix->rinit32, ix->metric == VDB_METRIC_COSINE, ix->d_xmax, ix->d_nonfinite, st));
+            if (ix->Xs)
+                HIP_TRY(launch_split_rows(ix->X, ix->G, ix->count + r, m,
+                                          ix->metric == VDB_METRIC_COSINE ? ix->inv32 : nullptr, ix->Xs, st));
         }
     }
     if (staging) (void)hipFree(staging);
@@ -670,14 +690,15 @@ static int32_t search_impl(vdb_index* ix, const float* queries, int32_t B, int32
     const int n_qblocks = (B + QB - 1) / QB;
     const int prec = prec_req;
     const int Gs = prec == PREC_FP32 ? ix->G : ix->G / 2;  // scan groups (8 or 16 dims)
-    int variant = (int)(prec == PREC_FP32 ? ix->scan_variant : ix->scan_variant_b3);  // (bf16 knob: both split modes)
-    if (!scan_variant_ok(prec, variant, Gs)) variant = 0;  // e.g. PX=8 needs Dp % 128 == 0
-    const int64_t step_rows = scan_rows_per_step(prec, variant);
+    // fp32: vdb_scan.hip (variants); split-bf16 (bf16x3, bf16): vdb_scan2.hip
+    const bool split_pass = prec != PREC_FP32;
+    int variant = split_pass ? 0 : (int)ix->scan_variant;
+    if (!split_pass && !scan_variant_ok(prec, variant, Gs)) variant = 0;  // e.g. PX=8 needs Dp % 128 == 0
+    const int64_t step_rows = split_pass ? scan2_rows_per_step() : scan_rows_per_step(prec, variant);
     const int64_t n_steps = std::max<int64_t>(1, round_up(N, step_rows) / step_rows);
     // one 4-wave workgroup per CU (1 wave per SIMD, all of its 512 registers):
     // measured faster than two per CU, whose top-k epilogues then overlap (profiles/)
-    int target = ix->n_wg_override > 0 ? (int)ix->n_wg_override
-                                       : std::max(1, ix->n_cu * scan_wgs_per_cu(prec, variant, KP) / n_qblocks);
+    int target = ix->n_wg_override > 0 ? (int)ix->n_wg_override : std::max(1, ix->n_cu / n_qblocks);
     int spw = (int)std::max<int64_t>(1, (n_steps + target - 1) / target);
     int n_wg = (int)((n_steps + spw - 1) / spw);
     const int64_t mask_words = round_up(N, 32) / 32;
@@ -702,12 +723,34 @@ static int32_t search_impl(vdb_index* ix, const float* queries, int32_t B, int32
     bytes += (size_t)(B + 64) * 4 + 256;                    // flags
     bytes += (size_t)Bp * 4 + 256;                          // shared thresholds
     bytes += (size_t)Bp * (KP_MAX + PILOT_SLOTS) * 4 + 256;  // shared threshold slots + pilot slots
-    const bool priv = !exact_all && scan_priv(prec, variant, KP);
+    const bool priv = !exact_all && !split_pass && scan_priv(prec, variant, KP);
     // global per-query candidate lists: at most 512 entries per workgroup and query
     // (the largest LDS buffer of any variant; 4 x 64 for the wave-private one)
     const int64_t gl_cap = exact_all ? 0 : (int64_t)((n_wg + 7) / 8 * 8) * 512;
     bytes += (size_t)B * gl_cap * 8 + (size_t)Bp * 4 + 768;
     const int n_pilot = (int)std::min<int64_t>(ix->pilot_tiles, round_up(N, 32) / 32);
+    // Rank of the pilot's bound among its sampled scores.  The KP-th best sample is a
+    // guaranteed lower bound of the global KP-th best but sits at global rank ~KP N / S (C2:
+    // ~2000), so the candidate pass inserts every score above that until its own buffers
+    // tighten (the warm-up: 140 us of a 680 us C2 scan without a pilot, ~65 us with one).
+    // The r-th best sample with the smallest r such that the sample holds r of the global
+    // top k with probability < 1e-6 (Poisson(k S / N) tail; rows in no particular order)
+    // starts much tighter (C2: r = 6, rank ~370).  Exactness does not depend on it: rows
+    // dropped below the bound are covered by the certificate (acut >= T), which sends a
+    // query whose bound was too high to the exact path.
+    int pilot_rank = KP;
+    if (n_pilot > 0) {
+        const double x = (double)k * std::min<int64_t>((int64_t)n_pilot * 32, N) / (double)N;
+        double term = std::exp(-x), cdf = term;
+        int r = 1;
+        while (1.0 - cdf >= 1e-6 && r < KP) {
+            term *= x / r;
+            cdf += term;
+            ++r;
+        }
+        pilot_rank = std::min(r, KP);
+    }
+    if (ix->pilot_rank_override > 0) pilot_rank = (int)std::min<int64_t>(ix->pilot_rank_override, KP);
     int rc = ws_reserve(w, bytes, st);
     if (rc) return rc;
     Carver c{w->dev};
@@ -769,13 +812,21 @@ static int32_t search_impl(vdb_index* ix, const float* queries, int32_t B, int32
             }
             const float* rowscale = ix->metric == 0 ? ix->inv32 : ix->sq32;
             const float* Xscan = prec == PREC_FP32 ? ix->X : ix->Xs;
-            if (n_pilot > 0)
-                HIP_TRY(launch_pilot(prec, ix->metric, KP, Xscan, rowscale, md, Qt, Gs, N, B, n_qblocks, QB, n_pilot,
-                                     pslots, gthr, st));
+            if (n_pilot > 0) {
+                if (split_pass)
+                    HIP_TRY(launch_pilot2(prec, ix->metric, pilot_rank, Xscan, ix->rinit32, md, Qt, Gs, N, B,
+                                          n_qblocks, QB, n_pilot, pslots, gthr, st));
+                else
+                    HIP_TRY(launch_pilot(prec, ix->metric, pilot_rank, Xscan, rowscale, md, Qt, Gs, N, B,
+                                         n_qblocks, QB, n_pilot, pslots, gthr, st));
+            }
             // scan_ns times the scan kernel alone (the roofline's kernel); pipeline_ns
             // everything from the pilot to the rerank
             if (timed) HIP_TRY(hipEventRecord(tev[0], st));
-            if (priv)
+            if (split_pass)
+                HIP_TRY(launch_scan2(prec, ix->metric, KP, Xscan, ix->rinit32, md, Qt, Gs, N, B, n_qblocks, n_steps,
+                                     n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, lockstep, st));
+            else if (priv)
                 HIP_TRY(launch_scan_topk_priv(prec, ix->metric, KP, Xscan, rowscale, md, Qt, Gs, N, B, n_qblocks,
                                               n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, st));
             else
@@ -808,7 +859,8 @@ static int32_t search_impl(vdb_index* ix, const float* queries, int32_t B, int32
             // Device-memory searches do not wait for the certificate: the exact path is
             // launched gated on the device's flag count (nothing runs when no query was
             // flagged), so the call returns with the whole search queued.
-            if (mem == VDB_MEM_DEVICE && exact_bytes(ix, B, k, true) <= kGatedExactBytes) {
+            if (ix->no_fallback && mem == VDB_MEM_DEVICE) return VDB_OK;
+            if (!ix->no_fallback && mem == VDB_MEM_DEVICE && exact_bytes(ix, B, k, true) <= kGatedExactBytes) {
                 if (!ix->d_totals) {
                     HIP_TRY(hipMalloc(&ix->d_totals, 2 * sizeof(unsigned long long)));
                     HIP_TRY(hipMemsetAsync(ix->d_totals, 0, 2 * sizeof(unsigned long long), st));
@@ -826,7 +878,7 @@ static int32_t search_impl(vdb_index* ix, const float* queries, int32_t B, int32
                 const int frc = flush_timing(ix, w);
                 if (frc) return frc;
             }
-            if (n_flag > 0) {
+            if (n_flag > 0 && !ix->no_fallback) {
                 ix->n_fallback += n_flag;
                 rc = run_exact(ix, w, Qd, qn64, flags + 1, n_flag, k, md, out_s, out_i, out_k, index_offset, row_ids,
                                st);

@@ -9,12 +9,15 @@ namespace vdb {
 // Ingest
 // =============================================================================
 // One wave per row.  Canonical fp64 norm (vdb_common.h), tiled store of whole
-// 16-byte pieces (padding dims of the row are written as zeros).
+// 16-byte pieces (padding dims of the row are written as zeros), the fp32 row terms of
+// the candidate passes, and (second pass over the row, cache-hot) the bf16 rounding
+// residual of the row the split copy holds (cosine: x * inv32, the normalised row; L2: x),
+// which bounds the PREC_BF16 certificate.
 __global__ void __launch_bounds__(256) pack_rows_kernel(const float* __restrict__ src, int64_t n, int D, int G,
                                                         float* __restrict__ X, int64_t row0,
                                                         double* __restrict__ nrm64, float* __restrict__ inv32,
-                                                        float* __restrict__ sq32,
-                                                        unsigned long long* __restrict__ xmax_bits,
+                                                        float* __restrict__ sq32, float* __restrict__ rinit32,
+                                                        int normalise, unsigned long long* __restrict__ xmax_bits,
                                                         int* __restrict__ nonfinite) {
     const int lane = threadIdx.x & 63;
     const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -23,7 +26,7 @@ __global__ void __launch_bounds__(256) pack_rows_kernel(const float* __restrict_
     const int np = (D + 255) / 256;
     const float* s = src + row * (int64_t)D;
     const uint64_t r = (uint64_t)(row0 + row);
-    double acc = 0.0, res = 0.0;  // |x|^2 and |x - bf16(x)|^2 (the PREC_BF16 residual)
+    double acc = 0.0;
     int bad = 0;
     for (int m = 0; m < np; ++m) {
         const int p = m * 64 + lane;
@@ -35,29 +38,42 @@ __global__ void __launch_bounds__(256) pack_rows_kernel(const float* __restrict_
             bad |= !isfinite(v[j]);
             const double dv = (double)v[j];
             acc = acc + dv * dv;
-            const double rv = dv - (double)__uint_as_float(bf16_rne_bits(v[j]) << 16);
-            res = res + rv * rv;
         }
         if (4 * p < Dp) *(f32x4*)(X + tiled_piece_offset(r, p, G)) = v;
     }
     acc = wave_sum_butterfly(acc);
+    const double nr = sqrt(acc);
+    const float iv = (float)(1.0 / fmax(nr, 1e-8));
+    // the split copy's row and its bf16 residual |y - bf16(y)|
+    double res = 0.0, yy = 0.0;
+    for (int m = 0; m < np; ++m) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int d = 4 * (m * 64 + lane) + j;
+            const float x = d < D ? s[d] : 0.0f;
+            const float y = normalise ? x * iv : x;
+            const double rv = (double)y - (double)__uint_as_float(bf16_rne_bits(y) << 16);
+            res = res + rv * rv;
+            yy = yy + (double)y * (double)y;
+        }
+    }
     res = wave_sum_butterfly(res);
+    yy = wave_sum_butterfly(yy);
     const int anybad = __any(bad);
     if (lane == 0) {
-        const double nr = sqrt(acc);
         nrm64[r] = nr;
-        inv32[r] = (float)(1.0 / fmax(nr, 1e-8));
+        inv32[r] = iv;
         sq32[r] = (float)acc;
+        rinit32[r] = -0.5f * (float)acc;
         if (anybad) {
             atomicAdd(nonfinite, 1);
         } else {
-            // xmax_bits[0] max |x|; [1] max |x - bf16(x)| / max(|x|, 1e-8); [2] max |x - bf16(x)|
-            // (non-negative doubles order like their bit patterns)
-            // (a plain read first: the maxima are monotone, so a stale value only lets an
-            // atomic through; one atomic per row on three shared words serialised ingest)
+            // xmax_bits[0] max |x|; [1] max |y - bf16(y)| / max(|y|, 1e-8); [2] max |y - bf16(y)|
+            // (non-negative doubles order like their bit patterns; a plain read first: the
+            // maxima are monotone, so a stale value only lets an atomic through)
             const double dr = sqrt(res);
             const unsigned long long v[3] = {(unsigned long long)__double_as_longlong(nr),
-                                             (unsigned long long)__double_as_longlong(dr / fmax(nr, 1e-8)),
+                                             (unsigned long long)__double_as_longlong(dr / fmax(sqrt(yy), 1e-8)),
                                              (unsigned long long)__double_as_longlong(dr)};
 #pragma unroll
             for (int i = 0; i < 3; ++i)
@@ -67,29 +83,36 @@ __global__ void __launch_bounds__(256) pack_rows_kernel(const float* __restrict_
 }
 
 hipError_t launch_pack_rows(const float* src, int64_t n, int D, int G, float* X, int64_t row0, double* nrm64,
-                            float* inv32, float* sq32, unsigned long long* xmax_bits, int* nonfinite,
-                            hipStream_t st) {
+                            float* inv32, float* sq32, float* rinit32, int normalise, unsigned long long* xmax_bits,
+                            int* nonfinite, hipStream_t st) {
     if (n <= 0) return hipSuccess;
     const int64_t blocks = (n + 3) / 4;
     hipLaunchKernelGGL(pack_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, st, src, n, D, G, X, row0, nrm64,
-                       inv32, sq32, xmax_bits, nonfinite);
+                       inv32, sq32, rinit32, normalise, xmax_bits, nonfinite);
     return hipGetLastError();
 }
 
 // fp32 tiles -> split-bf16 tiles.  Thread (tile t, fp32 group g8, row-in-tile i):
 // the 8 dims 8 g8 .. 8 g8 + 7 of row 32 t + i (two 16-byte pieces, lanes i and
-// i + 32 of the fp32 block) -> lane i + 32 (g8 & 1) of the hi and lo blocks of
-// 16-dim group g8 >> 1.  32 consecutive threads read and write 512 B runs.
+// i + 32 of the fp32 block), times inv32[row] for cosine (the normalised row the
+// candidate pass scores), -> lane i + 32 (g8 & 1) of the hi and lo blocks of 16-dim
+// group g8 >> 1.  32 consecutive threads read and write 512 B runs.
 __global__ void __launch_bounds__(256) split_rows_kernel(const float* __restrict__ X, int G, int64_t t0,
-                                                         int64_t n_tiles, float* __restrict__ Xs) {
+                                                         int64_t n_tiles, const float* __restrict__ inv32,
+                                                         float* __restrict__ Xs) {
     const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (idx >= n_tiles * G * 32) return;
     const int i = (int)(idx & 31);
     const int g8 = (int)((idx >> 5) % G);
     const uint64_t t = (uint64_t)(t0 + (idx >> 5) / G);
     const float* src = X + tiled_block(t, g8, G);
-    const f32x4 a = *(const f32x4*)(src + i * 4);
-    const f32x4 b = *(const f32x4*)(src + (32 + i) * 4);
+    f32x4 a = *(const f32x4*)(src + i * 4);
+    f32x4 b = *(const f32x4*)(src + (32 + i) * 4);
+    if (inv32) {
+        const float iv = inv32[t * 32 + i];
+        a *= iv;
+        b *= iv;
+    }
     f32x4 hi, lo;
     split8(a, b, hi, lo);
     float* dst = Xs + split_block(t, g8 >> 1, G >> 1) + (size_t)(i + 32 * (g8 & 1)) * 4;
@@ -97,12 +120,13 @@ __global__ void __launch_bounds__(256) split_rows_kernel(const float* __restrict
     *(f32x4*)(dst + 4 * BLOCK_FLOATS) = lo;
 }
 
-hipError_t launch_split_rows(const float* X, int G, int64_t row0, int64_t n, float* Xs, hipStream_t st) {
+hipError_t launch_split_rows(const float* X, int G, int64_t row0, int64_t n, const float* inv32, float* Xs,
+                             hipStream_t st) {
     if (n <= 0) return hipSuccess;
     const int64_t t0 = row0 >> 5, t1 = (row0 + n + 31) >> 5;
     const int64_t total = (t1 - t0) * G * 32;
     hipLaunchKernelGGL(split_rows_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, X, G, t0, t1 - t0,
-                       Xs);
+                       inv32, Xs);
     return hipGetLastError();
 }
 

@@ -27,13 +27,18 @@ constexpr int PREC_BF16 = 2;
 // canonical fp64 norms, fp32 inverse norms and squared norms, running maxima (as
 // fp64 bits) xmax_bits[0] = |x|, [1] = |x - bf16(x)| / |x|, [2] = |x - bf16(x)|,
 // and a non-finite counter.
+// Also rinit32[row] = -|x|^2 / 2 (the split pass's L2 accumulator start, vdb_scan2.hip), and the
+// residuals use the row the split copy will hold: x * inv32 for cosine (normalise = 1), x for L2.
 hipError_t launch_pack_rows(const float* src, int64_t n, int D, int G, float* X, int64_t row0,
-                            double* nrm64, float* inv32, float* sq32,
+                            double* nrm64, float* inv32, float* sq32, float* rinit32, int normalise,
                             unsigned long long* xmax_bits, int* nonfinite, hipStream_t st);
 
-// fp32 tiles -> split-bf16 tiles (hi = bf16(x), lo = bf16(x - hi)) for the whole row tiles
-// covering rows [row0, row0 + n).  G = fp32 groups (Dp/8); the split copy has G/2 groups.
-hipError_t launch_split_rows(const float* X, int G, int64_t row0, int64_t n, float* Xs, hipStream_t st);
+// fp32 tiles -> split-bf16 tiles (hi = bf16(y), lo = bf16(y - hi)) for the whole row tiles
+// covering rows [row0, row0 + n), y = x * inv32[row] (cosine: the normalised row, as the
+// candidate pass scores it) or y = x (inv32 == nullptr, L2).  G = fp32 groups (Dp/8); the
+// split copy has G/2 groups.
+hipError_t launch_split_rows(const float* X, int G, int64_t row0, int64_t n, const float* inv32, float* Xs,
+                             hipStream_t st);
 
 // Tiled corpus rows -> row-major fp32 (export for persistence).
 hipError_t launch_unpack_rows(const float* X, int G, int D, int64_t row0, int64_t n, float* dst, hipStream_t st);
@@ -76,10 +81,26 @@ hipError_t launch_select_topk(const float* gl_s, const uint32_t* gl_i, const uin
 
 // Pilot bound: scan-identical scores of n_sample evenly spaced row tiles; tile i's
 // best score per query goes into pilot slot (i mod PILOT_SLOTS) (atomicMax), then
-// gthr[q] = max(gthr[q], KP-th largest slot).  pslots zeroed by prep_queries.
+// gthr[q] = max(gthr[q], KP-th largest slot) -- `KP` here is the bound's rank (vdb_api.cpp
+// pilot_rank).  pslots zeroed by prep_queries.
 hipError_t launch_pilot(int prec, int metric, int KP, const float* X, const float* rowscale, const uint32_t* mask,
                         const float* Qt, int G, int64_t N, int B, int n_qblocks, int QB, int n_sample,
                         uint32_t* pslots, uint32_t* gthr, hipStream_t st);
+
+hipError_t launch_pilot_bound(uint32_t* pslots, int B, int KP, uint32_t* gthr, hipStream_t st);
+
+// Split-bf16 candidate pass (vdb_scan2.hip; PREC_BF16X3 / PREC_BF16): Xs = the split copy
+// (cosine: of the NORMALISED rows), rinit = -|x|^2/2 per row (L2 accumulator start), Qs =
+// split query tiles (prep_queries), G = 16-dim groups.  Steps of scan2_rows_per_step() rows.
+int scan2_rows_per_step();
+int scan2_qb(int KP);
+hipError_t launch_scan2(int prec, int metric, int KP, const float* Xs, const float* rinit, const uint32_t* mask,
+                        const float* Qs, int G, int64_t N, int B, int n_qblocks, int64_t n_steps, int n_wg, int spw,
+                        float* gl_s, uint32_t* gl_i, uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr,
+                        uint32_t* gslots, int lockstep, hipStream_t st);
+hipError_t launch_pilot2(int prec, int metric, int KP, const float* Xs, const float* rinit, const uint32_t* mask,
+                         const float* Qs, int G, int64_t N, int B, int n_qblocks, int QB, int n_sample,
+                         uint32_t* pslots, uint32_t* gthr, hipStream_t st);
 
 // Merge sorted per-workgroup lists -> sorted top-KP per query (fp32 keys).
 hipError_t launch_merge_f32(int KP, const float* ls, const uint32_t* li, int n_lists, int B,
