@@ -323,7 +323,8 @@ size_t exact_bytes(vdb_index* ix, int nq, int k, bool gated) {
 // when no query was flagged.
 int run_exact(vdb_index* ix, Workspace* w, const float* Qd, const double* qn64, const int* qlist_dev, int nq, int k,
               const uint32_t* mask_dev, float* out_s, int64_t* out_i, double* out_k, int64_t index_offset,
-              const int64_t* row_ids, hipStream_t st, const int* qcount_dev = nullptr, const int* ovf_dev = nullptr) {
+              const int64_t* row_ids, hipStream_t st, const int* qcount_dev = nullptr, const int* ovf_dev = nullptr,
+              int* done_dev = nullptr) {
     const int KE = std::max(32, next_pow2(k));
     const int64_t N = ix->count;
     const bool gated = qcount_dev != nullptr;
@@ -341,6 +342,12 @@ int run_exact(vdb_index* ix, Workspace* w, const float* Qd, const double* qn64, 
     uint32_t* li = c.take<uint32_t>(list_elems);
     double* mk = c.take<double>((size_t)nq * KE);
     uint32_t* mi = c.take<uint32_t>((size_t)nq * KE);
+    if (gated && done_dev) {  // one launch: the last workgroup per query merges and writes (ExactTail)
+        const ExactTail tail{done_dev, mk, mi, k, index_offset, out_s, out_i, out_k, row_ids};
+        HIP_TRY(launch_exact_scan(ix->metric, KE, Qd, qn64, qlist_dev, nq, ix->X, ix->G, ix->dim, ix->nrm64, mask_dev,
+                                  N, n_wg, rpw, lk, li, st, qcount_dev, ovf_dev, ix->d_totals, &tail));
+        return VDB_OK;
+    }
     HIP_TRY(launch_exact_scan(ix->metric, KE, Qd, qn64, qlist_dev, nq, ix->X, ix->G, ix->dim, ix->nrm64, mask_dev, N,
                               n_wg, rpw, lk, li, st, qcount_dev, ovf_dev, gated ? ix->d_totals : nullptr));
     HIP_TRY(launch_merge_f64_u32(KE, lk, li, n_lists, KE, (int64_t)n_lists * KE, KE, nq, mk, mi, st, qcount_dev));
@@ -721,6 +728,7 @@ static int32_t search_impl(vdb_index* ix, const float* queries, int32_t B, int32
     bytes += (size_t)Bp * KP * 8 + 512;                     // merged approx lists
     bytes += (size_t)B * k * 20 + 768;                      // outputs (host mode)
     bytes += (size_t)(B + 64) * 4 + 256;                    // flags
+    bytes += (size_t)Bp * 4 + 256;                          // gated fallback: workgroups done per query
     bytes += (size_t)Bp * 4 + 256;                          // shared thresholds
     bytes += (size_t)Bp * (KP_MAX + PILOT_SLOTS) * 4 + 256;  // shared threshold slots + pilot slots
     const bool priv = !exact_all && !split_pass && scan_priv(prec, variant, KP);
@@ -762,6 +770,7 @@ static int32_t search_impl(vdb_index* ix, const float* queries, int32_t B, int32
     int64_t* oi = c.take<int64_t>((size_t)B * k);
     double* ok = c.take<double>((size_t)B * k);
     int* flags = c.take<int>(B + 64);
+    int* done = c.take<int>(Bp);
     uint32_t* gthr = c.take<uint32_t>(Bp);
     uint32_t* gslots = c.take<uint32_t>((size_t)Bp * (KP_MAX + PILOT_SLOTS));
     uint32_t* pslots = gslots + (size_t)Bp * KP_MAX;
@@ -793,7 +802,7 @@ static int32_t search_impl(vdb_index* ix, const float* queries, int32_t B, int32
         if (out_k) HIP_TRY(hipMemsetAsync(out_k, 0, (size_t)B * k * 8, st));
     } else {
         HIP_TRY(launch_prep_queries(Qd, B, Bp, D, ix->G, ix->metric, prec == PREC_FP32 ? Qt : nullptr,
-                                    prec == PREC_FP32 ? nullptr : Qt, qn64, flags, gthr, gslots, gl_cnt, st));
+                                    prec == PREC_FP32 ? nullptr : Qt, qn64, flags, gthr, gslots, gl_cnt, done, st));
         int n_flag = 0;
         if (!exact_all) {
             const bool timed = ix->timing != 0;
@@ -866,7 +875,7 @@ static int32_t search_impl(vdb_index* ix, const float* queries, int32_t B, int32
                     HIP_TRY(hipMemsetAsync(ix->d_totals, 0, 2 * sizeof(unsigned long long), st));
                 }
                 rc = run_exact(ix, w, Qd, qn64, flags + 1, B, k, md, out_s, out_i, out_k, index_offset, row_ids, st,
-                               flags, flags + B + 1);
+                               flags, flags + B + 1, done);
                 return rc;
             }
             HIP_TRY(hipMemcpyAsync(w->host_flag, flags, sizeof(int), hipMemcpyDeviceToHost, st));

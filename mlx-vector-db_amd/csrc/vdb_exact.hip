@@ -2,6 +2,7 @@
 // (pipeline overview: vdb_scan.hip).  Built with -ffp-contract=off.
 #include "vdb_common.h"
 #include "vdb_internal.h"
+#include "vdb_merge_block.h"
 
 namespace vdb {
 
@@ -524,7 +525,7 @@ exact_scan_kernel(const float* __restrict__ Q, const double* __restrict__ qn64, 
                   const float* __restrict__ X, int G, int D, const double* __restrict__ nrm64,
                   const uint32_t* __restrict__ mask, int64_t N, int64_t rows_per_wg, int KE,
                   double* __restrict__ lk, uint32_t* __restrict__ li, const int* __restrict__ qcount, int nq_max,
-                  const int* __restrict__ ovf, unsigned long long* __restrict__ totals) {
+                  const int* __restrict__ ovf, unsigned long long* __restrict__ totals, ExactTail tail) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int cap = WaveTopK<double, uint32_t>::capacity(KE);
     const int lane = threadIdx.x & 63;
@@ -575,23 +576,56 @@ exact_scan_kernel(const float* __restrict__ Q, const double* __restrict__ qn64, 
             }
         }
         __syncthreads();  // the LDS buffers are reused by the next query slot
+        if (tail.done) {
+            // the last workgroup of this query slot merges every workgroup's list (release:
+            // wave 0's list stores before the count; acquire: the other lists after it)
+            __shared__ int s_last;
+            if (threadIdx.x == 0) {
+                __threadfence();
+                s_last = atomicAdd(tail.done + qi, 1) == (int)gridDim.x - 1;
+            }
+            __syncthreads();
+            if (s_last) {
+                __threadfence();
+                const size_t q0 = (size_t)qi * gridDim.x * KE;
+                merge_block<double, uint32_t>(lk + q0, li + q0, (int)gridDim.x, KE, KE, KE, tail.mk + (size_t)qi * KE,
+                                              tail.mi + (size_t)qi * KE, smem);
+                __syncthreads();
+                for (int e = threadIdx.x; e < tail.k; e += 256) {
+                    const double key = tail.mk[(size_t)qi * KE + e];
+                    const uint32_t r = tail.mi[(size_t)qi * KE + e];
+                    const bool valid = r != 0xFFFFFFFFu;
+                    const size_t o = (size_t)b * tail.k + e;
+                    write_result(METRIC, key, valid ? global_row(tail.row_ids, (uint64_t)r, tail.index_offset) : 0,
+                                 valid && key != -INFINITY, tail.out_s + o, tail.out_i + o,
+                                 tail.out_k ? tail.out_k + o : nullptr);
+                }
+                __syncthreads();
+            }
+        }
     }
 }
 
 hipError_t launch_exact_scan(int metric, int KE, const float* Q, const double* qn64, const int* qlist, int nq,
                              const float* X, int G, int D, const double* nrm64, const uint32_t* mask, int64_t N,
                              int n_wg, int64_t rows_per_wg, double* lk, uint32_t* li, hipStream_t st,
-                             const int* qcount, const int* ovf, unsigned long long* totals) {
-    const size_t lds = (size_t)4 * WaveTopK<double, uint32_t>::capacity(KE) * (sizeof(double) + sizeof(uint32_t));
+                             const int* qcount, const int* ovf, unsigned long long* totals, const ExactTail* tail) {
+    size_t lds = (size_t)4 * WaveTopK<double, uint32_t>::capacity(KE) * (sizeof(double) + sizeof(uint32_t));
+    ExactTail tl{};
+    if (tail) {
+        if (!qcount || KE > 1024) return hipErrorInvalidValue;  // the fused tail is the gated form's
+        tl = *tail;
+        lds = std::max(lds, merge_block_lds<double, uint32_t>(KE));
+    }
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     // gated: a few query slots per row range, each looping over the flagged queries
     const dim3 grid(n_wg, qcount ? (nq < 4 ? nq : 4) : nq);
     if (metric == 0)
         hipLaunchKernelGGL((exact_scan_kernel<0>), grid, dim3(256), lds, st, Q, qn64, qlist, X, G, D, nrm64, mask, N,
-                           rows_per_wg, KE, lk, li, qcount, nq, ovf, totals);
+                           rows_per_wg, KE, lk, li, qcount, nq, ovf, totals, tl);
     else
         hipLaunchKernelGGL((exact_scan_kernel<1>), grid, dim3(256), lds, st, Q, qn64, qlist, X, G, D, nrm64, mask, N,
-                           rows_per_wg, KE, lk, li, qcount, nq, ovf, totals);
+                           rows_per_wg, KE, lk, li, qcount, nq, ovf, totals, tl);
     return hipGetLastError();
 }
 

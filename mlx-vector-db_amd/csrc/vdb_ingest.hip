@@ -154,7 +154,8 @@ __global__ void __launch_bounds__(256) prep_queries_kernel(const float* __restri
                                                            int metric, float* __restrict__ Qt, float* __restrict__ Qs,
                                                            double* __restrict__ qn64, int* __restrict__ flag_count,
                                                            uint32_t* __restrict__ gthr,
-                                                           uint32_t* __restrict__ gslots, uint32_t* __restrict__ gl_cnt) {
+                                                           uint32_t* __restrict__ gslots, uint32_t* __restrict__ gl_cnt,
+                                                           int* __restrict__ done) {
     const int lane = threadIdx.x & 63;
     const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (b == 0 && lane == 0 && flag_count) {
@@ -164,6 +165,7 @@ __global__ void __launch_bounds__(256) prep_queries_kernel(const float* __restri
     if (b >= Bp) return;
     if (lane == 0 && gthr) gthr[b] = 0u;
     if (lane == 0 && gl_cnt) gl_cnt[b] = 0u;
+    if (lane == 0 && done) done[b] = 0;
     if (gslots)  // [Bp][KP_MAX] publish slots, then [Bp][PILOT_SLOTS] pilot slots
         for (int j = lane; j < KP_MAX + PILOT_SLOTS; j += 64)
             gslots[j < KP_MAX ? (size_t)b * KP_MAX + j : (size_t)Bp * KP_MAX + (size_t)b * PILOT_SLOTS + j - KP_MAX] = 0u;
@@ -222,9 +224,9 @@ __global__ void __launch_bounds__(256) prep_queries_kernel(const float* __restri
 
 hipError_t launch_prep_queries(const float* Q, int B, int Bp, int D, int G, int metric, float* Qt, float* Qs,
                                double* qn64, int* flag_count, uint32_t* gthr, uint32_t* gslots, uint32_t* gl_cnt,
-                               hipStream_t st) {
+                               int* done, hipStream_t st) {
     hipLaunchKernelGGL(prep_queries_kernel, dim3((Bp + 3) / 4), dim3(256), 0, st, Q, B, Bp, D, G, metric, Qt, Qs,
-                       qn64, flag_count, gthr, gslots, gl_cnt);
+                       qn64, flag_count, gthr, gslots, gl_cnt, done);
     return hipGetLastError();
 }
 }  // namespace vdb

@@ -51,10 +51,11 @@ constexpr int PILOT_SLOTS = 256;  // pilot bound slots per query (pslots [Bp][PI
 // Queries: row-major [B][D] -> tiled Qt [Bp/32 tiles] with G + QG_EXTRA groups
 // (the first QG_EXTRA groups repeated at the end; cosine: pre-normalised in
 // fp32; zero padding written) and/or the split-bf16 tiles Qs (G/2 + QG_EXTRA
-// groups, same wrap), canonical fp64 norms [Bp]; resets *flag_count.
+// groups, same wrap), canonical fp64 norms [Bp]; resets *flag_count and done[Bp] (the
+// gated fallback's per-query counters, ExactTail).
 hipError_t launch_prep_queries(const float* Q, int B, int Bp, int D, int G, int metric,
                                float* Qt, float* Qs, double* qn64, int* flag_count, uint32_t* gthr,
-                               uint32_t* gslots, uint32_t* gl_cnt, hipStream_t st);
+                               uint32_t* gslots, uint32_t* gl_cnt, int* done, hipStream_t st);
 
 // Candidate pass: MFMA fp32 scores fused with a per-workgroup top-KP.
 // Output lists cand_[s|i][B][n_wg][KP], each sorted best first.
@@ -135,11 +136,19 @@ hipError_t launch_finish(int metric, int KP, const FinishArgs& a, int B, hipStre
 // Device-gated form (qcount != nullptr): the flagged queries qlist[0 .. *qcount) are
 // only known on the device; nq is then the most the lists have room for, and block
 // (0, 0) adds *qcount / *ovf to the cumulative totals[0] / totals[1].
+// With a tail (device-gated form only), the workgroup that finishes a query slot's lists
+// last (done[slot] counts them; zeroed by prep_queries) merges them into mk / mi [nq][KE]
+// and writes the query's results: one launch instead of scan + merge + finalize.
+struct ExactTail {
+    int* done; double* mk; uint32_t* mi; int k; int64_t index_offset;
+    float* out_s; int64_t* out_i; double* out_k; const int64_t* row_ids;
+};
 hipError_t launch_exact_scan(int metric, int KE, const float* Q, const double* qn64, const int* qlist, int nq,
                              const float* X, int G, int D, const double* nrm64, const uint32_t* mask,
                              int64_t N, int n_wg, int64_t rows_per_wg,
                              double* lk, uint32_t* li, hipStream_t st, const int* qcount = nullptr,
-                             const int* ovf = nullptr, unsigned long long* totals = nullptr);
+                             const int* ovf = nullptr, unsigned long long* totals = nullptr,
+                             const ExactTail* tail = nullptr);
 
 // Merge sorted fp64-key lists.  Element (q, j, e) lives at q*sq + j*sj + e, lists
 // have Lk entries; output [nq][KP] sorted.

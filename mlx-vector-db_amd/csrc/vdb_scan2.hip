@@ -423,30 +423,38 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
 // =============================================================================
 // Pilot bound with the same arithmetic (vdb_scan.hip launch_pilot for the fp32 pass)
 // =============================================================================
+// The pilot only has to produce a number: rows the candidate pass drops below the bound are
+// covered by the certificate whatever the bound is (vdb_api.cpp pilot_rank), so the pilot
+// splits a tile's dimension groups over four waves (a quarter of the dependent load chain
+// of a one-wave tile) and sums the partial accumulators through LDS.
+constexpr int PILOT_WAVES = 4;
+
 template <int PREC, int METRIC, int QT>
-__global__ void __launch_bounds__(64) pilot2_scores_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit,
-                                                           const uint32_t* __restrict__ mask,
-                                                           const float* __restrict__ Qs, int G, int64_t N, int B,
-                                                           int64_t n_tiles, int n_sample, uint32_t* __restrict__ pslots) {
+__global__ void __launch_bounds__(64 * PILOT_WAVES)
+pilot2_scores_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, const uint32_t* __restrict__ mask,
+                     const float* __restrict__ Qs, int G, int64_t N, int B, int64_t n_tiles, int n_sample,
+                     uint32_t* __restrict__ pslots) {
     constexpr int QB = 32 * QT;
     constexpr int XPL = Planes<PREC>::XPL;
     constexpr size_t GSTEP = 8 * BLOCK_FLOATS, PLANE = 4 * BLOCK_FLOATS;
-    const int lane = threadIdx.x;
+    __shared__ float s_part[PILOT_WAVES - 1][QT][16][64];
+    const int lane = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6;
     const int i = blockIdx.x;
     const int qb = blockIdx.y;
     const uint64_t t = (uint64_t)((int64_t)i * n_tiles / n_sample);
     const float* xs = Xs + s2_blk(t, 0, G) + lane * 4;
     const float* qs = Qs + s2_blk((uint64_t)(qb * QT), 0, G + QG_EXTRA) + lane * 4;
     f32x16 acc[1][QT];
-    const float r1 = (METRIC == 1 && lane < 32) ? rinit[t * 32 + lane] : 0.0f;
+    const float r1 = (METRIC == 1 && wv == 0 && lane < 32) ? rinit[t * 32 + lane] : 0.0f;
 #pragma unroll
     for (int qt = 0; qt < QT; ++qt) {
 #pragma unroll
         for (int v = 0; v < 16; ++v) acc[0][qt][v] = 0.0f;
         if (METRIC == 1) acc[0][qt] = __builtin_amdgcn_mfma_f32_32x32x2f32(r1, lane < 32 ? 1.0f : 0.0f, acc[0][qt], 0, 0, 0);
     }
-    // one wave, groups in the scan's order (bit-identical accumulators), PP groups in flight
-    constexpr int PP = 8;
+    // wave wv: groups wv, wv + 4, ...; PP of them in flight
+    constexpr int PP = 4;
     f32x4 xr[PP][1][XPL], qr[PP][QT][2];
     auto load = [&](int slot, int g) {
         if (g < G) {
@@ -460,16 +468,31 @@ __global__ void __launch_bounds__(64) pilot2_scores_kernel(const float* __restri
         }
     };
 #pragma unroll
-    for (int p = 0; p < PP; ++p) load(p, p);
-    for (int g0 = 0; g0 < G; g0 += PP) {
+    for (int p = 0; p < PP; ++p) load(p, wv + PILOT_WAVES * p);
+    for (int g0 = wv; g0 < G; g0 += PILOT_WAVES * PP) {
 #pragma unroll
         for (int p = 0; p < PP; ++p) {
-            if (g0 + p < G) {
+            const int g = g0 + PILOT_WAVES * p;
+            if (g < G) {
                 group_mfma<PREC, 1, QT>(xr[p], qr[p], acc);
-                load(p, g0 + p + PP);
+                load(p, g + PILOT_WAVES * PP);
             }
         }
     }
+    if (wv > 0) {
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+            for (int v = 0; v < 16; ++v) s_part[wv - 1][qt][v][lane] = acc[0][qt][v];
+    }
+    __syncthreads();
+    if (wv > 0) return;
+#pragma unroll
+    for (int w = 0; w < PILOT_WAVES - 1; ++w)
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+            for (int v = 0; v < 16; ++v) acc[0][qt][v] += s_part[w][qt][v][lane];
     const uint32_t valid = tile_valid16(mask, (int64_t)t, N, lane);
 #pragma unroll
     for (int qt = 0; qt < QT; ++qt) {
@@ -493,8 +516,8 @@ hipError_t launch_pilot2(int prec, int metric, int KP, const float* Xs, const fl
     bool launched = false;
 #define VDB_PILOT2(P, M, QTV)                                                                                     \
     if (!launched && prec == P && metric == M && QB == 32 * QTV) {                                                \
-        hipLaunchKernelGGL((pilot2_scores_kernel<P, M, QTV>), grid, dim3(64), 0, st, Xs, rinit, mask, Qs, G, N, B, \
-                           n_tiles, n_sample, pslots);                                                            \
+        hipLaunchKernelGGL((pilot2_scores_kernel<P, M, QTV>), grid, dim3(64 * PILOT_WAVES), 0, st, Xs, rinit, mask, \
+                           Qs, G, N, B, n_tiles, n_sample, pslots);                                               \
         launched = true;                                                                                          \
     }
     VDB_PILOT2(1, 0, 2) VDB_PILOT2(1, 1, 2) VDB_PILOT2(1, 0, 1) VDB_PILOT2(1, 1, 1)

@@ -1,0 +1,32 @@
+"""finish_kernel phase breakdown (diagnostic stamp build, lib/libvdb_amd_stamp.so).
+
+    python profiles/scripts/fin_stamp.py CONFIG PRECISION
+Prints per-query candidate-list length and the cycles of load / select / exact keys /
+ranks / certificate, averaged over the batch of the last search.
+"""
+import ctypes, os, sys
+import numpy as np
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), "..", ".."))
+os.environ["VDB_LIB"] = os.path.join(ROOT, "mlx-vector-db_amd", "lib", "libvdb_amd_stamp.so")
+sys.path.insert(0, os.path.join(ROOT, "mlx-vector-db_amd")); sys.path.insert(0, ROOT)
+import torch  # noqa
+from service import _vdb
+import bench
+cfg = sys.argv[1] if len(sys.argv) > 1 else "c2"
+prec = sys.argv[2] if len(sys.argv) > 2 else "bf16x3"
+N, D, B, k, metric, _ = bench.CONFIGS[cfg]
+ix = _vdb.NativeIndex(D, metric, precision=prec)
+ix.reserve(N)
+for s in range(0, N, 1 << 19):
+    ix.add(bench.corpus_rows(N, D, s, min(s + (1 << 19), N)))
+Q = np.random.default_rng(1).random((B, D), dtype=np.float32)
+for _ in range(3):
+    ix.search(Q, k)
+lib = _vdb.load_library()
+fb = (ctypes.c_ulonglong * (B * 8))()
+lib.vdb_debug_finish_stamps(fb, B)
+f = np.array(fb, dtype=np.uint64).reshape(B, 8).astype(np.float64)
+print(f"{cfg} {prec}: list length mean {f[:, 7].mean():.0f} p50 {np.median(f[:, 7]):.0f} max {f[:, 7].max():.0f}")
+for i, name in enumerate(["load", "select", "exact keys", "ranks+write", "certificate"]):
+    d = f[:, i + 1] - f[:, i]
+    print(f"  {name:12s} mean {d.mean():9.0f}  max {d.max():9.0f}  (s_memtime ticks)")
