@@ -319,7 +319,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
                     help="N>1: weak = global batch B*N (fixed work per GPU), strong = global batch B")
-    ap.add_argument("--precision", default="bf16x3", choices=["bf16x3", "bf16", "fp32"],
+    ap.add_argument("--precision", default="auto", choices=["auto", "bf16x3", "bf16", "fp32"],
                     help="candidate-pass arithmetic (results identical; DESIGN.md §3)")
     ap.add_argument("--scan-variant", type=int, default=None, help="candidate-pass kernel variant (tuning)")
     ap.add_argument("--n-wg", type=int, default=None, help="candidate-pass workgroups (tuning)")
@@ -409,6 +409,7 @@ def main():
     # (DESIGN.md §3), so the host runs ahead and no step waits for its launch.
     ix.set_param("timing", 1)
     scan0, pipe0, n0 = ix.stat("scan_ns"), ix.stat("pipeline_ns"), ix.stat("timed_searches")
+    by_prec0 = {p: ix.stat(f"searches_{p}") for p in ("fp32", "bf16x3", "bf16")}
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -420,6 +421,9 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t_start
     n_t = ix.stat("timed_searches") - n0
+    # candidate passes per arithmetic in the timed region (precision "auto" picks per search)
+    by_prec = {p: ix.stat(f"searches_{p}") - by_prec0[p] for p in by_prec0}
+    prec = args.precision if args.precision != "auto" else max(by_prec, key=by_prec.get)
     scan_ms = (ix.stat("scan_ns") - scan0) / 1e6 / max(n_t, 1)
     pipe_ms = (ix.stat("pipeline_ns") - pipe0) / 1e6 / max(n_t, 1)
     ix.set_param("timing", 0)
@@ -445,12 +449,12 @@ def main():
         # scale, the queries; flops = 2 B N D (x3 bf16 MFMA flops for the split product)
         # (bf16: the hi plane only, 2 B per element; 2 bf16 MFMA per product)
         Dp = (D + 63) // 64 * 64
-        elem = 2 if args.precision == "bf16" else 4
+        elem = 2 if prec == "bf16" else 4
         hbm_bytes = n_local * Dp * elem + n_local * 4 + Bg * Dp * 4
-        if args.precision == "fp32":
+        if prec == "fp32":
             mfma_flops, mfma_peak = 2.0 * Bg * n_local * D, FP32_MFMA_PEAK_TFLOPS
         else:
-            mfma_flops, mfma_peak = (3 if args.precision == "bf16x3" else 2) * 2.0 * Bg * n_local * D, BF16_MFMA_PEAK_TFLOPS
+            mfma_flops, mfma_peak = (3 if prec == "bf16x3" else 2) * 2.0 * Bg * n_local * D, BF16_MFMA_PEAK_TFLOPS
         t_hbm = hbm_bytes / (HBM_PEAK_GBS * 1e9)
         t_mfma = mfma_flops / (mfma_peak * 1e12)
         achieved_gbs = hbm_bytes / (scan_ms * 1e-3) / 1e9
@@ -470,7 +474,7 @@ def main():
             except (OSError, ValueError):
                 continue
             if (pm.get("config") == args.config and pm.get("n_gpus") == world and "hbm_bytes_per_launch" in pm
-                    and pm.get("precision", "fp32") == args.precision):
+                    and pm.get("precision", "fp32") == prec):
                 traffic = pm["hbm_bytes_per_launch"]
                 traffic_src = os.path.relpath(path, ROOT)
                 break
@@ -487,13 +491,14 @@ def main():
             "scaling": args.scaling if world > 1 else "weak",
             "vs_baseline": None,
             "dtype": {"fp32": "f32", "bf16x3": "f32 (bf16x3 split MFMA candidates, fp64 exact rerank)",
-                      "bf16": "f32 (bf16 corpus x split query MFMA candidates, fp64 exact rerank)"}[args.precision],
+                      "bf16": "f32 (bf16 corpus x split query MFMA candidates, fp64 exact rerank)"}[prec],
             "data": "synthetic uniform [0,1) fp32 (numpy PCG64, corpus seed 0 per 65536-row chunk, queries seed 1)",
             "config": {"workload": f"{args.config}: {desc}", "n_rows": N, "dim": D, "global_batch": Bg,
                        "batch_per_gpu_equiv": B, "k": k,
                        "metric": metric, "parallelism": f"row-shard x{world}" if world > 1 else "single GPU",
                        "rows_per_gpu": n_local},
-            "roofline": dict(roof, traffic=traffic, kernel="scan_topk", precision=args.precision,
+            "roofline": dict(roof, traffic=traffic, kernel="scan2_kernel" if prec != "fp32" else "scan_topk", precision=prec,
+                             precision_requested=args.precision, searches_by_precision=by_prec,
                              traffic_source=traffic_src, algorithmic_bytes=hbm_bytes, algorithmic_flops=mfma_flops,
                              avg_launch_ms=scan_ms, hbm_gbs=achieved_gbs, mfma_tflops=achieved_tf,
                              hbm_frac=achieved_gbs / HBM_PEAK_GBS, mfma_frac=achieved_tf / mfma_peak),

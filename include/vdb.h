@@ -67,13 +67,19 @@ enum { VDB_MEM_HOST = 0, VDB_MEM_DEVICE = 1 };
  *   VDB_PREC_BF16X3  split-bf16 "x3": x = hi + lo, q = hi + lo,
  *                    x.q ~ xh.qh + xh.ql + xl.qh on v_mfma_f32_32x32x16_bf16,
  *                    fp32 accumulate; error bound of the same order as fp32
- *                    (HBM-bound).  Default.  Keeps a split copy of the corpus
- *                    (same bytes as the fp32 copy).
+ *                    (HBM-bound).  Keeps a split copy of the corpus (same bytes
+ *                    as the fp32 copy).
  *   VDB_PREC_BF16    the hi plane of the split copy only: x.q ~ xh.qh + xh.ql,
  *                    half the corpus bytes per search; the certificate adds the
  *                    largest row residual |x - bf16(x)| (measured at ingest), so
- *                    it is wider and takes a larger candidate margin. */
-enum { VDB_PREC_FP32 = 0, VDB_PREC_BF16X3 = 1, VDB_PREC_BF16 = 2 };
+ *                    it is wider and takes a larger candidate margin.
+ *   VDB_PREC_AUTO    (default) BF16 while its certificate holds; after a search in
+ *                    which more than 1/64 of the queries fell back to the exact
+ *                    scan, the next 32 searches run BF16X3 (same split copy, so
+ *                    switching costs nothing); each retry that falls back again
+ *                    doubles that period (up to 4096).  Device-memory searches see their
+ *                    fallback counts one or more searches late (no host sync). */
+enum { VDB_PREC_FP32 = 0, VDB_PREC_BF16X3 = 1, VDB_PREC_BF16 = 2, VDB_PREC_AUTO = 3 };
 
 typedef struct vdb_index vdb_index;
 
@@ -100,7 +106,9 @@ int32_t vdb_index_reserve(vdb_index* idx, int64_t rows);
  * 2 flag-gated compaction rounds; results identical, speed differs),
  * "timing" (0/1: HIP events around the candidate pass; stats "scan_ns",
  * "pipeline_ns", "timed_searches").  Stats also: "searches", "queries",
- * "fallback_queries", "overflow_queries", "capacity", "count", "device_bytes", "precision". */
+ * "fallback_queries", "overflow_queries", "capacity", "count", "device_bytes", "precision",
+ * "searches_fp32" / "searches_bf16x3" / "searches_bf16" (candidate passes run in each; with
+ * VDB_PREC_AUTO these show its choices). */
 int32_t vdb_index_set_param(vdb_index* idx, const char* name, int64_t value);
 int32_t vdb_index_get_stat(const vdb_index* idx, const char* name, int64_t* value);
 

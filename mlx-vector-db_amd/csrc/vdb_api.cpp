@@ -48,6 +48,8 @@ int set_error(int code, const char* fmt, ...) {
     } while (0)
 
 constexpr int64_t kRowAlign = ROW_ALIGN;   // capacity granule, a multiple of every scan step
+constexpr int kAutoB3Searches = 32;  // VDB_PREC_AUTO: BF16X3 searches after a BF16 search with fallbacks
+constexpr int kAutoB3Max = 4096;
 constexpr size_t kGatedExactBytes = 256u << 20;  // device-gated fallback lists sized for every query of a batch
 constexpr int kMaxApproxK = 200;          // k above this uses the exact path
 
@@ -108,7 +110,14 @@ struct vdb_index {
     hipStream_t stream = nullptr;
     int n_cu = 256;
     // knobs
-    int64_t precision = VDB_PREC_BF16X3;
+    int64_t precision = VDB_PREC_AUTO;
+    // VDB_PREC_AUTO: searches left in BF16X3 after a BF16 search with many fallbacks, and the
+    // device-gated fallback total last seen (pinned mirror of d_totals[0], copied after each
+    // device-memory search and read by the next one)
+    std::atomic<int> auto_b3_left{0};
+    std::atomic<int> auto_period{kAutoB3Searches};  // doubles on every BF16 retry that falls back again
+    std::atomic<unsigned long long> auto_seen{0};
+    unsigned long long* h_totals = nullptr;
     int64_t margin = -1;  // -1 = default
     int64_t force_exact = 0;
     int64_t n_wg_override = 0;
@@ -122,6 +131,7 @@ struct vdb_index {
     int64_t pilot_rank_override = 0;  // tuning: rank of the pilot bound (0 = the Poisson rule)
     // stats
     std::atomic<int64_t> n_searches{0}, n_queries{0}, n_fallback{0}, n_overflow{0};
+    std::atomic<int64_t> n_by_prec[3] = {{0}, {0}, {0}};  // candidate passes per PREC_* (VDB_PREC_AUTO's choices)
     std::atomic<int64_t> scan_ns{0}, pipe_ns{0}, n_timed{0};
     unsigned long long* d_totals = nullptr;  // device: flagged / overflowed queries of device-gated searches
     std::shared_mutex mu;  // add/clear/reserve exclusive; search shared
@@ -309,6 +319,15 @@ bool all_finite(const float* p, int64_t n) {
     return true;
 }
 
+// VDB_PREC_AUTO after a BF16 search with many fallbacks: the next `period` searches run
+// BF16X3, and the period doubles (up to kAutoB3Max) so data BF16 cannot certify pays for
+// a failed retry ever more rarely.
+void auto_backoff(vdb_index* ix) {
+    const int p = ix->auto_period.load();
+    ix->auto_b3_left = p;
+    ix->auto_period = std::min(2 * p, kAutoB3Max);
+}
+
 // Exact full scan for queries qlist[0..nq) (device list) -> writes outputs.
 // Bytes of the exact path's lists for nq queries (device-gated form: one list per CU).
 size_t exact_bytes(vdb_index* ix, int nq, int k, bool gated) {
@@ -435,6 +454,7 @@ int32_t vdb_index_destroy(vdb_index* ix) {
     if (ix->rinit32) (void)hipFree(ix->rinit32);
     if (ix->d_xmax) (void)hipFree(ix->d_xmax);
     if (ix->d_totals) (void)hipFree(ix->d_totals);
+    if (ix->h_totals) (void)hipHostFree(ix->h_totals);
     if (ix->stream) (void)hipStreamDestroy(ix->stream);
     delete ix;
     return VDB_OK;
@@ -452,9 +472,10 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
     if (!ix || !name) return set_error(VDB_ERR_INVALID, "NULL argument");
     std::string n(name);
     if (n == "precision") {
-        if (value != VDB_PREC_FP32 && value != VDB_PREC_BF16X3 && value != VDB_PREC_BF16)
-            return set_error(VDB_ERR_INVALID, "precision must be %d (fp32), %d (bf16x3) or %d (bf16), got %lld",
-                             VDB_PREC_FP32, VDB_PREC_BF16X3, VDB_PREC_BF16, (long long)value);
+        if (value != VDB_PREC_FP32 && value != VDB_PREC_BF16X3 && value != VDB_PREC_BF16 && value != VDB_PREC_AUTO)
+            return set_error(VDB_ERR_INVALID,
+                             "precision must be %d (fp32), %d (bf16x3), %d (bf16) or %d (auto), got %lld",
+                             VDB_PREC_FP32, VDB_PREC_BF16X3, VDB_PREC_BF16, VDB_PREC_AUTO, (long long)value);
         HIP_TRY(hipSetDevice(ix->device));
         std::unique_lock<std::shared_mutex> g(ix->mu);
         if (value == ix->precision) return VDB_OK;
@@ -530,6 +551,9 @@ int32_t vdb_index_get_stat(const vdb_index* cix, const char* name, int64_t* valu
     else if (n == "timed_searches") *value = ix->n_timed.load();
     else if (n == "count") *value = ix->count;
     else if (n == "precision") *value = ix->precision;
+    else if (n == "searches_fp32") *value = ix->n_by_prec[PREC_FP32].load();
+    else if (n == "searches_bf16x3") *value = ix->n_by_prec[PREC_BF16X3].load();
+    else if (n == "searches_bf16") *value = ix->n_by_prec[PREC_BF16].load();
     else if (n == "device_bytes")
         *value = (int64_t)(ix->cap_rows / 32) * ix->G * BLOCK_FLOATS * 4 * (ix->Xs ? 2 : 1) + ix->cap_rows * 20;
     else return set_error(VDB_ERR_INVALID, "unknown stat '%s'", name);
@@ -679,9 +703,22 @@ static int32_t search_impl(vdb_index* ix, const float* queries, int32_t B, int32
     // candidates beyond k: the certificate needs a gap of 2 eps between the k-th and the
     // KP-th approximate score; bf16x3's bound grows with D (3D additions), so large D
     // gets a wider margin (1M x 1536 uniform: KP = 32 left ~1.5% of queries uncertified)
+    const bool auto_prec = ix->precision == VDB_PREC_AUTO;
+    if (auto_prec && ix->h_totals) {  // fallbacks of earlier device-memory searches (lagged)
+        const unsigned long long seen = ix->h_totals[0];
+        const unsigned long long prev = ix->auto_seen.exchange(seen);
+        if (seen > prev && (seen - prev) * 64 > (unsigned long long)B) auto_backoff(ix);
+    }
     const int prec_req = !ix->Xs ? PREC_FP32
                          : ix->precision == VDB_PREC_BF16X3 ? PREC_BF16X3
-                         : ix->precision == VDB_PREC_BF16 ? PREC_BF16 : PREC_FP32;
+                         : ix->precision == VDB_PREC_BF16 ? PREC_BF16
+                         : auto_prec ? (ix->auto_b3_left.load() > 0 ? PREC_BF16X3 : PREC_BF16) : PREC_FP32;
+    if (N > 0 && !(ix->force_exact || k > kMaxApproxK)) ix->n_by_prec[prec_req]++;
+    if (auto_prec && prec_req == PREC_BF16X3) {
+        int left = ix->auto_b3_left.load();
+        while (left > 0 && !ix->auto_b3_left.compare_exchange_weak(left, left - 1)) {
+        }
+    }
     int margin_def = std::max(16, k / 4);
     if (prec_req == PREC_BF16X3 && D >= 1024) margin_def = std::max(margin_def, 48);
     // bf16 (hi plane only): eps ~ the rows' bf16 residual (~1.5e-3 relative on uniform data),
@@ -870,12 +907,23 @@ static int32_t search_impl(vdb_index* ix, const float* queries, int32_t B, int32
             // flagged), so the call returns with the whole search queued.
             if (ix->no_fallback && mem == VDB_MEM_DEVICE) return VDB_OK;
             if (!ix->no_fallback && mem == VDB_MEM_DEVICE && exact_bytes(ix, B, k, true) <= kGatedExactBytes) {
-                if (!ix->d_totals) {
-                    HIP_TRY(hipMalloc(&ix->d_totals, 2 * sizeof(unsigned long long)));
-                    HIP_TRY(hipMemsetAsync(ix->d_totals, 0, 2 * sizeof(unsigned long long), st));
+                {
+                    std::lock_guard<std::mutex> lg(ix->ws_mu);  // lazily, once (concurrent searches)
+                    if (!ix->d_totals) {
+                        HIP_TRY(hipHostMalloc(&ix->h_totals, 2 * sizeof(unsigned long long), hipHostMallocDefault));
+                        ix->h_totals[0] = ix->h_totals[1] = 0;
+                        unsigned long long* d = nullptr;
+                        HIP_TRY(hipMalloc(&d, 2 * sizeof(unsigned long long)));
+                        HIP_TRY(hipMemset(d, 0, 2 * sizeof(unsigned long long)));
+                        ix->d_totals = d;
+                    }
                 }
                 rc = run_exact(ix, w, Qd, qn64, flags + 1, B, k, md, out_s, out_i, out_k, index_offset, row_ids, st,
                                flags, flags + B + 1, done);
+                if (rc == VDB_OK && auto_prec) {
+                    HIP_TRY(hipMemcpyAsync(ix->h_totals, ix->d_totals, 2 * sizeof(unsigned long long),
+                                           hipMemcpyDeviceToHost, st));
+                }
                 return rc;
             }
             HIP_TRY(hipMemcpyAsync(w->host_flag, flags, sizeof(int), hipMemcpyDeviceToHost, st));
@@ -883,6 +931,10 @@ static int32_t search_impl(vdb_index* ix, const float* queries, int32_t B, int32
             HIP_TRY(hipStreamSynchronize(st));
             n_flag = w->host_flag[0];
             ix->n_overflow += w->host_flag[1];
+            if (auto_prec && prec == PREC_BF16) {
+                if (n_flag * 64 > B) auto_backoff(ix);
+                else ix->auto_period = kAutoB3Searches;  // certified: retries start short again
+            }
             if (timed) {
                 const int frc = flush_timing(ix, w);
                 if (frc) return frc;

@@ -31,7 +31,7 @@ def _mask_words(mask_bool):
     return np.packbits(bits, bitorder="little").view("<u4").astype(np.uint32)
 
 
-PRECISIONS = ["bf16x3", "bf16", "fp32"]
+PRECISIONS = ["bf16x3", "bf16", "fp32", "auto"]
 
 
 def _check(vdb, V, Q, k, metric, mask=None, force_exact=False, margin=None, chunked_add=False, precision="bf16x3",
@@ -136,6 +136,44 @@ def test_precision_switch_keeps_results(vdb):
         np.testing.assert_array_equal(i, ei)
         np.testing.assert_array_equal(kk, ek)
     assert ix.stat("fallback_queries") == 0
+
+
+@pytest.mark.parametrize("mem", ["host", "device"])
+def test_auto_precision_switches_on_fallbacks(vdb, mem):
+    """VDB_PREC_AUTO runs the bf16 pass while it certifies; rows closer together than the
+    bf16 residual bound make most queries fall back, after which the next searches run
+    bf16x3 (device-memory searches: once the earlier search's counts have landed)."""
+    import torch
+    rng = np.random.default_rng(31)
+    D, N, B, k = 256, 8000, 32, 10
+    far = rng.random((N, D), dtype=np.float32)
+    base = rng.random(D, dtype=np.float32)
+    near = (base + 1e-4 * rng.standard_normal((N, D))).astype(np.float32)
+    for V, expect_switch in ((far, False), (near, True)):
+        Q = (V[rng.integers(0, N, B)] + 1e-5 * rng.standard_normal((B, D))).astype(np.float32)
+        ix = vdb.NativeIndex(D, "cosine")
+        assert ix.precision == "auto"
+        ix.add(V)
+        es, ei, ek = ref_cpu.exact_search(Q, V, k, "cosine")
+        for _ in range(2):
+            if mem == "host":
+                s, i, kk = ix.search(Q, k, with_keys=True)
+            else:
+                qd = torch.from_numpy(Q).cuda()
+                sd = torch.empty((B, k), dtype=torch.float32, device="cuda")
+                idd = torch.empty((B, k), dtype=torch.int64, device="cuda")
+                kd = torch.empty((B, k), dtype=torch.float64, device="cuda")
+                ix.search_device(qd.data_ptr(), B, k, sd.data_ptr(), idd.data_ptr(), kd.data_ptr(), stream=0)
+                torch.cuda.synchronize()
+                i, kk = idd.cpu().numpy(), kd.cpu().numpy()
+            np.testing.assert_array_equal(i, ei)
+            np.testing.assert_array_equal(kk, ek)
+        assert ix.stat("searches_bf16") >= 1
+        if expect_switch:
+            assert ix.stat("fallback_queries") * 64 > B
+            assert ix.stat("searches_bf16x3") == 1
+        else:
+            assert ix.stat("searches_bf16x3") == 0 and ix.stat("fallback_queries") == 0
 
 
 def test_duplicates_force_certificate_fallback(vdb):
@@ -277,7 +315,7 @@ def test_device_search_gated_fallback(vdb, metric):
     V[2000:2060] = V[11]
     V[9000:9040] = V[29]
     Q = np.concatenate([V[[11, 29]], rng.random((14, 96), dtype=np.float32)])
-    ix = vdb.NativeIndex(96, metric)
+    ix = vdb.NativeIndex(96, metric, precision="bf16x3")  # KP = 32 < the 60 copies
     ix.add(V)
     es, ei, ek = ref_cpu.exact_search(Q, V, 12, metric)
     qd = torch.from_numpy(Q).cuda()
