@@ -97,8 +97,9 @@ struct vdb_index {
     int Dp = 0, G = 0;
     int64_t count = 0;
     int64_t cap_rows = 0;  // multiple of kRowAlign
-    float* X = nullptr;      // fp32 tiles (rerank, exact scan, export, fp32 candidate pass)
-    float* Xs = nullptr;     // split-bf16 tiles (bf16x3 candidate pass), same bytes as X
+    float* X = nullptr;   // row-major fp32 [cap_rows][Dp] (rerank, exact scan, export, graph)
+    float* Xs = nullptr;  // the candidate pass's copy, same bytes: split-bf16 tiles (PREC_BF16X3 / BF16 /
+                          // AUTO) or fp32 tiles (PREC_FP32), rebuilt from X when the precision class changes
     double* nrm64 = nullptr;
     float* inv32 = nullptr;
     float* sq32 = nullptr;
@@ -155,6 +156,13 @@ void free_workspace_memory(Workspace* w) {
     w->dev_bytes = w->exact_bytes = 0;
 }
 
+// The candidate copy of rows [row0, row0 + n) from the row-major rows (whole row tiles).
+hipError_t build_candidate_rows(const vdb_index* ix, const float* X, const float* inv32, int64_t row0, int64_t n,
+                                float* Xs, hipStream_t st) {
+    if (ix->precision == VDB_PREC_FP32) return launch_tile_rows(X, ix->G, row0, n, Xs, st);
+    return launch_split_rows(X, ix->G, row0, n, ix->metric == VDB_METRIC_COSINE ? inv32 : nullptr, Xs, st);
+}
+
 int ensure_capacity(vdb_index* ix, int64_t rows) {
     if (rows <= ix->cap_rows) return VDB_OK;
     int64_t cap = std::max<int64_t>(ix->cap_rows * 2, kRowAlign);
@@ -162,7 +170,6 @@ int ensure_capacity(vdb_index* ix, int64_t rows) {
     cap = round_up(cap, kRowAlign);
     const size_t tile_floats = (size_t)ix->G * BLOCK_FLOATS;
     const size_t x_bytes = (size_t)(cap / 32) * tile_floats * sizeof(float);
-    const bool split = ix->precision != VDB_PREC_FP32;
     float* X = nullptr;
     float* Xs = nullptr;
     double* n64 = nullptr;
@@ -183,10 +190,8 @@ int ensure_capacity(vdb_index* ix, int64_t rows) {
         if (_e != hipSuccess) return fail(_e, #expr); \
     } while (0)
     CAP_TRY(hipMalloc(&X, x_bytes));
-    if (split) {
-        CAP_TRY(hipMalloc(&Xs, x_bytes));
-        CAP_TRY(hipMemsetAsync(Xs, 0, x_bytes, ix->stream));
-    }
+    CAP_TRY(hipMalloc(&Xs, x_bytes));
+    CAP_TRY(hipMemsetAsync(Xs, 0, x_bytes, ix->stream));
     CAP_TRY(hipMalloc(&n64, cap * sizeof(double)));
     CAP_TRY(hipMalloc(&i32, cap * sizeof(float)));
     CAP_TRY(hipMalloc(&s32, cap * sizeof(float)));
@@ -200,14 +205,10 @@ int ensure_capacity(vdb_index* ix, int64_t rows) {
         // all searches that might read the old buffers must be finished
         CAP_TRY(hipDeviceSynchronize());
         const int64_t used_tiles = round_up(ix->count, 128) / 32;  // whole super tiles (prefix of the layout)
-        CAP_TRY(hipMemcpyAsync(X, ix->X, (size_t)used_tiles * tile_floats * sizeof(float), hipMemcpyDeviceToDevice,
+        CAP_TRY(hipMemcpyAsync(X, ix->X, (size_t)ix->count * ix->Dp * sizeof(float), hipMemcpyDeviceToDevice,
                                ix->stream));
-        if (split && ix->Xs)
-            CAP_TRY(hipMemcpyAsync(Xs, ix->Xs, (size_t)used_tiles * tile_floats * sizeof(float),
-                                   hipMemcpyDeviceToDevice, ix->stream));
-        else if (split)
-            CAP_TRY(launch_split_rows(X, ix->G, 0, ix->count, ix->metric == VDB_METRIC_COSINE ? i32 : nullptr, Xs,
-                                      ix->stream));
+        CAP_TRY(hipMemcpyAsync(Xs, ix->Xs, (size_t)used_tiles * tile_floats * sizeof(float), hipMemcpyDeviceToDevice,
+                               ix->stream));
         CAP_TRY(hipMemcpyAsync(n64, ix->nrm64, ix->count * sizeof(double), hipMemcpyDeviceToDevice, ix->stream));
         CAP_TRY(hipMemcpyAsync(i32, ix->inv32, ix->count * sizeof(float), hipMemcpyDeviceToDevice, ix->stream));
         CAP_TRY(hipMemcpyAsync(s32, ix->sq32, ix->count * sizeof(float), hipMemcpyDeviceToDevice, ix->stream));
@@ -480,18 +481,12 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
         std::unique_lock<std::shared_mutex> g(ix->mu);
         if (value == ix->precision) return VDB_OK;
         HIP_TRY(hipDeviceSynchronize());
-        if (value == VDB_PREC_FP32) {
-            if (ix->Xs) (void)hipFree(ix->Xs);  // the split copy is only read by the bf16 passes
-            ix->Xs = nullptr;
-        } else if (ix->cap_rows > 0 && !ix->Xs) {
-            const size_t x_bytes = (size_t)(ix->cap_rows / 32) * ix->G * BLOCK_FLOATS * sizeof(float);
-            HIP_TRY(hipMalloc(&ix->Xs, x_bytes));
-            HIP_TRY(hipMemsetAsync(ix->Xs, 0, x_bytes, ix->stream));
-            HIP_TRY(launch_split_rows(ix->X, ix->G, 0, ix->count, ix->metric == VDB_METRIC_COSINE ? ix->inv32 : nullptr,
-                                      ix->Xs, ix->stream));
+        const bool rebuild = (value == VDB_PREC_FP32) != (ix->precision == VDB_PREC_FP32);
+        ix->precision = value;
+        if (rebuild && ix->Xs && ix->count > 0) {  // fp32 tiles <-> split tiles
+            HIP_TRY(build_candidate_rows(ix, ix->X, ix->inv32, 0, ix->count, ix->Xs, ix->stream));
             HIP_TRY(hipStreamSynchronize(ix->stream));
         }
-        ix->precision = value;
     } else if (n == "margin") {
         ix->margin = value;
     } else if (n == "force_exact") {
@@ -555,7 +550,7 @@ int32_t vdb_index_get_stat(const vdb_index* cix, const char* name, int64_t* valu
     else if (n == "searches_bf16x3") *value = ix->n_by_prec[PREC_BF16X3].load();
     else if (n == "searches_bf16") *value = ix->n_by_prec[PREC_BF16].load();
     else if (n == "device_bytes")
-        *value = (int64_t)(ix->cap_rows / 32) * ix->G * BLOCK_FLOATS * 4 * (ix->Xs ? 2 : 1) + ix->cap_rows * 20;
+        *value = (int64_t)(ix->cap_rows / 32) * ix->G * BLOCK_FLOATS * 4 * 2 + ix->cap_rows * 20;
     else return set_error(VDB_ERR_INVALID, "unknown stat '%s'", name);
     return VDB_OK;
 }
@@ -584,9 +579,7 @@ int32_t vdb_index_add(vdb_index* ix, const float* vectors, int64_t n, int32_t me
             if (e == hipSuccess)
                 e = launch_pack_rows(staging, m, D, ix->G, ix->X, ix->count + r, ix->nrm64, ix->inv32, ix->sq32,
                                      ix->rinit32, ix->metric == VDB_METRIC_COSINE, ix->d_xmax, ix->d_nonfinite, st);
-            if (e == hipSuccess && ix->Xs)
-                e = launch_split_rows(ix->X, ix->G, ix->count + r, m, ix->metric == VDB_METRIC_COSINE ? ix->inv32 : nullptr,
-                                      ix->Xs, st);
+            if (e == hipSuccess) e = build_candidate_rows(ix, ix->X, ix->inv32, ix->count + r, m, ix->Xs, st);
             if (e == hipSuccess) e = hipStreamSynchronize(st);  // staging reuse
             if (e != hipSuccess) {
                 (void)hipFree(staging);
@@ -595,9 +588,7 @@ int32_t vdb_index_add(vdb_index* ix, const float* vectors, int64_t n, int32_t me
         } else {
             HIP_TRY(launch_pack_rows(src, m, D, ix->G, ix->X, ix->count + r, ix->nrm64, ix->inv32, ix->sq32,
                                      ix->rinit32, ix->metric == VDB_METRIC_COSINE, ix->d_xmax, ix->d_nonfinite, st));
-            if (ix->Xs)
-                HIP_TRY(launch_split_rows(ix->X, ix->G, ix->count + r, m,
-                                          ix->metric == VDB_METRIC_COSINE ? ix->inv32 : nullptr, ix->Xs, st));
+            HIP_TRY(build_candidate_rows(ix, ix->X, ix->inv32, ix->count + r, m, ix->Xs, st));
         }
     }
     if (staging) (void)hipFree(staging);
@@ -857,7 +848,7 @@ static int32_t search_impl(vdb_index* ix, const float* queries, int32_t B, int32
                 HIP_TRY(hipEventRecord(tev[3], st));
             }
             const float* rowscale = ix->metric == 0 ? ix->inv32 : ix->sq32;
-            const float* Xscan = prec == PREC_FP32 ? ix->X : ix->Xs;
+            const float* Xscan = ix->Xs;  // fp32 or split tiles, per the precision class
             if (n_pilot > 0) {
                 if (split_pass)
                     HIP_TRY(launch_pilot2(prec, ix->metric, pilot_rank, Xscan, ix->rinit32, md, Qt, Gs, N, B,

@@ -179,9 +179,16 @@ __device__ __forceinline__ double wave_sum_butterfly(double v) {
     return v;
 }
 
-// float offset of piece p (dims 4p..4p+3) of row r in the tiled corpus
+// float offset of piece p (dims 4p..4p+3) of row r in the tiled layout (fp32 candidate
+// copy, query tiles)
 __device__ __forceinline__ size_t tiled_piece_offset(uint64_t r, int p, int G) {
     return tiled_block(r >> 5, p >> 1, G) + (size_t)(r & 31) * 4 + (size_t)(p & 1) * 128;
+}
+
+// float offset of piece p of row r in the row-major fp32 corpus [cap][Dp] (Dp = 8 G): the
+// exact paths gather whole rows, one coalesced 1 KiB load per wave per 256 dims
+__device__ __forceinline__ size_t row_piece_offset(uint64_t r, int p, int G) {
+    return (size_t)r * (size_t)(8 * G) + (size_t)p * 4;
 }
 
 // Global id of local row r: row_ids[r] (a shard of a multi-device set, whose rows are

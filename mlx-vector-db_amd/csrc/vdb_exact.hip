@@ -27,7 +27,7 @@ __device__ __forceinline__ double exact_key(const float* __restrict__ q, double 
         for (int u = 0; u < 4; ++u) {
             const int p = (m0 + u) * 64 + lane;
             const bool in = (m0 + u) < np;
-            xv[u] = (in && 4 * p < Dp) ? *(const f32x4*)(X + tiled_piece_offset(r, p, G)) : f32x4{0.f, 0.f, 0.f, 0.f};
+            xv[u] = (in && 4 * p < Dp) ? *(const f32x4*)(X + row_piece_offset(r, p, G)) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int j = 0; j < 4; ++j) qv[u][j] = (in && 4 * p + j < D) ? q[4 * p + j] : 0.0f;
         }
@@ -76,7 +76,7 @@ __device__ __forceinline__ void exact_keys_regs(const float (&qv)[MP][4], double
         const int p = m * 64 + lane;
 #pragma unroll
         for (int u = 0; u < NB; ++u)
-            xv[m][u] = (m < np && u < nb && 4 * p < Dp) ? *(const f32x4*)(X + tiled_piece_offset(rows[u], p, G))
+            xv[m][u] = (m < np && u < nb && 4 * p < Dp) ? *(const f32x4*)(X + row_piece_offset(rows[u], p, G))
                                                        : f32x4{0.f, 0.f, 0.f, 0.f};
     }
     double acc[NB];
@@ -234,7 +234,7 @@ __device__ __forceinline__ void exact_keys_batch(const float* __restrict__ q, do
         f32x4 xv[NB];
 #pragma unroll
         for (int u = 0; u < NB; ++u)
-            xv[u] = (u < nb && 4 * p < Dp) ? *(const f32x4*)(X + tiled_piece_offset(rows[u], p, G)) : f32x4{0.f, 0.f, 0.f, 0.f};
+            xv[u] = (u < nb && 4 * p < Dp) ? *(const f32x4*)(X + row_piece_offset(rows[u], p, G)) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int u = 0; u < NB; ++u)
 #pragma unroll

@@ -330,13 +330,13 @@ __global__ void __launch_bounds__(64 * GP_WAVES) graph_prune_kernel(GraphPruneAr
     f32x16 t00, t01, t11;
 #pragma unroll
     for (int i = 0; i < 16; ++i) t00[i] = t01[i] = t11[i] = 0.0f;
-    f32x4 n0 = *(const f32x4*)(a.X + tiled_piece_offset((uint64_t)row0, h, a.G));
-    f32x4 n1 = *(const f32x4*)(a.X + tiled_piece_offset((uint64_t)row1, h, a.G));
+    f32x4 n0 = *(const f32x4*)(a.X + row_piece_offset((uint64_t)row0, h, a.G));
+    f32x4 n1 = *(const f32x4*)(a.X + row_piece_offset((uint64_t)row1, h, a.G));
     for (int j = 0; j < a.G; ++j) {
         const f32x4 x0 = n0, x1 = n1;
         if (j + 1 < a.G) {  // next pieces in flight during this step's MFMAs
-            n0 = *(const f32x4*)(a.X + tiled_piece_offset((uint64_t)row0, 2 * j + 2 + h, a.G));
-            n1 = *(const f32x4*)(a.X + tiled_piece_offset((uint64_t)row1, 2 * j + 2 + h, a.G));
+            n0 = *(const f32x4*)(a.X + row_piece_offset((uint64_t)row0, 2 * j + 2 + h, a.G));
+            n1 = *(const f32x4*)(a.X + row_piece_offset((uint64_t)row1, 2 * j + 2 + h, a.G));
         }
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
@@ -410,15 +410,15 @@ hipError_t launch_graph_prune(int metric, const GraphPruneArgs& a, hipStream_t s
 }
 
 // The graph's row-major copy of the corpus, [n][Dp] fp32 (Dp = D rounded up to 32,
-// zero padded): a gathered row is Dp/32 whole 128-byte lines, where the tiled scan
-// layout scatters it over 16-byte pieces of 2 * G different lines.
+// zero padded; the index's own row-major copy is padded to 64): a gathered row is Dp/32
+// whole 128-byte lines.
 __global__ void graph_rows_kernel(const float* __restrict__ X, int G, int64_t n, int Dp, float* __restrict__ out) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int ppr = Dp >> 2;
     if (t >= n * ppr) return;
     const int64_t r = t / ppr;
     const int p = (int)(t - r * ppr);
-    const f32x4 v = p < 2 * G ? *(const f32x4*)(X + tiled_piece_offset((uint64_t)r, p, G)) : f32x4{0.f, 0.f, 0.f, 0.f};
+    const f32x4 v = p < 2 * G ? *(const f32x4*)(X + row_piece_offset((uint64_t)r, p, G)) : f32x4{0.f, 0.f, 0.f, 0.f};
     *(f32x4*)(out + r * Dp + 4 * p) = v;
 }
 

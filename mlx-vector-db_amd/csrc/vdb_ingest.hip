@@ -8,7 +8,7 @@ namespace vdb {
 // =============================================================================
 // Ingest
 // =============================================================================
-// One wave per row.  Canonical fp64 norm (vdb_common.h), tiled store of whole
+// One wave per row.  Canonical fp64 norm (vdb_common.h), row-major store of whole
 // 16-byte pieces (padding dims of the row are written as zeros), the fp32 row terms of
 // the candidate passes, and (second pass over the row, cache-hot) the bf16 rounding
 // residual of the row the split copy holds (cosine: x * inv32, the normalised row; L2: x),
@@ -39,7 +39,7 @@ __global__ void __launch_bounds__(256) pack_rows_kernel(const float* __restrict_
             const double dv = (double)v[j];
             acc = acc + dv * dv;
         }
-        if (4 * p < Dp) *(f32x4*)(X + tiled_piece_offset(r, p, G)) = v;
+        if (4 * p < Dp) *(f32x4*)(X + row_piece_offset(r, p, G)) = v;
     }
     acc = wave_sum_butterfly(acc);
     const double nr = sqrt(acc);
@@ -92,11 +92,11 @@ hipError_t launch_pack_rows(const float* src, int64_t n, int D, int G, float* X,
     return hipGetLastError();
 }
 
-// fp32 tiles -> split-bf16 tiles.  Thread (tile t, fp32 group g8, row-in-tile i):
-// the 8 dims 8 g8 .. 8 g8 + 7 of row 32 t + i (two 16-byte pieces, lanes i and
-// i + 32 of the fp32 block), times inv32[row] for cosine (the normalised row the
-// candidate pass scores), -> lane i + 32 (g8 & 1) of the hi and lo blocks of 16-dim
-// group g8 >> 1.  32 consecutive threads read and write 512 B runs.
+// Row-major fp32 rows -> split-bf16 tiles.  Thread (tile t, fp32 group g8, row-in-tile i):
+// the 8 dims 8 g8 .. 8 g8 + 7 of row 32 t + i (32 contiguous bytes), times inv32[row] for
+// cosine (the normalised row the candidate pass scores), -> lane i + 32 (g8 & 1) of the hi
+// and lo blocks of 16-dim group g8 >> 1.  A block's 256 threads cover 8 groups of one
+// tile: 32 rows x 256 contiguous bytes read, 512 B runs written.
 __global__ void __launch_bounds__(256) split_rows_kernel(const float* __restrict__ X, int G, int64_t t0,
                                                          int64_t n_tiles, const float* __restrict__ inv32,
                                                          float* __restrict__ Xs) {
@@ -105,9 +105,9 @@ __global__ void __launch_bounds__(256) split_rows_kernel(const float* __restrict
     const int i = (int)(idx & 31);
     const int g8 = (int)((idx >> 5) % G);
     const uint64_t t = (uint64_t)(t0 + (idx >> 5) / G);
-    const float* src = X + tiled_block(t, g8, G);
-    f32x4 a = *(const f32x4*)(src + i * 4);
-    f32x4 b = *(const f32x4*)(src + (32 + i) * 4);
+    const float* src = X + row_piece_offset(t * 32 + i, 2 * g8, G);
+    f32x4 a = *(const f32x4*)src;
+    f32x4 b = *(const f32x4*)(src + 4);
     if (inv32) {
         const float iv = inv32[t * 32 + i];
         a *= iv;
@@ -130,12 +130,33 @@ hipError_t launch_split_rows(const float* X, int G, int64_t row0, int64_t n, con
     return hipGetLastError();
 }
 
+// Row-major fp32 rows -> fp32 tiles (the PREC_FP32 candidate copy), whole row tiles
+// covering [row0, row0 + n).  Thread (tile t, piece p, row-in-tile i).
+__global__ void __launch_bounds__(256) tile_rows_kernel(const float* __restrict__ X, int G, int64_t t0,
+                                                        int64_t n_tiles, float* __restrict__ Xt) {
+    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= n_tiles * 2 * G * 32) return;
+    const int i = (int)(idx & 31);
+    const int p = (int)((idx >> 5) % (2 * G));
+    const uint64_t r = (uint64_t)(t0 + (idx >> 5) / (2 * G)) * 32 + i;
+    *(f32x4*)(Xt + tiled_piece_offset(r, p, G)) = *(const f32x4*)(X + row_piece_offset(r, p, G));
+}
+
+hipError_t launch_tile_rows(const float* X, int G, int64_t row0, int64_t n, float* Xt, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    const int64_t t0 = row0 >> 5, t1 = (row0 + n + 31) >> 5;
+    const int64_t total = (t1 - t0) * 2 * G * 32;
+    hipLaunchKernelGGL(tile_rows_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, X, G, t0, t1 - t0,
+                       Xt);
+    return hipGetLastError();
+}
+
 __global__ void __launch_bounds__(256) unpack_rows_kernel(const float* __restrict__ X, int G, int D, int64_t row0,
                                                           int64_t n, float* __restrict__ dst) {
     const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= n) return;
     const int lane = threadIdx.x & 63;
-    for (int d = lane; d < D; d += 64) dst[row * D + d] = X[tiled_offset((uint64_t)(row0 + row), d, G)];
+    for (int d = lane; d < D; d += 64) dst[row * D + d] = X[(size_t)(row0 + row) * (size_t)(8 * G) + d];
 }
 
 hipError_t launch_unpack_rows(const float* X, int G, int D, int64_t row0, int64_t n, float* dst, hipStream_t st) {

@@ -23,7 +23,8 @@ constexpr int PREC_BF16X3 = 1;
 //               index's largest row residual |x - bf16(x)| (pack_rows)
 constexpr int PREC_BF16 = 2;
 
-// Ingest: row-major fp32 [n][D] (device) -> tiled corpus rows [row0, row0+n),
+// Ingest: row-major fp32 [n][D] (device) -> the index's row-major fp32 copy X [cap][Dp]
+// (zero padded to Dp = 8 G; read by the exact paths, export and the graph) rows [row0, row0+n),
 // canonical fp64 norms, fp32 inverse norms and squared norms, running maxima (as
 // fp64 bits) xmax_bits[0] = |x|, [1] = |x - bf16(x)| / |x|, [2] = |x - bf16(x)|,
 // and a non-finite counter.
@@ -33,14 +34,17 @@ hipError_t launch_pack_rows(const float* src, int64_t n, int D, int G, float* X,
                             double* nrm64, float* inv32, float* sq32, float* rinit32, int normalise,
                             unsigned long long* xmax_bits, int* nonfinite, hipStream_t st);
 
-// fp32 tiles -> split-bf16 tiles (hi = bf16(y), lo = bf16(y - hi)) for the whole row tiles
+// Row-major fp32 rows -> split-bf16 tiles (hi = bf16(y), lo = bf16(y - hi)) for the whole row tiles
 // covering rows [row0, row0 + n), y = x * inv32[row] (cosine: the normalised row, as the
 // candidate pass scores it) or y = x (inv32 == nullptr, L2).  G = fp32 groups (Dp/8); the
 // split copy has G/2 groups.
 hipError_t launch_split_rows(const float* X, int G, int64_t row0, int64_t n, const float* inv32, float* Xs,
                              hipStream_t st);
 
-// Tiled corpus rows -> row-major fp32 (export for persistence).
+// Row-major fp32 rows -> fp32 tiles (the PREC_FP32 candidate copy), whole row tiles.
+hipError_t launch_tile_rows(const float* X, int G, int64_t row0, int64_t n, float* Xt, hipStream_t st);
+
+// The index's rows -> row-major fp32 [n][D] (export for persistence).
 hipError_t launch_unpack_rows(const float* X, int G, int D, int64_t row0, int64_t n, float* dst, hipStream_t st);
 
 // gthr[B]: per-query shared threshold (order-preserving score key, 0 = none) and
