@@ -196,17 +196,16 @@ hipError_t launch_rerank(int metric, int KP, const RerankArgs& a, int B, hipStre
 // finish: select + exact rerank + certificate, one workgroup per query
 // =============================================================================
 // Input: the query's global candidate list (entries the candidate pass appended
-// above its shared bound; typically tens to a few hundred).  Wave 0 selects the
-// best min(KP, c) by (approx score desc, row asc) with ballot bisection (no sort
-// network: a dependent ds_bpermute costs ~140 cycles, a ballot a few); all four
-// waves compute exact fp64 keys, batched NB candidates per wave so the corpus
-// loads of a batch are in flight together; ranks come from counting (no sort);
-// thread 0 checks the certificate.  A list longer than FIN_CAP goes to the exact
-// scan.
+// above its shared bound; typically tens to a few hundred).  Entries below the final
+// bound are dropped while loading; the best min(KP, n) of the rest by (approx score
+// desc, row asc) come from a radix select over all waves (no sort); all waves compute
+// exact fp64 keys, batched NB candidates per wave so the corpus loads of a batch are
+// in flight together; ranks come from counting (no sort), several threads per
+// candidate; thread 0 checks the certificate.  A list longer than FIN_CAP goes to the
+// exact scan.
 constexpr int FIN_CAP = 16384;  // 128 KiB of (key, row) in LDS
 constexpr int FIN_NB = 2;        // candidates per wave per batch
 constexpr int FIN_WAVES = 16;
-constexpr int FIN_REG = 512;     // lists up to this length are selected from registers
 
 #ifdef VDB_STAMP
 // Diagnostic build only: per-query phase timestamps of finish_kernel + list length.
@@ -287,95 +286,125 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
     }
     const float* ls = a.gl_s + (size_t)b * a.gl_cap;
     const uint32_t* li = a.gl_i + (size_t)b * a.gl_cap;
-    for (int e = tid; e < c; e += 64 * FIN_WAVES) {
-        s_key[e] = order_key(ls[e]);
-        s_row[e] = li[e];
-    }
+    // Entries below the final shared bound T cannot be among the KP best (T is at most the
+    // KP-th best approx score, or the certificate fails on it anyway) and rows outside the
+    // candidates only need approx <= max(a_KP, T): drop them while loading.  Lists are
+    // appended by workgroups that flushed against older, lower bounds, so this typically
+    // leaves about KP entries.
+    const uint32_t tkey = a.gthr[b];
+    __shared__ int s_n;
     if (tid == 0) {
         s_ak = 0;
         s_akp = 0;
+        s_n = 0;
+    }
+    __syncthreads();
+    for (int e0 = wv * 64; e0 < c; e0 += 64 * FIN_WAVES) {
+        const int e = e0 + lane;
+        const uint32_t key = e < c ? order_key(ls[e]) : 0u;
+        const uint32_t row = e < c ? li[e] : 0u;
+        const bool keep = e < c && key >= tkey;
+        const unsigned long long bm = __ballot(keep);
+        int base = 0;
+        if (lane == 0 && bm) base = atomicAdd(&s_n, __popcll(bm));
+        base = __shfl(base, 0, 64);
+        if (keep) {
+            const int pos = base + __popcll(bm & ((1ull << lane) - 1ull));
+            s_key[pos] = key;
+            s_row[pos] = row;
+        }
     }
     __syncthreads();
     FIN_STAMP(1);
-    const int n = (int)c;
-    // long lists: all waves count for each bisection round (LDS counter per round)
+    const int n = s_n;
+    // Select the KP best by (approx key desc, row asc): T = the KP-th largest key by an 8-bit
+    // radix select over all waves (4 rounds: LDS histogram of the next digit among the
+    // entries matching the prefix, one wave finds the digit holding the KP-th), then, only
+    // if several entries tie at T, the rows kept at T by bisection on the row.
     __shared__ int s_cnt2[2];
-    __shared__ uint32_t s_T, s_I;
-    if (n > FIN_REG) {
-        auto count_all = [&](auto pred, int parity) -> int {
-            int cnt = 0;
-            for (int e0 = wv * 64; e0 < n; e0 += 64 * FIN_WAVES) {
-                const int e = e0 + lane;
-                cnt += __popcll(__ballot(e < n && pred(e)));
+    __shared__ uint32_t s_T, s_I, s_pref;
+    __shared__ int s_hist[256];
+    __shared__ int s_need, s_eq;
+    if (n > KP) {
+        uint32_t prefix = 0u, pmask = 0u;
+        int need = KP;
+        for (int shift = 24; shift >= 0; shift -= 8) {
+            if (tid < 256) s_hist[tid] = 0;
+            __syncthreads();
+            for (int e = tid; e < n; e += 64 * FIN_WAVES) {
+                const uint32_t kk = s_key[e];
+                if ((kk & pmask) == prefix) atomicAdd(&s_hist[(kk >> shift) & 255u], 1);
             }
-            if (lane == 0 && cnt) atomicAdd(&s_cnt2[parity], cnt);
             __syncthreads();
-            const int total = s_cnt2[parity];
+            if (wv == 0) {
+                int h[4], sum = 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {  // lane l: digits 255 - 4l .. 252 - 4l (descending)
+                    h[j] = s_hist[255 - 4 * lane - j];
+                    sum += h[j];
+                }
+                int incl = sum;
+#pragma unroll
+                for (int off = 1; off < 64; off <<= 1) {
+                    const int t = __shfl_up(incl, off, 64);
+                    if (lane >= off) incl += t;
+                }
+                int dsel = -1, above = incl - sum;
+                if (incl - sum < need && need <= incl) {  // exactly one lane
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        if (dsel < 0) {
+                            if (above + h[j] >= need) dsel = 255 - 4 * lane - j;
+                            else above += h[j];
+                        }
+                    }
+                }
+                const int src = __ffsll((unsigned long long)__ballot(dsel >= 0)) - 1;
+                dsel = __shfl(dsel, src, 64);
+                above = __shfl(above, src, 64);
+                if (lane == 0) {
+                    s_pref = prefix | ((uint32_t)dsel << shift);
+                    s_need = need - above;
+                    s_eq = s_hist[dsel];
+                }
+            }
             __syncthreads();
-            if (tid == 0) s_cnt2[parity] = 0;
-            return total;
-        };
-        if (tid == 0) s_cnt2[0] = s_cnt2[1] = 0;
-        __syncthreads();
-        uint32_t T = 0;
-        for (int bit = 31; bit >= 0; --bit) {
-            const uint32_t cand = T | (1u << bit);
-            if (count_all([&](int e) { return s_key[e] >= cand; }, bit & 1) >= KP) T = cand;
+            prefix = s_pref;
+            pmask |= 255u << shift;
+            need = s_need;
         }
-        const int gt = count_all([&](int e) { return s_key[e] > T; }, 0);
-        const int eq = count_all([&](int e) { return s_key[e] == T; }, 1);
-        const int need = KP - gt;
         uint32_t I = 0xFFFFFFFFu;
-        if (eq > need) {
+        if (s_eq > need) {  // ties at T: keep the `need` lowest rows among them
+            auto count_all = [&](auto pred, int parity) -> int {
+                int cnt = 0;
+                for (int e0 = wv * 64; e0 < n; e0 += 64 * FIN_WAVES) {
+                    const int e = e0 + lane;
+                    cnt += __popcll(__ballot(e < n && pred(e)));
+                }
+                if (lane == 0 && cnt) atomicAdd(&s_cnt2[parity], cnt);
+                __syncthreads();
+                const int total = s_cnt2[parity];
+                __syncthreads();
+                if (tid == 0) s_cnt2[parity] = 0;
+                return total;
+            };
+            if (tid == 0) s_cnt2[0] = s_cnt2[1] = 0;
+            __syncthreads();
             I = 0;
             for (int bit = 31; bit >= 0; --bit) {
                 const uint32_t cand = I | (1u << bit);
-                if (count_all([&](int e) { return s_key[e] == T && s_row[e] < cand; }, bit & 1) < need) I = cand;
+                if (count_all([&](int e) { return s_key[e] == prefix && s_row[e] < cand; }, bit & 1) < need) I = cand;
             }
         }
         if (tid == 0) {
-            s_T = T;
+            s_T = prefix;
             s_I = I;
         }
         __syncthreads();
     }
     if (wv == 0) {
-        int m = n < KP ? n : KP;
-        uint32_t T = n > FIN_REG ? s_T : 0u, I = n > FIN_REG ? s_I : 0xFFFFFFFFu;
-        if (n > KP && n <= FIN_REG) {
-            constexpr int E = FIN_REG / 64;
-            uint32_t kv[E], rv[E];
-#pragma unroll
-            for (int i = 0; i < E; ++i) {
-                const int e = i * 64 + lane;
-                kv[i] = e < n ? s_key[e] : 0u;  // 0 = below every real key (order keys of finite floats are > 0)
-                rv[i] = e < n ? s_row[e] : 0xFFFFFFFFu;
-            }
-            for (int bit = 31; bit >= 0; --bit) {
-                const uint32_t cand = T | (1u << bit);
-                int ge = 0;
-#pragma unroll
-                for (int i = 0; i < E; ++i) ge += __popcll(__ballot(kv[i] >= cand));
-                if (ge >= KP) T = cand;
-            }
-            int gt = 0, eq = 0;
-#pragma unroll
-            for (int i = 0; i < E; ++i) {
-                gt += __popcll(__ballot(kv[i] > T));
-                eq += __popcll(__ballot(kv[i] == T && rv[i] != 0xFFFFFFFFu));
-            }
-            const int need = KP - gt;
-            if (eq > need) {
-                I = 0;
-                for (int bit = 31; bit >= 0; --bit) {
-                    const uint32_t cand = I | (1u << bit);
-                    int lt = 0;
-#pragma unroll
-                    for (int i = 0; i < E; ++i) lt += __popcll(__ballot(kv[i] == T && rv[i] < cand));
-                    if (lt < need) I = cand;
-                }
-            }
-        }
+        const int m = n < KP ? n : KP;
+        const uint32_t T = n > KP ? s_T : 0u, I = n > KP ? s_I : 0xFFFFFFFFu;
         int base = 0;
         for (int e0 = 0; e0 < n; e0 += 64) {
             const int e = e0 + lane;
@@ -446,18 +475,32 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
     }
     __syncthreads();
     FIN_STAMP(3);
-    // ranks by counting: exact (output order) and approx (certificate)
-    for (int j = tid; j < KP; j += 64 * FIN_WAVES) {
+    // ranks by counting: exact (output order) and approx (certificate); TPC threads (adjacent
+    // lanes) per candidate, each counting m / TPC of the others, summed by an xor butterfly
+    constexpr int TPC = KP >= 64 * FIN_WAVES ? 1 : (64 * FIN_WAVES) / KP > 64 ? 64 : (64 * FIN_WAVES) / KP;
+    for (int jt = tid; jt < KP * TPC; jt += 64 * FIN_WAVES) {
+        const int j = jt / TPC, sub = jt % TPC;
+        int er = 0, ar = 0;
+        double ek = 0.0;
+        uint32_t ck = 0u, r = 0u;
         if (j < m) {
-            const double ek = s_ek[j];
-            const uint32_t ck = s_ck[j], r = s_cr[j];
-            int er = 0, ar = 0;
-            for (int i = 0; i < m; ++i) {
+            ek = s_ek[j];
+            ck = s_ck[j];
+            r = s_cr[j];
+            for (int i = sub; i < m; i += TPC) {
                 const double ei = s_ek[i];
                 const uint32_t ci = s_ck[i], ri = s_cr[i];
                 er += (ei > ek || (ei == ek && ri < r)) ? 1 : 0;
                 ar += (ci > ck || (ci == ck && ri < r)) ? 1 : 0;
             }
+        }
+#pragma unroll
+        for (int off = 1; off < TPC; off <<= 1) {
+            er += __shfl_xor(er, off, 64);
+            ar += __shfl_xor(ar, off, 64);
+        }
+        if (sub != 0) continue;
+        if (j < m) {
             if (er < a.k) {
                 const size_t o = (size_t)b * a.k + er;
                 write_result(METRIC, ek, global_row(a.row_ids, r, a.index_offset), true, a.out_s + o, a.out_i + o,
