@@ -327,6 +327,8 @@ def main():
                     help="candidate-pass step end: 1 lockstep barrier, 2 flag-gated rounds (tuning; default by D)")
     ap.add_argument("--pilot-tiles", type=int, default=None, help="row tiles sampled by the pilot bound (tuning)")
     ap.add_argument("--margin", type=int, default=None, help="candidates beyond k (tuning; default per precision)")
+    ap.add_argument("--pilot-fused", type=int, default=None, help="split pass: 1 the scan derives the pilot bound, "
+                    "0 a separate bound kernel (tuning)")
     ap.add_argument("--pilot-rank", type=int, default=None, help="rank of the pilot bound (tuning; default: Poisson rule)")
     ap.add_argument("--rows", type=int, default=None, help="override the corpus rows (exploration only)")
     ap.add_argument("--no-fallback", action="store_true",
@@ -374,6 +376,8 @@ def main():
         ix.set_param("pilot_tiles", args.pilot_tiles)
     if args.margin is not None:
         ix.set_param("margin", args.margin)
+    if args.pilot_fused is not None:
+        ix.set_param("pilot_fused", args.pilot_fused)
     if args.pilot_rank is not None:
         ix.set_param("pilot_rank", args.pilot_rank)
     if args.no_fallback:

@@ -113,8 +113,8 @@ struct vdb_index {
     // knobs
     int64_t precision = VDB_PREC_AUTO;
     // VDB_PREC_AUTO: searches left in BF16X3 after a BF16 search with many fallbacks, and the
-    // device-gated fallback total last seen (pinned mirror of d_totals[0], copied after each
-    // device-memory search and read by the next one)
+    // device-gated fallback total last seen (pinned mirror of d_totals[0], written by the
+    // gated exact kernel of a device-memory search and read by the next search)
     std::atomic<int> auto_b3_left{0};
     std::atomic<int> auto_period{kAutoB3Searches};  // doubles on every BF16 retry that falls back again
     std::atomic<unsigned long long> auto_seen{0};
@@ -130,6 +130,10 @@ struct vdb_index {
     int64_t scan_sync = 0;        // scan step end: 0 auto, 1 lockstep barrier, 2 flag-gated rounds
     int64_t no_fallback = 0;      // diagnostics only: skip the exact fallback (results may be wrong)
     int64_t pilot_rank_override = 0;  // tuning: rank of the pilot bound (0 = the Poisson rule)
+    // split pass: 1 = the scan's prologue derives the pilot bound (one launch fewer), 0 = the
+    // bound kernel.  Measured (profiles/r02_ab, C2): the prologue costs the scan ~25 us (bf16)
+    // / ~30 us (bf16x3) against ~5 us for the kernel, so 0 is the default.
+    int64_t pilot_fused = 0;
     // stats
     std::atomic<int64_t> n_searches{0}, n_queries{0}, n_fallback{0}, n_overflow{0};
     std::atomic<int64_t> n_by_prec[3] = {{0}, {0}, {0}};  // candidate passes per PREC_* (VDB_PREC_AUTO's choices)
@@ -344,7 +348,7 @@ size_t exact_bytes(vdb_index* ix, int nq, int k, bool gated) {
 int run_exact(vdb_index* ix, Workspace* w, const float* Qd, const double* qn64, const int* qlist_dev, int nq, int k,
               const uint32_t* mask_dev, float* out_s, int64_t* out_i, double* out_k, int64_t index_offset,
               const int64_t* row_ids, hipStream_t st, const int* qcount_dev = nullptr, const int* ovf_dev = nullptr,
-              int* done_dev = nullptr) {
+              int* done_dev = nullptr, unsigned long long* host_totals = nullptr) {
     const int KE = std::max(32, next_pow2(k));
     const int64_t N = ix->count;
     const bool gated = qcount_dev != nullptr;
@@ -363,7 +367,7 @@ int run_exact(vdb_index* ix, Workspace* w, const float* Qd, const double* qn64, 
     double* mk = c.take<double>((size_t)nq * KE);
     uint32_t* mi = c.take<uint32_t>((size_t)nq * KE);
     if (gated && done_dev) {  // one launch: the last workgroup per query merges and writes (ExactTail)
-        const ExactTail tail{done_dev, mk, mi, k, index_offset, out_s, out_i, out_k, row_ids};
+        const ExactTail tail{done_dev, mk, mi, k, index_offset, out_s, out_i, out_k, row_ids, host_totals};
         HIP_TRY(launch_exact_scan(ix->metric, KE, Qd, qn64, qlist_dev, nq, ix->X, ix->G, ix->dim, ix->nrm64, mask_dev,
                                   N, n_wg, rpw, lk, li, st, qcount_dev, ovf_dev, ix->d_totals, &tail));
         return VDB_OK;
@@ -512,6 +516,8 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
         ix->timing = value != 0;
     } else if (n == "no_fallback") {
         ix->no_fallback = value != 0;
+    } else if (n == "pilot_fused") {
+        ix->pilot_fused = value != 0;
     } else if (n == "pilot_rank") {
         if (value < 0 || value > 256) return set_error(VDB_ERR_INVALID, "pilot_rank must be in [0, 256]");
         ix->pilot_rank_override = value;
@@ -850,9 +856,11 @@ static int32_t search_impl(vdb_index* ix, const float* queries, int32_t B, int32
             const float* rowscale = ix->metric == 0 ? ix->inv32 : ix->sq32;
             const float* Xscan = ix->Xs;  // fp32 or split tiles, per the precision class
             if (n_pilot > 0) {
-                if (split_pass)
+                if (split_pass) {
                     HIP_TRY(launch_pilot2(prec, ix->metric, pilot_rank, Xscan, ix->rinit32, md, Qt, Gs, N, B,
                                           n_qblocks, QB, n_pilot, pslots, gthr, st));
+                    if (!ix->pilot_fused) HIP_TRY(launch_pilot_bound(pslots, B, pilot_rank, gthr, st));
+                }
                 else
                     HIP_TRY(launch_pilot(prec, ix->metric, pilot_rank, Xscan, rowscale, md, Qt, Gs, N, B,
                                          n_qblocks, QB, n_pilot, pslots, gthr, st));
@@ -862,7 +870,8 @@ static int32_t search_impl(vdb_index* ix, const float* queries, int32_t B, int32
             if (timed) HIP_TRY(hipEventRecord(tev[0], st));
             if (split_pass)
                 HIP_TRY(launch_scan2(prec, ix->metric, KP, Xscan, ix->rinit32, md, Qt, Gs, N, B, n_qblocks, n_steps,
-                                     n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, lockstep, st));
+                                     n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, pslots,
+                                     n_pilot > 0 && ix->pilot_fused ? pilot_rank : 0, lockstep, st));
             else if (priv)
                 HIP_TRY(launch_scan_topk_priv(prec, ix->metric, KP, Xscan, rowscale, md, Qt, Gs, N, B, n_qblocks,
                                               n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, st));
@@ -910,11 +919,7 @@ static int32_t search_impl(vdb_index* ix, const float* queries, int32_t B, int32
                     }
                 }
                 rc = run_exact(ix, w, Qd, qn64, flags + 1, B, k, md, out_s, out_i, out_k, index_offset, row_ids, st,
-                               flags, flags + B + 1, done);
-                if (rc == VDB_OK && auto_prec) {
-                    HIP_TRY(hipMemcpyAsync(ix->h_totals, ix->d_totals, 2 * sizeof(unsigned long long),
-                                           hipMemcpyDeviceToHost, st));
-                }
+                               flags, flags + B + 1, done, auto_prec ? ix->h_totals : nullptr);
                 return rc;
             }
             HIP_TRY(hipMemcpyAsync(w->host_flag, flags, sizeof(int), hipMemcpyDeviceToHost, st));

@@ -582,7 +582,10 @@ exact_scan_kernel(const float* __restrict__ Q, const double* __restrict__ qn64, 
         const int c = *qcount;
         nq = c < nq_max ? c : nq_max;
         if (totals && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
-            if (c) atomicAdd(totals, (unsigned long long)c);
+            if (c) {
+                const unsigned long long old = atomicAdd(totals, (unsigned long long)c);
+                if (tail.host_totals) tail.host_totals[0] = old + (unsigned long long)c;  // pinned host mirror
+            }
             if (ovf && *ovf) atomicAdd(totals + 1, (unsigned long long)*ovf);
         }
     }

@@ -102,7 +102,9 @@ int scan2_qb(int KP);
 hipError_t launch_scan2(int prec, int metric, int KP, const float* Xs, const float* rinit, const uint32_t* mask,
                         const float* Qs, int G, int64_t N, int B, int n_qblocks, int64_t n_steps, int n_wg, int spw,
                         float* gl_s, uint32_t* gl_i, uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr,
-                        uint32_t* gslots, int lockstep, hipStream_t st);
+                        uint32_t* gslots, const uint32_t* pslots, int prank, int lockstep, hipStream_t st);
+// Pilot scores for the split pass: fills pslots only; scan2 derives the bound (rank prank of
+// the slots) in its prologue, so there is no separate bound kernel.
 hipError_t launch_pilot2(int prec, int metric, int KP, const float* Xs, const float* rinit, const uint32_t* mask,
                          const float* Qs, int G, int64_t N, int B, int n_qblocks, int QB, int n_sample,
                          uint32_t* pslots, uint32_t* gthr, hipStream_t st);
@@ -143,9 +145,12 @@ hipError_t launch_finish(int metric, int KP, const FinishArgs& a, int B, hipStre
 // With a tail (device-gated form only), the workgroup that finishes a query slot's lists
 // last (done[slot] counts them; zeroed by prep_queries) merges them into mk / mi [nq][KE]
 // and writes the query's results: one launch instead of scan + merge + finalize.
+// host_totals (optional): pinned host memory that block (0, 0) updates with the new total of
+// flagged queries (VDB_PREC_AUTO reads it on the next search, without a copy or a sync).
 struct ExactTail {
     int* done; double* mk; uint32_t* mi; int k; int64_t index_offset;
     float* out_s; int64_t* out_i; double* out_k; const int64_t* row_ids;
+    unsigned long long* host_totals = nullptr;
 };
 hipError_t launch_exact_scan(int metric, int KE, const float* Q, const double* qn64, const int* qlist, int nq,
                              const float* X, int G, int D, const double* nrm64, const uint32_t* mask,

@@ -56,12 +56,56 @@ __device__ __forceinline__ size_t s2_blk(uint64_t t, int g, int GG) {
     return (((size_t)(t >> 2) * GG + g) * 8 + (t & 3)) * BLOCK_FLOATS;
 }
 
+// The pilot bound of one query (one wave): the rank-th largest of its PILOT_SLOTS pilot slots
+// (vdb_api.cpp pilot_rank), 0 when fewer slots are filled.  Small ranks by repeated wave
+// maxima (remove one copy of the maximum per round), larger ones by ballot bisection.
+constexpr int PILOT_E = PILOT_SLOTS / 64;  // slots per lane
+
+__device__ __forceinline__ uint32_t pilot_slot_rank(uint32_t (&v)[PILOT_E], int rank) {
+    constexpr int E = PILOT_E;
+    const int lane = threadIdx.x & 63;
+    int filled = 0;
+#pragma unroll
+    for (int i = 0; i < E; ++i) filled += __popcll(__ballot(v[i] != 0u));
+    if (filled < rank) return 0u;
+    if (rank <= 16) {
+        for (int r = 1;; ++r) {
+            uint32_t m = v[0];
+#pragma unroll
+            for (int i = 1; i < E; ++i) m = max(m, v[i]);
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off, 64));
+            if (r == rank) return m;
+            // drop one copy of m: the lowest lane holding it, its first register
+            int hit = -1;
+#pragma unroll
+            for (int i = E - 1; i >= 0; --i) hit = v[i] == m ? i : hit;
+            const unsigned long long who = __ballot(hit >= 0);
+            if (lane == __ffsll((long long)who) - 1) {
+#pragma unroll
+                for (int i = 0; i < E; ++i)
+                    if (i == hit) v[i] = 0u;
+            }
+        }
+    }
+    uint32_t T = 0;
+    for (int bit = 31; bit >= 0; --bit) {
+        const uint32_t c = T | (1u << bit);
+        int n = 0;
+#pragma unroll
+        for (int i = 0; i < E; ++i) n += __popcll(__ballot(v[i] >= c));
+        if (n >= rank) T = c;
+    }
+    return T;
+}
+
 template <int PREC, int METRIC, int QT, int PX, int KP, int CAP, bool NT, bool QLDS, bool FLAGSYNC>
 __global__ void __launch_bounds__(256, 1)
 scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, const uint32_t* __restrict__ mask,
              const float* __restrict__ Qs, int G, int64_t N, int B, int64_t n_steps, int steps_per_wg, int n_qb,
              float* __restrict__ gl_s, uint32_t* __restrict__ gl_i, uint32_t* __restrict__ gl_cnt, int64_t gl_cap,
-             uint32_t* __restrict__ gthr, uint32_t* __restrict__ gslots) {
+             uint32_t* __restrict__ gthr, uint32_t* __restrict__ gslots, const uint32_t* __restrict__ pslots,
+             int prank) {
     constexpr int RT = S2_RT, NW = S2_NW;
     constexpr int QB = 32 * QT;
     constexpr int XPL = Planes<PREC>::XPL, QPL = 2;
@@ -97,6 +141,30 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
         }
         s_sh[i] = 0;
         s_thr[i] = -INFINITY;
+    }
+    // the pilot's bound (pilot2_scores_kernel filled the slots): every workgroup derives it for
+    // its query block into s_sh; range 0 also raises gthr, which the finish pass reads (it must
+    // cover every bound a workgroup dropped rows against)
+    if (prank > 0) {
+        __syncthreads();
+        constexpr int QW = QB / NW;  // queries per wave: all their slots loaded before the first
+        uint32_t pv[QW][PILOT_E];    // selection (one round trip, not QW of them)
+#pragma unroll
+        for (int i = 0; i < QW; ++i) {
+            const int q = qb * QB + wv + NW * i;
+#pragma unroll
+            for (int e = 0; e < PILOT_E; ++e) pv[i][e] = q < B ? pslots[(size_t)q * PILOT_SLOTS + e * 64 + lane] : 0u;
+        }
+#pragma unroll
+        for (int i = 0; i < QW; ++i) {
+            const int ql = wv + NW * i;
+            if (qb * QB + ql >= B) break;
+            const uint32_t T = pilot_slot_rank(pv[i], prank);
+            if (lane == 0 && T != 0u) {
+                s_sh[ql] = T;
+                if (wg == 0) atomicMax(gthr + qb * QB + ql, T);
+            }
+        }
     }
     const float* Qbase = Qs + s2_blk((uint64_t)(qb * QT), 0, G + QG_EXTRA);
     if constexpr (QLDS) {
@@ -524,9 +592,9 @@ hipError_t launch_pilot2(int prec, int metric, int KP, const float* Xs, const fl
     VDB_PILOT2(2, 0, 2) VDB_PILOT2(2, 1, 2) VDB_PILOT2(2, 0, 1) VDB_PILOT2(2, 1, 1)
 #undef VDB_PILOT2
     if (!launched) return hipErrorInvalidValue;
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    return launch_pilot_bound(pslots, B, KP, gthr, st);
+    (void)KP;
+    (void)gthr;  // the bound itself is taken by the candidate pass (scan2_kernel, pilot_slot_rank)
+    return hipGetLastError();
 }
 
 // =============================================================================
@@ -543,7 +611,7 @@ template <int P, int M, int QT, int PX, int KP, int CAP, bool NT, bool QL, bool 
 static hipError_t scan2_launch(const float* Xs, const float* rinit, const uint32_t* mask, const float* Qs, int G,
                                int64_t N, int B, int n_qblocks, int64_t n_steps, int n_wg, int spw, float* gl_s,
                                uint32_t* gl_i, uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr, uint32_t* gslots,
-                               hipStream_t st) {
+                               const uint32_t* pslots, int prank, hipStream_t st) {
     auto k = scan2_kernel<P, M, QT, PX, KP, CAP, NT, QL, FS>;
     const size_t lds = QL ? (size_t)G * 2 * QT * 1024 : 0;
     if (QL) {
@@ -560,18 +628,19 @@ static hipError_t scan2_launch(const float* Xs, const float* rinit, const uint32
     }
     const int n_wg8 = (n_wg + 7) / 8 * 8;
     hipLaunchKernelGGL(k, dim3(n_wg8 * n_qblocks), dim3(256), lds, st, Xs, rinit, mask, Qs, G, N, B, n_steps, spw,
-                       n_qblocks, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots);
+                       n_qblocks, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, pslots, prank);
     return hipGetLastError();
 }
 
 hipError_t launch_scan2(int prec, int metric, int KP, const float* Xs, const float* rinit, const uint32_t* mask,
                         const float* Qs, int G, int64_t N, int B, int n_qblocks, int64_t n_steps, int n_wg, int spw,
                         float* gl_s, uint32_t* gl_i, uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr,
-                        uint32_t* gslots, int lockstep, hipStream_t st) {
+                        uint32_t* gslots, const uint32_t* pslots, int prank, int lockstep, hipStream_t st) {
     const bool ql = scan2_qlds(G, KP);
     const bool fs = !lockstep;
     const bool nt = !ql && n_qblocks == 1 && !fs;
-#define S2_ARGS Xs, rinit, mask, Qs, G, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, st
+#define S2_ARGS Xs, rinit, mask, Qs, G, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, \
+                pslots, prank, st
 #define S2_ONE(P, M, KPV, QTV, PXV, CAPV, NTV, QLV, FSV)                                              \
     if (prec == P && metric == M && KP == KPV && nt == NTV && ql == QLV && fs == FSV)                \
         return scan2_launch<P, M, QTV, PXV, KPV, CAPV, NTV, QLV, FSV>(S2_ARGS);
