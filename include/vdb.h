@@ -200,6 +200,12 @@ int32_t vdb_graph_build(vdb_index* idx, int32_t degree, int32_t knn, int32_t n_e
 int32_t vdb_graph_import(vdb_index* idx, int32_t degree, int64_t n, const int32_t* nbr, int32_t n_entries,
                          const int32_t* entries, vdb_graph** out);
 int32_t vdb_graph_export(const vdb_graph* g, int32_t* nbr_host, int32_t* entries_host);
+/* Incremental maintenance (replaces the rebuild per add of
+ * service/optimized_vector_store.py:110-112): inserts the rows the index gained since the
+ * graph was built or last extended (exact kNN of the new rows, hnswlib's heuristic for their
+ * out-edges, re-selection of every list that gains an in-edge).  A graph must be extended
+ * before it is searched again after its index grew (vdb_graph_search reports it stale). */
+int32_t vdb_graph_add(vdb_graph* g);
 int32_t vdb_graph_info(const vdb_graph* g, int64_t* n_rows, int32_t* degree, int32_t* n_entries);
 /* hnswlib knn_query semantics (hnsw_index.py:98-101): labels [n_queries, k] int64
  * (-1 = none), distances [n_queries, k] fp32: cosine 1 - cos, euclidean squared L2;

@@ -16,6 +16,7 @@
 #include <cstring>
 #include <mutex>
 #include <set>
+#include <unordered_map>
 #include <shared_mutex>
 #include <string>
 #include <vector>
@@ -1070,12 +1071,13 @@ int32_t vdb_topk_scores(const float* scores, int32_t rows, int64_t n, int32_t k,
 struct vdb_graph {
     vdb_index* ix = nullptr;
     int R = 0;
+    int knn = 0;                 // kNN candidates per row of the build (vdb_graph_add reuses it)
     int64_t n = 0;
+    int64_t cap = 0;             // rows the device neighbour array holds
     int n_entries = 0;
-    int32_t* nbr = nullptr;      // device [n][R]
+    int32_t* nbr = nullptr;      // device [cap][R]
     int32_t* entries = nullptr;  // device [n_entries]
-    float* rows = nullptr;       // device [n][Dp] row-major copy of the corpus (gathers)
-    int Dp = 0;
+    std::vector<int32_t> h_nbr;  // host mirror [n][R] (incremental updates re-prune from it)
     int teams = 1;               // workgroups per query (vdb_graph_set_param "teams")
     unsigned long long* d_stats = nullptr;
     std::atomic<int64_t> n_queries{0};
@@ -1088,18 +1090,13 @@ int graph_upload(vdb_index* ix, int R, int64_t n, const int32_t* nbr_host, const
     vdb_graph* g = new vdb_graph();
     g->ix = ix;
     g->R = R;
+    g->knn = R;
     g->n = n;
+    g->cap = std::max<int64_t>(n, 1);
     g->n_entries = n_ent;
-    hipError_t e = hipMalloc(&g->nbr, (size_t)std::max<int64_t>(n, 1) * R * sizeof(int32_t));
+    hipError_t e = hipMalloc(&g->nbr, (size_t)g->cap * R * sizeof(int32_t));
     if (e == hipSuccess) e = hipMalloc(&g->entries, (size_t)std::max(n_ent, 1) * sizeof(int32_t));
     if (e == hipSuccess) e = hipMalloc(&g->d_stats, 64);
-    g->Dp = (ix->dim + 31) / 32 * 32;
-    if (e == hipSuccess) e = hipMalloc(&g->rows, (size_t)std::max<int64_t>(n, 1) * g->Dp * sizeof(float));
-    if (e == hipSuccess) {
-        std::shared_lock<std::shared_mutex> lk(ix->mu);
-        e = launch_graph_rows(ix->X, ix->G, n, g->Dp, g->rows, ix->stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(ix->stream);
-    }
     if (e == hipSuccess) e = hipMemset(g->d_stats, 0, 64);
     if (e == hipSuccess && n > 0) e = hipMemcpy(g->nbr, nbr_host, (size_t)n * R * sizeof(int32_t), hipMemcpyHostToDevice);
     if (e == hipSuccess && n_ent > 0)
@@ -1108,13 +1105,98 @@ int graph_upload(vdb_index* ix, int R, int64_t n, const int32_t* nbr_host, const
         (void)hipFree(g->nbr);
         (void)hipFree(g->entries);
         (void)hipFree(g->d_stats);
-        (void)hipFree(g->rows);
         delete g;
         return set_error(e == hipErrorOutOfMemory ? VDB_ERR_OOM : VDB_ERR_HIP, "graph upload failed: %s",
                          hipGetErrorString(e));
     }
+    g->h_nbr.assign(nbr_host, nbr_host + (size_t)n * R);
     *out = g;
     return VDB_OK;
+}
+
+// Exact kNN (kk incl. the row itself) of rows [r0, r1) over the whole index: the brute-force
+// path with the rows as queries, 512 per launch.  kid [(r1 - r0) * kk] on the host.
+int graph_knn(vdb_index* ix, int64_t r0, int64_t r1, int kk, std::vector<int64_t>& kid) {
+    const int Bq = 512;
+    const int D = ix->dim;
+    kid.assign((size_t)(r1 - r0) * kk, -1);
+    float* qbuf = nullptr;
+    float* dsc = nullptr;
+    int64_t* did = nullptr;
+    hipStream_t st = ix->stream;
+    hipError_t e = hipMalloc(&qbuf, (size_t)Bq * D * sizeof(float));
+    if (e == hipSuccess) e = hipMalloc(&dsc, (size_t)Bq * kk * sizeof(float));
+    if (e == hipSuccess) e = hipMalloc(&did, (size_t)Bq * kk * sizeof(int64_t));
+    int rc = e == hipSuccess ? VDB_OK : set_error(VDB_ERR_OOM, "graph build buffers: %s", hipGetErrorString(e));
+    for (int64_t q0 = r0; rc == VDB_OK && q0 < r1; q0 += Bq) {
+        const int m = (int)std::min<int64_t>(Bq, r1 - q0);
+        {
+            std::shared_lock<std::shared_mutex> g(ix->mu);
+            e = launch_unpack_rows(ix->X, ix->G, D, q0, m, qbuf, st);
+        }
+        if (e != hipSuccess) {
+            rc = set_error(VDB_ERR_HIP, "graph build: %s", hipGetErrorString(e));
+            break;
+        }
+        rc = vdb_index_search(ix, qbuf, m, kk, nullptr, VDB_MEM_DEVICE, dsc, did, nullptr, 0, st);
+        if (rc) break;
+        e = hipMemcpyAsync(kid.data() + (size_t)(q0 - r0) * kk, did, (size_t)m * kk * sizeof(int64_t),
+                           hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) rc = set_error(VDB_ERR_HIP, "graph build: %s", hipGetErrorString(e));
+    }
+    (void)hipFree(qbuf);
+    (void)hipFree(dsc);
+    (void)hipFree(did);
+    return rc;
+}
+
+// graph_prune over n work items: candidate rows cv [n][cw] (-1 padded), optional node ids
+// (else items 0..n), results hn [n][limit] (and distances hd).
+int graph_prune_host(vdb_index* ix, const std::vector<int32_t>& cv, int cw, const std::vector<int32_t>* nodes,
+                     int64_t n, int limit, int fill, int sort, int32_t* hn, float* hd) {
+    if (n <= 0) return VDB_OK;
+    hipStream_t st = ix->stream;
+    int32_t *dcand = nullptr, *dnbr = nullptr, *dnodes = nullptr;
+    float* ddist = nullptr;
+    hipError_t e = hipMalloc(&dcand, (size_t)n * cw * sizeof(int32_t));
+    if (e == hipSuccess) e = hipMalloc(&dnbr, (size_t)n * limit * sizeof(int32_t));
+    if (e == hipSuccess) e = hipMalloc(&ddist, (size_t)n * limit * sizeof(float));
+    if (e == hipSuccess && nodes) e = hipMalloc(&dnodes, (size_t)n * sizeof(int32_t));
+    if (e == hipSuccess) e = hipMemcpyAsync(dcand, cv.data(), (size_t)n * cw * sizeof(int32_t), hipMemcpyHostToDevice, st);
+    if (e == hipSuccess && nodes)
+        e = hipMemcpyAsync(dnodes, nodes->data(), (size_t)n * sizeof(int32_t), hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) {
+        GraphPruneArgs pa;
+        std::shared_lock<std::shared_mutex> g(ix->mu);
+        pa.X = ix->X; pa.G = ix->G;
+        pa.rowscale = ix->metric == VDB_METRIC_COSINE ? ix->inv32 : ix->sq32;
+        pa.cand = dcand; pa.cw = cw; pa.n_nodes = n; pa.limit = limit; pa.rw = limit; pa.fill = fill;
+        pa.out_nbr = dnbr; pa.out_dist = ddist; pa.nodes = dnodes; pa.sort = sort;
+        e = launch_graph_prune(ix->metric, pa, st);
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(hn, dnbr, (size_t)n * limit * sizeof(int32_t), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess && hd) e = hipMemcpyAsync(hd, ddist, (size_t)n * limit * sizeof(float), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    (void)hipFree(dcand);
+    (void)hipFree(dnbr);
+    (void)hipFree(ddist);
+    (void)hipFree(dnodes);
+    return e == hipSuccess ? VDB_OK : set_error(VDB_ERR_HIP, "graph prune: %s", hipGetErrorString(e));
+}
+
+// Candidate rows of rows [r0, r1) from their kNN lists (self and -1 dropped), cw per row.
+std::vector<int32_t> knn_candidates(const std::vector<int64_t>& kid, int64_t r0, int64_t r1, int kk, int cw) {
+    std::vector<int32_t> cand((size_t)(r1 - r0) * cw, -1);
+    for (int64_t i = r0; i < r1; ++i) {
+        int c = 0;
+        for (int j = 0; j < kk && c < cw; ++j) {
+            const int64_t v = kid[(size_t)(i - r0) * kk + j];
+            if (v < 0 || v == i) continue;
+            cand[(size_t)(i - r0) * cw + c++] = (int32_t)v;
+        }
+    }
+    return cand;
 }
 
 }  // namespace
@@ -1132,130 +1214,162 @@ int32_t vdb_graph_build(vdb_index* ix, int32_t degree, int32_t knn, int32_t n_en
     if (N > 0x7FFFFFFF) return set_error(VDB_ERR_INVALID, "graph rows are int32");
     const int R = degree, F = degree / 2;
     const int kk = (int)std::min<int64_t>(knn + 1, std::max<int64_t>(N, 1));  // + the row itself
-    const int D = ix->dim;
     std::vector<int32_t> nbr((size_t)N * R, -1);
     if (N > 1) {
         // 1. exact kNN of every row (the brute-force path, rows as queries)
-        const int Bq = 512;
-        std::vector<int64_t> kid((size_t)N * kk);
-        std::vector<float> ksc((size_t)N * kk);
-        float* qbuf = nullptr;
-        float* dsc = nullptr;
-        int64_t* did = nullptr;
-        hipStream_t st = ix->stream;
-        hipError_t e = hipMalloc(&qbuf, (size_t)Bq * D * sizeof(float));
-        if (e == hipSuccess) e = hipMalloc(&dsc, (size_t)Bq * kk * sizeof(float));
-        if (e == hipSuccess) e = hipMalloc(&did, (size_t)Bq * kk * sizeof(int64_t));
-        int rc = e == hipSuccess ? VDB_OK : set_error(VDB_ERR_OOM, "graph build buffers: %s", hipGetErrorString(e));
-        for (int64_t r0 = 0; rc == VDB_OK && r0 < N; r0 += Bq) {
-            const int m = (int)std::min<int64_t>(Bq, N - r0);
-            {
-                std::shared_lock<std::shared_mutex> g(ix->mu);
-                e = launch_unpack_rows(ix->X, ix->G, D, r0, m, qbuf, st);
-            }
-            if (e != hipSuccess) {
-                rc = set_error(VDB_ERR_HIP, "graph build: %s", hipGetErrorString(e));
-                break;
-            }
-            rc = vdb_index_search(ix, qbuf, m, kk, nullptr, VDB_MEM_DEVICE, dsc, did, nullptr, 0, st);
-            if (rc) break;
-            e = hipMemcpyAsync(kid.data() + (size_t)r0 * kk, did, (size_t)m * kk * sizeof(int64_t),
-                               hipMemcpyDeviceToHost, st);
-            if (e == hipSuccess)
-                e = hipMemcpyAsync(ksc.data() + (size_t)r0 * kk, dsc, (size_t)m * kk * sizeof(float),
-                                   hipMemcpyDeviceToHost, st);
-            if (e == hipSuccess) e = hipStreamSynchronize(st);
-            if (e != hipSuccess) rc = set_error(VDB_ERR_HIP, "graph build: %s", hipGetErrorString(e));
-        }
-        (void)hipFree(qbuf);
-        (void)hipFree(dsc);
-        (void)hipFree(did);
+        std::vector<int64_t> kid;
+        int rc = graph_knn(ix, 0, N, kk, kid);
         if (rc) return rc;
         // 2. hnswlib-style selection: pass 1 keeps <= M = R/2 diverse
         //    out-edges from the kNN; pass 2 re-selects <= R from out- plus in-edges
         //    (hnswlib's level-0 lists: the node's own links plus the links of later
         //    insertions that chose it, re-pruned when they exceed 2M).
         const int CW = std::min(knn, 63);
-        std::vector<int32_t> cand((size_t)N * CW, -1);
-        for (int64_t i = 0; i < N; ++i) {
-            int c = 0;
-            for (int j = 0; j < kk && c < CW; ++j) {
-                const int64_t v = kid[(size_t)i * kk + j];
-                if (v < 0 || v == i) continue;
-                cand[(size_t)i * CW + c++] = (int32_t)v;
-            }
-        }
+        std::vector<int32_t> cand = knn_candidates(kid, 0, N, kk, CW);
         kid.clear(); kid.shrink_to_fit();
-        ksc.clear(); ksc.shrink_to_fit();
-        int32_t* dcand = nullptr;
-        int32_t* dnbr = nullptr;
-        float* ddist = nullptr;
-        e = hipMalloc(&dcand, (size_t)N * 63 * sizeof(int32_t));
-        if (e == hipSuccess) e = hipMalloc(&dnbr, (size_t)N * R * sizeof(int32_t));
-        if (e == hipSuccess) e = hipMalloc(&ddist, (size_t)N * R * sizeof(float));
-        rc = e == hipSuccess ? VDB_OK : set_error(VDB_ERR_OOM, "graph build buffers: %s", hipGetErrorString(e));
-        auto prune = [&](const std::vector<int32_t>& cv, int cw, int limit, int fill, int32_t* hn, float* hd) -> int {
-            hipError_t pe = hipMemcpyAsync(dcand, cv.data(), (size_t)N * cw * sizeof(int32_t), hipMemcpyHostToDevice, st);
-            GraphPruneArgs pa;
-            {
-                std::shared_lock<std::shared_mutex> g(ix->mu);
-                pa.X = ix->X; pa.G = ix->G;
-                pa.rowscale = ix->metric == VDB_METRIC_COSINE ? ix->inv32 : ix->sq32;
-                pa.cand = dcand; pa.cw = cw; pa.n_nodes = N; pa.limit = limit; pa.rw = limit; pa.fill = fill;
-                pa.out_nbr = dnbr; pa.out_dist = ddist;
-                if (pe == hipSuccess) pe = launch_graph_prune(ix->metric, pa, st);
-            }
-            if (pe == hipSuccess) pe = hipMemcpyAsync(hn, dnbr, (size_t)N * limit * sizeof(int32_t), hipMemcpyDeviceToHost, st);
-            if (pe == hipSuccess && hd) pe = hipMemcpyAsync(hd, ddist, (size_t)N * limit * sizeof(float), hipMemcpyDeviceToHost, st);
-            if (pe == hipSuccess) pe = hipStreamSynchronize(st);
-            return pe == hipSuccess ? VDB_OK : set_error(VDB_ERR_HIP, "graph prune: %s", hipGetErrorString(pe));
-        };
         std::vector<int32_t> fwd((size_t)N * F);
         std::vector<float> fdist((size_t)N * F);
-        if (rc == VDB_OK) rc = prune(cand, CW, F, 0, fwd.data(), fdist.data());
-        if (rc == VDB_OK) {
-            // pool of v: out-edges of v and in-edges u -> v, nearest first, <= 63
-            std::vector<int64_t> roff(N + 1, 0);
-            for (size_t t = 0; t < fwd.size(); ++t)
-                if (fwd[t] >= 0) roff[fwd[t] + 1]++;
-            for (int64_t i = 0; i < N; ++i) roff[i + 1] += roff[i];
-            std::vector<std::pair<float, int32_t>> rev(roff[N]);
-            std::vector<int64_t> rpos(roff.begin(), roff.end() - 1);
-            for (int64_t u = 0; u < N; ++u)
-                for (int j = 0; j < F; ++j) {
-                    const int32_t w = fwd[(size_t)u * F + j];
-                    if (w >= 0) rev[rpos[w]++] = {fdist[(size_t)u * F + j], (int32_t)u};
-                }
-            std::vector<int32_t> cand2((size_t)N * 63, -1);
-            std::vector<std::pair<float, int32_t>> pool;
-            for (int64_t v = 0; v < N; ++v) {
-                pool.clear();
-                for (int j = 0; j < F; ++j)
-                    if (fwd[(size_t)v * F + j] >= 0) pool.push_back({fdist[(size_t)v * F + j], fwd[(size_t)v * F + j]});
-                pool.insert(pool.end(), rev.begin() + roff[v], rev.begin() + roff[v + 1]);
-                std::sort(pool.begin(), pool.end(), [](const std::pair<float, int32_t>& x, const std::pair<float, int32_t>& y) {
-                    return x.first < y.first || (x.first == y.first && x.second < y.second);
-                });
-                int c = 0;
-                int32_t* row = cand2.data() + (size_t)v * 63;
-                for (size_t t = 0; t < pool.size() && c < 63; ++t) {
-                    bool dup = false;
-                    for (int q = c - 1; q >= 0 && !dup; --q) dup = row[q] == pool[t].second;
-                    if (!dup) row[c++] = pool[t].second;
-                }
+        rc = graph_prune_host(ix, cand, CW, nullptr, N, F, 0, 0, fwd.data(), fdist.data());
+        if (rc) return rc;
+        cand.clear(); cand.shrink_to_fit();
+        // pool of v: out-edges of v and in-edges u -> v, nearest first, <= 63
+        std::vector<int64_t> roff(N + 1, 0);
+        for (size_t t = 0; t < fwd.size(); ++t)
+            if (fwd[t] >= 0) roff[fwd[t] + 1]++;
+        for (int64_t i = 0; i < N; ++i) roff[i + 1] += roff[i];
+        std::vector<std::pair<float, int32_t>> rev(roff[N]);
+        std::vector<int64_t> rpos(roff.begin(), roff.end() - 1);
+        for (int64_t u = 0; u < N; ++u)
+            for (int j = 0; j < F; ++j) {
+                const int32_t w = fwd[(size_t)u * F + j];
+                if (w >= 0) rev[rpos[w]++] = {fdist[(size_t)u * F + j], (int32_t)u};
             }
-            rc = prune(cand2, 63, R, (int)ix->graph_fill, nbr.data(), nullptr);
+        std::vector<int32_t> cand2((size_t)N * 63, -1);
+        std::vector<std::pair<float, int32_t>> pool;
+        for (int64_t v = 0; v < N; ++v) {
+            pool.clear();
+            for (int j = 0; j < F; ++j)
+                if (fwd[(size_t)v * F + j] >= 0) pool.push_back({fdist[(size_t)v * F + j], fwd[(size_t)v * F + j]});
+            pool.insert(pool.end(), rev.begin() + roff[v], rev.begin() + roff[v + 1]);
+            std::sort(pool.begin(), pool.end(), [](const std::pair<float, int32_t>& x, const std::pair<float, int32_t>& y) {
+                return x.first < y.first || (x.first == y.first && x.second < y.second);
+            });
+            int c = 0;
+            int32_t* row = cand2.data() + (size_t)v * 63;
+            for (size_t t = 0; t < pool.size() && c < 63; ++t) {
+                bool dup = false;
+                for (int q = c - 1; q >= 0 && !dup; --q) dup = row[q] == pool[t].second;
+                if (!dup) row[c++] = pool[t].second;
+            }
         }
-        (void)hipFree(dcand);
-        (void)hipFree(dnbr);
-        (void)hipFree(ddist);
+        rc = graph_prune_host(ix, cand2, 63, nullptr, N, R, (int)ix->graph_fill, 0, nbr.data(), nullptr);
         if (rc) return rc;
     }
     // 3. entry rows: evenly spread
     const int E = (int)std::min<int64_t>(n_entries, std::max<int64_t>(N, 1));
     std::vector<int32_t> ent(E);
     for (int i = 0; i < E; ++i) ent[i] = (int32_t)((int64_t)i * N / E);
-    return graph_upload(ix, R, N, nbr.data(), ent.data(), N > 0 ? E : 0, out);
+    const int rc = graph_upload(ix, R, N, nbr.data(), ent.data(), N > 0 ? E : 0, out);
+    if (rc == VDB_OK) (*out)->knn = knn;
+    return rc;
+}
+
+// Incremental insertion of the rows the index gained since the graph was built (hnswlib
+// inserts one row at a time; here a whole batch): exact kNN of the new rows over all rows,
+// pass-1 selection of their out-edges, then every node that gains an in-edge (old or new)
+// re-selects <= R from its current list plus the new in-edges (pass 2 with the candidates
+// ordered by distance in the kernel).  Old rows' other links are kept.
+int32_t vdb_graph_add(vdb_graph* g) {
+    if (!g) return set_error(VDB_ERR_INVALID, "graph is NULL");
+    vdb_index* ix = g->ix;
+    HIP_TRY(hipSetDevice(ix->device));
+    const int64_t n0 = g->n, N = ix->count;
+    if (N < n0) return set_error(VDB_ERR_INVALID, "index has fewer rows (%lld) than the graph (%lld)", (long long)N,
+                                 (long long)n0);
+    if (N == n0) return VDB_OK;
+    if (N > 0x7FFFFFFF) return set_error(VDB_ERR_INVALID, "graph rows are int32");
+    const int R = g->R, F = std::max(1, R / 2);
+    const int knn = std::max(g->knn, F);
+    const int kk = (int)std::min<int64_t>(knn + 1, N);
+    const int64_t nn = N - n0;
+    // 1. new rows' out-edges
+    std::vector<int64_t> kid;
+    int rc = graph_knn(ix, n0, N, kk, kid);
+    if (rc) return rc;
+    const int CW = std::min(knn, 63);
+    std::vector<int32_t> cand = knn_candidates(kid, n0, N, kk, CW);
+    kid.clear(); kid.shrink_to_fit();
+    std::vector<int32_t> nodes(nn);
+    for (int64_t i = 0; i < nn; ++i) nodes[i] = (int32_t)(n0 + i);
+    std::vector<int32_t> fwd((size_t)nn * F);
+    rc = graph_prune_host(ix, cand, CW, &nodes, nn, F, 0, 0, fwd.data(), nullptr);
+    if (rc) return rc;
+    // 2. pools: affected node v -> its current list (new rows: their out-edges) + in-edges
+    std::unordered_map<int32_t, std::vector<int32_t>> in;
+    for (int64_t i = 0; i < nn; ++i)
+        for (int j = 0; j < F; ++j) {
+            const int32_t w = fwd[(size_t)i * F + j];
+            if (w >= 0) in[w].push_back((int32_t)(n0 + i));
+        }
+    std::vector<int32_t> aff(nodes);
+    for (const auto& kv : in)
+        if (kv.first < n0) aff.push_back(kv.first);
+    std::vector<int32_t> cand2(aff.size() * 63, -1);
+    for (size_t a = 0; a < aff.size(); ++a) {
+        const int32_t v = aff[a];
+        int32_t* row = cand2.data() + a * 63;
+        int c = 0;
+        auto push = [&](int32_t u) {
+            if (u < 0 || u == v || c >= 63) return;
+            for (int q = 0; q < c; ++q)
+                if (row[q] == u) return;
+            row[c++] = u;
+        };
+        if (v >= n0) {
+            for (int j = 0; j < F; ++j) push(fwd[(size_t)(v - n0) * F + j]);
+        } else {
+            for (int j = 0; j < R; ++j) push(g->h_nbr[(size_t)v * R + j]);
+        }
+        auto it = in.find(v);
+        if (it != in.end())
+            for (int32_t u : it->second) push(u);
+    }
+    std::vector<int32_t> upd(aff.size() * R);
+    rc = graph_prune_host(ix, cand2, 63, &aff, (int64_t)aff.size(), R, (int)ix->graph_fill, 1, upd.data(), nullptr);
+    if (rc) return rc;
+    // 3. device array: grow (doubling) and scatter the updated lists
+    hipStream_t st = ix->stream;
+    if (N > g->cap) {
+        int64_t cap = std::max<int64_t>(g->cap * 2, 1024);
+        while (cap < N) cap *= 2;
+        int32_t* nb = nullptr;
+        HIP_TRY(hipMalloc(&nb, (size_t)cap * R * sizeof(int32_t)));
+        hipError_t e = hipMemcpyAsync(nb, g->nbr, (size_t)n0 * R * sizeof(int32_t), hipMemcpyDeviceToDevice, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) {
+            (void)hipFree(nb);
+            return set_error(VDB_ERR_HIP, "graph grow: %s", hipGetErrorString(e));
+        }
+        HIP_TRY(hipDeviceSynchronize());  // searches that read the old array are done
+        (void)hipFree(g->nbr);
+        g->nbr = nb;
+        g->cap = cap;
+    }
+    g->h_nbr.resize((size_t)N * R, -1);
+    for (size_t a = 0; a < aff.size(); ++a)
+        std::memcpy(g->h_nbr.data() + (size_t)aff[a] * R, upd.data() + a * R, R * sizeof(int32_t));
+    int32_t *dids = nullptr, *drows = nullptr;
+    hipError_t e = hipMalloc(&dids, aff.size() * sizeof(int32_t));
+    if (e == hipSuccess) e = hipMalloc(&drows, upd.size() * sizeof(int32_t));
+    if (e == hipSuccess) e = hipMemcpyAsync(dids, aff.data(), aff.size() * sizeof(int32_t), hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(drows, upd.data(), upd.size() * sizeof(int32_t), hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = launch_graph_scatter(g->nbr, R, dids, drows, (int64_t)aff.size(), st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    (void)hipFree(dids);
+    (void)hipFree(drows);
+    if (e != hipSuccess) return set_error(VDB_ERR_HIP, "graph update: %s", hipGetErrorString(e));
+    g->n = N;
+    return VDB_OK;
 }
 
 int32_t vdb_graph_import(vdb_index* ix, int32_t degree, int64_t n, const int32_t* nbr, int32_t n_entries,
@@ -1327,7 +1441,7 @@ int32_t vdb_graph_search(vdb_graph* g, const float* queries, int32_t nq, int32_t
         }
     }
     GraphSearchArgs a;
-    a.rows = g->rows; a.Dp = g->Dp; a.D = D; a.rowscale = ix->metric == 0 ? ix->inv32 : ix->sq32; a.n_rows = g->n;
+    a.rows = ix->X; a.Dp = ix->Dp; a.D = D; a.rowscale = ix->metric == 0 ? ix->inv32 : ix->sq32; a.n_rows = g->n;
     a.nbr = g->nbr; a.R = g->R; a.entries = g->entries; a.n_entries = g->n_entries;
     a.Q = Qd; a.k = k; a.ef = ef; a.out_lab = ol; a.out_dist = od; a.stats = g->d_stats;
     a.teams = T;
@@ -1385,7 +1499,6 @@ int32_t vdb_graph_destroy(vdb_graph* g) {
     (void)hipFree(g->nbr);
     (void)hipFree(g->entries);
     (void)hipFree(g->d_stats);
-    (void)hipFree(g->rows);
     delete g;
     return VDB_OK;
 }

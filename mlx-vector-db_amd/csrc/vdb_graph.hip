@@ -315,12 +315,14 @@ constexpr int GP_LD = 65;  // Gram row stride in LDS (floats)
 template <int METRIC>
 __global__ void __launch_bounds__(64 * GP_WAVES) graph_prune_kernel(GraphPruneArgs a) {
     __shared__ float s_gram[GP_WAVES][64 * GP_LD];
+    __shared__ int s_ord[GP_WAVES][64];
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
-    const int64_t v = (int64_t)blockIdx.x * GP_WAVES + wv;
-    if (v >= a.n_nodes) return;  // wave-uniform; no block barrier below
+    const int64_t it = (int64_t)blockIdx.x * GP_WAVES + wv;  // work item: candidates / output row
+    if (it >= a.n_nodes) return;  // wave-uniform; no block barrier below
+    const int64_t v = a.nodes ? (int64_t)a.nodes[it] : it;  // the node
     float* gram = s_gram[wv];
-    const int32_t* cand = a.cand + v * a.cw;
+    const int32_t* cand = a.cand + it * a.cw;
     // Gram index i: 0 = the node, i >= 1 = candidate i-1 (-1 padded at the tail)
     const int h = lane >> 5, r = lane & 31;
     const int32_t c0 = r == 0 ? -1 : (r - 1 < a.cw ? cand[r - 1] : -1);
@@ -360,11 +362,30 @@ __global__ void __launch_bounds__(64 * GP_WAVES) graph_prune_kernel(GraphPruneAr
     const float sc = a.rowscale[my_row >= 0 ? my_row : (int32_t)v];
     const float sc0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sc), 0));  // the node's
     const unsigned long long valid = __ballot(my_row >= 0);
-    uint64_t kept = 0;
+    uint64_t kept = 0, kept_r = 0;  // by lane / by visiting rank
     int nk = 0;
     const float my_d0 = METRIC == 0 ? 1.0f - gram[lane] * sc * sc0 : fmaf(-2.0f, gram[lane], sc + sc0);
-    for (int c = 1; c < 64 && nk < a.limit; ++c) {
-        if (!((valid >> c) & 1ull)) break;
+    // visiting order: lane order (candidates arrive nearest first, -1 padded at the tail) or,
+    // with a.sort, by (distance to the node, lane) computed here (candidate pools of unknown
+    // order: incremental insertion, vdb_graph_add)
+    int* ord = s_ord[wv];
+    int nvalid = 0, my_rank = lane - 1;
+    if (a.sort) {
+        nvalid = __popcll(valid & ~1ull);
+        int rank = 0;
+        for (int c2 = 1; c2 < 64; ++c2) {
+            const float d2 = __shfl(my_d0, c2, 64);
+            rank += (((valid >> c2) & 1ull) && (d2 < my_d0 || (d2 == my_d0 && c2 < lane))) ? 1 : 0;
+        }
+        my_rank = rank;
+        if (lane >= 1 && ((valid >> lane) & 1ull)) ord[rank] = lane;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    } else {
+        while (nvalid < 63 && ((valid >> (nvalid + 1)) & 1ull)) ++nvalid;
+    }
+    for (int j = 0; j < nvalid && nk < a.limit; ++j) {
+        const int c = a.sort ? ord[j] : j + 1;
         const float g = gram[c * GP_LD + lane];
         const float scc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sc), c));
         const float d0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_d0), c));
@@ -372,22 +393,24 @@ __global__ void __launch_bounds__(64 * GP_WAVES) graph_prune_kernel(GraphPruneAr
         const bool bad = ((kept >> lane) & 1ull) && dcr < d0;
         if (__ballot(bad) == 0ull) {
             kept |= 1ull << c;
+            kept_r |= 1ull << j;
             ++nk;
         }
     }
     if (a.fill) {  // hnswlib keepPrunedConnections: top up with the nearest pruned ones
-        for (int c = 1; c < 64 && nk < a.limit; ++c) {
-            if (!((valid >> c) & 1ull)) break;
+        for (int j = 0; j < nvalid && nk < a.limit; ++j) {
+            const int c = a.sort ? ord[j] : j + 1;
             if (!((kept >> c) & 1ull)) {
                 kept |= 1ull << c;
+                kept_r |= 1ull << j;
                 ++nk;
             }
         }
     }
-    const bool mine = (kept >> lane) & 1ull;
-    const int pos = __popcll(kept & ((1ull << lane) - 1ull));
-    int32_t* on = a.out_nbr + v * a.rw;
-    float* od = a.out_dist + v * a.rw;
+    const bool mine = lane >= 1 && ((kept >> lane) & 1ull);
+    const int pos = __popcll(kept_r & ((1ull << (my_rank < 0 ? 0 : my_rank)) - 1ull));  // nearest first
+    int32_t* on = a.out_nbr + it * a.rw;
+    float* od = a.out_dist + it * a.rw;
     if (mine) {
         on[pos] = my_row;
         od[pos] = my_d0;
@@ -409,23 +432,21 @@ hipError_t launch_graph_prune(int metric, const GraphPruneArgs& a, hipStream_t s
     return hipGetLastError();
 }
 
-// The graph's row-major copy of the corpus, [n][Dp] fp32 (Dp = D rounded up to 32,
-// zero padded; the index's own row-major copy is padded to 64): a gathered row is Dp/32
-// whole 128-byte lines.
-__global__ void graph_rows_kernel(const float* __restrict__ X, int G, int64_t n, int Dp, float* __restrict__ out) {
+// nbr[ids[i]][*] = rows[i][*]: one thread per entry.
+__global__ void graph_scatter_kernel(int32_t* __restrict__ nbr, int R, const int32_t* __restrict__ ids,
+                                     const int32_t* __restrict__ rows, int64_t n) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int ppr = Dp >> 2;
-    if (t >= n * ppr) return;
-    const int64_t r = t / ppr;
-    const int p = (int)(t - r * ppr);
-    const f32x4 v = p < 2 * G ? *(const f32x4*)(X + row_piece_offset((uint64_t)r, p, G)) : f32x4{0.f, 0.f, 0.f, 0.f};
-    *(f32x4*)(out + r * Dp + 4 * p) = v;
+    if (t >= n * R) return;
+    const int64_t i = t / R;
+    nbr[(int64_t)ids[i] * R + (t - i * R)] = rows[t];
 }
 
-hipError_t launch_graph_rows(const float* X, int G, int64_t n, int Dp, float* out, hipStream_t st) {
+hipError_t launch_graph_scatter(int32_t* nbr, int R, const int32_t* ids, const int32_t* rows, int64_t n,
+                                hipStream_t st) {
     if (n <= 0) return hipSuccess;
-    const int64_t total = n * (Dp >> 2);
-    hipLaunchKernelGGL(graph_rows_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, X, G, n, Dp, out);
+    const int64_t total = n * R;
+    hipLaunchKernelGGL(graph_scatter_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, nbr, R, ids, rows,
+                       n);
     return hipGetLastError();
 }
 

@@ -178,7 +178,7 @@ hipError_t launch_finalize_i64(int metric, const double* sk, const int64_t* si, 
 // Graph search (vdb_graph.hip): one workgroup per query, beam of ef over a [N][R]
 // int32 neighbour array (-1 = none), started from the best of n_entries entry rows.
 struct GraphSearchArgs {
-    const float* rows; int Dp; int D; const float* rowscale; int64_t n_rows;  // rows: [n_rows][Dp] row-major
+    const float* rows; int Dp; int D; const float* rowscale; int64_t n_rows;  // rows: the index's row-major X [.][Dp]
     const int32_t* nbr; int R; const int32_t* entries; int n_entries;
     const float* Q; int k; int ef;
     int64_t* out_lab; float* out_dist; unsigned long long* stats;
@@ -186,18 +186,24 @@ struct GraphSearchArgs {
     int64_t* tmp_lab = nullptr; float* tmp_dist = nullptr;  // teams > 1: per-team lists [nq][teams][k]
 };
 hipError_t launch_graph_search(int metric, const GraphSearchArgs& a, int nq, hipStream_t st);
-// row-major [n][Dp] copy of the tiled corpus for the graph's gathers (Dp % 32 == 0)
-hipError_t launch_graph_rows(const float* X, int G, int64_t n, int Dp, float* out, hipStream_t st);
+
 
 // Graph build: hnswlib's neighbour-selection heuristic per node over up to 63
 // candidates cand[v][0..cw) (nearest first, -1 padded at the tail); out_nbr /
 // out_dist [v][rw] get the kept rows (nearest first) and their distances
 // (cosine 1 - cos, L2 squared), -1 / +inf padded.  fill: top up with pruned ones.
+// nodes (optional): node id of work item i (else i); cand / out rows are per work item.
+// sort: visit the candidates by distance to the node (computed in the kernel) instead of
+// in the given order (the given order must then be nearest first, -1 padded at the tail).
 struct GraphPruneArgs {
     const float* X; int G; const float* rowscale;
     const int32_t* cand; int cw; int64_t n_nodes; int limit; int rw; int fill;
     int32_t* out_nbr; float* out_dist;
+    const int32_t* nodes = nullptr; int sort = 0;
 };
+// nbr[ids[i]][0..R) = rows[i][0..R) for i < n (incremental graph updates)
+hipError_t launch_graph_scatter(int32_t* nbr, int R, const int32_t* ids, const int32_t* rows, int64_t n,
+                                hipStream_t st);
 hipError_t launch_graph_prune(int metric, const GraphPruneArgs& a, hipStream_t st);
 
 // Operator slot (vdb_ops.hip): full score matrix out[B][N] of row-major X [N][D], Q [B][D]:

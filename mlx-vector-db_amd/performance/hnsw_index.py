@@ -11,9 +11,10 @@ l2 -> squared L2, hnsw_index.py:35,101), ``save_index`` / ``_load_index``,
 What differs: the graph is one level of out-degree 2M (hnswlib's
 level-0 degree) built on the GPU from the exact kNN of every row — hnswlib's
 neighbour heuristic selects <= M out-edges, then <= 2M of out- and in-edges —
-instead of hnswlib's incremental insertion, so ``ef_construction`` and
-``num_threads`` have nothing to control; the upper levels' job (a good start) is
-done by scoring 256 spread entry rows, and each query is searched by TEAMS
+instead of hnswlib's one-at-a-time insertion, so ``ef_construction`` and
+``num_threads`` have nothing to control; rows added later are inserted as a batch
+(``add_rows``, vdb_graph_add) instead of rebuilding; the upper levels' job (a good
+start) is done by scoring 256 spread entry rows, and each query is searched by TEAMS
 workgroups from disjoint slices of them.
 The file is ``hnsw_graph.npz`` (neighbour array + entry rows); hnswlib's
 ``hnsw_index.bin`` format is not produced (its compatibility is unpinned,
@@ -89,10 +90,22 @@ class ProductionHNSWIndex:
         self.save_index()
 
     def add_rows(self, native_index: _vdb.NativeIndex, first_new_row: int):
-        """The store appended rows [first_new_row, count) to `native_index`: bring the graph
-        up to date (the reference rebuilds hnswlib from scratch on every add,
-        service/optimized_vector_store.py:110-112)."""
-        self.build(None, native_index=native_index)
+        """The store appended rows [first_new_row, count) to `native_index`: insert them into
+        the graph (vdb_graph_add: kNN of the new rows, hnswlib's heuristic, re-selection of
+        the lists they link into) instead of the reference's rebuild from scratch on every
+        add (service/optimized_vector_store.py:110-112).  Builds when there is no graph on
+        these rows yet."""
+        if not isinstance(native_index, _vdb.NativeIndex):
+            logger.warning("graph path needs a single-device index; queries use brute force")
+            return
+        if self.index is None or self._native is not native_index or self.index.info()[0] != first_new_row:
+            self.build(None, native_index=native_index)
+            return
+        t0 = time.time()
+        self.index.add()
+        self.max_elements = max(self.max_elements, native_index.count())
+        logger.info("graph index: %d rows inserted in %.2f s", native_index.count() - first_new_row, time.time() - t0)
+        self.save_index()
 
     def search(self, query_data: np.ndarray, k: int, ef_search: int = 100) -> Tuple[np.ndarray, np.ndarray]:
         """hnsw_index.py:79-103: (labels uint64 [n, k], distances fp32 [n, k])."""

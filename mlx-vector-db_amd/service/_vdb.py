@@ -41,7 +41,7 @@ EXPORTED_SYMBOLS = (
     "vdb_index_set_param", "vdb_index_get_stat",
     "vdb_index_add", "vdb_index_count", "vdb_index_clear", "vdb_index_get_vectors",
     "vdb_index_search", "vdb_merge_topk", "vdb_similarity_matrix", "vdb_normalize_rows", "vdb_topk_scores",
-    "vdb_graph_build", "vdb_graph_import", "vdb_graph_export", "vdb_graph_info", "vdb_graph_search",
+    "vdb_graph_build", "vdb_graph_import", "vdb_graph_export", "vdb_graph_add", "vdb_graph_info", "vdb_graph_search",
     "vdb_graph_stat", "vdb_graph_set_param", "vdb_graph_destroy",
     "vdb_shards_create", "vdb_shards_destroy", "vdb_shards_add", "vdb_shards_count", "vdb_shards_shard_count",
     "vdb_shards_search", "vdb_shards_get_vectors", "vdb_shards_clear", "vdb_shards_reserve",
@@ -105,6 +105,7 @@ def load_library():
             "vdb_graph_build": (c_i32, [c_vp, c_i32, c_i32, c_i32, ctypes.POINTER(c_vp)]),
             "vdb_graph_import": (c_i32, [c_vp, c_i32, c_i64, c_vp, c_i32, c_vp, ctypes.POINTER(c_vp)]),
             "vdb_graph_export": (c_i32, [c_vp, c_vp, c_vp]),
+            "vdb_graph_add": (c_i32, [c_vp]),
             "vdb_graph_info": (c_i32, [c_vp, p_i64, ctypes.POINTER(c_i32), ctypes.POINTER(c_i32)]),
             "vdb_graph_search": (c_i32, [c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp]),
             "vdb_graph_stat": (c_i32, [c_vp, ctypes.c_char_p, p_i64]),
@@ -388,6 +389,11 @@ class NativeGraph:
         _check(index._lib.vdb_graph_import(index._h, nb.shape[1], nb.shape[0], _ptr(nb) if nb.size else None,
                                            en.size, _ptr(en) if en.size else None, ctypes.byref(h)))
         return cls(index, h)
+
+    def add(self) -> None:
+        """include/vdb.h vdb_graph_add: insert the rows the index gained since the last
+        build / add (incremental, instead of a rebuild)."""
+        _check(self._lib.vdb_graph_add(self._h))
 
     def info(self) -> Tuple[int, int, int]:
         n, d, e = ctypes.c_int64(0), ctypes.c_int32(0), ctypes.c_int32(0)

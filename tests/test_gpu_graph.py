@@ -48,6 +48,39 @@ def test_graph_recall_and_distances(vdb, metric):
     assert g.stat("queries") == nq and g.stat("iterations") > 0
 
 
+@pytest.mark.parametrize("metric", ["cosine", "euclidean"])
+def test_graph_incremental_add(vdb, metric):
+    """vdb_graph_add (the store's add path, instead of the reference's rebuild per add):
+    a graph built on 70% of the rows and extended twice reaches the recall of a graph built
+    on all rows, finds every new row from itself, and a stale graph refuses to search."""
+    rng = np.random.default_rng(41)
+    N, D, nq, k = 20000, 64, 100, 10
+    V = rng.random((N, D), dtype=np.float32)
+    Q = rng.random((nq, D), dtype=np.float32)
+    es, ei, ek = ref_cpu.exact_search(Q, V, k, metric)
+    full = vdb.NativeIndex(D, metric)
+    full.add(V)
+    r_full = _recall(vdb.NativeGraph.build(full, degree=48, knn=48).search(Q, k, ef=128)[0], ei)
+    ix = vdb.NativeIndex(D, metric)
+    ix.add(V[:14000])
+    g = vdb.NativeGraph.build(ix, degree=48, knn=48)
+    ix.add(V[14000:17000])
+    with pytest.raises(vdb.VDBError):
+        g.search(Q, k, ef=128)  # stale until extended
+    g.add()
+    ix.add(V[17000:])
+    g.add()
+    assert g.info()[0] == N
+    nb, _ = g.to_arrays()
+    assert ((nb >= -1) & (nb < N)).all() and (nb[14000:] >= 0).any(axis=1).all()
+    r_inc = _recall(g.search(Q, k, ef=128)[0], ei)
+    assert r_inc >= 0.95 and r_inc >= r_full - 0.02, (r_inc, r_full)
+    sel = np.arange(14000, N, 131)
+    labels, _ = g.search(V[sel], 1, ef=64)
+    assert (labels[:, 0] == sel).mean() >= 0.98
+    g.add()  # nothing new: no-op
+
+
 def test_graph_self_queries_and_batch_equals_single(vdb):
     rng = np.random.default_rng(32)
     V = rng.standard_normal((5000, 48)).astype(np.float32)
