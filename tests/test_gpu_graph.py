@@ -65,7 +65,7 @@ def test_graph_incremental_add(vdb, metric):
     ix.add(V[:14000])
     g = vdb.NativeGraph.build(ix, degree=48, knn=48)
     ix.add(V[14000:17000])
-    with pytest.raises(vdb.VDBError):
+    with pytest.raises(ValueError, match="stale"):
         g.search(Q, k, ef=128)  # stale until extended
     g.add()
     ix.add(V[17000:])
