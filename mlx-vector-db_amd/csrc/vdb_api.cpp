@@ -677,9 +677,14 @@ int32_t vdb_index_get_vectors(vdb_index* ix, int64_t start, int64_t n, float* ou
 // vdb_index_search with an optional global id per row (row_ids, device memory, read by
 // the result write-out): a shard of a multi-device set holds pieces of the global
 // insertion order (vdb_shards_*).
+// search_impl's answer when VDB_PREC_AUTO's bf16 pass left too many queries uncertified in a
+// host-memory search: nothing was written, the caller runs the search again in bf16x3 (two
+// candidate passes cost far less than the exact scan of most of the batch)
+constexpr int32_t kRetryBf16x3 = 1 << 20;
+
 static int32_t search_impl(vdb_index* ix, const float* queries, int32_t B, int32_t k, const uint32_t* row_mask,
                            int32_t mem, float* out_scores, int64_t* out_indices, double* out_keys,
-                           int64_t index_offset, void* stream, const int64_t* row_ids) {
+                           int64_t index_offset, void* stream, const int64_t* row_ids, bool force_b3 = false) {
     if (!ix) return set_error(VDB_ERR_INVALID, "index is NULL");
     if (B <= 0) return set_error(VDB_ERR_INVALID, "n_queries must be >= 1, got %d", B);
     if (k <= 0 || k > 1024) return set_error(VDB_ERR_INVALID, "k must be in [1, 1024], got %d", k);
@@ -710,7 +715,8 @@ static int32_t search_impl(vdb_index* ix, const float* queries, int32_t B, int32
     const int prec_req = !ix->Xs ? PREC_FP32
                          : ix->precision == VDB_PREC_BF16X3 ? PREC_BF16X3
                          : ix->precision == VDB_PREC_BF16 ? PREC_BF16
-                         : auto_prec ? (ix->auto_b3_left.load() > 0 ? PREC_BF16X3 : PREC_BF16) : PREC_FP32;
+                         : auto_prec ? (force_b3 || ix->auto_b3_left.load() > 0 ? PREC_BF16X3 : PREC_BF16)
+                                     : PREC_FP32;
     if (N > 0 && !(ix->force_exact || k > kMaxApproxK)) ix->n_by_prec[prec_req]++;
     if (auto_prec && prec_req == PREC_BF16X3) {
         int left = ix->auto_b3_left.load();
@@ -929,8 +935,12 @@ static int32_t search_impl(vdb_index* ix, const float* queries, int32_t B, int32
             n_flag = w->host_flag[0];
             ix->n_overflow += w->host_flag[1];
             if (auto_prec && prec == PREC_BF16) {
-                if (n_flag * 64 > B) auto_backoff(ix);
-                else ix->auto_period = kAutoB3Searches;  // certified: retries start short again
+                if (n_flag * 64 > B) {
+                    auto_backoff(ix);
+                    if (!ix->no_fallback) return kRetryBf16x3;
+                } else {
+                    ix->auto_period = kAutoB3Searches;  // certified: retries start short again
+                }
             }
             if (timed) {
                 const int frc = flush_timing(ix, w);
@@ -985,8 +995,12 @@ int32_t vdb_shutdown(void) {
 int32_t vdb_index_search(vdb_index* ix, const float* queries, int32_t B, int32_t k, const uint32_t* row_mask,
                          int32_t mem, float* out_scores, int64_t* out_indices, double* out_keys,
                          int64_t index_offset, void* stream) {
-    return search_impl(ix, queries, B, k, row_mask, mem, out_scores, out_indices, out_keys, index_offset, stream,
-                       nullptr);
+    int32_t rc = search_impl(ix, queries, B, k, row_mask, mem, out_scores, out_indices, out_keys, index_offset, stream,
+                             nullptr);
+    if (rc == kRetryBf16x3)
+        rc = search_impl(ix, queries, B, k, row_mask, mem, out_scores, out_indices, out_keys, index_offset, stream,
+                         nullptr, true);
+    return rc;
 }
 
 }  // extern "C"

@@ -14,6 +14,9 @@ finishes in seconds at these sizes).
       own arithmetic.  The count goes to $VDB_TEST_REPORT_DIR/c2_fp32_ref.json.
   C3  1M x 1536 cosine, B=256, k=10 (4 query blocks).
   C4  10M x 128 L2, B=512, k=100 (8 query blocks), both step-end modes of the scan.
+  C3 and C4 run the default precision (VDB_PREC_AUTO) twice: its first, bf16 pass does not
+  certify these configurations and falls back (results still exact), after which the index
+  runs bf16x3, which must certify (<= 2% fallbacks); both searches are checked.
   C5  5M x 384 graph (M=16 -> degree 32, efSearch=128), batch 1: hnswlib's distance
       conventions (performance/hnsw_index.py:35,101) checked against exact keys of the
       returned rows, recall@10 against the exact path on 100 queries.
@@ -92,7 +95,9 @@ def test_c2_exact_vs_reference_fp32_order(vdb):
     assert ix.stat("fallback_queries") == 0
     _report("c2_fp32_ref.json", {"queries": len(sub), "k": k, "positions_differing": pos_diff,
                                  "rows_differing": set_diff, "max_exact_key_gap_of_a_swap": worst,
-                                 "fp32_bound_2eps": 2 * eps32})
+                                 "fp32_bound_2eps": 2 * eps32, "precision": ix.precision,
+                                 "searches_by_precision": {p: ix.stat(f"searches_{p}")
+                                                           for p in ("bf16", "bf16x3", "fp32")}})
 
 
 def test_c3_1m_x_1536_b256(vdb):
@@ -104,19 +109,23 @@ def test_c3_1m_x_1536_b256(vdb):
         Q[b] = V[r]
     ix = vdb.NativeIndex(D, "cosine")
     ix.add(V)
-    t0 = time.perf_counter()
-    s, i, kk = ix.search(Q, k, with_keys=True)
-    dt = time.perf_counter() - t0
-    _properties(s, i, "cosine", N)
-    for b, r in plant.items():
-        assert i[b, 0] == r and s[b, 0] > 0.9999
     sub = [0, 1, 63, 64, 100, 127, 128, 191, 200, 255]  # all 4 query blocks
     es, ei, ek = ref_cpu.exact_search(Q[sub], V, k, "cosine")
-    np.testing.assert_array_equal(i[sub], ei)
-    np.testing.assert_array_equal(kk[sub], ek)
-    fb = ix.stat("fallback_queries")
-    _report("c3.json", {"fallback_queries": fb, "host_search_s": dt})
-    assert fb <= B // 50  # certified by the candidate pass (a fallback is still exact, only slower)
+    fbs, dts = [], []
+    for _ in range(2):
+        fb0 = ix.stat("fallback_queries")
+        t0 = time.perf_counter()
+        s, i, kk = ix.search(Q, k, with_keys=True)
+        dts.append(time.perf_counter() - t0)
+        fbs.append(ix.stat("fallback_queries") - fb0)
+        _properties(s, i, "cosine", N)
+        for b, r in plant.items():
+            assert i[b, 0] == r and s[b, 0] > 0.9999
+        np.testing.assert_array_equal(i[sub], ei)
+        np.testing.assert_array_equal(kk[sub], ek)
+    by_prec = {p: ix.stat(f"searches_{p}") for p in ("bf16", "bf16x3", "fp32")}
+    _report("c3.json", {"fallback_queries_per_search": fbs, "host_search_s": dts, "searches_by_precision": by_prec})
+    assert fbs[-1] <= B // 50  # certified by the candidate pass (a fallback is still exact, only slower)
 
 
 @pytest.mark.parametrize("sync", [0, 1])
@@ -132,17 +141,21 @@ def test_c4_10m_x_128_l2_b512_top100(vdb, sync):
     ix.reserve(N)
     for s0 in range(0, N, 1 << 21):
         ix.add(V[s0:s0 + (1 << 21)])
-    s, i, kk = ix.search(Q, k, with_keys=True)
-    _properties(s, i, "euclidean", N)
-    for b, r in plant.items():
-        assert i[b, 0] == r and s[b, 0] == 0.0
     sub = [0, 3, 70, 130, 200, 290, 300, 350, 450, 511]  # all 8 query blocks
     es, ei, ek = ref_cpu.exact_search(Q[sub], V, k, "euclidean")
-    np.testing.assert_array_equal(i[sub], ei)
-    np.testing.assert_array_equal(kk[sub], ek)
-    fb = ix.stat("fallback_queries")
-    _report(f"c4_sync{sync}.json", {"fallback_queries": fb})
-    assert fb <= B // 50
+    fbs = []
+    for _ in range(2):
+        fb0 = ix.stat("fallback_queries")
+        s, i, kk = ix.search(Q, k, with_keys=True)
+        fbs.append(ix.stat("fallback_queries") - fb0)
+        _properties(s, i, "euclidean", N)
+        for b, r in plant.items():
+            assert i[b, 0] == r and s[b, 0] == 0.0
+        np.testing.assert_array_equal(i[sub], ei)
+        np.testing.assert_array_equal(kk[sub], ek)
+    by_prec = {p: ix.stat(f"searches_{p}") for p in ("bf16", "bf16x3", "fp32")}
+    _report(f"c4_sync{sync}.json", {"fallback_queries_per_search": fbs, "searches_by_precision": by_prec})
+    assert fbs[-1] <= B // 50
 
 
 @pytest.mark.timeout(600)

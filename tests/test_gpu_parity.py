@@ -141,8 +141,9 @@ def test_precision_switch_keeps_results(vdb):
 @pytest.mark.parametrize("mem", ["host", "device"])
 def test_auto_precision_switches_on_fallbacks(vdb, mem):
     """VDB_PREC_AUTO runs the bf16 pass while it certifies; rows closer together than the
-    bf16 residual bound make most queries fall back, after which the next searches run
-    bf16x3 (device-memory searches: once the earlier search's counts have landed)."""
+    bf16 residual bound leave most queries uncertified, after which the next searches run
+    bf16x3 (host memory: the batch itself is rerun in bf16x3; device memory: it falls back,
+    and the switch happens once the earlier search's counts have landed)."""
     import torch
     rng = np.random.default_rng(31)
     D, N, B, k = 256, 8000, 32, 10
@@ -170,8 +171,11 @@ def test_auto_precision_switches_on_fallbacks(vdb, mem):
             np.testing.assert_array_equal(kk, ek)
         assert ix.stat("searches_bf16") >= 1
         if expect_switch:
-            assert ix.stat("fallback_queries") * 64 > B
-            assert ix.stat("searches_bf16x3") == 1
+            assert ix.stat("fallback_queries") * 64 > B  # bf16x3 cannot separate these rows either
+            # host memory: the uncertified bf16 pass is rerun at once in bf16x3, then the second
+            # search runs bf16x3; device memory: the first search falls back, the second runs bf16x3
+            assert ix.stat("searches_bf16x3") == (2 if mem == "host" else 1)
+            assert ix.stat("searches_bf16") == 1
         else:
             assert ix.stat("searches_bf16x3") == 0 and ix.stat("fallback_queries") == 0
 
