@@ -124,7 +124,7 @@ struct vdb_index {
     int64_t force_exact = 0;
     int64_t n_wg_override = 0;
     int64_t timing = 0;  // record HIP events around the candidate pass
-    int64_t pilot_tiles = 512;  // row tiles sampled by the pilot bound (0 = off)
+    int64_t pilot_tiles = -1;  // row tiles sampled by the pilot bound (0 = off, -1 = by k)
     int64_t graph_fill = 0;     // graph build: top up pruned neighbour lists (hnswlib keepPrunedConnections)
     int64_t scan_variant = 0;     // fp32 candidate pass variant (vdb_scan.hip)
     int64_t scan_variant_b3 = 0;  // bf16x3 candidate pass variant
@@ -511,7 +511,7 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
         if (value < 0 || value > 1) return set_error(VDB_ERR_INVALID, "graph_fill must be 0 or 1");
         ix->graph_fill = value;
     } else if (n == "pilot_tiles") {
-        if (value < 0 || value > 4096) return set_error(VDB_ERR_INVALID, "pilot_tiles must be in [0, 4096]");
+        if (value < -1 || value > 4096) return set_error(VDB_ERR_INVALID, "pilot_tiles must be in [-1, 4096]");
         ix->pilot_tiles = value;
     } else if (n == "timing") {
         ix->timing = value != 0;
@@ -777,19 +777,27 @@ static int32_t search_impl(vdb_index* ix, const float* queries, int32_t B, int32
     // (the largest LDS buffer of any variant; 4 x 64 for the wave-private one)
     const int64_t gl_cap = exact_all ? 0 : (int64_t)((n_wg + 7) / 8 * 8) * 512;
     bytes += (size_t)B * gl_cap * 8 + (size_t)Bp * 4 + 768;
-    const int n_pilot = (int)std::min<int64_t>(ix->pilot_tiles, round_up(N, 32) / 32);
+    // Pilot sample: 512 row tiles, more for large k (its bound then saves more insert work than
+    // the sample costs: C4, k = 100, 512 -> 4096 tiles: 89.5 K -> 96.4 K QPS, profiles/r02_ab).
+    const int64_t pilot_def = std::min<int64_t>(4096, 512 * std::max(1, k / 12));
+    const int n_pilot = (int)std::min<int64_t>(ix->pilot_tiles >= 0 ? ix->pilot_tiles : pilot_def, round_up(N, 32) / 32);
     // Rank of the pilot's bound among its sampled scores.  The KP-th best sample is a
     // guaranteed lower bound of the global KP-th best but sits at global rank ~KP N / S (C2:
     // ~2000), so the candidate pass inserts every score above that until its own buffers
     // tighten (the warm-up: 140 us of a 680 us C2 scan without a pilot, ~65 us with one).
-    // The r-th best sample with the smallest r such that the sample holds r of the global
-    // top k with probability < 1e-6 (Poisson(k S / N) tail; rows in no particular order)
-    // starts much tighter (C2: r = 6, rank ~370).  Exactness does not depend on it: rows
-    // dropped below the bound are covered by the certificate (acut >= T), which sends a
-    // query whose bound was too high to the exact path.
+    // Instead: the r-th best sample, r the smallest rank such that (1) the sample holds r of
+    // the global top k with probability < 1e-6 (Poisson(k S / N) tail; rows in no particular
+    // order), so T stays below a_k, and (2) T's expected global rank r N / S is >= 2 KP, so T
+    // mostly stays below a_KP too and the certificate's cut max(a_KP, T) is what it would be
+    // without a pilot (T near a_k failed bf16's wide certificate: C2 with 2048 tiles and rule
+    // (1) alone; the KP-based Poisson rule instead cost C2 bf16 7%, profiles/r02_ab).  C2: r = 5,
+    // T at rank ~300 instead of ~2000.  Exactness does not depend on it: rows dropped below the
+    // bound are covered by the certificate (acut >= T), which sends a query whose bound was too
+    // high to the exact path.
     int pilot_rank = KP;
     if (n_pilot > 0) {
-        const double x = (double)k * std::min<int64_t>((int64_t)n_pilot * 32, N) / (double)N;
+        const double S = (double)std::min<int64_t>((int64_t)n_pilot * 32, N);
+        const double x = (double)k * S / (double)N;
         double term = std::exp(-x), cdf = term;
         int r = 1;
         while (1.0 - cdf >= 1e-6 && r < KP) {
@@ -797,7 +805,8 @@ static int32_t search_impl(vdb_index* ix, const float* queries, int32_t B, int32
             cdf += term;
             ++r;
         }
-        pilot_rank = std::min(r, KP);
+        const int r_min = (int)std::ceil(2.0 * KP * S / (double)N);
+        pilot_rank = std::min(std::max(r, r_min), KP);
     }
     if (ix->pilot_rank_override > 0) pilot_rank = (int)std::min<int64_t>(ix->pilot_rank_override, KP);
     int rc = ws_reserve(w, bytes, st);
