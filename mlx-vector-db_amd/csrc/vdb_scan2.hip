@@ -99,16 +99,20 @@ __device__ __forceinline__ uint32_t pilot_slot_rank(uint32_t (&v)[PILOT_E], int 
     return T;
 }
 
-template <int PREC, int METRIC, int QT, int PX, int KP, int CAP, bool NT, bool QLDS, bool FLAGSYNC>
+// GC > 0: the dimension groups as a compile-time constant (short rows, C4: 8), so the group
+// loop unrolls; the runtime loop made the register allocator copy 4 of the 8 accumulator
+// tiles between register sets on every step (256 v_accvgpr_mov per step at C4).
+template <int PREC, int METRIC, int QT, int PX, int KP, int CAP, bool NT, bool QLDS, bool FLAGSYNC, int GC = 0>
 __global__ void __launch_bounds__(256, 1)
 scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, const uint32_t* __restrict__ mask,
-             const float* __restrict__ Qs, int G, int64_t N, int B, int64_t n_steps, int steps_per_wg, int n_qb,
+             const float* __restrict__ Qs, int G_arg, int64_t N, int B, int64_t n_steps, int steps_per_wg, int n_qb,
              float* __restrict__ gl_s, uint32_t* __restrict__ gl_i, uint32_t* __restrict__ gl_cnt, int64_t gl_cap,
              uint32_t* __restrict__ gthr, uint32_t* __restrict__ gslots, const uint32_t* __restrict__ pslots,
              int prank) {
     constexpr int RT = S2_RT, NW = S2_NW;
     constexpr int QB = 32 * QT;
     constexpr int XPL = Planes<PREC>::XPL, QPL = 2;
+    const int G = GC > 0 ? GC : G_arg;
     constexpr int PQ = QLDS ? 1 : PX;
     constexpr size_t GSTEP = 8 * BLOCK_FLOATS;  // consecutive groups of one super tile
     constexpr size_t PLANE = 4 * BLOCK_FLOATS;  // lo plane after hi
@@ -493,9 +497,13 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
 // =============================================================================
 // The pilot only has to produce a number: rows the candidate pass drops below the bound are
 // covered by the certificate whatever the bound is (vdb_api.cpp pilot_rank), so the pilot
-// splits a tile's dimension groups over four waves (a quarter of the dependent load chain
-// of a one-wave tile) and sums the partial accumulators through LDS.
+// splits a tile's dimension groups over W waves (a 1/W of the dependent load chain of a
+// one-wave tile) and sums the partial accumulators through LDS; a 4-wave block scores 4/W
+// tiles (W = 4 for long rows, fewer for short ones: C4's 8 groups per tile take W = 2, half
+// the blocks of one tile per block).
 constexpr int PILOT_WAVES = 4;
+
+__host__ __device__ inline int pilot2_w(int G) { return G >= 16 ? 4 : G >= 6 ? 2 : 1; }
 
 template <int PREC, int METRIC, int QT>
 __global__ void __launch_bounds__(64 * PILOT_WAVES)
@@ -505,23 +513,26 @@ pilot2_scores_kernel(const float* __restrict__ Xs, const float* __restrict__ rin
     constexpr int QB = 32 * QT;
     constexpr int XPL = Planes<PREC>::XPL;
     constexpr size_t GSTEP = 8 * BLOCK_FLOATS, PLANE = 4 * BLOCK_FLOATS;
-    __shared__ float s_part[PILOT_WAVES - 1][QT][16][64];
+    __shared__ float s_part[PILOT_WAVES][QT][16][64];
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
-    const int i = blockIdx.x;
+    const int W = pilot2_w(G);  // waves per tile (block-uniform)
+    const int part = wv % W;    // this wave's share of the tile's groups
+    const int i = blockIdx.x * (PILOT_WAVES / W) + wv / W;  // sample index
     const int qb = blockIdx.y;
-    const uint64_t t = (uint64_t)((int64_t)i * n_tiles / n_sample);
+    const bool live = i < n_sample;
+    const uint64_t t = live ? (uint64_t)((int64_t)i * n_tiles / n_sample) : 0;
     const float* xs = Xs + s2_blk(t, 0, G) + lane * 4;
     const float* qs = Qs + s2_blk((uint64_t)(qb * QT), 0, G + QG_EXTRA) + lane * 4;
     f32x16 acc[1][QT];
-    const float r1 = (METRIC == 1 && wv == 0 && lane < 32) ? rinit[t * 32 + lane] : 0.0f;
+    const float r1 = (METRIC == 1 && part == 0 && lane < 32) ? rinit[t * 32 + lane] : 0.0f;
 #pragma unroll
     for (int qt = 0; qt < QT; ++qt) {
 #pragma unroll
         for (int v = 0; v < 16; ++v) acc[0][qt][v] = 0.0f;
         if (METRIC == 1) acc[0][qt] = __builtin_amdgcn_mfma_f32_32x32x2f32(r1, lane < 32 ? 1.0f : 0.0f, acc[0][qt], 0, 0, 0);
     }
-    // wave wv: groups wv, wv + 4, ...; PP of them in flight
+    // groups part, part + W, ...; PP of them in flight
     constexpr int PP = 4;
     f32x4 xr[PP][1][XPL], qr[PP][QT][2];
     auto load = [&](int slot, int g) {
@@ -536,31 +547,30 @@ pilot2_scores_kernel(const float* __restrict__ Xs, const float* __restrict__ rin
         }
     };
 #pragma unroll
-    for (int p = 0; p < PP; ++p) load(p, wv + PILOT_WAVES * p);
-    for (int g0 = wv; g0 < G; g0 += PILOT_WAVES * PP) {
+    for (int p = 0; p < PP; ++p) load(p, part + W * p);
+    for (int g0 = part; g0 < G; g0 += W * PP) {
 #pragma unroll
         for (int p = 0; p < PP; ++p) {
-            const int g = g0 + PILOT_WAVES * p;
+            const int g = g0 + W * p;
             if (g < G) {
                 group_mfma<PREC, 1, QT>(xr[p], qr[p], acc);
-                load(p, g + PILOT_WAVES * PP);
+                load(p, g + W * PP);
             }
         }
     }
-    if (wv > 0) {
+    if (part > 0) {
 #pragma unroll
         for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
-            for (int v = 0; v < 16; ++v) s_part[wv - 1][qt][v][lane] = acc[0][qt][v];
+            for (int v = 0; v < 16; ++v) s_part[wv][qt][v][lane] = acc[0][qt][v];
     }
     __syncthreads();
-    if (wv > 0) return;
-#pragma unroll
-    for (int w = 0; w < PILOT_WAVES - 1; ++w)
+    if (part > 0 || !live) return;
+    for (int w = 1; w < W; ++w)
 #pragma unroll
         for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
-            for (int v = 0; v < 16; ++v) acc[0][qt][v] += s_part[w][qt][v][lane];
+            for (int v = 0; v < 16; ++v) acc[0][qt][v] += s_part[wv + w][qt][v][lane];
     const uint32_t valid = tile_valid16(mask, (int64_t)t, N, lane);
 #pragma unroll
     for (int qt = 0; qt < QT; ++qt) {
@@ -580,7 +590,8 @@ hipError_t launch_pilot2(int prec, int metric, int KP, const float* Xs, const fl
     const int64_t n_tiles = (N + 31) / 32;
     if (n_sample > n_tiles) n_sample = (int)n_tiles;
     if (n_sample <= 0 || KP > PILOT_SLOTS) return hipSuccess;
-    const dim3 grid(n_sample, n_qblocks);
+    const int tpb = PILOT_WAVES / pilot2_w(G);  // tiles per block
+    const dim3 grid((n_sample + tpb - 1) / tpb, n_qblocks);
     bool launched = false;
 #define VDB_PILOT2(P, M, QTV)                                                                                     \
     if (!launched && prec == P && metric == M && QB == 32 * QTV) {                                                \
@@ -607,12 +618,12 @@ int scan2_qb(int KP) { return KP == 256 ? 32 : 64; }
 // The query block goes to LDS when it is small (C4: 64 queries x 128 dims = 32 KiB).
 bool scan2_qlds(int G16, int KP) { return (size_t)G16 * 2 * (scan2_qb(KP) / 32) * 1024 <= 32 * 1024; }
 
-template <int P, int M, int QT, int PX, int KP, int CAP, bool NT, bool QL, bool FS>
-static hipError_t scan2_launch(const float* Xs, const float* rinit, const uint32_t* mask, const float* Qs, int G,
-                               int64_t N, int B, int n_qblocks, int64_t n_steps, int n_wg, int spw, float* gl_s,
-                               uint32_t* gl_i, uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr, uint32_t* gslots,
-                               const uint32_t* pslots, int prank, hipStream_t st) {
-    auto k = scan2_kernel<P, M, QT, PX, KP, CAP, NT, QL, FS>;
+template <int P, int M, int QT, int PX, int KP, int CAP, bool NT, bool QL, bool FS, int GC>
+static hipError_t scan2_launch_g(const float* Xs, const float* rinit, const uint32_t* mask, const float* Qs, int G,
+                                 int64_t N, int B, int n_qblocks, int64_t n_steps, int n_wg, int spw, float* gl_s,
+                                 uint32_t* gl_i, uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr, uint32_t* gslots,
+                                 const uint32_t* pslots, int prank, hipStream_t st) {
+    auto k = scan2_kernel<P, M, QT, PX, KP, CAP, NT, QL, FS, GC>;
     const size_t lds = QL ? (size_t)G * 2 * QT * 1024 : 0;
     if (QL) {
         // the dynamic part (query block) plus the static top-k buffers must fit the 160 KiB of a
@@ -630,6 +641,24 @@ static hipError_t scan2_launch(const float* Xs, const float* rinit, const uint32
     hipLaunchKernelGGL(k, dim3(n_wg8 * n_qblocks), dim3(256), lds, st, Xs, rinit, mask, Qs, G, N, B, n_steps, spw,
                        n_qblocks, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, pslots, prank);
     return hipGetLastError();
+}
+
+// query block in LDS (short rows): the common short row (D = 128 -> 8 groups) gets its own
+// instantiation with the group count built in
+template <int P, int M, int QT, int PX, int KP, int CAP, bool NT, bool QL, bool FS>
+static hipError_t scan2_launch(const float* Xs, const float* rinit, const uint32_t* mask, const float* Qs, int G,
+                               int64_t N, int B, int n_qblocks, int64_t n_steps, int n_wg, int spw, float* gl_s,
+                               uint32_t* gl_i, uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr, uint32_t* gslots,
+                               const uint32_t* pslots, int prank, hipStream_t st) {
+    if constexpr (QL) {
+        if (G == 8)
+            return scan2_launch_g<P, M, QT, PX, KP, CAP, NT, QL, FS, 8>(Xs, rinit, mask, Qs, G, N, B, n_qblocks, n_steps,
+                                                                        n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr,
+                                                                        gslots, pslots, prank, st);
+    }
+    return scan2_launch_g<P, M, QT, PX, KP, CAP, NT, QL, FS, 0>(Xs, rinit, mask, Qs, G, N, B, n_qblocks, n_steps, n_wg,
+                                                                spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, pslots,
+                                                                prank, st);
 }
 
 hipError_t launch_scan2(int prec, int metric, int KP, const float* Xs, const float* rinit, const uint32_t* mask,
