@@ -414,6 +414,7 @@ def main():
     ix.set_param("timing", 1)
     scan0, pipe0, n0 = ix.stat("scan_ns"), ix.stat("pipeline_ns"), ix.stat("timed_searches")
     by_prec0 = {p: ix.stat(f"searches_{p}") for p in ("fp32", "bf16x3", "bf16")}
+    fb0 = ix.stat("fallback_queries")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -427,6 +428,7 @@ def main():
     n_t = ix.stat("timed_searches") - n0
     # candidate passes per arithmetic in the timed region (precision "auto" picks per search)
     by_prec = {p: ix.stat(f"searches_{p}") - by_prec0[p] for p in by_prec0}
+    fb_timed = ix.stat("fallback_queries") - fb0
     prec = args.precision if args.precision != "auto" else max(by_prec, key=by_prec.get)
     scan_ms = (ix.stat("scan_ns") - scan0) / 1e6 / max(n_t, 1)
     pipe_ms = (ix.stat("pipeline_ns") - pipe0) / 1e6 / max(n_t, 1)
@@ -508,6 +510,7 @@ def main():
                              hbm_frac=achieved_gbs / HBM_PEAK_GBS, mfma_frac=achieved_tf / mfma_peak),
             "pipeline_ms": pipe_ms,
             "fallback_queries_total": fallback,
+            "fallback_queries_timed": fb_timed,  # (auto's bf16 probe falls back in warm-up at C3 / C4)
             "fallback_list_overflow": overflow,
         }
         if world == 1 and not args.no_cpu_baseline:

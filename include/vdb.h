@@ -74,11 +74,12 @@ enum { VDB_MEM_HOST = 0, VDB_MEM_DEVICE = 1 };
  *                    largest row residual |x - bf16(x)| (measured at ingest), so
  *                    it is wider and takes a larger candidate margin.
  *   VDB_PREC_AUTO    (default) BF16 while its certificate holds; after a search in
- *                    which more than 1/64 of the queries fell back to the exact
- *                    scan, the next 32 searches run BF16X3 (same split copy, so
- *                    switching costs nothing); each retry that falls back again
- *                    doubles that period (up to 4096).  Device-memory searches see their
- *                    fallback counts one or more searches late (no host sync). */
+ *                    which more than 1/64 of the queries were not certified, BF16X3
+ *                    until the index's rows change (add / clear; same split copy, so
+ *                    switching costs nothing).  A host-memory search reruns such a
+ *                    batch in BF16X3 at once; a device-memory search sees the counts
+ *                    a search or more late (no host sync) and its flagged queries take
+ *                    the exact path. */
 enum { VDB_PREC_FP32 = 0, VDB_PREC_BF16X3 = 1, VDB_PREC_BF16 = 2, VDB_PREC_AUTO = 3 };
 
 typedef struct vdb_index vdb_index;

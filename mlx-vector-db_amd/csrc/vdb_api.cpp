@@ -49,8 +49,7 @@ int set_error(int code, const char* fmt, ...) {
     } while (0)
 
 constexpr int64_t kRowAlign = ROW_ALIGN;   // capacity granule, a multiple of every scan step
-constexpr int kAutoB3Searches = 32;  // VDB_PREC_AUTO: BF16X3 searches after a BF16 search with fallbacks
-constexpr int kAutoB3Max = 4096;
+
 constexpr size_t kGatedExactBytes = 256u << 20;  // device-gated fallback lists sized for every query of a batch
 constexpr int kMaxApproxK = 200;          // k above this uses the exact path
 
@@ -113,11 +112,12 @@ struct vdb_index {
     int n_cu = 256;
     // knobs
     int64_t precision = VDB_PREC_AUTO;
-    // VDB_PREC_AUTO: searches left in BF16X3 after a BF16 search with many fallbacks, and the
-    // device-gated fallback total last seen (pinned mirror of d_totals[0], written by the
-    // gated exact kernel of a device-memory search and read by the next search)
-    std::atomic<int> auto_b3_left{0};
-    std::atomic<int> auto_period{kAutoB3Searches};  // doubles on every BF16 retry that falls back again
+    // VDB_PREC_AUTO: set when a BF16 search left more than 1/64 of its queries uncertified;
+    // BF16X3 from then on, until the rows change (add / clear).  (Periodic BF16 retries cost a
+    // device-memory search the exact scan of most of its batch: C4 93 ms instead of 4.4.)
+    // The device-gated fallback total last seen: pinned mirror of d_totals[0], written by the
+    // gated exact kernel of a device-memory search and read by the next search.
+    std::atomic<bool> auto_b3{false};
     std::atomic<unsigned long long> auto_seen{0};
     unsigned long long* h_totals = nullptr;
     int64_t margin = -1;  // -1 = default
@@ -139,7 +139,7 @@ struct vdb_index {
     std::atomic<int64_t> n_searches{0}, n_queries{0}, n_fallback{0}, n_overflow{0};
     std::atomic<int64_t> n_by_prec[3] = {{0}, {0}, {0}};  // candidate passes per PREC_* (VDB_PREC_AUTO's choices)
     std::atomic<int64_t> scan_ns{0}, pipe_ns{0}, n_timed{0};
-    unsigned long long* d_totals = nullptr;  // device: flagged / overflowed queries of device-gated searches
+    unsigned long long* d_totals = nullptr;  // device: flagged / overflowed / flagged-in-bf16 queries of device-gated searches
     std::shared_mutex mu;  // add/clear/reserve exclusive; search shared
     std::mutex ws_mu;
     std::vector<Workspace*> pool;
@@ -325,14 +325,6 @@ bool all_finite(const float* p, int64_t n) {
     return true;
 }
 
-// VDB_PREC_AUTO after a BF16 search with many fallbacks: the next `period` searches run
-// BF16X3, and the period doubles (up to kAutoB3Max) so data BF16 cannot certify pays for
-// a failed retry ever more rarely.
-void auto_backoff(vdb_index* ix) {
-    const int p = ix->auto_period.load();
-    ix->auto_b3_left = p;
-    ix->auto_period = std::min(2 * p, kAutoB3Max);
-}
 
 // Exact full scan for queries qlist[0..nq) (device list) -> writes outputs.
 // Bytes of the exact path's lists for nq queries (device-gated form: one list per CU).
@@ -617,6 +609,7 @@ int32_t vdb_index_add(vdb_index* ix, const float* vectors, int64_t n, int32_t me
     ix->xres_rel = xm[1];
     ix->xres_abs = xm[2];
     ix->count += n;
+    ix->auto_b3 = false;  // new rows: VDB_PREC_AUTO tries BF16 again
     return VDB_OK;
 }
 
@@ -642,6 +635,7 @@ int32_t vdb_index_clear(vdb_index* ix) {
     HIP_TRY(hipMemsetAsync(ix->d_xmax, 0, 64, ix->stream));
     HIP_TRY(hipStreamSynchronize(ix->stream));
     ix->count = 0;
+    ix->auto_b3 = false;
     ix->xmax = 0.0;
     ix->xres_rel = ix->xres_abs = 0.0;
     return VDB_OK;
@@ -710,19 +704,15 @@ static int32_t search_impl(vdb_index* ix, const float* queries, int32_t B, int32
     if (auto_prec && ix->h_totals) {  // fallbacks of earlier device-memory searches (lagged)
         const unsigned long long seen = ix->h_totals[0];
         const unsigned long long prev = ix->auto_seen.exchange(seen);
-        if (seen > prev && (seen - prev) * 64 > (unsigned long long)B) auto_backoff(ix);
+        if (seen > prev && (seen - prev) * 64 > (unsigned long long)B) ix->auto_b3 = true;
     }
     const int prec_req = !ix->Xs ? PREC_FP32
                          : ix->precision == VDB_PREC_BF16X3 ? PREC_BF16X3
                          : ix->precision == VDB_PREC_BF16 ? PREC_BF16
-                         : auto_prec ? (force_b3 || ix->auto_b3_left.load() > 0 ? PREC_BF16X3 : PREC_BF16)
+                         : auto_prec ? (force_b3 || ix->auto_b3.load() ? PREC_BF16X3 : PREC_BF16)
                                      : PREC_FP32;
     if (N > 0 && !(ix->force_exact || k > kMaxApproxK)) ix->n_by_prec[prec_req]++;
-    if (auto_prec && prec_req == PREC_BF16X3) {
-        int left = ix->auto_b3_left.load();
-        while (left > 0 && !ix->auto_b3_left.compare_exchange_weak(left, left - 1)) {
-        }
-    }
+
     int margin_def = std::max(16, k / 4);
     if (prec_req == PREC_BF16X3 && D >= 1024) margin_def = std::max(margin_def, 48);
     // bf16 (hi plane only): eps ~ the rows' bf16 residual (~1.5e-3 relative on uniform data),
@@ -929,13 +919,13 @@ static int32_t search_impl(vdb_index* ix, const float* queries, int32_t B, int32
                         HIP_TRY(hipHostMalloc(&ix->h_totals, 2 * sizeof(unsigned long long), hipHostMallocDefault));
                         ix->h_totals[0] = ix->h_totals[1] = 0;
                         unsigned long long* d = nullptr;
-                        HIP_TRY(hipMalloc(&d, 2 * sizeof(unsigned long long)));
-                        HIP_TRY(hipMemset(d, 0, 2 * sizeof(unsigned long long)));
+                        HIP_TRY(hipMalloc(&d, 3 * sizeof(unsigned long long)));  // flagged, overflowed, flagged bf16
+                        HIP_TRY(hipMemset(d, 0, 3 * sizeof(unsigned long long)));
                         ix->d_totals = d;
                     }
                 }
                 rc = run_exact(ix, w, Qd, qn64, flags + 1, B, k, md, out_s, out_i, out_k, index_offset, row_ids, st,
-                               flags, flags + B + 1, done, auto_prec ? ix->h_totals : nullptr);
+                               flags, flags + B + 1, done, auto_prec && prec == PREC_BF16 ? ix->h_totals : nullptr);
                 return rc;
             }
             HIP_TRY(hipMemcpyAsync(w->host_flag, flags, sizeof(int), hipMemcpyDeviceToHost, st));
@@ -943,13 +933,9 @@ static int32_t search_impl(vdb_index* ix, const float* queries, int32_t B, int32
             HIP_TRY(hipStreamSynchronize(st));
             n_flag = w->host_flag[0];
             ix->n_overflow += w->host_flag[1];
-            if (auto_prec && prec == PREC_BF16) {
-                if (n_flag * 64 > B) {
-                    auto_backoff(ix);
-                    if (!ix->no_fallback) return kRetryBf16x3;
-                } else {
-                    ix->auto_period = kAutoB3Searches;  // certified: retries start short again
-                }
+            if (auto_prec && prec == PREC_BF16 && n_flag * 64 > B) {
+                ix->auto_b3 = true;
+                if (!ix->no_fallback) return kRetryBf16x3;
             }
             if (timed) {
                 const int frc = flush_timing(ix, w);

@@ -583,8 +583,11 @@ exact_scan_kernel(const float* __restrict__ Q, const double* __restrict__ qn64, 
         nq = c < nq_max ? c : nq_max;
         if (totals && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
             if (c) {
-                const unsigned long long old = atomicAdd(totals, (unsigned long long)c);
-                if (tail.host_totals) tail.host_totals[0] = old + (unsigned long long)c;  // pinned host mirror
+                atomicAdd(totals, (unsigned long long)c);
+                if (tail.host_totals) {  // a bf16 search (VDB_PREC_AUTO): its own counter, mirrored to the host
+                    const unsigned long long old = atomicAdd(totals + 2, (unsigned long long)c);
+                    tail.host_totals[0] = old + (unsigned long long)c;
+                }
             }
             if (ovf && *ovf) atomicAdd(totals + 1, (unsigned long long)*ovf);
         }

@@ -145,8 +145,9 @@ hipError_t launch_finish(int metric, int KP, const FinishArgs& a, int B, hipStre
 // With a tail (device-gated form only), the workgroup that finishes a query slot's lists
 // last (done[slot] counts them; zeroed by prep_queries) merges them into mk / mi [nq][KE]
 // and writes the query's results: one launch instead of scan + merge + finalize.
-// host_totals (optional): pinned host memory that block (0, 0) updates with the new total of
-// flagged queries (VDB_PREC_AUTO reads it on the next search, without a copy or a sync).
+// host_totals (optional, bf16 searches of VDB_PREC_AUTO): block (0, 0) adds the flagged
+// count to totals[2] too and writes that total to this pinned host word (read by the next
+// search, without a copy or a sync).
 struct ExactTail {
     int* done; double* mk; uint32_t* mi; int k; int64_t index_offset;
     float* out_s; int64_t* out_i; double* out_k; const int64_t* row_ids;

@@ -88,6 +88,15 @@ class ShardedSearcher:
                 out_keys.copy_(lk)
             return
         # [G*B, k] views: gloo wants the output split along dim 0 in input-shaped chunks
-        dist.all_gather_into_tensor(g_keys.view(self.world * B, k), lk, group=self.group)
-        dist.all_gather_into_tensor(g_idx.view(self.world * B, k), li, group=self.group)
+        if q.is_cuda and dist.get_backend(self.group) == "gloo":
+            # gloo moves host memory only (tests run several ranks on one GPU this way; RCCL
+            # takes the device buffers directly)
+            hk, hi = g_keys.cpu(), g_idx.cpu()
+            dist.all_gather_into_tensor(hk.view(self.world * B, k), lk.cpu(), group=self.group)
+            dist.all_gather_into_tensor(hi.view(self.world * B, k), li.cpu(), group=self.group)
+            g_keys.copy_(hk)
+            g_idx.copy_(hi)
+        else:
+            dist.all_gather_into_tensor(g_keys.view(self.world * B, k), lk, group=self.group)
+            dist.all_gather_into_tensor(g_idx.view(self.world * B, k), li, group=self.group)
         self.merge(g_keys, g_idx, k, out_scores, out_idx, out_keys)

@@ -141,9 +141,9 @@ def test_precision_switch_keeps_results(vdb):
 @pytest.mark.parametrize("mem", ["host", "device"])
 def test_auto_precision_switches_on_fallbacks(vdb, mem):
     """VDB_PREC_AUTO runs the bf16 pass while it certifies; rows closer together than the
-    bf16 residual bound leave most queries uncertified, after which the next searches run
-    bf16x3 (host memory: the batch itself is rerun in bf16x3; device memory: it falls back,
-    and the switch happens once the earlier search's counts have landed)."""
+    bf16 residual bound leave most queries uncertified, after which the index runs bf16x3
+    until its rows change (host memory: the batch itself is rerun in bf16x3; device memory:
+    it falls back, and the switch happens once the earlier search's counts have landed)."""
     import torch
     rng = np.random.default_rng(31)
     D, N, B, k = 256, 8000, 32, 10
@@ -176,6 +176,9 @@ def test_auto_precision_switches_on_fallbacks(vdb, mem):
             # search runs bf16x3; device memory: the first search falls back, the second runs bf16x3
             assert ix.stat("searches_bf16x3") == (2 if mem == "host" else 1)
             assert ix.stat("searches_bf16") == 1
+            ix.add(V[:1])  # new rows: bf16 gets another chance
+            ix.search(Q, k)
+            assert ix.stat("searches_bf16") == 2
         else:
             assert ix.stat("searches_bf16x3") == 0 and ix.stat("fallback_queries") == 0
 
