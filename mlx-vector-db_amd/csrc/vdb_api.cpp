@@ -135,6 +135,7 @@ struct vdb_index {
     // bound kernel.  Measured (profiles/r02_ab, C2): the prologue costs the scan ~25 us (bf16)
     // / ~30 us (bf16x3) against ~5 us for the kernel, so 0 is the default.
     int64_t pilot_fused = 0;
+    int64_t finish_split = 1;  // workgroups per query in the finish kernel (tuning)
     // stats
     std::atomic<int64_t> n_searches{0}, n_queries{0}, n_fallback{0}, n_overflow{0};
     std::atomic<int64_t> n_by_prec[3] = {{0}, {0}, {0}};  // candidate passes per PREC_* (VDB_PREC_AUTO's choices)
@@ -509,6 +510,9 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
         ix->timing = value != 0;
     } else if (n == "no_fallback") {
         ix->no_fallback = value != 0;
+    } else if (n == "finish_split") {
+        if (value < 1 || value > 8) return set_error(VDB_ERR_INVALID, "finish_split must be in [1, 8]");
+        ix->finish_split = value;
     } else if (n == "pilot_fused") {
         ix->pilot_fused = value != 0;
     } else if (n == "pilot_rank") {
@@ -760,6 +764,11 @@ static int32_t search_impl(vdb_index* ix, const float* queries, int32_t B, int32
     bytes += (size_t)B * k * 20 + 768;                      // outputs (host mode)
     bytes += (size_t)(B + 64) * 4 + 256;                    // flags
     bytes += (size_t)Bp * 4 + 256;                          // gated fallback: workgroups done per query
+    // finish: optionally several workgroups per query share the exact rerank (tuning knob
+    // "finish_split"; measured at C2 bf16, B = 64: split 4 took the finish 24.5 -> 45.9 us,
+    // profiles/r02_ab, so the default is 1)
+    const int fin_split = (int)ix->finish_split;
+    bytes += fin_split > 1 ? (size_t)B * fin_split * (KP_MAX * 16 + 4) + 1024 : 0;
     bytes += (size_t)Bp * 4 + 256;                          // shared thresholds
     bytes += (size_t)Bp * (KP_MAX + PILOT_SLOTS) * 4 + 256;  // shared threshold slots + pilot slots
     const bool priv = !exact_all && !split_pass && scan_priv(prec, variant, KP);
@@ -817,6 +826,10 @@ static int32_t search_impl(vdb_index* ix, const float* queries, int32_t B, int32
     float* gl_s = c.take<float>((size_t)B * gl_cap);
     uint32_t* gl_i = c.take<uint32_t>((size_t)B * gl_cap);
     uint32_t* gl_cnt = c.take<uint32_t>(Bp);
+    double* fx_ek = fin_split > 1 ? c.take<double>((size_t)B * fin_split * KP_MAX) : nullptr;
+    uint32_t* fx_ck = fin_split > 1 ? c.take<uint32_t>((size_t)B * fin_split * KP_MAX) : nullptr;
+    uint32_t* fx_cr = fin_split > 1 ? c.take<uint32_t>((size_t)B * fin_split * KP_MAX) : nullptr;
+    int* fx_n = fin_split > 1 ? c.take<int>((size_t)B * fin_split) : nullptr;
 
     const float* Qd = queries;
     const uint32_t* md = row_mask;
@@ -906,6 +919,7 @@ static int32_t search_impl(vdb_index* ix, const float* queries, int32_t B, int32
             fa.out_s = out_s; fa.out_i = out_i; fa.out_k = out_k; fa.index_offset = index_offset;
             fa.row_ids = row_ids;
             fa.flag_count = flags; fa.flag_list = flags + 1; fa.gthr = gthr; fa.overflow_count = flags + B + 1;
+            fa.split = fin_split; fa.sx_ek = fx_ek; fa.sx_ck = fx_ck; fa.sx_cr = fx_cr; fa.sx_n = fx_n; fa.done = done;
             HIP_TRY(launch_finish(ix->metric, KP, fa, B, st));
             if (timed) HIP_TRY(hipEventRecord(tev[2], st));
             // Device-memory searches do not wait for the certificate: the exact path is

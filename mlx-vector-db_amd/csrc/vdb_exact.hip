@@ -265,19 +265,23 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
     __shared__ uint32_t s_ck[KP];
     __shared__ uint32_t s_cr[KP];
     __shared__ double s_ek[KP];
-    __shared__ int s_m;
+    __shared__ uint32_t s_ock[KP];  // split > 1: this workgroup's share of the candidates
+    __shared__ uint32_t s_ocr[KP];
+    __shared__ double s_oek[KP];
+    __shared__ int s_m, s_mown, s_last;
     __shared__ uint32_t s_ak, s_akp;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wv = tid >> 6;
     const int b = blockIdx.x;
+    const int S = a.split, sp = blockIdx.y;  // split > 1: S workgroups per query share the rerank
     FIN_STAMP(0);
     const int64_t c = min((int64_t)a.gl_cnt[b], a.gl_cap);
 #ifdef VDB_STAMP
     if (threadIdx.x == 0) g_fin_stamps[b][7] = (unsigned long long)c;
 #endif
     if (c > FIN_CAP) {
-        if (tid == 0) {
+        if (tid == 0 && sp == 0) {
             const int pos = atomicAdd(a.flag_count, 1);
             a.flag_list[pos] = b;
             if (a.overflow_count) atomicAdd(a.overflow_count, 1);
@@ -424,7 +428,33 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
     }
     __syncthreads();
     FIN_STAMP(2);
-    const int m = s_m;
+    int m = s_m;
+    // split > 1: the candidates with row % S == sp are this workgroup's (the selected set is
+    // the same in every workgroup of the query, its LDS order is not)
+    uint32_t* xr = s_cr;
+    double* xek = s_ek;
+    int mx = m;
+    if (S > 1) {
+        if (wv == 0) {
+            int base = 0;
+            for (int e0 = 0; e0 < m; e0 += 64) {
+                const int e = e0 + lane;
+                const bool mine = e < m && (int)(s_cr[e] % (uint32_t)S) == sp;
+                const unsigned long long bm = __ballot(mine);
+                if (mine) {
+                    const int pos = base + __popcll(bm & ((1ull << lane) - 1ull));
+                    s_ock[pos] = s_ck[e];
+                    s_ocr[pos] = s_cr[e];
+                }
+                base += __popcll(bm);
+            }
+            if (lane == 0) s_mown = base;
+        }
+        __syncthreads();
+        xr = s_ocr;
+        xek = s_oek;
+        mx = s_mown;
+    }
     const float* q = a.Q + (int64_t)b * a.D;
     const double qn = a.qn64[b];
     // exact keys: wave wv takes candidates wv NB, ... in batches of NB
@@ -438,13 +468,13 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
                 const int d = 4 * (mm * 64 + lane) + j;
                 qv[mm][j] = (mm < np && d < a.D) ? q[d] : 0.0f;
             }
-        for (int j0 = wv * FIN_NB4; j0 < m; j0 += FIN_WAVES * FIN_NB4) {
+        for (int j0 = wv * FIN_NB4; j0 < mx; j0 += FIN_WAVES * FIN_NB4) {
             uint32_t rows[FIN_NB4];
             double xn[FIN_NB4];
-            const int nb = min(FIN_NB4, m - j0);
+            const int nb = min(FIN_NB4, mx - j0);
 #pragma unroll
             for (int u = 0; u < FIN_NB4; ++u) {
-                rows[u] = u < nb ? s_cr[j0 + u] : 0u;
+                rows[u] = u < nb ? xr[j0 + u] : 0u;
                 xn[u] = (METRIC == 0 && u < nb) ? a.nrm64[rows[u]] : 1.0;
             }
             double keys[FIN_NB4];
@@ -452,17 +482,17 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
             if (lane == 0) {
 #pragma unroll
                 for (int u = 0; u < FIN_NB4; ++u)
-                    if (u < nb) s_ek[j0 + u] = keys[u];
+                    if (u < nb) xek[j0 + u] = keys[u];
             }
         }
     } else
-    for (int j0 = wv * FIN_NB; j0 < m; j0 += FIN_WAVES * FIN_NB) {
+    for (int j0 = wv * FIN_NB; j0 < mx; j0 += FIN_WAVES * FIN_NB) {
         uint32_t rows[FIN_NB];
         double xn[FIN_NB];
-        const int nb = min(FIN_NB, m - j0);
+        const int nb = min(FIN_NB, mx - j0);
 #pragma unroll
         for (int u = 0; u < FIN_NB; ++u) {
-            rows[u] = u < nb ? s_cr[j0 + u] : 0u;
+            rows[u] = u < nb ? xr[j0 + u] : 0u;
             xn[u] = (METRIC == 0 && u < nb) ? a.nrm64[rows[u]] : 1.0;
         }
         double keys[FIN_NB];
@@ -470,10 +500,43 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
         if (lane == 0) {
 #pragma unroll
             for (int u = 0; u < FIN_NB; ++u)
-                if (u < nb) s_ek[j0 + u] = keys[u];
+                if (u < nb) xek[j0 + u] = keys[u];
         }
     }
     __syncthreads();
+    if (S > 1) {
+        // publish this share; the workgroup that finishes the query's shares last gathers them
+        // (release: the share before the count; acquire: the other shares after it)
+        const size_t base = ((size_t)b * S + sp) * KP;
+        for (int j = tid; j < mx; j += 64 * FIN_WAVES) {
+            a.sx_ek[base + j] = s_oek[j];
+            a.sx_ck[base + j] = s_ock[j];
+            a.sx_cr[base + j] = s_ocr[j];
+        }
+        if (tid == 0) a.sx_n[(size_t)b * S + sp] = mx;
+        __syncthreads();
+        if (tid == 0) {
+            __threadfence();
+            s_last = atomicAdd(a.done + b, 1) == S - 1;
+        }
+        __syncthreads();
+        if (!s_last) return;
+        __threadfence();
+        int off = 0;
+        for (int p = 0; p < S; ++p) {
+            const int np_ = a.sx_n[(size_t)b * S + p];
+            const size_t pb = ((size_t)b * S + p) * KP;
+            for (int j = tid; j < np_; j += 64 * FIN_WAVES) {
+                s_ek[off + j] = a.sx_ek[pb + j];
+                s_ck[off + j] = a.sx_ck[pb + j];
+                s_cr[off + j] = a.sx_cr[pb + j];
+            }
+            off += np_;
+        }
+        if (tid == 0) a.done[b] = 0;  // the gated fallback counts from zero again
+        m = off;
+        __syncthreads();
+    }
     FIN_STAMP(3);
     // ranks by counting: exact (output order) and approx (certificate); TPC threads (adjacent
     // lanes) per candidate, each counting m / TPC of the others, summed by an xor butterfly
@@ -547,9 +610,11 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
 }
 
 hipError_t launch_finish(int metric, int KP, const FinishArgs& a, int B, hipStream_t st) {
+    if (a.split < 1 || (a.split > 1 && (!a.sx_ek || !a.sx_ck || !a.sx_cr || !a.sx_n || !a.done)))
+        return hipErrorInvalidValue;
 #define VDB_FIN(M, KPV)                                                                         \
     if (metric == M && KP == KPV) {                                                             \
-        hipLaunchKernelGGL((finish_kernel<M, KPV>), dim3(B), dim3(64 * FIN_WAVES), 0, st, a);   \
+        hipLaunchKernelGGL((finish_kernel<M, KPV>), dim3(B, a.split), dim3(64 * FIN_WAVES), 0, st, a); \
         return hipGetLastError();                                                               \
     }
     VDB_FIN(0, 32) VDB_FIN(0, 64) VDB_FIN(0, 128) VDB_FIN(0, 256)

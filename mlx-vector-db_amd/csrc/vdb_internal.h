@@ -134,6 +134,12 @@ struct FinishArgs {
     int* flag_count; int* flag_list; const uint32_t* gthr;
     int* overflow_count;  // lists longer than the finish kernel holds (they take the exact path)
     const int64_t* row_ids = nullptr;  // global id per row (multi-device shard), else row + index_offset
+    // split > 1: split workgroups per query share the exact rerank (rows by row % split); their
+    // shares go to sx_* [B][split][KP] (+ counts sx_n [B][split]) and the last one (done[b],
+    // zero on entry, reset on exit) ranks and writes
+    int split = 1;
+    double* sx_ek = nullptr; uint32_t* sx_ck = nullptr; uint32_t* sx_cr = nullptr; int* sx_n = nullptr;
+    int* done = nullptr;
 };
 hipError_t launch_finish(int metric, int KP, const FinishArgs& a, int B, hipStream_t st);
 

@@ -98,6 +98,18 @@ def test_normal_with_mask_and_chunked_add(vdb, metric, precision):
     _check(vdb, V, Q, 10, metric, mask=mask, chunked_add=True, precision=precision)
 
 
+@pytest.mark.parametrize("split", [2, 4])
+@pytest.mark.parametrize("metric", ["cosine", "euclidean"])
+def test_finish_split(vdb, split, metric):
+    """The finish kernel with several workgroups per query (index param finish_split): the
+    shares of the exact rerank are merged by the last workgroup; same results."""
+    rng = np.random.default_rng(split)
+    V = rng.random((30000, 200), dtype=np.float32)
+    Q = rng.random((40, 200), dtype=np.float32)
+    _check(vdb, V, Q, 25, metric, params={"finish_split": split})
+    _check(vdb, V, Q, 25, metric, precision="bf16", params={"finish_split": split})
+
+
 @pytest.mark.parametrize("sync", [1, 2])
 @pytest.mark.parametrize("metric", ["cosine", "euclidean"])
 @pytest.mark.parametrize("D,B,k", [(128, 150, 100), (384, 70, 10)])
