@@ -325,12 +325,20 @@ def main():
     ap.add_argument("--n-wg", type=int, default=None, help="candidate-pass workgroups (tuning)")
     ap.add_argument("--scan-sync", type=int, default=None,
                     help="candidate-pass step end: 1 lockstep barrier, 2 flag-gated rounds (tuning; default by D)")
+    ap.add_argument("--scan-publish", type=int, default=None,
+                    help="split pass slot publishing: -1 auto, 0 off, 1 on (tuning)")
     ap.add_argument("--pilot-tiles", type=int, default=None, help="row tiles sampled by the pilot bound (tuning)")
     ap.add_argument("--margin", type=int, default=None, help="candidates beyond k (tuning; default per precision)")
     ap.add_argument("--pilot-fused", type=int, default=None, help="split pass: 1 the scan derives the pilot bound, "
                     "0 a separate bound kernel (tuning)")
     ap.add_argument("--pilot-rank", type=int, default=None, help="rank of the pilot bound (tuning; default: Poisson rule)")
     ap.add_argument("--rows", type=int, default=None, help="override the corpus rows (exploration only)")
+    ap.add_argument("--timing", type=int, default=1,
+                    help="1: the library's HIP events around the scan in the timed region (roofline); 0: none "
+                         "(A/B of their cost; the roofline then comes from an untimed second loop)")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="single GPU: batches queued round-robin on this many HIP streams (a server's request "
+                         "streams; each batch still runs the whole search)")
     ap.add_argument("--no-fallback", action="store_true",
                     help="diagnostics only (kernel-variant timing): skip the exact fallback; results may be wrong")
     ap.add_argument("--graph-knn", type=int, default=None, help="c5: kNN candidates per row for the build")
@@ -374,6 +382,8 @@ def main():
         ix.set_param("scan_sync", args.scan_sync)
     if args.pilot_tiles is not None:
         ix.set_param("pilot_tiles", args.pilot_tiles)
+    if args.scan_publish is not None:
+        ix.set_param("scan_publish", args.scan_publish)
     if args.margin is not None:
         ix.set_param("margin", args.margin)
     if args.pilot_fused is not None:
@@ -393,14 +403,20 @@ def main():
     Bg = B * world if (world > 1 and args.scaling == "weak") else B  # global batch
     Q = np.random.default_rng(1).random((Bg, D), dtype=np.float32)  # large_scale_benchmark.py:61
     q_dev = torch.from_numpy(Q).to(dev)
-    out_s = torch.empty((Bg, k), dtype=torch.float32, device=dev)
-    out_i = torch.empty((Bg, k), dtype=torch.int64, device=dev)
-    stream = torch.cuda.current_stream(dev).cuda_stream
+    n_str = max(1, args.streams) if world == 1 else 1
+    outs = [(torch.empty((Bg, k), dtype=torch.float32, device=dev), torch.empty((Bg, k), dtype=torch.int64, device=dev))
+            for _ in range(n_str)]
+    out_s, out_i = outs[0]
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(n_str - 1)]
     searcher = ShardedSearcher.from_index(ix, lo) if world > 1 else None
+    n_step = [0]
 
     def step():
         if searcher is None:
-            ix.search_device(q_dev.data_ptr(), Bg, k, out_s.data_ptr(), out_i.data_ptr(), 0, stream=stream)
+            j = n_step[0] % n_str
+            n_step[0] += 1
+            os_, oi_ = outs[j]
+            ix.search_device(q_dev.data_ptr(), Bg, k, os_.data_ptr(), oi_.data_ptr(), 0, stream=streams[j].cuda_stream)
         else:
             searcher.search(q_dev, k, out_s, out_i)
 
@@ -411,7 +427,7 @@ def main():
     # Throughput (value): K batches queued back to back on the stream, as a server
     # keeps the device fed; device-memory searches return without a host wait
     # (DESIGN.md §3), so the host runs ahead and no step waits for its launch.
-    ix.set_param("timing", 1)
+    ix.set_param("timing", args.timing)
     scan0, pipe0, n0 = ix.stat("scan_ns"), ix.stat("pipeline_ns"), ix.stat("timed_searches")
     by_prec0 = {p: ix.stat(f"searches_{p}") for p in ("fp32", "bf16x3", "bf16")}
     fb0 = ix.stat("fallback_queries")
@@ -432,8 +448,18 @@ def main():
     prec = args.precision if args.precision != "auto" else max(by_prec, key=by_prec.get)
     scan_ms = (ix.stat("scan_ns") - scan0) / 1e6 / max(n_t, 1)
     pipe_ms = (ix.stat("pipeline_ns") - pipe0) / 1e6 / max(n_t, 1)
+    if not args.timing:  # the scan's launch time from a second (untimed) run of the same loop
+        ix.set_param("timing", 1)
+        torch.cuda.synchronize()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        n_t = ix.stat("timed_searches") - n0
+        scan_ms = (ix.stat("scan_ns") - scan0) / 1e6 / max(n_t, 1)
+        pipe_ms = (ix.stat("pipeline_ns") - pipe0) / 1e6 / max(n_t, 1)
     ix.set_param("timing", 0)
     # Latency (p50_ms): one batch at a time, each waited for
+    n_str = 1
     lat = []
     for _ in range(min(args.steps, 50)):
         t0 = time.perf_counter()
@@ -509,6 +535,7 @@ def main():
                              avg_launch_ms=scan_ms, hbm_gbs=achieved_gbs, mfma_tflops=achieved_tf,
                              hbm_frac=achieved_gbs / HBM_PEAK_GBS, mfma_frac=achieved_tf / mfma_peak),
             "pipeline_ms": pipe_ms,
+            "streams": max(1, args.streams) if world == 1 else 1,
             "fallback_queries_total": fallback,
             "fallback_queries_timed": fb_timed,  # (auto's bf16 probe falls back in warm-up at C3 / C4)
             "fallback_list_overflow": overflow,

@@ -88,6 +88,7 @@ struct Workspace {
     int t_head = 0, t_pending = 0;
     bool busy = false;
     bool used = false;
+    hipStream_t last_st = nullptr;  // stream of the last search that used it
 };
 
 }  // namespace
@@ -135,6 +136,7 @@ struct vdb_index {
     // bound kernel.  Measured (profiles/r02_ab, C2): the prologue costs the scan ~25 us (bf16)
     // / ~30 us (bf16x3) against ~5 us for the kernel, so 0 is the default.
     int64_t pilot_fused = 0;
+    int64_t scan_publish = -1;    // split pass slot publishing: -1 auto (>= 16 steps per workgroup), 0 off, 1 on
     int64_t finish_split = 1;  // workgroups per query in the finish kernel (tuning)
     // stats
     std::atomic<int64_t> n_searches{0}, n_queries{0}, n_fallback{0}, n_overflow{0};
@@ -240,17 +242,32 @@ int ensure_capacity(vdb_index* ix, int64_t rows) {
     return VDB_OK;
 }
 
-Workspace* acquire_ws(vdb_index* ix) {
+// A free workspace whose last search was queued on the same stream (stream order makes the
+// reuse safe without a wait), else one whose last search has finished, else a new one (up to
+// kMaxWs; then any free one, its reuse waiting on its last search): searches queued on several
+// streams from one host thread (a server's request streams) then run concurrently instead of
+// serialising on one workspace.
+constexpr size_t kMaxWs = 16;
+
+Workspace* acquire_ws(vdb_index* ix, hipStream_t st) {
     std::lock_guard<std::mutex> g(ix->ws_mu);
+    Workspace* idle = nullptr;
+    Workspace* any = nullptr;
     for (Workspace* w : ix->pool) {
-        if (!w->busy) {
+        if (w->busy) continue;
+        if (!w->used || w->last_st == st) {
             w->busy = true;
             return w;
         }
+        if (!idle && w->done && hipEventQuery(w->done) == hipSuccess) idle = w;
+        if (!any) any = w;
     }
-    Workspace* w = new Workspace();
+    Workspace* w = idle ? idle : ix->pool.size() >= kMaxWs ? any : nullptr;
+    if (!w) {
+        w = new Workspace();
+        ix->pool.push_back(w);
+    }
     w->busy = true;
-    ix->pool.push_back(w);
     return w;
 }
 
@@ -258,6 +275,7 @@ void release_ws(vdb_index* ix, Workspace* w, hipStream_t st) {
     if (w->done == nullptr) (void)hipEventCreateWithFlags(&w->done, hipEventDisableTiming);
     (void)hipEventRecord(w->done, st);
     w->used = true;
+    w->last_st = st;
     std::lock_guard<std::mutex> g(ix->ws_mu);
     w->busy = false;
 }
@@ -513,6 +531,9 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
     } else if (n == "finish_split") {
         if (value < 1 || value > 8) return set_error(VDB_ERR_INVALID, "finish_split must be in [1, 8]");
         ix->finish_split = value;
+    } else if (n == "scan_publish") {
+        if (value < -1 || value > 1) return set_error(VDB_ERR_INVALID, "scan_publish must be -1, 0 or 1");
+        ix->scan_publish = value;
     } else if (n == "pilot_fused") {
         ix->pilot_fused = value != 0;
     } else if (n == "pilot_rank") {
@@ -748,8 +769,13 @@ static int32_t search_impl(vdb_index* ix, const float* queries, int32_t B, int32
     // groups per step, the epilogue ~half of it) gain from dropping the per-step workgroup barrier
     // (C4 scan 7.58 -> 6.22 ms); long steps lose (C2 0.57 -> 0.65 ms, C3 2.62 -> 2.90 ms), measured.
     const int lockstep = ix->scan_sync == 0 ? (ix->Dp > 128) : ix->scan_sync == 1;
+    // Slot publishing (shared bound from the workgroups' own bests, vdb_scan2.hip) pays off
+    // over many steps (C4: 610 per workgroup); with few (C2: 8) its global round trips at
+    // steps 1, 2, 4, 8 cost more than the pilot's bound leaves to gain (measured: stamps,
+    // profiles/r02_ab/).
+    const int publish = ix->scan_publish >= 0 ? (int)ix->scan_publish : spw >= 16;
 
-    Workspace* w = acquire_ws(ix);
+    Workspace* w = acquire_ws(ix, st);
     struct Releaser {
         vdb_index* ix; Workspace* w; hipStream_t st;
         ~Releaser() { release_ws(ix, w, st); }
@@ -890,7 +916,7 @@ static int32_t search_impl(vdb_index* ix, const float* queries, int32_t B, int32
             if (split_pass)
                 HIP_TRY(launch_scan2(prec, ix->metric, KP, Xscan, ix->rinit32, md, Qt, Gs, N, B, n_qblocks, n_steps,
                                      n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, pslots,
-                                     n_pilot > 0 && ix->pilot_fused ? pilot_rank : 0, lockstep, st));
+                                     n_pilot > 0 && ix->pilot_fused ? pilot_rank : 0, lockstep, publish, st));
             else if (priv)
                 HIP_TRY(launch_scan_topk_priv(prec, ix->metric, KP, Xscan, rowscale, md, Qt, Gs, N, B, n_qblocks,
                                               n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, st));

@@ -198,11 +198,12 @@ hipError_t launch_rerank(int metric, int KP, const RerankArgs& a, int B, hipStre
 // Input: the query's global candidate list (entries the candidate pass appended
 // above its shared bound; typically tens to a few hundred).  Entries below the final
 // bound are dropped while loading; the best min(KP, n) of the rest by (approx score
-// desc, row asc) come from a radix select over all waves (no sort); all waves compute
-// exact fp64 keys, batched NB candidates per wave so the corpus loads of a batch are
-// in flight together; ranks come from counting (no sort), several threads per
-// candidate; thread 0 checks the certificate.  A list longer than FIN_CAP goes to the
-// exact scan.
+// desc, row asc) come from a radix select over all waves (no sort); thread 0 checks the
+// certificate on the approximate scores (a_k, a_KP by rank counting); then only the
+// candidates that can still be in the exact top k (approx >= a_k - 2 eps: ~2.5 k of KP = 128
+// at C2 bf16) get exact fp64 keys, all waves, batched NB candidates per wave so the corpus
+// loads of a batch are in flight together; exact ranks come from counting (no sort),
+// several threads per candidate.  A list longer than FIN_CAP goes to the exact scan.
 constexpr int FIN_CAP = 16384;  // 128 KiB of (key, row) in LDS
 constexpr int FIN_NB = 2;        // candidates per wave per batch
 constexpr int FIN_WAVES = 16;
@@ -429,6 +430,91 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
     __syncthreads();
     FIN_STAMP(2);
     int m = s_m;
+    const double qn = a.qn64[b];
+    // ---- the certificate first, from the approximate scores alone ----
+    // a_k / a_KP: the k-th / KP-th best approx key of the selection (rank counting, TPC threads
+    // per candidate).  Rows outside the candidates scored (approx) <= acut = max(a_KP, T)
+    // (DESIGN.md §3.2); with |approx - exact| <= eps per row the certificate is
+    // acut + eps < a_k - eps.
+    constexpr int TPC = KP >= 64 * FIN_WAVES ? 1 : (64 * FIN_WAVES) / KP > 64 ? 64 : (64 * FIN_WAVES) / KP;
+    for (int jt = tid; jt < KP * TPC; jt += 64 * FIN_WAVES) {
+        const int j = jt / TPC, sub = jt % TPC;
+        int ar = 0;
+        uint32_t ck = 0u, r = 0u;
+        if (j < m) {
+            ck = s_ck[j];
+            r = s_cr[j];
+            for (int i = sub; i < m; i += TPC) {
+                const uint32_t ci = s_ck[i], ri = s_cr[i];
+                ar += (ci > ck || (ci == ck && ri < r)) ? 1 : 0;
+            }
+        }
+#pragma unroll
+        for (int off = 1; off < TPC; off <<= 1) ar += __shfl_xor(ar, off, 64);
+        if (sub == 0 && j < m) {
+            if (ar == a.k - 1) s_ak = ck;
+            if (ar == KP - 1) s_akp = ck;
+        }
+    }
+    __shared__ int s_ok;
+    __shared__ double s_cut;
+    __syncthreads();
+    if (tid == 0) {
+        const bool full = m == KP;
+        const double T = (double)key_to_float(a.gthr[b]);
+        const bool have_k = m >= a.k;
+        const double ak = have_k ? (double)key_to_float(s_ak) : -INFINITY;
+        bool ok = true;
+        double eps = 0.0;
+        if (full || T > -INFINITY) {
+            const double akp = full ? (double)key_to_float(s_akp) : -INFINITY;
+            const double acut = fmax(akp, T);
+            if (METRIC == 0) {
+                eps = a.eps_rel + a.xres;
+            } else {
+                eps = a.eps_rel * (2.0 * qn * a.xmax + a.xmax * a.xmax) + 2.0 * qn * a.xres +
+                      2.4e-7 * fmax(fabs(ak), fabs(acut));
+            }
+            ok = have_k && acut + eps < ak - eps;
+        } else if (have_k) {  // the list holds every eligible row: only the rerank cut needs eps
+            eps = METRIC == 0 ? a.eps_rel + a.xres
+                              : a.eps_rel * (2.0 * qn * a.xmax + a.xmax * a.xmax) + 2.0 * qn * a.xres +
+                                    2.4e-7 * fabs(ak);
+        }
+        if (!ok && sp == 0) {
+            const int pos = atomicAdd(a.flag_count, 1);
+            a.flag_list[pos] = b;
+        }
+        s_ok = ok;
+        // Rerank cut: the k best approx rows score (exact) >= a_k - eps, so the exact k-th best
+        // is >= a_k - eps, and a row with approx < a_k - 2 eps scores (exact) < a_k - eps:
+        // only candidates with approx >= a_k - 2 eps can be in the exact top k (2.001: the L2
+        // bound's rounding term grows with |approx| below a_k).
+        s_cut = ok && have_k ? ak - 2.001 * eps : -INFINITY;
+    }
+    __syncthreads();
+    if (s_cut > -INFINITY) {
+        const double cut = s_cut;
+        if (wv == 0) {
+            int base = 0;
+            for (int e0 = 0; e0 < m; e0 += 64) {  // in-place compaction (reads run ahead of writes)
+                const int e = e0 + lane;
+                const bool in = e < m;
+                const uint32_t kk = in ? s_ck[e] : 0u, rr = in ? s_cr[e] : 0u;
+                const bool keep = in && (double)key_to_float(kk) >= cut;
+                const unsigned long long bm = __ballot(keep);
+                if (keep) {
+                    const int pos = base + __popcll(bm & ((1ull << lane) - 1ull));
+                    s_ck[pos] = kk;
+                    s_cr[pos] = rr;
+                }
+                base += __popcll(bm);
+            }
+            if (lane == 0) s_m = base;
+        }
+        __syncthreads();
+        m = s_m;
+    }
     // split > 1: the candidates with row % S == sp are this workgroup's (the selected set is
     // the same in every workgroup of the query, its LDS order is not)
     uint32_t* xr = s_cr;
@@ -456,7 +542,6 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
         mx = s_mown;
     }
     const float* q = a.Q + (int64_t)b * a.D;
-    const double qn = a.qn64[b];
     // exact keys: wave wv takes candidates wv NB, ... in batches of NB
     const int np = (a.D + 255) / 256;
     if (np <= FIN_MP) {
@@ -538,30 +623,23 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
         __syncthreads();
     }
     FIN_STAMP(3);
-    // ranks by counting: exact (output order) and approx (certificate); TPC threads (adjacent
-    // lanes) per candidate, each counting m / TPC of the others, summed by an xor butterfly
-    constexpr int TPC = KP >= 64 * FIN_WAVES ? 1 : (64 * FIN_WAVES) / KP > 64 ? 64 : (64 * FIN_WAVES) / KP;
+    // exact ranks by counting (output order), TPC threads per candidate as above
     for (int jt = tid; jt < KP * TPC; jt += 64 * FIN_WAVES) {
         const int j = jt / TPC, sub = jt % TPC;
-        int er = 0, ar = 0;
+        int er = 0;
         double ek = 0.0;
-        uint32_t ck = 0u, r = 0u;
+        uint32_t r = 0u;
         if (j < m) {
             ek = s_ek[j];
-            ck = s_ck[j];
             r = s_cr[j];
             for (int i = sub; i < m; i += TPC) {
                 const double ei = s_ek[i];
-                const uint32_t ci = s_ck[i], ri = s_cr[i];
+                const uint32_t ri = s_cr[i];
                 er += (ei > ek || (ei == ek && ri < r)) ? 1 : 0;
-                ar += (ci > ck || (ci == ck && ri < r)) ? 1 : 0;
             }
         }
 #pragma unroll
-        for (int off = 1; off < TPC; off <<= 1) {
-            er += __shfl_xor(er, off, 64);
-            ar += __shfl_xor(ar, off, 64);
-        }
+        for (int off = 1; off < TPC; off <<= 1) er += __shfl_xor(er, off, 64);
         if (sub != 0) continue;
         if (j < m) {
             if (er < a.k) {
@@ -569,8 +647,6 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
                 write_result(METRIC, ek, global_row(a.row_ids, r, a.index_offset), true, a.out_s + o, a.out_i + o,
                              a.out_k ? a.out_k + o : nullptr);
             }
-            if (ar == a.k - 1) s_ak = ck;
-            if (ar == KP - 1) s_akp = ck;
         } else if (j < a.k) {
             const size_t o = (size_t)b * a.k + j;
             write_result(METRIC, -INFINITY, 0, false, a.out_s + o, a.out_i + o, a.out_k ? a.out_k + o : nullptr);
@@ -580,32 +656,7 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
         const size_t o = (size_t)b * a.k + j;
         write_result(METRIC, -INFINITY, 0, false, a.out_s + o, a.out_i + o, a.out_k ? a.out_k + o : nullptr);
     }
-    __syncthreads();
     FIN_STAMP(4);
-    if (tid == 0) {
-        // Rows outside the candidates scored (approx) <= max(a_KP, T).
-        const bool full = m == KP;
-        const double T = (double)key_to_float(a.gthr[b]);
-        bool ok = true;
-        if (full || T > -INFINITY) {
-            const bool have_k = m >= a.k;
-            const double ak = have_k ? (double)key_to_float(s_ak) : -INFINITY;
-            const double akp = full ? (double)key_to_float(s_akp) : -INFINITY;
-            const double acut = fmax(akp, T);
-            double eps;
-            if (METRIC == 0) {
-                eps = a.eps_rel + a.xres;
-            } else {
-                eps = a.eps_rel * (2.0 * qn * a.xmax + a.xmax * a.xmax) + 2.0 * qn * a.xres +
-                      2.4e-7 * fmax(fabs(ak), fabs(acut));
-            }
-            ok = have_k && acut + eps < ak - eps;
-        }
-        if (!ok) {
-            const int pos = atomicAdd(a.flag_count, 1);
-            a.flag_list[pos] = b;
-        }
-    }
     FIN_STAMP(5);
 }
 

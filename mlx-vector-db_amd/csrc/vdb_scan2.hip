@@ -1,496 +1,8 @@
 // vdb_scan2.hip — the split-bf16 candidate pass (PREC_BF16X3, the default, and PREC_BF16):
-// MFMA scores of a 64-query block against the whole corpus fused with a per-workgroup
-// top-KP, appended to global per-query candidate lists (pipeline: vdb_scan.hip header).
-//
-// Shape, from the K-loop ablation (profiles/scripts/scan_micro2.hip, MI355X, C2 1M x 768):
-//   * 4 waves, one per SIMD; each wave owns RT = 4 row tiles (128 rows) x 2 query tiles per
-//     step: per 16-dim group 4 corpus blocks per plane (HBM, default or nt policy) and
-//     2 x 2 query blocks (L2) feed 24 (bf16x3) or 16 (bf16) v_mfma_f32_32x32x16_bf16, so
-//     the query operand costs half the bytes of the corpus operand (RT = 2: twice as many):
-//     bf16x3 K-loop 515 -> 480 us (6.25 -> 6.7 TB/s), bf16 hi plane 308 -> 252 us.
-//   * the corpus loads run PX groups ahead in registers (bf16x3 PX = 2, bf16 PX = 4: equal
-//     bytes in flight); for small D (C4: D = 128) the query block sits in LDS instead
-//     (QLDS), which takes the query loads off the vector-memory path (TA) that the corpus
-//     stream of C4's 8 query blocks already saturates.
-//   * no row scale in the epilogue: for cosine the split copy holds the NORMALISED rows
-//     (x / |x| rounded to fp32, then split; the query is normalised too), so the
-//     accumulator IS the score; for L2 the accumulator starts at -|x|^2 / 2 (rinit), so it
-//     ends at q.x - |x|^2 / 2 = score / 2.  The start value is written by one fp32 MFMA per
-//     tile (A = the rows' rinit in column 0, B = ones in row 0: exact), so a lane holds one
-//     rinit value per tile instead of the 16 its accumulator rows need.  Per 16-score tile the common case is 16
-//     accumulator reads, 8 max3 and one compare; the pass bits, row validity (mask / N)
-//     and the LDS insert run only for tiles where some lane passes.
-// Invariant for the certificate (vdb_exact.hip finish_kernel): every row not in the final
-// list scored (this arithmetic) <= max(its workgroup's KP-th best, the final shared bound).
-#include "vdb_common.h"
-#include "vdb_internal.h"
-#include "vdb_scan_common.h"
-
-#include <atomic>
+// pilot kernel, dispatch to the instantiation units (kernel: vdb_scan2_kernel.h).
+#include "vdb_scan2_kernel.h"
 
 namespace vdb {
-
-constexpr int S2_RT = 4;  // row tiles (32 rows) per wave per step
-constexpr int S2_NW = 4;  // waves per workgroup
-constexpr int S2_ROWS = S2_RT * S2_NW * 32;
-
-// row-valid bits of row tile t for this lane: bit v <-> row 32 t + (v & 3) + 8 (v >> 2) + 4 (lane >> 5)
-__device__ __forceinline__ uint32_t tile_valid16(const uint32_t* mask, int64_t t, int64_t N, int lane) {
-    uint32_t w = 0xFFFFFFFFu;
-    if (mask) w = t < ((N + 31) >> 5) ? mask[t] : 0u;
-    const int64_t rem = N - t * 32;
-    if (rem < 32) w &= rem <= 0 ? 0u : ((1u << rem) - 1u);
-    w >>= 4 * (lane >> 5);
-    return (w & 0xFu) | ((w >> 4) & 0xF0u) | ((w >> 8) & 0xF00u) | ((w >> 12) & 0xF000u);
-}
-
-__device__ __forceinline__ float tile_max16(const f32x16& a) {
-    float m = fmaxf(a[0], a[1]);
-#pragma unroll
-    for (int v = 2; v < 16; v += 2) m = fmaxf(m, fmaxf(a[v], a[v + 1]));  // -> v_max3_f32
-    return m;
-}
-
-// split-layout block of (row tile t, 16-dim group g) with GG groups: [t/4][GG][2 planes][4][1 KiB]
-__device__ __forceinline__ size_t s2_blk(uint64_t t, int g, int GG) {
-    return (((size_t)(t >> 2) * GG + g) * 8 + (t & 3)) * BLOCK_FLOATS;
-}
-
-// The pilot bound of one query (one wave): the rank-th largest of its PILOT_SLOTS pilot slots
-// (vdb_api.cpp pilot_rank), 0 when fewer slots are filled.  Small ranks by repeated wave
-// maxima (remove one copy of the maximum per round), larger ones by ballot bisection.
-constexpr int PILOT_E = PILOT_SLOTS / 64;  // slots per lane
-
-__device__ __forceinline__ uint32_t pilot_slot_rank(uint32_t (&v)[PILOT_E], int rank) {
-    constexpr int E = PILOT_E;
-    const int lane = threadIdx.x & 63;
-    int filled = 0;
-#pragma unroll
-    for (int i = 0; i < E; ++i) filled += __popcll(__ballot(v[i] != 0u));
-    if (filled < rank) return 0u;
-    if (rank <= 16) {
-        for (int r = 1;; ++r) {
-            uint32_t m = v[0];
-#pragma unroll
-            for (int i = 1; i < E; ++i) m = max(m, v[i]);
-#pragma unroll
-            for (int off = 32; off >= 1; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off, 64));
-            if (r == rank) return m;
-            // drop one copy of m: the lowest lane holding it, its first register
-            int hit = -1;
-#pragma unroll
-            for (int i = E - 1; i >= 0; --i) hit = v[i] == m ? i : hit;
-            const unsigned long long who = __ballot(hit >= 0);
-            if (lane == __ffsll((long long)who) - 1) {
-#pragma unroll
-                for (int i = 0; i < E; ++i)
-                    if (i == hit) v[i] = 0u;
-            }
-        }
-    }
-    uint32_t T = 0;
-    for (int bit = 31; bit >= 0; --bit) {
-        const uint32_t c = T | (1u << bit);
-        int n = 0;
-#pragma unroll
-        for (int i = 0; i < E; ++i) n += __popcll(__ballot(v[i] >= c));
-        if (n >= rank) T = c;
-    }
-    return T;
-}
-
-// GC > 0: the dimension groups as a compile-time constant (short rows, C4: 8), so the group
-// loop unrolls; the runtime loop made the register allocator copy 4 of the 8 accumulator
-// tiles between register sets on every step (256 v_accvgpr_mov per step at C4).
-template <int PREC, int METRIC, int QT, int PX, int KP, int CAP, bool NT, bool QLDS, bool FLAGSYNC, int GC = 0>
-__global__ void __launch_bounds__(256, 1)
-scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, const uint32_t* __restrict__ mask,
-             const float* __restrict__ Qs, int G_arg, int64_t N, int B, int64_t n_steps, int steps_per_wg, int n_qb,
-             float* __restrict__ gl_s, uint32_t* __restrict__ gl_i, uint32_t* __restrict__ gl_cnt, int64_t gl_cap,
-             uint32_t* __restrict__ gthr, uint32_t* __restrict__ gslots, const uint32_t* __restrict__ pslots,
-             int prank) {
-    constexpr int RT = S2_RT, NW = S2_NW;
-    constexpr int QB = 32 * QT;
-    constexpr int XPL = Planes<PREC>::XPL, QPL = 2;
-    const int G = GC > 0 ? GC : G_arg;
-    constexpr int PQ = QLDS ? 1 : PX;
-    constexpr size_t GSTEP = 8 * BLOCK_FLOATS;  // consecutive groups of one super tile
-    constexpr size_t PLANE = 4 * BLOCK_FLOATS;  // lo plane after hi
-    static_assert(PX <= QG_EXTRA, "query prefetch deeper than the duplicated groups");
-    __shared__ float s_sc[QB * CAP];
-    __shared__ uint32_t s_ix[QB * CAP];
-    __shared__ int s_cnt[QB];
-    __shared__ float s_thr[QB];
-    __shared__ uint32_t s_best[NW][QB];
-    __shared__ uint32_t s_pub[NW][QB];
-    __shared__ uint32_t s_sh[QB];
-    __shared__ int s_need, s_done;
-    extern __shared__ __attribute__((aligned(16))) float s_q[];  // QLDS: [G][plane][QT][256]
-
-    const int lane = threadIdx.x & 63;
-    const int lane4 = lane * 4;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    int wg, qb;
-    xcd_map(n_qb, wg, qb);
-    if (threadIdx.x == 0) {
-        s_need = 0;
-        s_done = 0;
-    }
-    for (int i = threadIdx.x; i < QB; i += 64 * NW) {
-        s_cnt[i] = 0;
-#pragma unroll
-        for (int w = 0; w < NW; ++w) {
-            s_best[w][i] = 0;
-            s_pub[w][i] = 0;
-        }
-        s_sh[i] = 0;
-        s_thr[i] = -INFINITY;
-    }
-    // the pilot's bound (pilot2_scores_kernel filled the slots): every workgroup derives it for
-    // its query block into s_sh; range 0 also raises gthr, which the finish pass reads (it must
-    // cover every bound a workgroup dropped rows against)
-    if (prank > 0) {
-        __syncthreads();
-        constexpr int QW = QB / NW;  // queries per wave: all their slots loaded before the first
-        uint32_t pv[QW][PILOT_E];    // selection (one round trip, not QW of them)
-#pragma unroll
-        for (int i = 0; i < QW; ++i) {
-            const int q = qb * QB + wv + NW * i;
-#pragma unroll
-            for (int e = 0; e < PILOT_E; ++e) pv[i][e] = q < B ? pslots[(size_t)q * PILOT_SLOTS + e * 64 + lane] : 0u;
-        }
-#pragma unroll
-        for (int i = 0; i < QW; ++i) {
-            const int ql = wv + NW * i;
-            if (qb * QB + ql >= B) break;
-            const uint32_t T = pilot_slot_rank(pv[i], prank);
-            if (lane == 0 && T != 0u) {
-                s_sh[ql] = T;
-                if (wg == 0) atomicMax(gthr + qb * QB + ql, T);
-            }
-        }
-    }
-    const float* Qbase = Qs + s2_blk((uint64_t)(qb * QT), 0, G + QG_EXTRA);
-    if constexpr (QLDS) {
-        for (int e = threadIdx.x; e < G * 2 * QT * 64; e += 64 * NW) {
-            const int l = e & 63, qt = (e >> 6) % QT, pl = (e / (64 * QT)) & 1, g = e / (128 * QT);
-            *(f32x4*)(s_q + (size_t)e * 4) = *(const f32x4*)(Qbase + g * GSTEP + pl * PLANE + qt * BLOCK_FLOATS + 4 * l);
-        }
-    }
-    __syncthreads();
-
-    // slot publishing (as vdb_scan.hip): lane group pq_r of LPQ lanes serves query wv + NW (lane / LPQ)
-    constexpr int QPW = QB / NW;
-    constexpr int LPQ = 64 / QPW;
-    constexpr int SL = KP / LPQ;
-    constexpr int SLV = SL / 4 > 0 ? SL / 4 : 1;
-    static_assert(SL % 4 == 0, "slots per lane must be whole uint4 loads");
-    static_assert(LPQ >= NW, "a lane group publishes one best per wave");
-    const int pq_r = lane % LPQ;
-    const int pq = wv + NW * (lane / LPQ);
-    const int pqg = qb * QB + pq;
-
-    const int64_t s_begin = (int64_t)wg * steps_per_wg;
-    const int64_t s_end = s_begin + steps_per_wg < n_steps ? s_begin + steps_per_wg : n_steps;
-
-    f32x4 xr[PX][RT][XPL];
-    f32x4 qr[PQ][QT][QPL];
-    auto q_lds = [&](int g, f32x4 (&q)[QT][QPL]) {
-#pragma unroll
-        for (int qt = 0; qt < QT; ++qt)
-#pragma unroll
-            for (int pl = 0; pl < QPL; ++pl) q[qt][pl] = *(const f32x4*)(s_q + ((size_t)(g * 2 + pl) * QT + qt) * 256 + lane4);
-    };
-    if (s_begin < s_end) {
-        const float* xs = Xs + s2_blk((uint64_t)((s_begin * NW + wv) * RT), 0, G);
-#pragma unroll
-        for (int p = 0; p < PX; ++p)
-#pragma unroll
-            for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-                for (int pl = 0; pl < XPL; ++pl)
-                    xr[p][rt][pl] = corpus_ld<NT>(xs + p * GSTEP + pl * PLANE + rt * BLOCK_FLOATS + lane4);
-        if constexpr (!QLDS) {
-#pragma unroll
-            for (int p = 0; p < PQ; ++p)
-#pragma unroll
-                for (int qt = 0; qt < QT; ++qt)
-#pragma unroll
-                    for (int pl = 0; pl < QPL; ++pl)
-                        qr[p][qt][pl] = *(const f32x4*)(Qbase + p * GSTEP + pl * PLANE + qt * BLOCK_FLOATS + lane4);
-        } else {
-            q_lds(0, qr[0]);
-        }
-    }
-    // the next step's shared bounds and (L2) accumulator start values, loaded one step ahead:
-    // lanes 0-31 hold rinit of row 32 t + lane of each tile (the A column of the init MFMA)
-    constexpr int NRI = METRIC == 1 ? RT : 1;
-    auto load_epi = [&](int64_t st_, uint32_t (&g_)[QT], float (&r_)[NRI]) {
-#pragma unroll
-        for (int qt = 0; qt < QT; ++qt) {
-            const int qg = qb * QB + qt * 32 + (lane & 31);
-            g_[qt] = qg < B ? gthr[qg] : 0u;
-        }
-        if constexpr (METRIC == 1) {
-            const int64_t tt = (st_ * NW + wv) * RT;
-#pragma unroll
-            for (int rt = 0; rt < RT; ++rt) r_[rt] = lane < 32 ? rinit[(tt + rt) * 32 + lane] : 0.0f;
-        }
-    };
-    uint32_t gkn[QT];
-    float rin[NRI];
-    if (s_begin < s_end) load_epi(s_begin, gkn, rin);
-    const float ones = lane < 32 ? 1.0f : 0.0f;  // B of the init MFMA: row k = 0 all ones
-
-    for (int64_t s = s_begin; s < s_end; ++s) {
-        const int64_t t0 = (s * NW + wv) * RT;
-        const float* xs = Xs + s2_blk((uint64_t)t0, 0, G);
-        const float* xn = (s + 1 < s_end) ? Xs + s2_blk((uint64_t)(t0 + NW * RT), 0, G) : xs;
-        f32x16 acc[RT][QT];
-#pragma unroll
-        for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-            for (int qt = 0; qt < QT; ++qt) {
-#pragma unroll
-                for (int v = 0; v < 16; ++v) acc[rt][qt][v] = 0.0f;
-                if constexpr (METRIC == 1)  // acc[i][j] = rinit[row i] * 1 (exact)
-                    acc[rt][qt] = __builtin_amdgcn_mfma_f32_32x32x2f32(rin[METRIC == 1 ? rt : 0], ones, acc[rt][qt], 0,
-                                                                       0, 0);
-            }
-        uint32_t gk[QT];
-#pragma unroll
-        for (int qt = 0; qt < QT; ++qt) gk[qt] = gkn[qt];
-
-        // one group: MFMAs of slot p, then refill slot p with the group PX ahead (this step's,
-        // or the next step's first groups); refills pinned right behind the MFMAs
-        auto group = [&](const int p, const int g, const float* xsrc, const float* qsrc) {
-            if constexpr (QLDS) {
-                f32x4 qn[1][QT][QPL];
-                q_lds(g + 1 < G ? g + 1 : 0, qn[0]);
-                group_mfma<PREC, RT, QT>(xr[p], qr[0], acc);
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-                    for (int pl = 0; pl < XPL; ++pl)
-                        xr[p][rt][pl] = corpus_ld<NT>(xsrc + pl * PLANE + rt * BLOCK_FLOATS + lane4);
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int qt = 0; qt < QT; ++qt)
-#pragma unroll
-                    for (int pl = 0; pl < QPL; ++pl) qr[0][qt][pl] = qn[0][qt][pl];
-            } else {
-                group_mfma<PREC, RT, QT>(xr[p], qr[p], acc);
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-                    for (int pl = 0; pl < XPL; ++pl)
-                        xr[p][rt][pl] = corpus_ld<NT>(xsrc + pl * PLANE + rt * BLOCK_FLOATS + lane4);
-#pragma unroll
-                for (int qt = 0; qt < QT; ++qt)
-#pragma unroll
-                    for (int pl = 0; pl < QPL; ++pl)
-                        qr[p][qt][pl] = *(const f32x4*)(qsrc + pl * PLANE + qt * BLOCK_FLOATS + lane4);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        };
-        int gb = 0;
-        for (; gb < G - PX; gb += PX) {
-#pragma unroll
-            for (int p = 0; p < PX; ++p)
-                group(p, gb + p, xs + (size_t)(gb + p + PX) * GSTEP, Qbase + (size_t)(gb + p + PQ) * GSTEP);
-        }
-        if (s + 1 < s_end) load_epi(s + 1, gkn, rin);
-#pragma unroll
-        for (int p = 0; p < PX; ++p)
-            group(p, gb + p, xn + (size_t)p * GSTEP, Qbase + (size_t)(gb + p + PQ) * GSTEP);
-
-#ifdef VDB_SCAN2_KLOOP_ONLY
-        {  // diagnostic build (make variant): the K-loop alone, results are garbage
-            float f = 0.0f;
-#pragma unroll
-            for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-                for (int qt = 0; qt < QT; ++qt) f += tile_max16(acc[rt][qt]);
-            if (f == 1234.5f) gl_s[0] = f;
-            continue;
-        }
-#endif
-        // ---- epilogue: the accumulators are the scores (cosine) or half of them (L2) ----
-        float thrh[QT];
-        bool qok[QT];
-#pragma unroll
-        for (int qt = 0; qt < QT; ++qt) {
-            const int ql = qt * 32 + (lane & 31);
-            const float thr = fmaxf(s_thr[ql], key_to_float(max(gk[qt], s_sh[ql])));
-            thrh[qt] = METRIC == 0 ? thr : 0.5f * thr;
-            qok[qt] = qb * QB + ql < B;
-        }
-        // Insertion, score by score: v_cmp + a wave-uniform branch per accumulator register;
-        // only the lanes whose score passes append (one returning LDS atomic each), so a tile
-        // with a few passing scores (C4, k = 100: most tiles early on) costs ~4 instructions per
-        // register plus its appends.  Scores that find the buffer full stay pending (`pend`) for
-        // the compaction rounds below.  The lane's best appended score goes to s_best (publish).
-        auto insert_pass = [&](int rt, int qt, float th, uint32_t cand) -> uint32_t {
-            const int ql = qt * 32 + (lane & 31);
-            uint32_t left = 0;
-            float mx = -INFINITY;
-#pragma unroll
-            for (int v = 0; v < 16; ++v) {
-                const bool p = ((cand >> v) & 1u) && acc[rt][qt][v] > th;
-                if (__any(p)) {
-                    if (p) {
-                        const float sc = METRIC == 0 ? acc[rt][qt][v] : 2.0f * acc[rt][qt][v];
-                        const int pos = atomicAdd(&s_cnt[ql], 1);
-                        if (pos < CAP) {
-                            const int ro = (v & 3) + 8 * (v >> 2) + 4 * (lane >> 5);
-                            s_sc[ql * CAP + pos] = sc;
-                            s_ix[ql * CAP + pos] = (uint32_t)((t0 + rt) * 32 + ro);
-                        } else {
-                            left |= 1u << v;
-                        }
-                        mx = fmaxf(mx, sc);
-                    }
-                }
-            }
-            if (mx != -INFINITY) atomicMax(&s_best[wv][ql], order_key(mx));
-            return left;
-        };
-        // (experiment) per-lane batch: one returning LDS atomic per lane reserves slots for all
-        // of its passing scores of the tile
-        auto insert_batch = [&](int rt, int qt, uint32_t pm) -> uint32_t {
-            if (!__any(pm != 0)) return 0u;
-            const int ql = qt * 32 + (lane & 31);
-            const int base = pm ? atomicAdd(&s_cnt[ql], __popc(pm)) : 0;
-            float mx = -INFINITY;
-#pragma unroll
-            for (int v = 0; v < 16; ++v) mx = ((pm >> v) & 1u) ? fmaxf(mx, acc[rt][qt][v]) : mx;
-            if (pm) atomicMax(&s_best[wv][ql], order_key(METRIC == 0 ? mx : 2.0f * mx));
-            uint32_t left = 0;
-#pragma unroll
-            for (int v = 0; v < 16; ++v) {
-                if ((pm >> v) & 1u) {
-                    const int pos = base + __popc(pm & ((1u << v) - 1u));
-                    if (pos < CAP) {
-                        const int ro = (v & 3) + 8 * (v >> 2) + 4 * (lane >> 5);
-                        s_sc[ql * CAP + pos] = METRIC == 0 ? acc[rt][qt][v] : 2.0f * acc[rt][qt][v];
-                        s_ix[ql * CAP + pos] = (uint32_t)((t0 + rt) * 32 + ro);
-                    } else {
-                        left |= 1u << v;
-                    }
-                }
-            }
-            return left;
-        };
-        uint32_t pend[RT][QT];
-        uint32_t any_left = 0;
-#pragma unroll
-        for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-            for (int qt = 0; qt < QT; ++qt) {
-                pend[rt][qt] = 0u;
-                if (__any(qok[qt] && tile_max16(acc[rt][qt]) > thrh[qt])) {
-                    const uint32_t valid = qok[qt] ? tile_valid16(mask, t0 + rt, N, lane) : 0u;
-#ifdef VDB_S2_BATCH_INSERT
-                    uint32_t pm = 0;
-#pragma unroll
-                    for (int v = 0; v < 16; ++v) pm |= acc[rt][qt][v] > thrh[qt] ? (1u << v) : 0u;
-                    pend[rt][qt] = insert_batch(rt, qt, pm & valid);
-#else
-                    pend[rt][qt] = insert_pass(rt, qt, thrh[qt], valid);
-#endif
-                    any_left |= pend[rt][qt];
-                }
-            }
-        // compaction rounds (vdb_scan.hip): lockstep = one workgroup barrier per step;
-        // FLAGSYNC = a wave with leftovers raises s_need and the others join at their step end
-        for (bool joined = false;; joined = true) {
-            if constexpr (!FLAGSYNC) {
-                if (!__syncthreads_or(any_left != 0)) break;
-            } else {
-                const bool mine = __any(any_left != 0);
-                if (mine && lane == 0) *(volatile int*)&s_need = 1;
-                if (!mine && (joined || !__builtin_amdgcn_readfirstlane(*(volatile int*)&s_need))) break;
-                __syncthreads();  // B1
-            }
-            for (int q = wv; q < QB; q += NW)
-                if (s_cnt[q] >= CAP)
-                    compact_query<KP, CAP>(s_sc + q * CAP, s_ix + q * CAP, s_cnt + q, s_thr + q,
-                                           qb * QB + q < B ? gthr + qb * QB + q : nullptr);
-            if (FLAGSYNC && threadIdx.x == 0) *(volatile int*)&s_need = 0;
-            __syncthreads();  // B2
-            any_left = 0;
-#pragma unroll
-            for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-                for (int qt = 0; qt < QT; ++qt) {
-                    if (!__any(pend[rt][qt] != 0)) continue;
-                    const int ql = qt * 32 + (lane & 31);
-                    const float thr = fmaxf(s_thr[ql], key_to_float(max(gk[qt], s_sh[ql])));
-                    pend[rt][qt] = insert_pass(rt, qt, METRIC == 0 ? thr : 0.5f * thr, pend[rt][qt]);
-                    any_left |= pend[rt][qt];
-                }
-        }
-        // ---- publish (as vdb_scan.hip): per-wave bests into KP slots per query; the slot
-        // minimum is a lower bound of the global KP-th best.  Only at steps 1, 2, 4, 8, ... and
-        // the last, so the slots are read back right away (a few waits per launch) instead of
-        // holding KP/4 registers per lane across the next step ----
-        const int64_t sd = s - s_begin + 1;
-#ifdef VDB_S2_NO_PUBLISH
-        if (false) {
-#else
-        if ((sd & (sd - 1)) == 0 || s + 1 == s_end) {
-#endif
-            int improved = 0;
-            if (pq_r < NW && pqg < B) {
-                const uint32_t best = s_best[pq_r][pq];
-                improved = best > s_pub[pq_r][pq];
-                if (improved) {
-                    s_pub[pq_r][pq] = best;
-                    atomicMax(gslots + (size_t)pqg * KP_MAX + ((wg * NW + pq_r) % KP), best);
-                }
-            }
-#pragma unroll
-            for (int off = 1; off < LPQ; off <<= 1) improved |= __shfl_xor(improved, off, 64);
-            if (improved) {
-                const uint32_t* sl = gslots + (size_t)pqg * KP_MAX + pq_r * SL;
-                uint32_t mn = 0xFFFFFFFFu;
-#pragma unroll
-                for (int j = 0; j < SLV; ++j) {
-                    const uint4 sv = *(const uint4*)(sl + 4 * j);
-                    mn = min(min(mn, min(sv.x, sv.y)), min(sv.z, sv.w));
-                }
-#pragma unroll
-                for (int off = 1; off < LPQ; off <<= 1) mn = min(mn, (uint32_t)__shfl_xor((int)mn, off, 64));
-                if (pq_r == 0 && pqg < B) {
-                    atomicMax(gthr + pqg, mn);
-                    atomicMax(&s_sh[pq], mn);
-                }
-            }
-        }
-    }
-
-    // FLAGSYNC: keep answering compaction rounds until every wave is past its last step
-    if (FLAGSYNC && lane == 0) atomicAdd(&s_done, 1);
-    for (; FLAGSYNC;) {
-        if (lane == 0) *(volatile int*)&s_need = 1;
-        __syncthreads();  // B1
-        if (__builtin_amdgcn_readfirstlane(*(volatile int*)&s_done) == NW) break;
-        for (int q = wv; q < QB; q += NW)
-            if (s_cnt[q] >= CAP)
-                compact_query<KP, CAP>(s_sc + q * CAP, s_ix + q * CAP, s_cnt + q, s_thr + q,
-                                       qb * QB + q < B ? gthr + qb * QB + q : nullptr);
-        if (threadIdx.x == 0) *(volatile int*)&s_need = 0;
-        __syncthreads();  // B2
-    }
-
-    // ---- flush: entries above the shared bound -> global per-query lists ----
-    __syncthreads();
-    uint32_t tkey = 0;
-    if (lane < QPW && qb * QB + wv + NW * lane < B) tkey = max(gthr[qb * QB + wv + NW * lane], s_sh[wv + NW * lane]);
-    append_flush<CAP>(s_sc, s_ix, s_cnt, wv, NW, QPW, qb * QB, B, tkey, gl_s, gl_i, gl_cnt, gl_cap);
-}
 
 // =============================================================================
 // Pilot bound with the same arithmetic (vdb_scan.hip launch_pilot for the fp32 pass)
@@ -613,86 +125,20 @@ hipError_t launch_pilot2(int prec, int metric, int KP, const float* Xs, const fl
 // =============================================================================
 int scan2_rows_per_step() { return S2_ROWS; }
 
-int scan2_qb(int KP) { return KP == 256 ? 32 : 64; }
-
-// The query block goes to LDS when it is small (C4: 64 queries x 128 dims = 32 KiB).
-bool scan2_qlds(int G16, int KP) { return (size_t)G16 * 2 * (scan2_qb(KP) / 32) * 1024 <= 32 * 1024; }
-
-template <int P, int M, int QT, int PX, int KP, int CAP, bool NT, bool QL, bool FS, int GC>
-static hipError_t scan2_launch_g(const float* Xs, const float* rinit, const uint32_t* mask, const float* Qs, int G,
-                                 int64_t N, int B, int n_qblocks, int64_t n_steps, int n_wg, int spw, float* gl_s,
-                                 uint32_t* gl_i, uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr, uint32_t* gslots,
-                                 const uint32_t* pslots, int prank, hipStream_t st) {
-    auto k = scan2_kernel<P, M, QT, PX, KP, CAP, NT, QL, FS, GC>;
-    const size_t lds = QL ? (size_t)G * 2 * QT * 1024 : 0;
-    if (QL) {
-        // the dynamic part (query block) plus the static top-k buffers must fit the 160 KiB of a
-        // CU: raise the dynamic limit to what this call needs (monotone; racing calls only
-        // raise it to values that fit)
-        static std::atomic<size_t> lds_set{0};
-        size_t cur = lds_set.load();
-        while (lds > cur) {
-            hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            if (e != hipSuccess) return e;
-            if (lds_set.compare_exchange_weak(cur, lds)) break;
-        }
-    }
-    const int n_wg8 = (n_wg + 7) / 8 * 8;
-    hipLaunchKernelGGL(k, dim3(n_wg8 * n_qblocks), dim3(256), lds, st, Xs, rinit, mask, Qs, G, N, B, n_steps, spw,
-                       n_qblocks, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, pslots, prank);
-    return hipGetLastError();
-}
-
-// query block in LDS (short rows): the common short row (D = 128 -> 8 groups) gets its own
-// instantiation with the group count built in
-template <int P, int M, int QT, int PX, int KP, int CAP, bool NT, bool QL, bool FS>
-static hipError_t scan2_launch(const float* Xs, const float* rinit, const uint32_t* mask, const float* Qs, int G,
-                               int64_t N, int B, int n_qblocks, int64_t n_steps, int n_wg, int spw, float* gl_s,
-                               uint32_t* gl_i, uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr, uint32_t* gslots,
-                               const uint32_t* pslots, int prank, hipStream_t st) {
-    if constexpr (QL) {
-        if (G == 8)
-            return scan2_launch_g<P, M, QT, PX, KP, CAP, NT, QL, FS, 8>(Xs, rinit, mask, Qs, G, N, B, n_qblocks, n_steps,
-                                                                        n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr,
-                                                                        gslots, pslots, prank, st);
-    }
-    return scan2_launch_g<P, M, QT, PX, KP, CAP, NT, QL, FS, 0>(Xs, rinit, mask, Qs, G, N, B, n_qblocks, n_steps, n_wg,
-                                                                spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, pslots,
-                                                                prank, st);
-}
-
 hipError_t launch_scan2(int prec, int metric, int KP, const float* Xs, const float* rinit, const uint32_t* mask,
                         const float* Qs, int G, int64_t N, int B, int n_qblocks, int64_t n_steps, int n_wg, int spw,
                         float* gl_s, uint32_t* gl_i, uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr,
-                        uint32_t* gslots, const uint32_t* pslots, int prank, int lockstep, hipStream_t st) {
+                        uint32_t* gslots, const uint32_t* pslots, int prank, int lockstep, int publish,
+                        hipStream_t st) {
     const bool ql = scan2_qlds(G, KP);
     const bool fs = !lockstep;
-    const bool nt = !ql && n_qblocks == 1 && !fs;
-#define S2_ARGS Xs, rinit, mask, Qs, G, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, \
-                pslots, prank, st
-#define S2_ONE(P, M, KPV, QTV, PXV, CAPV, NTV, QLV, FSV)                                              \
-    if (prec == P && metric == M && KP == KPV && nt == NTV && ql == QLV && fs == FSV)                \
-        return scan2_launch<P, M, QTV, PXV, KPV, CAPV, NTV, QLV, FSV>(S2_ARGS);
-#define S2_KP(P, M, PXV, NTV, QLV, FSV)                    \
-    S2_ONE(P, M, 32, 2, PXV, 128, NTV, QLV, FSV)           \
-    S2_ONE(P, M, 64, 2, PXV, 128, NTV, QLV, FSV)           \
-    S2_ONE(P, M, 128, 2, PXV, 192, NTV, QLV, FSV)          \
-    S2_ONE(P, M, 256, 1, PXV, 320, NTV, QLV, FSV)
-// PX (corpus groups in flight): bf16x3 2 (query operand in registers too), 4 with the query
-// block in LDS; bf16 (half the corpus registers per group) 4
-#define S2_MODES(P, M, PXV, PXL)                                                   \
-    S2_KP(P, M, PXV, false, false, false) S2_KP(P, M, PXV, true, false, false)     \
-    S2_KP(P, M, PXL, false, true, false) S2_KP(P, M, PXL, false, true, true)       \
-    S2_KP(P, M, PXV, false, false, true)
-#ifndef VDB_S2_QLDS_PX
-#define VDB_S2_QLDS_PX 2
-#endif
-    S2_MODES(1, 0, 2, VDB_S2_QLDS_PX) S2_MODES(1, 1, 2, VDB_S2_QLDS_PX) S2_MODES(2, 0, 4, 4) S2_MODES(2, 1, 4, 4)
-#undef S2_MODES
-#undef S2_KP
-#undef S2_ONE
-#undef S2_ARGS
-    return hipErrorInvalidValue;
+    const bool nt = !ql && n_qblocks == 1;
+    auto* unit = prec == PREC_BF16X3 ? (metric == 0 ? launch_scan2_b3c : launch_scan2_b3l)
+                 : prec == PREC_BF16 ? (metric == 0 ? launch_scan2_b1c : launch_scan2_b1l)
+                                     : nullptr;
+    if (!unit || metric < 0 || metric > 1) return hipErrorInvalidValue;
+    return unit(KP, Xs, rinit, mask, Qs, G, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr,
+                gslots, pslots, prank, nt, ql, fs, publish, st);
 }
 
 }  // namespace vdb

@@ -1,0 +1,9 @@
+// vdb_scan2_b1c.hip — instantiation unit of the split candidate pass: bf16, cosine
+// (every KP / load policy / step-end variant; kernel in vdb_scan2_kernel.h).
+#include "vdb_scan2_kernel.h"
+
+namespace vdb {
+S2_UNIT(launch_scan2_b1c, 2, 0, 4, 4)
+}  // namespace vdb
+
+S2_STAMP_READER(b1c)

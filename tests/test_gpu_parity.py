@@ -354,6 +354,40 @@ def test_device_search_gated_fallback(vdb, metric):
     assert ix.stat("fallback_queries") >= 3 * 2  # the two duplicated queries, every search
 
 
+@pytest.mark.parametrize("metric", ["cosine", "euclidean"])
+def test_device_search_several_streams(vdb, metric):
+    """Batches queued round-robin on three streams from one host thread (a server's request
+    streams; bench.py --streams) get workspaces of their own and run concurrently; every
+    batch equals the oracle, including those whose duplicates take the gated fallback."""
+    import torch
+    rng = np.random.default_rng(31)
+    V = rng.random((40000, 160), dtype=np.float32)
+    V[3000:3050] = V[17]
+    Qs = [rng.random((40, 160), dtype=np.float32) for _ in range(6)]
+    Qs[2][5] = V[17]
+    ix = vdb.NativeIndex(160, metric)
+    ix.add(V)
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    outs = []
+    torch.cuda.synchronize()
+    for rep in range(2):
+        for j, Q in enumerate(Qs):
+            qd = torch.from_numpy(Q).cuda()
+            sd = torch.empty((40, 10), dtype=torch.float32, device="cuda")
+            idd = torch.empty((40, 10), dtype=torch.int64, device="cuda")
+            kd = torch.empty((40, 10), dtype=torch.float64, device="cuda")
+            st = streams[(rep * len(Qs) + j) % 3]
+            st.wait_stream(torch.cuda.current_stream())  # the query copy
+            ix.search_device(qd.data_ptr(), 40, 10, sd.data_ptr(), idd.data_ptr(), kd.data_ptr(),
+                             stream=st.cuda_stream)
+            outs.append((j, qd, idd, kd))
+    torch.cuda.synchronize()
+    for j, _, idd, kd in outs:
+        _, ei, ek = ref_cpu.exact_search(Qs[j], V, 10, metric)
+        np.testing.assert_array_equal(idd.cpu().numpy(), ei)
+        np.testing.assert_array_equal(kd.cpu().numpy(), ek)
+
+
 def test_similarity_matrix_operator_slot(vdb):
     import torch
     rng = np.random.default_rng(19)
