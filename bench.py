@@ -325,6 +325,8 @@ def main():
     ap.add_argument("--n-wg", type=int, default=None, help="candidate-pass workgroups (tuning)")
     ap.add_argument("--scan-sync", type=int, default=None,
                     help="candidate-pass step end: 1 lockstep barrier, 2 flag-gated rounds (tuning; default by D)")
+    ap.add_argument("--dir-bound", type=int, default=None,
+                    help="bf16 certificate: 1 residual bound along the rows' mean direction (default), 0 Cauchy-Schwarz")
     ap.add_argument("--scan-publish", type=int, default=None,
                     help="split pass slot publishing: -1 auto, 0 off, 1 on (tuning)")
     ap.add_argument("--pilot-tiles", type=int, default=None, help="row tiles sampled by the pilot bound (tuning)")
@@ -336,7 +338,7 @@ def main():
     ap.add_argument("--timing", type=int, default=1,
                     help="1: the library's HIP events around the scan in the timed region (roofline); 0: none "
                          "(A/B of their cost; the roofline then comes from an untimed second loop)")
-    ap.add_argument("--streams", type=int, default=1,
+    ap.add_argument("--streams", type=int, default=3,
                     help="single GPU: batches queued round-robin on this many HIP streams (a server's request "
                          "streams; each batch still runs the whole search)")
     ap.add_argument("--no-fallback", action="store_true",
@@ -382,6 +384,8 @@ def main():
         ix.set_param("scan_sync", args.scan_sync)
     if args.pilot_tiles is not None:
         ix.set_param("pilot_tiles", args.pilot_tiles)
+    if args.dir_bound is not None:
+        ix.set_param("dir_bound", args.dir_bound)
     if args.scan_publish is not None:
         ix.set_param("scan_publish", args.scan_publish)
     if args.margin is not None:
@@ -427,7 +431,10 @@ def main():
     # Throughput (value): K batches queued back to back on the stream, as a server
     # keeps the device fed; device-memory searches return without a host wait
     # (DESIGN.md §3), so the host runs ahead and no step waits for its launch.
-    ix.set_param("timing", args.timing)
+    # HIP events around the scan inside the throughput loop only with one stream: with several,
+    # an event pair also spans the other streams' kernels running beside the scan
+    ev_in_loop = bool(args.timing) and n_str == 1
+    ix.set_param("timing", int(ev_in_loop))
     scan0, pipe0, n0 = ix.stat("scan_ns"), ix.stat("pipeline_ns"), ix.stat("timed_searches")
     by_prec0 = {p: ix.stat(f"searches_{p}") for p in ("fp32", "bf16x3", "bf16")}
     fb0 = ix.stat("fallback_queries")
@@ -448,7 +455,10 @@ def main():
     prec = args.precision if args.precision != "auto" else max(by_prec, key=by_prec.get)
     scan_ms = (ix.stat("scan_ns") - scan0) / 1e6 / max(n_t, 1)
     pipe_ms = (ix.stat("pipeline_ns") - pipe0) / 1e6 / max(n_t, 1)
-    if not args.timing:  # the scan's launch time from a second (untimed) run of the same loop
+    roof_timing = "hip events in the timed loop"
+    if not ev_in_loop:  # the scan's launch time from a second run of the loop on one stream
+        roof_timing = "hip events in a one-stream rerun of the timed loop (no events in the timed loop)"
+        n_str = 1
         ix.set_param("timing", 1)
         torch.cuda.synchronize()
         for _ in range(args.steps):
@@ -536,6 +546,7 @@ def main():
                              hbm_frac=achieved_gbs / HBM_PEAK_GBS, mfma_frac=achieved_tf / mfma_peak),
             "pipeline_ms": pipe_ms,
             "streams": max(1, args.streams) if world == 1 else 1,
+            "roofline_timing": roof_timing,
             "fallback_queries_total": fallback,
             "fallback_queries_timed": fb_timed,  # (auto's bf16 probe falls back in warm-up at C3 / C4)
             "fallback_list_overflow": overflow,

@@ -109,6 +109,12 @@ struct vdb_index {
     int* d_nonfinite = nullptr;
     double xmax = 0.0;
     double xres_rel = 0.0, xres_abs = 0.0;  // max |x - bf16(x)| / |x| and max |x - bf16(x)| (PREC_BF16 bound)
+    // PREC_BF16 bound along a direction: dir = the normalised mean of the split
+    // copy's rows of the first add (up to kDirRows of them), frozen until clear();
+    // xres_dir = max |dir . (y - bf16(y))| over all rows
+    float* d_dir = nullptr;  // [Dp], zero padded
+    bool dir_set = false;
+    double xres_dir = 0.0;
     hipStream_t stream = nullptr;
     int n_cu = 256;
     // knobs
@@ -136,7 +142,8 @@ struct vdb_index {
     // bound kernel.  Measured (profiles/r02_ab, C2): the prologue costs the scan ~25 us (bf16)
     // / ~30 us (bf16x3) against ~5 us for the kernel, so 0 is the default.
     int64_t pilot_fused = 0;
-    int64_t scan_publish = -1;    // split pass slot publishing: -1 auto (>= 16 steps per workgroup), 0 off, 1 on
+    int64_t scan_publish = -1;
+    bool no_dir_bound = false;    // diagnostics: PREC_BF16 certificate with Cauchy-Schwarz only    // split pass slot publishing: -1 auto (>= 16 steps per workgroup), 0 off, 1 on
     int64_t finish_split = 1;  // workgroups per query in the finish kernel (tuning)
     // stats
     std::atomic<int64_t> n_searches{0}, n_queries{0}, n_fallback{0}, n_overflow{0};
@@ -470,6 +477,7 @@ int32_t vdb_index_destroy(vdb_index* ix) {
     if (ix->sq32) (void)hipFree(ix->sq32);
     if (ix->rinit32) (void)hipFree(ix->rinit32);
     if (ix->d_xmax) (void)hipFree(ix->d_xmax);
+    if (ix->d_dir) (void)hipFree(ix->d_dir);
     if (ix->d_totals) (void)hipFree(ix->d_totals);
     if (ix->h_totals) (void)hipHostFree(ix->h_totals);
     if (ix->stream) (void)hipStreamDestroy(ix->stream);
@@ -531,6 +539,8 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
     } else if (n == "finish_split") {
         if (value < 1 || value > 8) return set_error(VDB_ERR_INVALID, "finish_split must be in [1, 8]");
         ix->finish_split = value;
+    } else if (n == "dir_bound") {
+        ix->no_dir_bound = value == 0;
     } else if (n == "scan_publish") {
         if (value < -1 || value > 1) return set_error(VDB_ERR_INVALID, "scan_publish must be -1, 0 or 1");
         ix->scan_publish = value;
@@ -579,6 +589,39 @@ int32_t vdb_index_get_stat(const vdb_index* cix, const char* name, int64_t* valu
     return VDB_OK;
 }
 
+// Rows [row0, row0 + n) were just packed: on the first add, fix the residual direction
+// (normalised column sums of up to kDirRows of these rows; a host round trip, once per
+// index); then the maximum of |dir . (y - bf16(y))| over these rows (d_xmax[3]).
+constexpr int64_t kDirRows = 65536;
+
+static hipError_t residual_direction(vdb_index* ix, int64_t row0, int64_t n, hipStream_t st) {
+    const float* inv = ix->metric == VDB_METRIC_COSINE ? ix->inv32 : nullptr;
+    if (!ix->dir_set) {
+        const int D = ix->dim;
+        hipError_t e = hipSuccess;
+        if (!ix->d_dir) e = hipMalloc(&ix->d_dir, (size_t)ix->Dp * sizeof(float));
+        double* sums = nullptr;
+        if (e == hipSuccess) e = hipMalloc(&sums, (size_t)D * sizeof(double));
+        if (e == hipSuccess) e = hipMemsetAsync(sums, 0, (size_t)D * sizeof(double), st);
+        if (e == hipSuccess) e = launch_dir_sum(ix->X, inv, row0, std::min(n, kDirRows), D, ix->G, sums, st);
+        std::vector<double> h(D);
+        if (e == hipSuccess) e = hipMemcpyAsync(h.data(), sums, (size_t)D * sizeof(double), hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (sums) (void)hipFree(sums);
+        if (e != hipSuccess) return e;
+        double nn = 0.0;
+        for (double v : h) nn += v * v;
+        std::vector<float> dir(ix->Dp, 0.0f);
+        if (nn > 0.0 && std::isfinite(nn))
+            for (int d = 0; d < D; ++d) dir[d] = (float)(h[d] / std::sqrt(nn));
+        e = hipMemcpyAsync(ix->d_dir, dir.data(), (size_t)ix->Dp * sizeof(float), hipMemcpyHostToDevice, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);  // dir is a stack buffer
+        if (e != hipSuccess) return e;
+        ix->dir_set = true;
+    }
+    return launch_resid_dir(ix->X, inv, row0, n, ix->dim, ix->G, ix->d_dir, ix->d_xmax + 3, st);
+}
+
 int32_t vdb_index_add(vdb_index* ix, const float* vectors, int64_t n, int32_t mem, void* stream) {
     if (!ix) return set_error(VDB_ERR_INVALID, "index is NULL");
     if (n < 0) return set_error(VDB_ERR_INVALID, "n must be >= 0");
@@ -604,6 +647,7 @@ int32_t vdb_index_add(vdb_index* ix, const float* vectors, int64_t n, int32_t me
                 e = launch_pack_rows(staging, m, D, ix->G, ix->X, ix->count + r, ix->nrm64, ix->inv32, ix->sq32,
                                      ix->rinit32, ix->metric == VDB_METRIC_COSINE, ix->d_xmax, ix->d_nonfinite, st);
             if (e == hipSuccess) e = build_candidate_rows(ix, ix->X, ix->inv32, ix->count + r, m, ix->Xs, st);
+            if (e == hipSuccess) e = residual_direction(ix, ix->count + r, m, st);
             if (e == hipSuccess) e = hipStreamSynchronize(st);  // staging reuse
             if (e != hipSuccess) {
                 (void)hipFree(staging);
@@ -613,12 +657,13 @@ int32_t vdb_index_add(vdb_index* ix, const float* vectors, int64_t n, int32_t me
             HIP_TRY(launch_pack_rows(src, m, D, ix->G, ix->X, ix->count + r, ix->nrm64, ix->inv32, ix->sq32,
                                      ix->rinit32, ix->metric == VDB_METRIC_COSINE, ix->d_xmax, ix->d_nonfinite, st));
             HIP_TRY(build_candidate_rows(ix, ix->X, ix->inv32, ix->count + r, m, ix->Xs, st));
+            HIP_TRY(residual_direction(ix, ix->count + r, m, st));
         }
     }
     if (staging) (void)hipFree(staging);
     (void)stream;  // ingest always runs on the index's own stream (serialised with growth)
     int nonfinite = 0;
-    unsigned long long xb[3] = {0, 0, 0};
+    unsigned long long xb[4] = {0, 0, 0, 0};
     HIP_TRY(hipMemcpyAsync(&nonfinite, ix->d_nonfinite, sizeof(int), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(xb, ix->d_xmax, sizeof(xb), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
@@ -628,11 +673,12 @@ int32_t vdb_index_add(vdb_index* ix, const float* vectors, int64_t n, int32_t me
         (void)used_tiles;
         return set_error(VDB_ERR_NONFINITE, "%d row(s) contain NaN or Inf; nothing was added", nonfinite);
     }
-    double xm[3];
+    double xm[4];
     std::memcpy(xm, xb, sizeof(xm));
     ix->xmax = xm[0];
     ix->xres_rel = xm[1];
     ix->xres_abs = xm[2];
+    ix->xres_dir = xm[3];
     ix->count += n;
     ix->auto_b3 = false;  // new rows: VDB_PREC_AUTO tries BF16 again
     return VDB_OK;
@@ -663,6 +709,8 @@ int32_t vdb_index_clear(vdb_index* ix) {
     ix->auto_b3 = false;
     ix->xmax = 0.0;
     ix->xres_rel = ix->xres_abs = 0.0;
+    ix->dir_set = false;  // the next add picks a new direction (xres_dir's bits were cleared above)
+    ix->xres_dir = 0.0;
     return VDB_OK;
 }
 
@@ -729,7 +777,7 @@ static int32_t search_impl(vdb_index* ix, const float* queries, int32_t B, int32
     if (auto_prec && ix->h_totals) {  // fallbacks of earlier device-memory searches (lagged)
         const unsigned long long seen = ix->h_totals[0];
         const unsigned long long prev = ix->auto_seen.exchange(seen);
-        if (seen > prev && (seen - prev) * 64 > (unsigned long long)B) ix->auto_b3 = true;
+        if (seen > prev) ix->auto_b3 = true;
     }
     const int prec_req = !ix->Xs ? PREC_FP32
                          : ix->precision == VDB_PREC_BF16X3 ? PREC_BF16X3
@@ -942,6 +990,8 @@ static int32_t search_impl(vdb_index* ix, const float* queries, int32_t B, int32
                                        8.0 * std::ldexp(1.0, -24));
             fa.xmax = ix->xmax;
             fa.xres = prec != PREC_BF16 ? 0.0 : 1.01 * (ix->metric == 0 ? ix->xres_rel : ix->xres_abs);
+            fa.dir = prec == PREC_BF16 && ix->dir_set && !ix->no_dir_bound ? ix->d_dir : nullptr;
+            fa.dres = 1.01 * ix->xres_dir;
             fa.out_s = out_s; fa.out_i = out_i; fa.out_k = out_k; fa.index_offset = index_offset;
             fa.row_ids = row_ids;
             fa.flag_count = flags; fa.flag_list = flags + 1; fa.gthr = gthr; fa.overflow_count = flags + B + 1;
@@ -973,7 +1023,7 @@ static int32_t search_impl(vdb_index* ix, const float* queries, int32_t B, int32
             HIP_TRY(hipStreamSynchronize(st));
             n_flag = w->host_flag[0];
             ix->n_overflow += w->host_flag[1];
-            if (auto_prec && prec == PREC_BF16 && n_flag * 64 > B) {
+            if (auto_prec && prec == PREC_BF16 && n_flag > 0) {
                 ix->auto_b3 = true;
                 if (!ix->no_fallback) return kRetryBf16x3;
             }

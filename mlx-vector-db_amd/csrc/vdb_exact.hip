@@ -456,6 +456,33 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
             if (ar == KP - 1) s_akp = ck;
         }
     }
+    // bf16 corpus rounding: |q.(y - bf16(y))| <= bq, Cauchy-Schwarz |q| R or, along the index's
+    // residual direction, |q - c dir| R + |c| M with c = q.dir (vdb_ingest.hip resid_dir_kernel);
+    // cosine on the unit query
+    __shared__ double s_bq;
+    if (wv == 0) {
+        double bq = 0.0;
+        if (a.xres > 0.0) {
+            bq = METRIC == 0 ? a.xres : qn * a.xres;
+            if (a.dir) {
+                const float* qq = a.Q + (int64_t)b * a.D;
+                const double qs = METRIC == 0 ? 1.0 / fmax(qn, 1e-8) : 1.0;
+                double c = 0.0;
+                for (int d = lane; d < a.D; d += 64) c += (double)qq[d] * qs * (double)a.dir[d];
+                c = wave_sum_butterfly(c);
+                double w2 = 0.0;
+                for (int d = lane; d < a.D; d += 64) {
+                    const double w = (double)qq[d] * qs - c * (double)a.dir[d];
+                    w2 += w * w;
+                }
+                w2 = wave_sum_butterfly(w2);
+                // (1 + 1e-6) and + 1e-6 R: the fp64 evaluation and the fp32-normalised query
+                const double bd = (sqrt(w2) * a.xres + fabs(c) * a.dres) * (1.0 + 1e-6) + 1e-6 * a.xres;
+                bq = fmin(bq, bd);
+            }
+        }
+        if (lane == 0) s_bq = bq;
+    }
     __shared__ int s_ok;
     __shared__ double s_cut;
     __syncthreads();
@@ -470,15 +497,15 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
             const double akp = full ? (double)key_to_float(s_akp) : -INFINITY;
             const double acut = fmax(akp, T);
             if (METRIC == 0) {
-                eps = a.eps_rel + a.xres;
+                eps = a.eps_rel + s_bq;
             } else {
-                eps = a.eps_rel * (2.0 * qn * a.xmax + a.xmax * a.xmax) + 2.0 * qn * a.xres +
+                eps = a.eps_rel * (2.0 * qn * a.xmax + a.xmax * a.xmax) + 2.0 * s_bq +
                       2.4e-7 * fmax(fabs(ak), fabs(acut));
             }
             ok = have_k && acut + eps < ak - eps;
         } else if (have_k) {  // the list holds every eligible row: only the rerank cut needs eps
-            eps = METRIC == 0 ? a.eps_rel + a.xres
-                              : a.eps_rel * (2.0 * qn * a.xmax + a.xmax * a.xmax) + 2.0 * qn * a.xres +
+            eps = METRIC == 0 ? a.eps_rel + s_bq
+                              : a.eps_rel * (2.0 * qn * a.xmax + a.xmax * a.xmax) + 2.0 * s_bq +
                                     2.4e-7 * fabs(ak);
         }
         if (!ok && sp == 0) {

@@ -92,6 +92,75 @@ hipError_t launch_pack_rows(const float* src, int64_t n, int D, int G, float* X,
     return hipGetLastError();
 }
 
+// Direction of the bf16 residual bound (PREC_BF16): column sums of the split
+// copy's rows y (cosine: x / |x| rounded as the split rounds it) over rows [row0, row0 + n).
+// Block: 64 rows; thread d0: dims d0, d0 + 256, ...; fp64 partial sums, one atomic per dim.
+__global__ void __launch_bounds__(256) dir_sum_kernel(const float* __restrict__ X, const float* __restrict__ inv32,
+                                                      int64_t row0, int64_t n, int D, int G,
+                                                      double* __restrict__ sums) {
+    const int64_t r0 = (int64_t)blockIdx.x * 64;
+    const int64_t r1 = r0 + 64 < n ? r0 + 64 : n;
+    for (int d = threadIdx.x; d < D; d += 256) {
+        double acc = 0.0;
+        for (int64_t i = r0; i < r1; ++i) {
+            const uint64_t r = (uint64_t)(row0 + i);
+            const float x = X[row_piece_offset(r, d >> 2, G) + (d & 3)];
+            acc += (double)(inv32 ? x * inv32[r] : x);
+        }
+        atomicAdd(sums + d, acc);
+    }
+}
+
+hipError_t launch_dir_sum(const float* X, const float* inv32, int64_t row0, int64_t n, int D, int G, double* sums,
+                          hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(dir_sum_kernel, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, st, X, inv32, row0, n, D, G,
+                       sums);
+    return hipGetLastError();
+}
+
+// |dir . (y - bf16(y))| per row (one wave per row), maximum into *out (fp64 bits): with
+// R = max |y - bf16(y)| (pack_rows) and M = this maximum, a query q scores every row's
+// bf16 copy within |q - c dir| R + |c| M, c = q . dir (finish_kernel) -- a fraction of
+// Cauchy-Schwarz's |q| R when the rows share a mean direction (uniform data: ~0.6).
+__global__ void __launch_bounds__(256) resid_dir_kernel(const float* __restrict__ X, const float* __restrict__ inv32,
+                                                        int64_t row0, int64_t n, int D, int G,
+                                                        const float* __restrict__ dir,
+                                                        unsigned long long* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= n) return;
+    const uint64_t r = (uint64_t)(row0 + i);
+    const float iv = inv32 ? inv32[r] : 1.0f;
+    const int np = (D + 255) / 256;
+    double acc = 0.0;
+    for (int m = 0; m < np; ++m) {
+        const int p = m * 64 + lane;
+        if (4 * p >= D) break;
+        const f32x4 xv = *(const f32x4*)(X + row_piece_offset(r, p, G));
+        const f32x4 dv = *(const f32x4*)(dir + 4 * p);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float y = inv32 ? xv[j] * iv : xv[j];
+            const double rv = (double)y - (double)__uint_as_float(bf16_rne_bits(y) << 16);
+            acc = acc + (double)dv[j] * rv;
+        }
+    }
+    acc = wave_sum_butterfly(acc);
+    if (lane == 0) {
+        const unsigned long long v = (unsigned long long)__double_as_longlong(fabs(acc));
+        if (v > __atomic_load_n(out, __ATOMIC_RELAXED)) atomicMax(out, v);
+    }
+}
+
+hipError_t launch_resid_dir(const float* X, const float* inv32, int64_t row0, int64_t n, int D, int G,
+                            const float* dir, unsigned long long* out, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(resid_dir_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, X, inv32, row0, n, D, G, dir,
+                       out);
+    return hipGetLastError();
+}
+
 // Row-major fp32 rows -> split-bf16 tiles.  Thread (tile t, fp32 group g8, row-in-tile i):
 // the 8 dims 8 g8 .. 8 g8 + 7 of row 32 t + i (32 contiguous bytes), times inv32[row] for
 // cosine (the normalised row the candidate pass scores), -> lane i + 32 (g8 & 1) of the hi

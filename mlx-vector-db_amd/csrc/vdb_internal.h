@@ -38,6 +38,12 @@ hipError_t launch_pack_rows(const float* src, int64_t n, int D, int G, float* X,
 // covering rows [row0, row0 + n), y = x * inv32[row] (cosine: the normalised row, as the
 // candidate pass scores it) or y = x (inv32 == nullptr, L2).  G = fp32 groups (Dp/8); the
 // split copy has G/2 groups.
+// PREC_BF16 residual bound along a direction (vdb_ingest.hip): column sums of the split
+// copy's rows, then max |dir . (y - bf16(y))| over rows.
+hipError_t launch_dir_sum(const float* X, const float* inv32, int64_t row0, int64_t n, int D, int G, double* sums,
+                          hipStream_t st);
+hipError_t launch_resid_dir(const float* X, const float* inv32, int64_t row0, int64_t n, int D, int G,
+                            const float* dir, unsigned long long* out, hipStream_t st);
 hipError_t launch_split_rows(const float* X, int G, int64_t row0, int64_t n, const float* inv32, float* Xs,
                              hipStream_t st);
 
@@ -131,6 +137,10 @@ struct FinishArgs {
     const float* Q; const double* qn64; const float* X; int G; int D; const double* nrm64;
     int k; double eps_rel; double xmax;
     double xres;  // PREC_BF16: bound of |q.(x - bf16(x))| per unit |q| (cosine: relative, L2: absolute)
+    // PREC_BF16, optional: unit-ish direction dir [D] and M = 1.01 max |dir.(y - bf16(y))|: the
+    // bound per query becomes min(|q| R, |q - c dir| R + |c| M), c = q.dir (R = xres)
+    const float* dir = nullptr;
+    double dres = 0.0;
     float* out_s; int64_t* out_i; double* out_k; int64_t index_offset;
     int* flag_count; int* flag_list; const uint32_t* gthr;
     int* overflow_count;  // lists longer than the finish kernel holds (they take the exact path)

@@ -59,7 +59,11 @@ __device__ __forceinline__ uint32_t tile_valid16(const uint32_t* mask, int64_t t
 // v_maximum3_f32, 8 instructions per 16 scores instead of 16 canonicalising v_max_f32 +
 // 8 v_max3_f32 under IEEE mode (the scores are never NaN: non-finite rows are rejected
 // at ingest, queries on the host / by the caller's contract)
+#ifdef VDB_S2_IEEE_MAX  // A/B build: IEEE fmaxf (canonicalising) tile maxima
+#define S2_MAXIMUM(a, b) fmaxf(a, b)
+#else
 #define S2_MAXIMUM(a, b) __builtin_elementwise_maximum(a, b)
+#endif
 __device__ __forceinline__ float tile_max16(const f32x16& a) {
     float m = S2_MAXIMUM(S2_MAXIMUM(a[0], a[1]), a[2]);
 #pragma unroll
@@ -375,12 +379,17 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
                 const bool p = ((cand >> v) & 1u) && acc[rt][qt][v] > th;
                 if (__any(p)) {
                     if (p) {
-                        const float sc = METRIC == 0 ? acc[rt][qt][v] : 2.0f * acc[rt][qt][v];
+                        // the empty volatile asm keeps the score scaling and the row id inside
+                        // this rare branch: hoisted, they cost 2 VALU per accumulator register
+                        // and step (the row ids of all 128 registers parked in AGPRs)
+                        float a_ = acc[rt][qt][v];
+                        uint32_t rb = (uint32_t)((t0 + rt) * 32) + 4u * (uint32_t)(lane >> 5);
+                        asm volatile("" : "+v"(a_), "+v"(rb));
+                        const float sc = METRIC == 0 ? a_ : 2.0f * a_;
                         const int pos = atomicAdd(&s_cnt[ql], 1);
                         if (pos < CAP) {
-                            const int ro = (v & 3) + 8 * (v >> 2) + 4 * (lane >> 5);
                             s_sc[ql * CAP + pos] = sc;
-                            s_ix[ql * CAP + pos] = (uint32_t)((t0 + rt) * 32 + ro);
+                            s_ix[ql * CAP + pos] = rb + (uint32_t)((v & 3) + 8 * (v >> 2));
                         } else {
                             left |= 1u << v;
                         }
