@@ -150,6 +150,32 @@ def test_precision_switch_keeps_results(vdb):
     assert ix.stat("fallback_queries") == 0
 
 
+@pytest.mark.parametrize("metric", ["cosine", "euclidean"])
+def test_bf16_directional_residual_bound(vdb, metric):
+    """bf16 certificate with the corpus-rounding bound taken along the rows' mean direction
+    (|q - c dir| R + |c| M): on uniform rows (one shared direction) it certifies the queries
+    that Cauchy-Schwarz's |q| R leaves uncertified; results are exact either way."""
+    rng = np.random.default_rng(41)
+    N, D, B, k = 300_000, 1536, 32, 10
+    V = rng.random((N, D), dtype=np.float32)
+    Q = rng.random((B, D), dtype=np.float32)
+    es, ei, ek = ref_cpu.exact_search(Q, V, k, metric)
+    fb = {}
+    for dirb in (1, 0):
+        ix = vdb.NativeIndex(D, metric, precision="bf16")
+        ix.set_param("dir_bound", dirb)
+        ix.add(V)
+        s, i, kk = ix.search(Q, k, with_keys=True)
+        np.testing.assert_array_equal(i, ei)
+        np.testing.assert_array_equal(kk, ek)
+        fb[dirb] = ix.stat("fallback_queries")
+        ix.close()
+    print(f"{metric}: bf16 fallbacks with the directional bound {fb[1]}, Cauchy-Schwarz {fb[0]} of {B}")
+    assert fb[1] <= fb[0], fb
+    if metric == "cosine":  # (1M x 1536, B = 256: 0 vs every query, profiles/r02s_ab/s4_c3_bf16*.json)
+        assert fb[1] == 0, fb
+
+
 @pytest.mark.parametrize("mem", ["host", "device"])
 def test_auto_precision_switches_on_fallbacks(vdb, mem):
     """VDB_PREC_AUTO runs the bf16 pass while it certifies; rows closer together than the
