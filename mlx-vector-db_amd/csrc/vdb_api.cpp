@@ -142,9 +142,8 @@ struct vdb_index {
     // bound kernel.  Measured (profiles/r02_ab, C2): the prologue costs the scan ~25 us (bf16)
     // / ~30 us (bf16x3) against ~5 us for the kernel, so 0 is the default.
     int64_t pilot_fused = 0;
-    int64_t scan_publish = -1;
-    bool no_dir_bound = false;
-    bool scan_pipe = true;        // split pass, short rows: software-pipelined epilogue (scan2p_kernel)    // diagnostics: PREC_BF16 certificate with Cauchy-Schwarz only    // split pass slot publishing: -1 auto (>= 16 steps per workgroup), 0 off, 1 on
+    int64_t scan_publish = -1;    // split pass slot publishing: -1 auto (>= 16 steps per workgroup), 0 off, 1 on
+    bool no_dir_bound = false;    // diagnostics: PREC_BF16 certificate with Cauchy-Schwarz only
     int64_t finish_split = 1;  // workgroups per query in the finish kernel (tuning)
     // stats
     std::atomic<int64_t> n_searches{0}, n_queries{0}, n_fallback{0}, n_overflow{0};
@@ -540,8 +539,6 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
     } else if (n == "finish_split") {
         if (value < 1 || value > 8) return set_error(VDB_ERR_INVALID, "finish_split must be in [1, 8]");
         ix->finish_split = value;
-    } else if (n == "scan_pipe") {
-        ix->scan_pipe = value != 0;
     } else if (n == "dir_bound") {
         ix->no_dir_bound = value == 0;
     } else if (n == "scan_publish") {
@@ -824,7 +821,7 @@ static int32_t search_impl(vdb_index* ix, const float* queries, int32_t B, int32
     // over many steps (C4: 610 per workgroup); with few (C2: 8) its global round trips at
     // steps 1, 2, 4, 8 cost more than the pilot's bound leaves to gain (measured: stamps,
     // profiles/r02_ab/).
-    const int publish = (ix->scan_publish >= 0 ? (int)ix->scan_publish : spw >= 16) | (ix->scan_pipe ? 2 : 0);
+    const int publish = ix->scan_publish >= 0 ? (int)ix->scan_publish : spw >= 16;
 
     Workspace* w = acquire_ws(ix, st);
     struct Releaser {

@@ -566,360 +566,6 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
 }
 
 
-// =============================================================================
-// Software-pipelined variant for short rows (query block in LDS, compile-time group count
-// GC: C4's D = 128), the epilogue of step s - 1 interleaved with the MFMAs of step s
-// =============================================================================
-// With D = 128 a step is 8 groups x 24 MFMAs per wave, and the epilogue (accumulator reads,
-// tile maxima, threshold tests; stamps: 38% of the scan at C4) ran after the step's last
-// MFMA, with the matrix core idle.  Here the accumulators are double-buffered (2 x 128
-// registers: the 256 AGPRs) and the tile test of tile g of step s - 1 is issued right after
-// group g's MFMAs of step s, so the VALU work runs while the MFMA pipe drains; the rare
-// inserts of step s - 1 (and the compaction rounds / publishing) follow step s's K-loop.
-// Same invariant as scan2_kernel (a step's rows are tested against a bound read one step
-// later, i.e. a higher one: still a valid bound).
-template <int PREC, int METRIC, int QT, int PX, int KP, int CAP, bool FLAGSYNC, int GC>
-__global__ void __launch_bounds__(256, 1)
-scan2p_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, const uint32_t* __restrict__ mask,
-              const float* __restrict__ Qs, int G_arg, int64_t N, int B, int64_t n_steps, int steps_per_wg, int n_qb,
-              float* __restrict__ gl_s, uint32_t* __restrict__ gl_i, uint32_t* __restrict__ gl_cnt, int64_t gl_cap,
-              uint32_t* __restrict__ gthr, uint32_t* __restrict__ gslots, const uint32_t* __restrict__ pslots,
-              int prank, int publish) {
-    constexpr int RT = S2_RT, NW = S2_NW;
-    constexpr int QB = 32 * QT;
-    constexpr int XPL = Planes<PREC>::XPL, QPL = 2;
-    constexpr int G = GC;
-    constexpr int NTILE = RT * QT;
-    static_assert(NTILE <= G, "one tile test per group");
-    constexpr size_t GSTEP = 8 * BLOCK_FLOATS;
-    constexpr size_t PLANE = 4 * BLOCK_FLOATS;
-    (void)G_arg;
-    __shared__ float s_sc[QB * CAP];
-    __shared__ uint32_t s_ix[QB * CAP];
-    __shared__ int s_cnt[QB];
-    __shared__ float s_thr[QB];
-    __shared__ uint32_t s_best[NW][QB];
-    __shared__ uint32_t s_pub[NW][QB];
-    __shared__ uint32_t s_sh[QB];
-    __shared__ int s_need, s_done;
-    extern __shared__ __attribute__((aligned(16))) float s_q[];  // [G][plane][QT][256]
-
-    const int lane = threadIdx.x & 63;
-    const int lane4 = lane * 4;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    int wg, qb;
-    xcd_map(n_qb, wg, qb);
-    if (threadIdx.x == 0) {
-        s_need = 0;
-        s_done = 0;
-    }
-    for (int i = threadIdx.x; i < QB; i += 64 * NW) {
-        s_cnt[i] = 0;
-#pragma unroll
-        for (int w = 0; w < NW; ++w) {
-            s_best[w][i] = 0;
-            s_pub[w][i] = 0;
-        }
-        s_sh[i] = 0;
-        s_thr[i] = -INFINITY;
-    }
-    if (prank > 0) {
-        __syncthreads();
-        constexpr int QW = QB / NW;
-        uint32_t pv[QW][PILOT_E];
-#pragma unroll
-        for (int i = 0; i < QW; ++i) {
-            const int q = qb * QB + wv + NW * i;
-#pragma unroll
-            for (int e = 0; e < PILOT_E; ++e) pv[i][e] = q < B ? pslots[(size_t)q * PILOT_SLOTS + e * 64 + lane] : 0u;
-        }
-#pragma unroll
-        for (int i = 0; i < QW; ++i) {
-            const int ql = wv + NW * i;
-            if (qb * QB + ql >= B) break;
-            const uint32_t T = pilot_slot_rank(pv[i], prank);
-            if (lane == 0 && T != 0u) {
-                s_sh[ql] = T;
-                if (wg == 0) atomicMax(gthr + qb * QB + ql, T);
-            }
-        }
-    }
-    const float* Qbase = Qs + s2_blk((uint64_t)(qb * QT), 0, G + QG_EXTRA);
-    for (int e = threadIdx.x; e < G * 2 * QT * 64; e += 64 * NW) {
-        const int l = e & 63, qt = (e >> 6) % QT, pl = (e / (64 * QT)) & 1, g = e / (128 * QT);
-        *(f32x4*)(s_q + (size_t)e * 4) = *(const f32x4*)(Qbase + g * GSTEP + pl * PLANE + qt * BLOCK_FLOATS + 4 * l);
-    }
-    __syncthreads();
-
-    constexpr int QPW = QB / NW;
-    constexpr int LPQ = 64 / QPW;
-    constexpr int SL = KP / LPQ;
-    constexpr int SLV = SL / 4 > 0 ? SL / 4 : 1;
-    static_assert(SL % 4 == 0, "slots per lane must be whole uint4 loads");
-    static_assert(LPQ >= NW, "a lane group publishes one best per wave");
-    const int pq_r = lane % LPQ;
-    const int pq = wv + NW * (lane / LPQ);
-    const int pqg = qb * QB + pq;
-
-    const int64_t s_begin = (int64_t)wg * steps_per_wg;
-    const int64_t s_end = s_begin + steps_per_wg < n_steps ? s_begin + steps_per_wg : n_steps;
-
-    // half-step h of a step: row tiles 2h, 2h + 1 of the wave's 4 (accumulator buffer h)
-    constexpr int RTH = 2;
-    constexpr int NTH = RTH * QT;  // tiles per half-step
-    static_assert(NTH <= G, "one tile test per group");
-    f32x4 xr[PX][RTH][XPL];
-    f32x4 qr[QT][QPL];
-    auto q_lds = [&](int g, f32x4 (&q)[QT][QPL]) __attribute__((always_inline)) {
-#pragma unroll
-        for (int qt = 0; qt < QT; ++qt)
-#pragma unroll
-            for (int pl = 0; pl < QPL; ++pl) q[qt][pl] = *(const f32x4*)(s_q + ((size_t)(g * 2 + pl) * QT + qt) * 256 + lane4);
-    };
-    // corpus blocks of (step st_, half h_, group g_): the two tiles are adjacent 1 KiB blocks
-    auto xaddr = [&](int64_t st_, int h_, int g_) __attribute__((always_inline)) -> const float* {
-        return Xs + s2_blk((uint64_t)((st_ * NW + wv) * RT + 2 * h_), g_, G);
-    };
-    if (s_begin < s_end) {
-#pragma unroll
-        for (int p = 0; p < PX; ++p) {
-            const float* xs = xaddr(s_begin, 0, p);
-#pragma unroll
-            for (int rt = 0; rt < RTH; ++rt)
-#pragma unroll
-                for (int pl = 0; pl < XPL; ++pl)
-                    xr[p][rt][pl] = *(const f32x4*)(xs + pl * PLANE + rt * BLOCK_FLOATS + lane4);
-        }
-        q_lds(0, qr);
-    }
-    constexpr int NRI = METRIC == 1 ? RT : 1;
-    auto load_epi = [&](int64_t st_, uint32_t (&g_)[QT], float (&r_)[NRI]) __attribute__((always_inline)) {
-#pragma unroll
-        for (int qt = 0; qt < QT; ++qt) {
-            const int qg = qb * QB + qt * 32 + (lane & 31);
-            g_[qt] = qg < B ? gthr[qg] : 0u;
-        }
-        if constexpr (METRIC == 1) {
-            const int64_t tt = (st_ * NW + wv) * RT;
-#pragma unroll
-            for (int rt = 0; rt < RT; ++rt) r_[rt] = lane < 32 ? rinit[(tt + rt) * 32 + lane] : 0.0f;
-        }
-    };
-    uint32_t gkn[QT];
-    float rin[NRI];
-    if (s_begin < s_end) load_epi(s_begin, gkn, rin);
-    const float ones = lane < 32 ? 1.0f : 0.0f;
-
-    f32x16 acc[2][RTH][QT];
-    uint32_t gk[QT];   // shared bounds of the step being tested
-    float thrh[QT];
-    bool qok[QT];
-#pragma unroll
-    for (int qt = 0; qt < QT; ++qt) qok[qt] = qb * QB + qt * 32 + (lane & 31) < B;
-    auto set_thr = [&]() __attribute__((always_inline)) {
-#pragma unroll
-        for (int qt = 0; qt < QT; ++qt) {
-            const int ql = qt * 32 + (lane & 31);
-            const float thr = fmaxf(s_thr[ql], key_to_float(max(gk[qt], s_sh[ql])));
-            thrh[qt] = METRIC == 0 ? thr : 0.5f * thr;
-        }
-    };
-    auto tile_test = [&](auto bc, int i) __attribute__((always_inline)) -> bool {
-        constexpr int bb = decltype(bc)::value;
-        const int rt = i / QT, qt = i % QT;
-        return __any(qok[qt] && tile_max16(acc[bb][rt][qt]) > thrh[qt]);
-    };
-    // phase 2 of half-step (s, h) (buffer h): inserts of its passing tiles, compaction rounds,
-    // and after the second half the step's publishing (as scan2_kernel)
-    auto epilogue2 = [&](auto bc, uint32_t hot, int64_t s) __attribute__((always_inline)) {
-        constexpr int h = decltype(bc)::value;
-        auto& a = acc[h];
-        const int64_t t0 = (s * NW + wv) * RT + 2 * h;
-        auto insert_pass = [&](int rt, int qt, float th, uint32_t cand) __attribute__((always_inline)) -> uint32_t {
-            const int ql = qt * 32 + (lane & 31);
-            uint32_t left = 0;
-            float mx = -INFINITY;
-#pragma unroll
-            for (int v = 0; v < 16; ++v) {
-                const bool p = ((cand >> v) & 1u) && a[rt][qt][v] > th;
-                if (__any(p)) {
-                    if (p) {
-                        float a_ = a[rt][qt][v];
-                        uint32_t rb = (uint32_t)((t0 + rt) * 32) + 4u * (uint32_t)(lane >> 5);
-                        asm volatile("" : "+v"(a_), "+v"(rb));
-                        const float sc = METRIC == 0 ? a_ : 2.0f * a_;
-                        const int pos = atomicAdd(&s_cnt[ql], 1);
-                        if (pos < CAP) {
-                            s_sc[ql * CAP + pos] = sc;
-                            s_ix[ql * CAP + pos] = rb + (uint32_t)((v & 3) + 8 * (v >> 2));
-                        } else {
-                            left |= 1u << v;
-                        }
-                        mx = fmaxf(mx, sc);
-                    }
-                }
-            }
-            if (mx != -INFINITY) atomicMax(&s_best[wv][ql], order_key(mx));
-            return left;
-        };
-        uint32_t pend[RTH][QT];
-        uint32_t any_left = 0;
-#pragma unroll
-        for (int rt = 0; rt < RTH; ++rt)
-#pragma unroll
-            for (int qt = 0; qt < QT; ++qt) {
-                pend[rt][qt] = 0u;
-                if ((hot >> (rt * QT + qt)) & 1u) {
-                    const uint32_t valid = qok[qt] ? tile_valid16(mask, t0 + rt, N, lane) : 0u;
-                    pend[rt][qt] = insert_pass(rt, qt, thrh[qt], valid);
-                    any_left |= pend[rt][qt];
-                }
-            }
-        for (bool joined = false;; joined = true) {
-            if constexpr (!FLAGSYNC) {
-                if (!__syncthreads_or(any_left != 0)) break;
-            } else {
-                const bool mine = __any(any_left != 0);
-                if (mine && lane == 0) *(volatile int*)&s_need = 1;
-                if (!mine && (joined || !__builtin_amdgcn_readfirstlane(*(volatile int*)&s_need))) break;
-                __syncthreads();  // B1
-            }
-            for (int q = wv; q < QB; q += NW)
-                if (s_cnt[q] >= CAP)
-                    compact_query<KP, CAP>(s_sc + q * CAP, s_ix + q * CAP, s_cnt + q, s_thr + q,
-                                           qb * QB + q < B ? gthr + qb * QB + q : nullptr);
-            if (FLAGSYNC && threadIdx.x == 0) *(volatile int*)&s_need = 0;
-            __syncthreads();  // B2
-            any_left = 0;
-#pragma unroll
-            for (int rt = 0; rt < RTH; ++rt)
-#pragma unroll
-                for (int qt = 0; qt < QT; ++qt) {
-                    if (!__any(pend[rt][qt] != 0)) continue;
-                    const int ql = qt * 32 + (lane & 31);
-                    const float thr = fmaxf(s_thr[ql], key_to_float(max(gk[qt], s_sh[ql])));
-                    pend[rt][qt] = insert_pass(rt, qt, METRIC == 0 ? thr : 0.5f * thr, pend[rt][qt]);
-                    any_left |= pend[rt][qt];
-                }
-        }
-        const int64_t sd = s - s_begin + 1;
-        if (h == 1 && publish && ((sd & (sd - 1)) == 0 || s + 1 == s_end)) {
-            int improved = 0;
-            if (pq_r < NW && pqg < B) {
-                const uint32_t best = s_best[pq_r][pq];
-                improved = best > s_pub[pq_r][pq];
-                if (improved) {
-                    s_pub[pq_r][pq] = best;
-                    atomicMax(gslots + (size_t)pqg * KP_MAX + ((wg * NW + pq_r) % KP), best);
-                }
-            }
-#pragma unroll
-            for (int off = 1; off < LPQ; off <<= 1) improved |= __shfl_xor(improved, off, 64);
-            if (improved) {
-                const uint32_t* sl = gslots + (size_t)pqg * KP_MAX + pq_r * SL;
-                uint32_t mn = 0xFFFFFFFFu;
-#pragma unroll
-                for (int j = 0; j < SLV; ++j) {
-                    const uint4 sv = *(const uint4*)(sl + 4 * j);
-                    mn = min(min(mn, min(sv.x, sv.y)), min(sv.z, sv.w));
-                }
-#pragma unroll
-                for (int off = 1; off < LPQ; off <<= 1) mn = min(mn, (uint32_t)__shfl_xor((int)mn, off, 64));
-                if (pq_r == 0 && pqg < B) {
-                    atomicMax(gthr + pqg, mn);
-                    atomicMax(&s_sh[pq], mn);
-                }
-            }
-        }
-    };
-
-    // half-step (s, h) into acc[h]; with `prev`, the previous half-step's tile tests (buffer
-    // h ^ 1: (s, 0) when h = 1, (s - 1, 1) when h = 0) ride along the groups and its inserts
-    // follow the K-loop
-    auto half = [&](auto hc, int64_t s, bool prev) __attribute__((always_inline)) {
-        constexpr int h = decltype(hc)::value;
-        constexpr int hp = h ^ 1;
-        // next half-step's corpus (the prefetch wraps into it)
-        const bool more = h == 0 || s + 1 < s_end;
-        const int64_t sn = h == 0 ? s : (more ? s + 1 : s);
-        const int hn = h == 0 ? 1 : 0;
-#pragma unroll
-        for (int rt = 0; rt < RTH; ++rt)
-#pragma unroll
-            for (int qt = 0; qt < QT; ++qt) {
-#pragma unroll
-                for (int v = 0; v < 16; ++v) acc[h][rt][qt][v] = 0.0f;
-                if constexpr (METRIC == 1)
-                    acc[h][rt][qt] = __builtin_amdgcn_mfma_f32_32x32x2f32(rin[METRIC == 1 ? 2 * h + rt : 0], ones,
-                                                                          acc[h][rt][qt], 0, 0, 0);
-            }
-        if (prev) set_thr();
-        uint32_t hot = 0;
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            const int p = g % PX;
-            f32x4 qn[QT][QPL];
-            q_lds(g + 1 < G ? g + 1 : 0, qn);
-            group_mfma<PREC, RTH, QT>(xr[p], qr, acc[h]);
-            __builtin_amdgcn_sched_barrier(0);
-            const float* src = g + PX < G ? xaddr(s, h, g + PX) : xaddr(sn, hn, g + PX - G);
-#pragma unroll
-            for (int rt = 0; rt < RTH; ++rt)
-#pragma unroll
-                for (int pl = 0; pl < XPL; ++pl)
-                    xr[p][rt][pl] = *(const f32x4*)(src + pl * PLANE + rt * BLOCK_FLOATS + lane4);
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int qt = 0; qt < QT; ++qt)
-#pragma unroll
-                for (int pl = 0; pl < QPL; ++pl) qr[qt][pl] = qn[qt][pl];
-            if (g < NTH && prev) hot |= tile_test(std::integral_constant<int, hp>{}, g) ? (1u << g) : 0u;
-            if (h == 1 && g == G - PX) {
-                // the next step's accumulator start values and shared bounds, a few groups
-                // ahead (any bound read earlier is still a valid one)
-#pragma unroll
-                for (int qt = 0; qt < QT; ++qt) gk[qt] = gkn[qt];
-                if (s + 1 < s_end) load_epi(s + 1, gkn, rin);
-            }
-        }
-        if (prev) epilogue2(std::integral_constant<int, hp>{}, hot, h == 1 ? s : s - 1);
-    };
-    using H0 = std::integral_constant<int, 0>;
-    using H1 = std::integral_constant<int, 1>;
-    if (s_begin < s_end) {
-#pragma unroll
-        for (int qt = 0; qt < QT; ++qt) gk[qt] = gkn[qt];
-    }
-    for (int64_t s = s_begin; s < s_end; ++s) {
-        half(H0{}, s, s > s_begin);
-        half(H1{}, s, true);
-    }
-    if (s_begin < s_end) {  // the last half-step's epilogue, alone
-        set_thr();
-        uint32_t hot = 0;
-#pragma unroll
-        for (int i = 0; i < NTH; ++i) hot |= tile_test(H1{}, i) ? (1u << i) : 0u;
-        epilogue2(H1{}, hot, s_end - 1);
-    }
-
-    if (FLAGSYNC && lane == 0) atomicAdd(&s_done, 1);
-    for (; FLAGSYNC;) {
-        if (lane == 0) *(volatile int*)&s_need = 1;
-        __syncthreads();  // B1
-        if (__builtin_amdgcn_readfirstlane(*(volatile int*)&s_done) == NW) break;
-        for (int q = wv; q < QB; q += NW)
-            if (s_cnt[q] >= CAP)
-                compact_query<KP, CAP>(s_sc + q * CAP, s_ix + q * CAP, s_cnt + q, s_thr + q,
-                                       qb * QB + q < B ? gthr + qb * QB + q : nullptr);
-        if (threadIdx.x == 0) *(volatile int*)&s_need = 0;
-        __syncthreads();  // B2
-    }
-    __syncthreads();
-    uint32_t tkey = 0;
-    if (lane < QPW && qb * QB + wv + NW * lane < B) tkey = max(gthr[qb * QB + wv + NW * lane], s_sh[wv + NW * lane]);
-    append_flush<CAP>(s_sc, s_ix, s_cnt, wv, NW, QPW, qb * QB, B, tkey, gl_s, gl_i, gl_cnt, gl_cap);
-}
-
 // ---- launch templates ----
 inline int scan2_qb(int KP) { return KP == 256 ? 32 : 64; }
 
@@ -931,16 +577,13 @@ static hipError_t scan2_launch_g(const float* Xs, const float* rinit, const uint
                                  int64_t N, int B, int n_qblocks, int64_t n_steps, int n_wg, int spw, float* gl_s,
                                  uint32_t* gl_i, uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr, uint32_t* gslots,
                                  const uint32_t* pslots, int prank, int publish, hipStream_t st) {
-    // the pipelined kernel loads half the tiles per group: twice the groups in flight, same bytes
-    auto k = (QL && GC > 0 && (publish & 2)) ? scan2p_kernel<P, M, QT, 2 * PX, KP, CAP, FS, (GC > 0 ? GC : 8)>
-                                             : scan2_kernel<P, M, QT, PX, KP, CAP, NT, QL, FS, GC>;
+    auto k = scan2_kernel<P, M, QT, PX, KP, CAP, NT, QL, FS, GC>;
     const size_t lds = QL ? (size_t)G * 2 * QT * 1024 : 0;
     if (QL) {
         // the dynamic part (query block) plus the static top-k buffers must fit the 160 KiB of a
         // CU: raise the dynamic limit to what this call needs (monotone; racing calls only
         // raise it to values that fit)
-        static std::atomic<size_t> lds_set_k[2];  // per kernel (plain / pipelined)
-        std::atomic<size_t>& lds_set = lds_set_k[(publish & 2) ? 1 : 0];
+        static std::atomic<size_t> lds_set{0};
         size_t cur = lds_set.load();
         while (lds > cur) {
             hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -950,7 +593,7 @@ static hipError_t scan2_launch_g(const float* Xs, const float* rinit, const uint
     }
     const int n_wg8 = (n_wg + 7) / 8 * 8;
     hipLaunchKernelGGL(k, dim3(n_wg8 * n_qblocks), dim3(256), lds, st, Xs, rinit, mask, Qs, G, N, B, n_steps, spw,
-                       n_qblocks, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, pslots, prank, publish & 1);
+                       n_qblocks, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, pslots, prank, publish);
     return hipGetLastError();
 }
 
