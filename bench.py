@@ -407,7 +407,7 @@ def main():
     Bg = B * world if (world > 1 and args.scaling == "weak") else B  # global batch
     Q = np.random.default_rng(1).random((Bg, D), dtype=np.float32)  # large_scale_benchmark.py:61
     q_dev = torch.from_numpy(Q).to(dev)
-    n_str = max(1, args.streams) if world == 1 else 1
+    n_str = max(1, args.streams)
     outs = [(torch.empty((Bg, k), dtype=torch.float32, device=dev), torch.empty((Bg, k), dtype=torch.int64, device=dev))
             for _ in range(n_str)]
     out_s, out_i = outs[0]
@@ -416,13 +416,14 @@ def main():
     n_step = [0]
 
     def step():
+        j = n_step[0] % n_str
+        n_step[0] += 1
+        os_, oi_ = outs[j]
         if searcher is None:
-            j = n_step[0] % n_str
-            n_step[0] += 1
-            os_, oi_ = outs[j]
             ix.search_device(q_dev.data_ptr(), Bg, k, os_.data_ptr(), oi_.data_ptr(), 0, stream=streams[j].cuda_stream)
-        else:
-            searcher.search(q_dev, k, out_s, out_i)
+        else:  # the rank's shard search, the RCCL all-gather and the merge, queued on stream j
+            with torch.cuda.stream(streams[j]):
+                searcher.search(q_dev, k, os_, oi_)
 
     for _ in range(args.warmup):
         step()
@@ -545,7 +546,7 @@ def main():
                              avg_launch_ms=scan_ms, hbm_gbs=achieved_gbs, mfma_tflops=achieved_tf,
                              hbm_frac=achieved_gbs / HBM_PEAK_GBS, mfma_frac=achieved_tf / mfma_peak),
             "pipeline_ms": pipe_ms,
-            "streams": max(1, args.streams) if world == 1 else 1,
+            "streams": max(1, args.streams),
             "roofline_timing": roof_timing,
             "fallback_queries_total": fallback,
             "fallback_queries_timed": fb_timed,  # (auto's bf16 probe falls back in warm-up at C3 / C4)

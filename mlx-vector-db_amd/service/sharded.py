@@ -65,7 +65,9 @@ class ShardedSearcher:
                                out_k.data_ptr() if out_k is not None else 0, stream)
 
     def _buffers(self, B: int, k: int, device):
-        key = (B, k, str(device))
+        # per stream: searches queued on several streams (bench.py --streams) each need their own
+        stream = torch.cuda.current_stream(device).cuda_stream if device.type == "cuda" else 0
+        key = (B, k, str(device), stream)
         if key not in self._bufs:
             f = dict(device=device)
             self._bufs[key] = (
