@@ -325,6 +325,8 @@ def main():
     ap.add_argument("--n-wg", type=int, default=None, help="candidate-pass workgroups (tuning)")
     ap.add_argument("--scan-sync", type=int, default=None,
                     help="candidate-pass step end: 1 lockstep barrier, 2 flag-gated rounds (tuning; default by D)")
+    ap.add_argument("--scan-realign", type=int, default=None,
+                    help="flag-gated step ends: a workgroup barrier every n steps (tuning)")
     ap.add_argument("--dir-bound", type=int, default=None,
                     help="bf16 certificate: 1 residual bound along the rows' mean direction (default), 0 Cauchy-Schwarz")
     ap.add_argument("--scan-publish", type=int, default=None,
@@ -384,6 +386,8 @@ def main():
         ix.set_param("scan_sync", args.scan_sync)
     if args.pilot_tiles is not None:
         ix.set_param("pilot_tiles", args.pilot_tiles)
+    if args.scan_realign is not None:
+        ix.set_param("scan_realign", args.scan_realign)
     if args.dir_bound is not None:
         ix.set_param("dir_bound", args.dir_bound)
     if args.scan_publish is not None:

@@ -70,16 +70,18 @@ enum { VDB_MEM_HOST = 0, VDB_MEM_DEVICE = 1 };
  *                    (HBM-bound).  Keeps a split copy of the corpus (same bytes
  *                    as the fp32 copy).
  *   VDB_PREC_BF16    the hi plane of the split copy only: x.q ~ xh.qh + xh.ql,
- *                    half the corpus bytes per search; the certificate adds the
- *                    largest row residual |x - bf16(x)| (measured at ingest), so
- *                    it is wider and takes a larger candidate margin.
+ *                    half the corpus bytes per search; the certificate adds a bound
+ *                    of the corpus rounding q.(x - bf16(x)) measured at ingest:
+ *                    min(|q| R, |q - c d| R + |c| M), R the largest row residual,
+ *                    d the normalised mean row of the first add, M the largest
+ *                    |d.(x - bf16(x))|, c = q.d, so it is wider
+ *                    and takes a larger candidate margin.
  *   VDB_PREC_AUTO    (default) BF16 while its certificate holds; after a search in
- *                    which more than 1/64 of the queries were not certified, BF16X3
- *                    until the index's rows change (add / clear; same split copy, so
- *                    switching costs nothing).  A host-memory search reruns such a
- *                    batch in BF16X3 at once; a device-memory search sees the counts
- *                    a search or more late (no host sync) and its flagged queries take
- *                    the exact path. */
+ *                    which any query was not certified, BF16X3 until the index's rows
+ *                    change (add / clear; same split copy, so switching costs nothing).
+ *                    A host-memory search reruns such a batch in BF16X3 at once; a
+ *                    device-memory search sees the counts a search or more late (no
+ *                    host sync) and its flagged queries take the exact path. */
 enum { VDB_PREC_FP32 = 0, VDB_PREC_BF16X3 = 1, VDB_PREC_BF16 = 2, VDB_PREC_AUTO = 3 };
 
 typedef struct vdb_index vdb_index;
@@ -105,6 +107,10 @@ int32_t vdb_index_reserve(vdb_index* idx, int64_t rows);
  * "scan_variant" / "scan_variant_bf16x3" (0..2, kernel tiling variants),
  * "scan_sync" (candidate-pass step end: 0 auto by dimension, 1 per-step barrier,
  * 2 flag-gated compaction rounds; results identical, speed differs),
+ * "scan_publish" (split pass slot publishing: -1 auto = on with >= 16 steps per
+ * workgroup, 0 off, 1 on), "dir_bound" (0: BF16 certificate with |q| R only;
+ * diagnostics), "pilot_tiles", "pilot_rank", "pilot_fused", "finish_split",
+ * "no_fallback" (diagnostics: flagged queries keep the approximate order),
  * "timing" (0/1: HIP events around the candidate pass; stats "scan_ns",
  * "pipeline_ns", "timed_searches").  Stats also: "searches", "queries",
  * "fallback_queries", "overflow_queries", "capacity", "count", "device_bytes", "precision",

@@ -144,6 +144,7 @@ struct vdb_index {
     int64_t pilot_fused = 0;
     int64_t scan_publish = -1;    // split pass slot publishing: -1 auto (>= 16 steps per workgroup), 0 off, 1 on
     bool no_dir_bound = false;    // diagnostics: PREC_BF16 certificate with Cauchy-Schwarz only
+    int64_t scan_realign = 0;     // flag-gated step ends: a workgroup barrier every n steps (0 none)
     int64_t finish_split = 1;  // workgroups per query in the finish kernel (tuning)
     // stats
     std::atomic<int64_t> n_searches{0}, n_queries{0}, n_fallback{0}, n_overflow{0};
@@ -539,6 +540,9 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
     } else if (n == "finish_split") {
         if (value < 1 || value > 8) return set_error(VDB_ERR_INVALID, "finish_split must be in [1, 8]");
         ix->finish_split = value;
+    } else if (n == "scan_realign") {
+        if (value < 0 || value > 255) return set_error(VDB_ERR_INVALID, "scan_realign must be in [0, 255]");
+        ix->scan_realign = value;
     } else if (n == "dir_bound") {
         ix->no_dir_bound = value == 0;
     } else if (n == "scan_publish") {
@@ -821,7 +825,7 @@ static int32_t search_impl(vdb_index* ix, const float* queries, int32_t B, int32
     // over many steps (C4: 610 per workgroup); with few (C2: 8) its global round trips at
     // steps 1, 2, 4, 8 cost more than the pilot's bound leaves to gain (measured: stamps,
     // profiles/r02_ab/).
-    const int publish = ix->scan_publish >= 0 ? (int)ix->scan_publish : spw >= 16;
+    const int publish = (ix->scan_publish >= 0 ? (int)ix->scan_publish : spw >= 16) | (int)(ix->scan_realign << 8);
 
     Workspace* w = acquire_ws(ix, st);
     struct Releaser {

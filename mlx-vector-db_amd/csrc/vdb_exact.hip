@@ -483,7 +483,6 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
         }
         if (lane == 0) s_bq = bq;
     }
-    __shared__ int s_ok;
     __shared__ double s_cut;
     __syncthreads();
     if (tid == 0) {
@@ -512,7 +511,6 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
             const int pos = atomicAdd(a.flag_count, 1);
             a.flag_list[pos] = b;
         }
-        s_ok = ok;
         // Rerank cut: the k best approx rows score (exact) >= a_k - eps, so the exact k-th best
         // is >= a_k - eps, and a row with approx < a_k - 2 eps scores (exact) < a_k - eps:
         // only candidates with approx >= a_k - 2 eps can be in the exact top k (2.001: the L2

@@ -400,32 +400,6 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
             if (mx != -INFINITY) atomicMax(&s_best[wv][ql], order_key(mx));
             return left;
         };
-        // (experiment) per-lane batch: one returning LDS atomic per lane reserves slots for all
-        // of its passing scores of the tile
-        auto insert_batch = [&](int rt, int qt, uint32_t pm) -> uint32_t {
-            if (!__any(pm != 0)) return 0u;
-            const int ql = qt * 32 + (lane & 31);
-            const int base = pm ? atomicAdd(&s_cnt[ql], __popc(pm)) : 0;
-            float mx = -INFINITY;
-#pragma unroll
-            for (int v = 0; v < 16; ++v) mx = ((pm >> v) & 1u) ? fmaxf(mx, acc[rt][qt][v]) : mx;
-            if (pm) atomicMax(&s_best[wv][ql], order_key(METRIC == 0 ? mx : 2.0f * mx));
-            uint32_t left = 0;
-#pragma unroll
-            for (int v = 0; v < 16; ++v) {
-                if ((pm >> v) & 1u) {
-                    const int pos = base + __popc(pm & ((1u << v) - 1u));
-                    if (pos < CAP) {
-                        const int ro = (v & 3) + 8 * (v >> 2) + 4 * (lane >> 5);
-                        s_sc[ql * CAP + pos] = METRIC == 0 ? acc[rt][qt][v] : 2.0f * acc[rt][qt][v];
-                        s_ix[ql * CAP + pos] = (uint32_t)((t0 + rt) * 32 + ro);
-                    } else {
-                        left |= 1u << v;
-                    }
-                }
-            }
-            return left;
-        };
         uint32_t pend[RT][QT];
         uint32_t any_left = 0;
 #pragma unroll
@@ -435,14 +409,7 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
                 pend[rt][qt] = 0u;
                 if (__any(qok[qt] && tile_max16(acc[rt][qt]) > thrh[qt])) {
                     const uint32_t valid = qok[qt] ? tile_valid16(mask, t0 + rt, N, lane) : 0u;
-#ifdef VDB_S2_BATCH_INSERT
-                    uint32_t pm = 0;
-#pragma unroll
-                    for (int v = 0; v < 16; ++v) pm |= acc[rt][qt][v] > thrh[qt] ? (1u << v) : 0u;
-                    pend[rt][qt] = insert_batch(rt, qt, pm & valid);
-#else
                     pend[rt][qt] = insert_pass(rt, qt, thrh[qt], valid);
-#endif
                     any_left |= pend[rt][qt];
                 }
             }
@@ -487,10 +454,16 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
         }
 #endif
         const int64_t sd = s - s_begin + 1;
+        // flag-gated step ends: an optional plain barrier every `realign` steps (bits 8-15 of
+        // `publish`) bounds how far the waves drift apart (they share the query operand's lines)
+        if constexpr (FLAGSYNC) {
+            const int realign = (publish >> 8) & 255;
+            if (realign > 0 && sd % realign == 0) __syncthreads();
+        }
 #ifdef VDB_S2_NO_PUBLISH
         if (false) {
 #else
-        if (publish && ((sd & (sd - 1)) == 0 || s + 1 == s_end)) {
+        if ((publish & 1) && ((sd & (sd - 1)) == 0 || s + 1 == s_end)) {
 #endif
             int improved = 0;
             if (pq_r < NW && pqg < B) {
