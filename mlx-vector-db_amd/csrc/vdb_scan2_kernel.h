@@ -41,8 +41,14 @@ static __device__ unsigned long long g_scan2_stamps[1 << 16][8];
 #define S2_NOW() __builtin_amdgcn_s_memtime()
 #endif
 
-constexpr int S2_RT = 4;  // row tiles (32 rows) per wave per step
-constexpr int S2_NW = 4;  // waves per workgroup
+#ifndef VDB_S2_RT
+#define VDB_S2_RT 4
+#endif
+#ifndef VDB_S2_NW
+#define VDB_S2_NW 4
+#endif
+constexpr int S2_RT = VDB_S2_RT;  // row tiles (32 rows) per wave per step
+constexpr int S2_NW = VDB_S2_NW;  // waves per workgroup
 constexpr int S2_ROWS = S2_RT * S2_NW * 32;
 
 // row-valid bits of row tile t for this lane: bit v <-> row 32 t + (v & 3) + 8 (v >> 2) + 4 (lane >> 5)
@@ -123,7 +129,7 @@ __device__ __forceinline__ uint32_t pilot_slot_rank(uint32_t (&v)[PILOT_E], int 
 // loop unrolls; the runtime loop made the register allocator copy 4 of the 8 accumulator
 // tiles between register sets on every step (256 v_accvgpr_mov per step at C4).
 template <int PREC, int METRIC, int QT, int PX, int KP, int CAP, bool NT, bool QLDS, bool FLAGSYNC, int GC = 0>
-__global__ void __launch_bounds__(256, 1)
+__global__ void __launch_bounds__(64 * S2_NW, 1)
 scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, const uint32_t* __restrict__ mask,
              const float* __restrict__ Qs, int G_arg, int64_t N, int B, int64_t n_steps, int steps_per_wg, int n_qb,
              float* __restrict__ gl_s, uint32_t* __restrict__ gl_i, uint32_t* __restrict__ gl_cnt, int64_t gl_cap,
@@ -565,7 +571,7 @@ static hipError_t scan2_launch_g(const float* Xs, const float* rinit, const uint
         }
     }
     const int n_wg8 = (n_wg + 7) / 8 * 8;
-    hipLaunchKernelGGL(k, dim3(n_wg8 * n_qblocks), dim3(256), lds, st, Xs, rinit, mask, Qs, G, N, B, n_steps, spw,
+    hipLaunchKernelGGL(k, dim3(n_wg8 * n_qblocks), dim3(64 * S2_NW), lds, st, Xs, rinit, mask, Qs, G, N, B, n_steps, spw,
                        n_qblocks, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, pslots, prank, publish);
     return hipGetLastError();
 }
