@@ -3,7 +3,10 @@
 #include "vdb_scan2_kernel.h"
 
 namespace vdb {
-S2_UNIT(launch_scan2_b1c, 2, 0, 4, 4)
+#ifndef VDB_S2_B1_PX
+#define VDB_S2_B1_PX 4
+#endif
+S2_UNIT(launch_scan2_b1c, 2, 0, VDB_S2_B1_PX, 4)
 }  // namespace vdb
 
 S2_STAMP_READER(b1c)

@@ -139,7 +139,12 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
     constexpr int QB = 32 * QT;
     constexpr int XPL = Planes<PREC>::XPL, QPL = 2;
     const int G = GC > 0 ? GC : G_arg;
-    constexpr int PQ = QLDS ? 1 : PX;
+    // query groups in flight (global query operand): PX, or VDB_S2_PQ when it divides PX (the
+    // query block is L2-resident, so it needs less lead than the corpus stream)
+#ifndef VDB_S2_PQ
+#define VDB_S2_PQ 0
+#endif
+    constexpr int PQ = QLDS ? 1 : (VDB_S2_PQ > 0 && VDB_S2_PQ < PX && PX % VDB_S2_PQ == 0 ? VDB_S2_PQ : PX);
     constexpr size_t GSTEP = 8 * BLOCK_FLOATS;  // consecutive groups of one super tile
     constexpr size_t PLANE = 4 * BLOCK_FLOATS;  // lo plane after hi
     static_assert(PX <= QG_EXTRA, "query prefetch deeper than the duplicated groups");
@@ -317,7 +322,7 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
 #pragma unroll
                     for (int pl = 0; pl < QPL; ++pl) qr[0][qt][pl] = qn[0][qt][pl];
             } else {
-                group_mfma<PREC, RT, QT>(xr[p], qr[p], acc);
+                group_mfma<PREC, RT, QT>(xr[p], qr[p % PQ], acc);
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int rt = 0; rt < RT; ++rt)
@@ -328,7 +333,7 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
                 for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
                     for (int pl = 0; pl < QPL; ++pl)
-                        qr[p][qt][pl] = *(const f32x4*)(qsrc + pl * PLANE + qt * BLOCK_FLOATS + lane4);
+                        qr[p % PQ][qt][pl] = *(const f32x4*)(qsrc + pl * PLANE + qt * BLOCK_FLOATS + lane4);
                 __builtin_amdgcn_sched_barrier(0);
             }
         };
