@@ -47,6 +47,23 @@ __device__ __forceinline__ size_t tiled_offset(uint64_t r, int d, int G) {
 __device__ __forceinline__ size_t split_block(uint64_t t, int g, int G16) {
     return (((size_t)(t >> 2) * G16 + g) * 8 + (t & 3)) * BLOCK_FLOATS;
 }
+// The CORPUS copy's block of (tile t, group g, plane pl).  Default: the query layout above
+// (the planes of a group adjacent).  VDB_PLANE_MAJOR: [T/4][2 planes][G16][4][1 KiB], so the hi
+// plane of a super tile is G16 x 4 KiB contiguous (the bf16 pass reads only that plane).
+#ifdef VDB_PLANE_MAJOR
+constexpr bool kPlaneMajor = true;
+#else
+constexpr bool kPlaneMajor = false;
+#endif
+__host__ __device__ __forceinline__ size_t corpus_block(uint64_t t, int g, int pl, int G16) {
+    if constexpr (kPlaneMajor) return ((((size_t)(t >> 2) * 2 + pl) * G16 + g) * 4 + (t & 3)) * BLOCK_FLOATS;
+    return (((size_t)(t >> 2) * G16 + g) * 8 + 4 * pl + (t & 3)) * BLOCK_FLOATS;
+}
+// corpus offsets (floats) between consecutive groups / from the hi to the lo plane of a block
+__host__ __device__ __forceinline__ constexpr size_t corpus_gstep() { return (kPlaneMajor ? 4 : 8) * BLOCK_FLOATS; }
+__host__ __device__ __forceinline__ size_t corpus_plane(int G16) {
+    return kPlaneMajor ? (size_t)G16 * 4 * BLOCK_FLOATS : 4 * BLOCK_FLOATS;
+}
 
 // Round-to-nearest-even fp32 -> bf16 bits for finite x (an overflow to inf falls
 // back to truncation so that hi stays finite and hi + lo still tracks x).

@@ -184,9 +184,9 @@ __global__ void __launch_bounds__(256) split_rows_kernel(const float* __restrict
     }
     f32x4 hi, lo;
     split8(a, b, hi, lo);
-    float* dst = Xs + split_block(t, g8 >> 1, G >> 1) + (size_t)(i + 32 * (g8 & 1)) * 4;
+    float* dst = Xs + corpus_block(t, g8 >> 1, 0, G >> 1) + (size_t)(i + 32 * (g8 & 1)) * 4;
     *(f32x4*)dst = hi;
-    *(f32x4*)(dst + 4 * BLOCK_FLOATS) = lo;
+    *(f32x4*)(dst + corpus_plane(G >> 1)) = lo;
 }
 
 hipError_t launch_split_rows(const float* X, int G, int64_t row0, int64_t n, const float* inv32, float* Xs,

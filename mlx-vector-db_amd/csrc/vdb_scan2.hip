@@ -34,7 +34,8 @@ pilot2_scores_kernel(const float* __restrict__ Xs, const float* __restrict__ rin
     const int qb = blockIdx.y;
     const bool live = i < n_sample;
     const uint64_t t = live ? (uint64_t)((int64_t)i * n_tiles / n_sample) : 0;
-    const float* xs = Xs + s2_blk(t, 0, G) + lane * 4;
+    const float* xs = Xs + corpus_block(t, 0, 0, G) + lane * 4;
+    const size_t XGSTEP = corpus_gstep(), XPLANE = corpus_plane(G);
     const float* qs = Qs + s2_blk((uint64_t)(qb * QT), 0, G + QG_EXTRA) + lane * 4;
     f32x16 acc[1][QT];
     const float r1 = (METRIC == 1 && part == 0 && lane < 32) ? rinit[t * 32 + lane] : 0.0f;
@@ -50,7 +51,7 @@ pilot2_scores_kernel(const float* __restrict__ Xs, const float* __restrict__ rin
     auto load = [&](int slot, int g) {
         if (g < G) {
 #pragma unroll
-            for (int pl = 0; pl < XPL; ++pl) xr[slot][0][pl] = *(const f32x4*)(xs + g * GSTEP + pl * PLANE);
+            for (int pl = 0; pl < XPL; ++pl) xr[slot][0][pl] = *(const f32x4*)(xs + g * XGSTEP + pl * XPLANE);
 #pragma unroll
             for (int qt = 0; qt < QT; ++qt)
 #pragma unroll

@@ -145,8 +145,10 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
 #define VDB_S2_PQ 0
 #endif
     constexpr int PQ = QLDS ? 1 : (VDB_S2_PQ > 0 && VDB_S2_PQ < PX && PX % VDB_S2_PQ == 0 ? VDB_S2_PQ : PX);
-    constexpr size_t GSTEP = 8 * BLOCK_FLOATS;  // consecutive groups of one super tile
-    constexpr size_t PLANE = 4 * BLOCK_FLOATS;  // lo plane after hi
+    constexpr size_t GSTEP = 8 * BLOCK_FLOATS;  // query: consecutive groups of one super tile
+    constexpr size_t PLANE = 4 * BLOCK_FLOATS;  // query: lo plane after hi
+    constexpr size_t XGSTEP = corpus_gstep();   // corpus (vdb_common.h corpus_block)
+    const size_t XPLANE = corpus_plane(G);
     static_assert(PX <= QG_EXTRA, "query prefetch deeper than the duplicated groups");
     __shared__ float s_sc[QB * CAP];
     __shared__ uint32_t s_ix[QB * CAP];
@@ -237,14 +239,14 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
             for (int pl = 0; pl < QPL; ++pl) q[qt][pl] = *(const f32x4*)(s_q + ((size_t)(g * 2 + pl) * QT + qt) * 256 + lane4);
     };
     if (s_begin < s_end) {
-        const float* xs = Xs + s2_blk((uint64_t)((s_begin * NW + wv) * RT), 0, G);
+        const float* xs = Xs + corpus_block((uint64_t)((s_begin * NW + wv) * RT), 0, 0, G);
 #pragma unroll
         for (int p = 0; p < PX; ++p)
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
                 for (int pl = 0; pl < XPL; ++pl)
-                    xr[p][rt][pl] = corpus_ld<NT>(xs + p * GSTEP + pl * PLANE + rt * BLOCK_FLOATS + lane4);
+                    xr[p][rt][pl] = corpus_ld<NT>(xs + p * XGSTEP + pl * XPLANE + rt * BLOCK_FLOATS + lane4);
         if constexpr (!QLDS) {
 #pragma unroll
             for (int p = 0; p < PQ; ++p)
@@ -286,8 +288,8 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
         ++st_n;
 #endif
         const int64_t t0 = (s * NW + wv) * RT;
-        const float* xs = Xs + s2_blk((uint64_t)t0, 0, G);
-        const float* xn = (s + 1 < s_end) ? Xs + s2_blk((uint64_t)(t0 + NW * RT), 0, G) : xs;
+        const float* xs = Xs + corpus_block((uint64_t)t0, 0, 0, G);
+        const float* xn = (s + 1 < s_end) ? Xs + corpus_block((uint64_t)(t0 + NW * RT), 0, 0, G) : xs;
         f32x16 acc[RT][QT];
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt)
@@ -315,7 +317,7 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
                 for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
                     for (int pl = 0; pl < XPL; ++pl)
-                        xr[p][rt][pl] = corpus_ld<NT>(xsrc + pl * PLANE + rt * BLOCK_FLOATS + lane4);
+                        xr[p][rt][pl] = corpus_ld<NT>(xsrc + pl * XPLANE + rt * BLOCK_FLOATS + lane4);
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int qt = 0; qt < QT; ++qt)
@@ -328,7 +330,7 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
                 for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
                     for (int pl = 0; pl < XPL; ++pl)
-                        xr[p][rt][pl] = corpus_ld<NT>(xsrc + pl * PLANE + rt * BLOCK_FLOATS + lane4);
+                        xr[p][rt][pl] = corpus_ld<NT>(xsrc + pl * XPLANE + rt * BLOCK_FLOATS + lane4);
 #pragma unroll
                 for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
@@ -341,12 +343,12 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
         for (; gb < G - PX; gb += PX) {
 #pragma unroll
             for (int p = 0; p < PX; ++p)
-                group(p, gb + p, xs + (size_t)(gb + p + PX) * GSTEP, Qbase + (size_t)(gb + p + PQ) * GSTEP);
+                group(p, gb + p, xs + (size_t)(gb + p + PX) * XGSTEP, Qbase + (size_t)(gb + p + PQ) * GSTEP);
         }
         if (s + 1 < s_end) load_epi(s + 1, gkn, rin);
 #pragma unroll
         for (int p = 0; p < PX; ++p)
-            group(p, gb + p, xn + (size_t)p * GSTEP, Qbase + (size_t)(gb + p + PQ) * GSTEP);
+            group(p, gb + p, xn + (size_t)p * XGSTEP, Qbase + (size_t)(gb + p + PQ) * GSTEP);
 
 #ifdef VDB_SCAN2_KLOOP_ONLY
         {  // diagnostic build (make variant): the K-loop alone, results are garbage
