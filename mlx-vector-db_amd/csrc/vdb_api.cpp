@@ -145,6 +145,7 @@ struct vdb_index {
     int64_t scan_publish = -1;    // split pass slot publishing: -1 auto (>= 16 steps per workgroup), 0 off, 1 on
     bool no_dir_bound = false;    // diagnostics: PREC_BF16 certificate with Cauchy-Schwarz only
     int64_t scan_realign = 0;     // flag-gated step ends: a workgroup barrier every n steps (0 none)
+    int64_t scan_qring = 0;       // split pass, global query operand: query chunks through an LDS ring
     int64_t finish_split = 1;  // workgroups per query in the finish kernel (tuning)
     // stats
     std::atomic<int64_t> n_searches{0}, n_queries{0}, n_fallback{0}, n_overflow{0};
@@ -439,6 +440,8 @@ int32_t vdb_index_create(int32_t dim, int32_t metric, int32_t device, vdb_index*
     ix->Dp = (int)round_up(dim, 64);  // G = Dp/8 is a multiple of the scan prefetch depth
     ix->G = ix->Dp / GROUP_DIMS;
     ix->n_cu = prop.multiProcessorCount;
+    // start value of the scan_qring parameter (A/B runs of whole test suites)
+    if (const char* qr = std::getenv("VDB_SCAN_QRING")) ix->scan_qring = std::atoi(qr) != 0;
     hipError_t e = hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMalloc(&ix->d_xmax, 64);
     if (e == hipSuccess) e = hipMemset(ix->d_xmax, 0, 64);
@@ -540,6 +543,9 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
     } else if (n == "finish_split") {
         if (value < 1 || value > 8) return set_error(VDB_ERR_INVALID, "finish_split must be in [1, 8]");
         ix->finish_split = value;
+    } else if (n == "scan_qring") {
+        if (value < 0 || value > 1) return set_error(VDB_ERR_INVALID, "scan_qring must be 0 or 1");
+        ix->scan_qring = value;
     } else if (n == "scan_realign") {
         if (value < 0 || value > 255) return set_error(VDB_ERR_INVALID, "scan_realign must be in [0, 255]");
         ix->scan_realign = value;
@@ -968,7 +974,8 @@ static int32_t search_impl(vdb_index* ix, const float* queries, int32_t B, int32
             if (split_pass)
                 HIP_TRY(launch_scan2(prec, ix->metric, KP, Xscan, ix->rinit32, md, Qt, Gs, N, B, n_qblocks, n_steps,
                                      n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, pslots,
-                                     n_pilot > 0 && ix->pilot_fused ? pilot_rank : 0, lockstep, publish, st));
+                                     n_pilot > 0 && ix->pilot_fused ? pilot_rank : 0, lockstep, publish, (int)ix->scan_qring,
+                                     st));
             else if (priv)
                 HIP_TRY(launch_scan_topk_priv(prec, ix->metric, KP, Xscan, rowscale, md, Qt, Gs, N, B, n_qblocks,
                                               n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, st));

@@ -108,7 +108,7 @@ int scan2_qb(int KP);
 hipError_t launch_scan2(int prec, int metric, int KP, const float* Xs, const float* rinit, const uint32_t* mask,
                         const float* Qs, int G, int64_t N, int B, int n_qblocks, int64_t n_steps, int n_wg, int spw,
                         float* gl_s, uint32_t* gl_i, uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr,
-                        uint32_t* gslots, const uint32_t* pslots, int prank, int lockstep, int publish,
+                        uint32_t* gslots, const uint32_t* pslots, int prank, int lockstep, int publish, int qring,
                         hipStream_t st);
 // Pilot scores for the split pass: fills pslots only; scan2 derives the bound (rank prank of
 // the slots) in its prologue, so there is no separate bound kernel.

@@ -129,17 +129,18 @@ int scan2_rows_per_step() { return S2_ROWS; }
 hipError_t launch_scan2(int prec, int metric, int KP, const float* Xs, const float* rinit, const uint32_t* mask,
                         const float* Qs, int G, int64_t N, int B, int n_qblocks, int64_t n_steps, int n_wg, int spw,
                         float* gl_s, uint32_t* gl_i, uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr,
-                        uint32_t* gslots, const uint32_t* pslots, int prank, int lockstep, int publish,
+                        uint32_t* gslots, const uint32_t* pslots, int prank, int lockstep, int publish, int qring,
                         hipStream_t st) {
     const bool ql = scan2_qlds(G, KP);
     const bool fs = !lockstep;
+    const bool qch = qring && !ql && !fs && G % S2_QCG == 0;
     const bool nt = !ql && n_qblocks == 1;
     auto* unit = prec == PREC_BF16X3 ? (metric == 0 ? launch_scan2_b3c : launch_scan2_b3l)
                  : prec == PREC_BF16 ? (metric == 0 ? launch_scan2_b1c : launch_scan2_b1l)
                                      : nullptr;
     if (!unit || metric < 0 || metric > 1) return hipErrorInvalidValue;
     return unit(KP, Xs, rinit, mask, Qs, G, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr,
-                gslots, pslots, prank, nt, ql, fs, publish, st);
+                gslots, pslots, prank, nt, ql, fs, qch, publish, st);
 }
 
 }  // namespace vdb

@@ -128,7 +128,12 @@ __device__ __forceinline__ uint32_t pilot_slot_rank(uint32_t (&v)[PILOT_E], int 
 // GC > 0: the dimension groups as a compile-time constant (short rows, C4: 8), so the group
 // loop unrolls; the runtime loop made the register allocator copy 4 of the 8 accumulator
 // tiles between register sets on every step (256 v_accvgpr_mov per step at C4).
-template <int PREC, int METRIC, int QT, int PX, int KP, int CAP, bool NT, bool QLDS, bool FLAGSYNC, int GC = 0>
+// QCH: the global query operand goes through a double-buffered LDS ring of S2_QCG-group chunks,
+// loaded once per workgroup instead of once per wave (lockstep step ends only: one workgroup
+// barrier per chunk, which every wave reaches since all run the same steps).
+constexpr int S2_QCG = 4;
+template <int PREC, int METRIC, int QT, int PX, int KP, int CAP, bool NT, bool QLDS, bool FLAGSYNC, int GC = 0,
+          bool QCH = false>
 __global__ void __launch_bounds__(64 * S2_NW, 1)
 scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, const uint32_t* __restrict__ mask,
              const float* __restrict__ Qs, int G_arg, int64_t N, int B, int64_t n_steps, int steps_per_wg, int n_qb,
@@ -144,7 +149,8 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
 #ifndef VDB_S2_PQ
 #define VDB_S2_PQ 0
 #endif
-    constexpr int PQ = QLDS ? 1 : (VDB_S2_PQ > 0 && VDB_S2_PQ < PX && PX % VDB_S2_PQ == 0 ? VDB_S2_PQ : PX);
+    static_assert(!QCH || (!QLDS && !FLAGSYNC), "query ring: global query operand, lockstep step ends");
+    constexpr int PQ = (QLDS || QCH) ? 1 : (VDB_S2_PQ > 0 && VDB_S2_PQ < PX && PX % (VDB_S2_PQ > 0 ? VDB_S2_PQ : 1) == 0 ? VDB_S2_PQ : PX);
     constexpr size_t GSTEP = 8 * BLOCK_FLOATS;  // query: consecutive groups of one super tile
     constexpr size_t PLANE = 4 * BLOCK_FLOATS;  // query: lo plane after hi
     constexpr size_t XGSTEP = corpus_gstep();   // corpus (vdb_common.h corpus_block)
@@ -214,6 +220,31 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
             *(f32x4*)(s_q + (size_t)e * 4) = *(const f32x4*)(Qbase + g * GSTEP + pl * PLANE + qt * BLOCK_FLOATS + 4 * l);
         }
     }
+    // query ring (QCH): chunk c = groups [CG c, CG c + CG) in buffer c & 1 ([g][plane][QT][256]
+    // floats, as the QLDS block); each thread moves QNE float4 of a chunk
+    constexpr int CG = S2_QCG;
+    constexpr int CHF = CG * 2 * QT * 256;  // floats per chunk buffer
+    constexpr int QNE = QCH ? CG * 2 * QT * 64 / (64 * NW) : 1;
+    static_assert(!QCH || (CG * 2 * QT * 64) % (64 * NW) == 0, "query chunk not a whole number of float4 per thread");
+    f32x4 qc[QNE];
+    auto ring_load = [&](int g0) {  // chunk starting at group g0 -> qc
+#pragma unroll
+        for (int j = 0; j < QNE; ++j) {
+            const int e = (int)threadIdx.x + 64 * NW * j;
+            const int l = e & 63, qt = (e >> 6) % QT, pl = (e / (64 * QT)) & 1, gi = e / (128 * QT);
+            qc[j] = *(const f32x4*)(Qbase + (size_t)(g0 + gi) * GSTEP + pl * PLANE + qt * BLOCK_FLOATS + 4 * l);
+        }
+    };
+    auto ring_store = [&](int buf) {
+#pragma unroll
+        for (int j = 0; j < QNE; ++j) *(f32x4*)(s_q + (size_t)buf * CHF + ((int)threadIdx.x + 64 * NW * j) * 4) = qc[j];
+    };
+    int cpar = 0;  // buffer of the chunk the next q_ring read falls in
+    if constexpr (QCH) {
+        ring_load(0);
+        ring_store(0);
+        ring_load(CG % G);
+    }
     __syncthreads();
 
     // slot publishing (as vdb_scan.hip): lane group pq_r of LPQ lanes serves query wv + NW (lane / LPQ)
@@ -238,6 +269,13 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
 #pragma unroll
             for (int pl = 0; pl < QPL; ++pl) q[qt][pl] = *(const f32x4*)(s_q + ((size_t)(g * 2 + pl) * QT + qt) * 256 + lane4);
     };
+    auto q_ring = [&](int g, f32x4 (&q)[QT][QPL]) {  // group g of the chunk in buffer cpar
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+            for (int pl = 0; pl < QPL; ++pl)
+                q[qt][pl] = *(const f32x4*)(s_q + (size_t)cpar * CHF + ((size_t)(g * 2 + pl) * QT + qt) * 256 + lane4);
+    };
     if (s_begin < s_end) {
         const float* xs = Xs + corpus_block((uint64_t)((s_begin * NW + wv) * RT), 0, 0, G);
 #pragma unroll
@@ -247,7 +285,9 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
 #pragma unroll
                 for (int pl = 0; pl < XPL; ++pl)
                     xr[p][rt][pl] = corpus_ld<NT>(xs + p * XGSTEP + pl * XPLANE + rt * BLOCK_FLOATS + lane4);
-        if constexpr (!QLDS) {
+        if constexpr (QCH) {
+            q_ring(0, qr[0]);
+        } else if constexpr (!QLDS) {
 #pragma unroll
             for (int p = 0; p < PQ; ++p)
 #pragma unroll
@@ -308,7 +348,30 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
         // one group: MFMAs of slot p, then refill slot p with the group PX ahead (this step's,
         // or the next step's first groups); refills pinned right behind the MFMAs
         auto group = [&](const int p, const int g, const float* xsrc, const float* qsrc) {
-            if constexpr (QLDS) {
+            if constexpr (QCH) {
+                const int gn = g + 1 < G ? g + 1 : 0;
+                if (gn % CG == 0) {  // the next group opens a chunk: publish the prefetched one
+                    ring_store(cpar ^ 1);
+                    cpar ^= 1;
+                    __syncthreads();
+                    ring_load(gn + CG < G ? gn + CG : 0);
+                }
+                f32x4 qn[1][QT][QPL];
+                q_ring(gn % CG, qn[0]);
+                group_mfma<PREC, RT, QT>(xr[p], qr[0], acc);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+                    for (int pl = 0; pl < XPL; ++pl)
+                        xr[p][rt][pl] = corpus_ld<NT>(xsrc + pl * XPLANE + rt * BLOCK_FLOATS + lane4);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+                    for (int pl = 0; pl < QPL; ++pl) qr[0][qt][pl] = qn[0][qt][pl];
+                (void)qsrc;
+            } else if constexpr (QLDS) {
                 f32x4 qn[1][QT][QPL];
                 q_lds(g + 1 < G ? g + 1 : 0, qn[0]);
                 group_mfma<PREC, RT, QT>(xr[p], qr[0], acc);
@@ -558,14 +621,14 @@ inline int scan2_qb(int KP) { return KP == 256 ? 32 : 64; }
 // The query block goes to LDS when it is small (C4: 64 queries x 128 dims = 32 KiB).
 inline bool scan2_qlds(int G16, int KP) { return (size_t)G16 * 2 * (scan2_qb(KP) / 32) * 1024 <= 32 * 1024; }
 
-template <int P, int M, int QT, int PX, int KP, int CAP, bool NT, bool QL, bool FS, int GC>
+template <int P, int M, int QT, int PX, int KP, int CAP, bool NT, bool QL, bool FS, int GC, bool QC = false>
 static hipError_t scan2_launch_g(const float* Xs, const float* rinit, const uint32_t* mask, const float* Qs, int G,
                                  int64_t N, int B, int n_qblocks, int64_t n_steps, int n_wg, int spw, float* gl_s,
                                  uint32_t* gl_i, uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr, uint32_t* gslots,
                                  const uint32_t* pslots, int prank, int publish, hipStream_t st) {
-    auto k = scan2_kernel<P, M, QT, PX, KP, CAP, NT, QL, FS, GC>;
-    const size_t lds = QL ? (size_t)G * 2 * QT * 1024 : 0;
-    if (QL) {
+    auto k = scan2_kernel<P, M, QT, PX, KP, CAP, NT, QL, FS, GC, QC>;
+    const size_t lds = QL ? (size_t)G * 2 * QT * 1024 : QC ? (size_t)2 * S2_QCG * 2 * QT * 1024 : 0;
+    if (QL || QC) {
         // the dynamic part (query block) plus the static top-k buffers must fit the 160 KiB of a
         // CU: raise the dynamic limit to what this call needs (monotone; racing calls only
         // raise it to values that fit)
@@ -606,12 +669,19 @@ static hipError_t scan2_launch(const float* Xs, const float* rinit, const uint32
     int KP, const float *Xs, const float *rinit, const uint32_t *mask, const float *Qs, int G, int64_t N, int B,    \
         int n_qblocks, int64_t n_steps, int n_wg, int spw, float *gl_s, uint32_t *gl_i, uint32_t *gl_cnt,          \
         int64_t gl_cap, uint32_t *gthr, uint32_t *gslots, const uint32_t *pslots, int prank, bool nt, bool ql,     \
-        bool fs, int publish, hipStream_t st
+        bool fs, bool qch, int publish, hipStream_t st
 #define S2_ARGS Xs, rinit, mask, Qs, G, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, \
                 pslots, prank, publish, st
 #define S2_ONE(P, M, KPV, QTV, PXV, CAPV, NTV, QLV, FSV)                 \
-    if (KP == KPV && nt == NTV && ql == QLV && fs == FSV)               \
+    if (KP == KPV && nt == NTV && ql == QLV && fs == FSV && !qch)       \
         return scan2_launch<P, M, QTV, PXV, KPV, CAPV, NTV, QLV, FSV>(S2_ARGS);
+// query ring variants (global query operand, lockstep step ends)
+#define S2_ONEQ(P, M, KPV, QTV, PXV, CAPV, NTV)                                      \
+    if (KP == KPV && nt == NTV && !ql && !fs && qch)                                \
+        return scan2_launch_g<P, M, QTV, PXV, KPV, CAPV, NTV, false, false, 0, true>(S2_ARGS);
+#define S2_KPQ(P, M, PXV, NTV)                                                       \
+    S2_ONEQ(P, M, 32, 2, PXV, 128, NTV) S2_ONEQ(P, M, 64, 2, PXV, 128, NTV)         \
+    S2_ONEQ(P, M, 128, 2, PXV, 192, NTV) S2_ONEQ(P, M, 256, 1, PXV, 320, NTV)
 #define S2_KP(P, M, PXV, NTV, QLV, FSV)                    \
     S2_ONE(P, M, 32, 2, PXV, 128, NTV, QLV, FSV)           \
     S2_ONE(P, M, 64, 2, PXV, 128, NTV, QLV, FSV)           \
@@ -622,7 +692,8 @@ static hipError_t scan2_launch(const float* Xs, const float* rinit, const uint32
 #define S2_MODES(P, M, PXV, PXL)                                                   \
     S2_KP(P, M, PXV, false, false, false) S2_KP(P, M, PXV, true, false, false)     \
     S2_KP(P, M, PXL, false, true, false) S2_KP(P, M, PXL, false, true, true)       \
-    S2_KP(P, M, PXV, false, false, true) S2_KP(P, M, PXV, true, false, true)
+    S2_KP(P, M, PXV, false, false, true) S2_KP(P, M, PXV, true, false, true)       \
+    S2_KPQ(P, M, PXV, false) S2_KPQ(P, M, PXV, true)
 #ifndef VDB_S2_QLDS_PX
 #define VDB_S2_QLDS_PX 2
 #endif
