@@ -108,7 +108,9 @@ int32_t vdb_index_reserve(vdb_index* idx, int64_t rows);
  * "scan_sync" (candidate-pass step end: 0 auto by dimension, 1 per-step barrier,
  * 2 flag-gated compaction rounds; results identical, speed differs),
  * "scan_publish" (split pass slot publishing: -1 auto = on with >= 16 steps per
- * workgroup, 0 off, 1 on), "dir_bound" (0: BF16 certificate with |q| R only;
+ * workgroup, 0 off, 1 on), "scan_qring" (split pass, lockstep step ends: 1 = the
+ * query operand through a per-workgroup LDS ring; start value from the environment
+ * variable VDB_SCAN_QRING, default 0), "dir_bound" (0: BF16 certificate with |q| R only;
  * diagnostics), "pilot_tiles", "pilot_rank", "pilot_fused", "finish_split",
  * "no_fallback" (diagnostics: flagged queries keep the approximate order),
  * "timing" (0/1: HIP events around the candidate pass; stats "scan_ns",

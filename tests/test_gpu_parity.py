@@ -110,6 +110,24 @@ def test_finish_split(vdb, split, metric):
     _check(vdb, V, Q, 25, metric, precision="bf16", params={"finish_split": split})
 
 
+@pytest.mark.parametrize("precision", ["bf16x3", "bf16"])
+@pytest.mark.parametrize("metric", ["cosine", "euclidean"])
+@pytest.mark.parametrize("D,B,k", [(320, 150, 100), (768, 40, 10), (1000, 20, 150)])
+def test_scan_query_ring(vdb, precision, metric, D, B, k):
+    """The candidate pass with the query operand through the per-workgroup LDS ring
+    (index param scan_qring: chunks of 4 dim groups, double-buffered, one barrier per chunk):
+    several query blocks, KP 32 to 256 (k 10 / 100 / 150 plus the margin), ragged D; the
+    overflowing data of test_scan_step_sync_modes keeps the compaction rounds busy."""
+    rng = np.random.default_rng(D + B)
+    N = 40000
+    Q = rng.random((B, D), dtype=np.float32)
+    t = (np.arange(N, dtype=np.float32) / N)[:, None]
+    V = (Q[rng.integers(0, B, N)] * t + rng.random((N, D), dtype=np.float32) * (1.0 - t)).astype(np.float32)
+    ix, _, _ = _check(vdb, V, Q, k, metric, precision=precision, params={"scan_qring": 1})
+    with pytest.raises(Exception):
+        ix.set_param("scan_qring", 2)
+
+
 @pytest.mark.parametrize("sync", [1, 2])
 @pytest.mark.parametrize("metric", ["cosine", "euclidean"])
 @pytest.mark.parametrize("D,B,k", [(128, 150, 100), (384, 70, 10)])
