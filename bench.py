@@ -328,6 +328,7 @@ def main():
     ap.add_argument("--n-wg", type=int, default=None, help="candidate-pass workgroups (tuning)")
     ap.add_argument("--scan-sync", type=int, default=None,
                     help="candidate-pass step end: 1 lockstep barrier, 2 flag-gated rounds (tuning; default by D)")
+    ap.add_argument("--gate-div", type=int, default=None, help="gated fallback: n_cu / d workgroups (tuning)")
     ap.add_argument("--scan-qring", type=int, default=None, help="1: query operand through an LDS ring (tuning)")
     ap.add_argument("--scan-realign", type=int, default=None,
                     help="flag-gated step ends: a workgroup barrier every n steps (tuning)")
@@ -392,6 +393,8 @@ def main():
         ix.set_param("pilot_tiles", args.pilot_tiles)
     if args.scan_realign is not None:
         ix.set_param("scan_realign", args.scan_realign)
+    if args.gate_div is not None:
+        ix.set_param("gate_div", args.gate_div)
     if args.scan_qring is not None:
         ix.set_param("scan_qring", args.scan_qring)
     if args.dir_bound is not None:

@@ -110,7 +110,9 @@ int32_t vdb_index_reserve(vdb_index* idx, int64_t rows);
  * "scan_publish" (split pass slot publishing: -1 auto = on with >= 16 steps per
  * workgroup, 0 off, 1 on), "scan_qring" (split pass, lockstep step ends: 1 = the
  * query operand through a per-workgroup LDS ring; start value from the environment
- * variable VDB_SCAN_QRING, default 0), "dir_bound" (0: BF16 certificate with |q| R only;
+ * variable VDB_SCAN_QRING, default 0), "gate_div" (1..64: the device-gated exact
+ * fallback runs on n_cu / gate_div row ranges, one query slot each when > 1; start value
+ * from VDB_GATE_DIV, default 1), "dir_bound" (0: BF16 certificate with |q| R only;
  * diagnostics), "pilot_tiles", "pilot_rank", "pilot_fused", "finish_split",
  * "no_fallback" (diagnostics: flagged queries keep the approximate order),
  * "timing" (0/1: HIP events around the candidate pass; stats "scan_ns",

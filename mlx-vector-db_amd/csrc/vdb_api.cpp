@@ -146,6 +146,7 @@ struct vdb_index {
     bool no_dir_bound = false;    // diagnostics: PREC_BF16 certificate with Cauchy-Schwarz only
     int64_t scan_realign = 0;     // flag-gated step ends: a workgroup barrier every n steps (0 none)
     int64_t scan_qring = 0;       // split pass, global query operand: query chunks through an LDS ring
+    int64_t gate_div = 1;         // gated exact fallback: n_cu / gate_div row ranges, one query slot each when > 1
     int64_t finish_split = 1;  // workgroups per query in the finish kernel (tuning)
     // stats
     std::atomic<int64_t> n_searches{0}, n_queries{0}, n_fallback{0}, n_overflow{0};
@@ -373,8 +374,10 @@ int run_exact(vdb_index* ix, Workspace* w, const float* Qd, const double* qn64, 
     const int KE = std::max(32, next_pow2(k));
     const int64_t N = ix->count;
     const bool gated = qcount_dev != nullptr;
-    // ~2 workgroups per CU of rows (gated: 1), at least 64 rows per wave
-    int n_wg = (int)std::min<int64_t>(std::max<int64_t>(1, ix->n_cu * (gated ? 1 : 2)), std::max<int64_t>(1, N / 256));
+    // ~2 workgroups per CU of rows (gated: 1 / gate_div, since an empty gated launch still has to
+    // find free CUs beside the next batch's scan), at least 64 rows per wave
+    const int64_t wg_target = gated ? std::max<int64_t>(1, ix->n_cu / std::max<int64_t>(1, ix->gate_div)) : 2 * ix->n_cu;
+    int n_wg = (int)std::min<int64_t>(wg_target, std::max<int64_t>(1, N / 256));
     const int64_t rpw = (N + n_wg - 1) / n_wg;
     n_wg = (int)((N + rpw - 1) / rpw);
     const int n_lists = n_wg;
@@ -390,7 +393,8 @@ int run_exact(vdb_index* ix, Workspace* w, const float* Qd, const double* qn64, 
     if (gated && done_dev) {  // one launch: the last workgroup per query merges and writes (ExactTail)
         const ExactTail tail{done_dev, mk, mi, k, index_offset, out_s, out_i, out_k, row_ids, host_totals};
         HIP_TRY(launch_exact_scan(ix->metric, KE, Qd, qn64, qlist_dev, nq, ix->X, ix->G, ix->dim, ix->nrm64, mask_dev,
-                                  N, n_wg, rpw, lk, li, st, qcount_dev, ovf_dev, ix->d_totals, &tail));
+                                  N, n_wg, rpw, lk, li, st, qcount_dev, ovf_dev, ix->d_totals, &tail,
+                                  ix->gate_div > 1 ? 1 : 4));
         return VDB_OK;
     }
     HIP_TRY(launch_exact_scan(ix->metric, KE, Qd, qn64, qlist_dev, nq, ix->X, ix->G, ix->dim, ix->nrm64, mask_dev, N,
@@ -442,6 +446,7 @@ int32_t vdb_index_create(int32_t dim, int32_t metric, int32_t device, vdb_index*
     ix->n_cu = prop.multiProcessorCount;
     // start value of the scan_qring parameter (A/B runs of whole test suites)
     if (const char* qr = std::getenv("VDB_SCAN_QRING")) ix->scan_qring = std::atoi(qr) != 0;
+    if (const char* gd = std::getenv("VDB_GATE_DIV")) ix->gate_div = std::min(64, std::max(1, std::atoi(gd)));
     hipError_t e = hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMalloc(&ix->d_xmax, 64);
     if (e == hipSuccess) e = hipMemset(ix->d_xmax, 0, 64);
@@ -543,6 +548,9 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
     } else if (n == "finish_split") {
         if (value < 1 || value > 8) return set_error(VDB_ERR_INVALID, "finish_split must be in [1, 8]");
         ix->finish_split = value;
+    } else if (n == "gate_div") {
+        if (value < 1 || value > 64) return set_error(VDB_ERR_INVALID, "gate_div must be in [1, 64]");
+        ix->gate_div = value;
     } else if (n == "scan_qring") {
         if (value < 0 || value > 1) return set_error(VDB_ERR_INVALID, "scan_qring must be 0 or 1");
         ix->scan_qring = value;

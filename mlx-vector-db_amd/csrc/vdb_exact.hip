@@ -799,7 +799,8 @@ exact_scan_kernel(const float* __restrict__ Q, const double* __restrict__ qn64, 
 hipError_t launch_exact_scan(int metric, int KE, const float* Q, const double* qn64, const int* qlist, int nq,
                              const float* X, int G, int D, const double* nrm64, const uint32_t* mask, int64_t N,
                              int n_wg, int64_t rows_per_wg, double* lk, uint32_t* li, hipStream_t st,
-                             const int* qcount, const int* ovf, unsigned long long* totals, const ExactTail* tail) {
+                             const int* qcount, const int* ovf, unsigned long long* totals, const ExactTail* tail,
+                             int gate_slots) {
     size_t lds = (size_t)4 * WaveTopK<double, uint32_t>::capacity(KE) * (sizeof(double) + sizeof(uint32_t));
     ExactTail tl{};
     if (tail) {
@@ -809,7 +810,7 @@ hipError_t launch_exact_scan(int metric, int KE, const float* Q, const double* q
     }
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     // gated: a few query slots per row range, each looping over the flagged queries
-    const dim3 grid(n_wg, qcount ? (nq < 4 ? nq : 4) : nq);
+    const dim3 grid(n_wg, qcount ? (nq < gate_slots ? nq : gate_slots) : nq);
     if (metric == 0)
         hipLaunchKernelGGL((exact_scan_kernel<0>), grid, dim3(256), lds, st, Q, qn64, qlist, X, G, D, nrm64, mask, N,
                            rows_per_wg, KE, lk, li, qcount, nq, ovf, totals, tl);
