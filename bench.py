@@ -43,14 +43,24 @@ from service.sharded import ShardedSearcher, shard_bounds  # noqa: E402
 
 METRIC = "QPS + p50 latency, cosine top-10 batch=64: 1M×768D @1 GPU; 10M×128D @8 GPU"
 CONFIGS = {
-    # name: (N, D, B, k, metric, description)
+    # name: (N, D, B, k, metric, description); c1-c5 = BASELINE.json configs[0..4], c6 = the
+    # second half of BASELINE.json's metric ("cosine top-10 batch=64: ... 10M x 128D @8 GPU")
     "c1": (10_000, 384, 1, 10, "cosine", "10K x 384 cosine top-10, single query"),
     "c2": (1_000_000, 768, 64, 10, "cosine", "1M x 768 fp32 cosine top-10, batch 64"),
-    "c3": (1_000_000, 1536, 256, 10, "cosine", "1M x 1536 cosine top-10, batch 256 (fp32 candidate pass)"),
+    "c3": (1_000_000, 1536, 256, 10, "cosine", "1M x 1536 cosine top-10, batch 256 (bf16 candidate pass)"),
     "c4": (10_000_000, 128, 512, 100, "euclidean", "10M x 128 L2 top-100, batch 512, row-sharded"),
     # graph path (performance/hnsw_index.py): batch 1, hnswlib M=16 -> out-degree 2M, efSearch 128
     "c5": (5_000_000, 384, 1, 10, "cosine", "5M x 384 graph index (HNSW M=16) cosine top-10, efSearch=128, batch 1"),
+    "c6": (10_000_000, 128, 64, 10, "cosine", "10M x 128 cosine top-10, batch 64, row-sharded (the metric's 8-GPU workload)"),
 }
+# --gpus N > 1 without --scaling: the configs BASELINE.json quotes with a fixed global batch sharded
+# over the GPUs (configs[3] "batch=512 ... sharded across 8"; the metric's "10M x 128D @8 GPU" at
+# batch 64) keep that batch (strong scaling); the single-GPU configs run B per GPU (weak scaling)
+DEFAULT_SCALING = {"c4": "strong", "c6": "strong"}
+# the binding roofline of each config's algorithmic work (fp32 arithmetic on fp32
+# rows): C2 / C4 (and c6, same intensity 2 B D / 4 D = B/2 F/B above the fp32 ridge) FP32-MFMA,
+# C3 HBM with the bf16 corpus it names (2 B per element)
+SURVEY_BOUND = {"c1": "hbm", "c2": "mfma_fp32", "c3": "hbm", "c4": "mfma_fp32", "c6": "mfma_fp32"}
 GRAPH_M, GRAPH_EF = 16, 128
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md, Peak FP32 (matrix)
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md, Peak BF16 MFMA, dense
@@ -75,45 +85,56 @@ def corpus_rows(N, D, start, stop, seed=0):
 
 
 def cpu_baseline(V, Q, k, metric="cosine", budget_s=10.0):
-    """BASELINE.md §2, both reference paths restated in numpy (oracle/ref_cpu.py), each
-    timed for at least `budget_s` on this host's cores:
-      (ii) batched  `optimized_batch_similarity_search` (performance/mlx_optimized.py:217-248):
-           whole batches of B queries (normalise + fp32 BLAS matmul + stable argsort);
+    """BASELINE.md §2, the reference's CPU paths restated in numpy (oracle/ref_cpu.py), each
+    timed for about `budget_s` on this host's cores on a BOUNDED sample of the workload (the
+    full corpus, a subset of the batch's queries), so the default bench stays within minutes:
+      (ii) batched `optimized_batch_similarity_search` (performance/mlx_optimized.py:217-248),
+           cosine only (the module has no batched L2): sub-batches of Bs queries (normalise +
+           fp32 BLAS matmul + stable argsort of [Bs, N]); Bs = B up to 64M scores per batch;
       (i)  per-query store path `_brute_force_search` (service/optimized_vector_store.py:149-192):
-           one query at a time (re-normalise the corpus, matvec, full stable argsort, [:k]).
-    `value` is the faster of the two (the batched path); p50 is per batch / per query."""
+           one query at a time (re-normalise the corpus / direct differences for L2, full stable
+           argsort, [:k]).
+    `value` is the faster of the two in queries/s."""
     from oracle import ref_cpu
     try:
         from threadpoolctl import threadpool_info
         threads = max([p.get("num_threads", 1) for p in threadpool_info() if p.get("user_api") == "blas"] or [1])
     except Exception:
         threads = int(os.environ.get("OMP_NUM_THREADS", "1"))
-    bt = []
-    t0 = time.perf_counter()
-    while not bt or (time.perf_counter() - t0 < budget_s and len(bt) < 50):
-        t1 = time.perf_counter()
-        if metric == "cosine":
-            ref_cpu.reference_batch_search(Q, V, k)
-        else:  # the store's euclidean operator, per query of the batch (the batched module has none)
-            for q in Q:
-                ref_cpu.reference_topk_indices(ref_cpu.reference_euclidean_distances(q, V), k, metric)
-        bt.append(time.perf_counter() - t1)
+    N = V.shape[0]
+    B = Q.shape[0]
+    res = {"unit": "queries/s", "cores": threads, "kind": "port"}
+    parts = []
+    batched_qps = 0.0
+    if metric == "cosine":
+        Bs = int(max(1, min(B, (64 << 20) // max(N, 1))))
+        bt = []
+        t0 = time.perf_counter()
+        j = 0
+        while not bt or (time.perf_counter() - t0 < budget_s and len(bt) < 50):
+            t1 = time.perf_counter()
+            ref_cpu.reference_batch_search(Q[(j * Bs) % B:(j * Bs) % B + Bs], V, k)
+            bt.append(time.perf_counter() - t1)
+            j += 1
+        batched_qps = Bs / float(np.mean(bt))
+        res["batched"] = {"qps": batched_qps, "p50_ms_per_batch": float(np.median(bt)) * 1e3, "batches": len(bt),
+                          "queries_per_batch": Bs}
+        parts.append(f"(ii) {len(bt)} batch(es) of {Bs} of the {B} queries x the full {N}x{V.shape[1]} corpus "
+                     f"({sum(bt):.1f} s)")
     qt = []
     t0 = time.perf_counter()
     i = 0
     while not qt or (time.perf_counter() - t0 < budget_s and len(qt) < 50):
         t1 = time.perf_counter()
-        ref_cpu.reference_store_search(Q[i % Q.shape[0]], V, k, metric)
+        ref_cpu.reference_store_search(Q[i % B], V, k, metric)
         qt.append(time.perf_counter() - t1)
         i += 1
-    batched_qps = Q.shape[0] / float(np.mean(bt))
     single_qps = 1.0 / float(np.mean(qt))
-    return {"value": max(batched_qps, single_qps), "unit": "queries/s", "cores": threads, "kind": "port",
-            "sample": f"numpy restatement on this host: (ii) {len(bt)} batch(es) of {Q.shape[0]} queries x the full "
-                      f"{V.shape[0]}x{V.shape[1]} corpus ({sum(bt):.1f} s) and (i) {len(qt)} single queries through "
-                      f"the store path ({sum(qt):.1f} s); value = the faster path",
-            "batched": {"qps": batched_qps, "p50_ms_per_batch": float(np.median(bt)) * 1e3, "batches": len(bt)},
-            "per_query": {"qps": single_qps, "p50_ms": float(np.median(qt)) * 1e3, "queries": len(qt)}}
+    res["per_query"] = {"qps": single_qps, "p50_ms": float(np.median(qt)) * 1e3, "queries": len(qt)}
+    parts.append(f"(i) {len(qt)} single queries through the store path ({sum(qt):.1f} s)")
+    res["value"] = max(batched_qps, single_qps)
+    res["sample"] = "numpy restatement on this host: " + " and ".join(parts) + "; value = the faster path"
+    return res
 
 
 def cpu_graph_baseline(V, nbr, entries, Q, k, ef, metric, gt, budget_s=15.0):
@@ -320,8 +341,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
-                    help="N>1: weak = global batch B*N (fixed work per GPU), strong = global batch B")
+    ap.add_argument("--scaling", default=None, choices=["weak", "strong"],
+                    help="N>1: weak = global batch B*N (fixed work per GPU), strong = global batch B "
+                         "(default: strong for c4 / c6, whose BASELINE batch is sharded, weak otherwise)")
     ap.add_argument("--precision", default="auto", choices=["auto", "bf16x3", "bf16", "fp32"],
                     help="candidate-pass arithmetic (results identical; DESIGN.md §3)")
     ap.add_argument("--scan-variant", type=int, default=None, help="candidate-pass kernel variant (tuning)")
@@ -377,6 +399,8 @@ def main():
         return main_graph(args, world, rank, local, dev)
 
     N, D, B, k, metric, desc = CONFIGS[args.config]
+    N = args.rows or N
+    scaling = args.scaling or DEFAULT_SCALING.get(args.config, "weak")
     lo, hi = shard_bounds(N, world, rank)
     n_local = hi - lo
 
@@ -417,7 +441,7 @@ def main():
         if keep_host:
             host_parts.append(part)
     assert ix.count() == n_local
-    Bg = B * world if (world > 1 and args.scaling == "weak") else B  # global batch
+    Bg = B * world if (world > 1 and scaling == "weak") else B  # global batch
     Q = np.random.default_rng(1).random((Bg, D), dtype=np.float32)  # large_scale_benchmark.py:61
     q_dev = torch.from_numpy(Q).to(dev)
     n_str = max(1, args.streams)
@@ -500,13 +524,20 @@ def main():
     fallback = ix.stat("fallback_queries")
     overflow = ix.stat("overflow_queries")
     if rank == 0:
-        # algorithmic work of one scan launch on this rank: every corpus row read once
-        # (fp32 tiles or the split hi/lo tiles: 4 B per element either way), its row
-        # scale, the queries; flops = 2 B N D (x3 bf16 MFMA flops for the split product)
-        # (bf16: the hi plane only, 2 B per element; 2 bf16 MFMA per product)
+        # Two rooflines of the scan kernel, each named:
+        # (1) "implementation" (the top-level fields): the work the kernel's own arithmetic must do
+        #     per launch -- every corpus row read once at the element size of the candidate copy it
+        #     scans (bf16: the hi plane, 2 B; bf16x3 / fp32: 4 B), the L2 row start values, the
+        #     queries; its own MFMA count (fp32: 2BND on the FP32 peak; bf16 2x and bf16x3 3x the
+        #     products on the bf16 peak) -- bound by whichever floor is longer;
+        # (2) "survey_8d": SURVEY.md §8(d)'s algorithmic work for the config (fp32 arithmetic:
+        #     2BND flops, 4 B per element; C3 names the bf16 corpus, 2 B) on the roofline §8(d) calls
+        #     binding.  frac > 1 there means the kernel does that fp32-equivalent work in cheaper
+        #     MFMAs (split bf16) than §8(d)'s FP32-MFMA roofline assumes; exactness comes from the
+        #     fp64 rerank + certificate.
         Dp = (D + 63) // 64 * 64
         elem = 2 if prec == "bf16" else 4
-        hbm_bytes = n_local * Dp * elem + n_local * 4 + Bg * Dp * 4
+        hbm_bytes = n_local * Dp * elem + (n_local * 4 if metric == "euclidean" else 0) + Bg * Dp * 4
         if prec == "fp32":
             mfma_flops, mfma_peak = 2.0 * Bg * n_local * D, FP32_MFMA_PEAK_TFLOPS
         else:
@@ -521,6 +552,22 @@ def main():
         else:
             roof = {"bound": "mfma", "achieved": achieved_tf, "peak": mfma_peak, "unit": "TFLOP/s",
                     "frac": achieved_tf / mfma_peak}
+        roof["basis"] = (f"implementation: {elem} B per corpus element read once + queries; "
+                         f"{ {'fp32': 1, 'bf16x3': 3, 'bf16': 2}[prec]} MFMA product(s) per fp32 product "
+                         f"({'fp32' if prec == 'fp32' else 'bf16'} peak)")
+        s_bound = SURVEY_BOUND.get(args.config, "mfma_fp32")
+        s_flops = 2.0 * Bg * n_local * D
+        s_bytes = n_local * D * (2 if args.config == "c3" else 4) + 4 * n_local + 4 * Bg * D + 12 * Bg * k
+        if s_bound == "hbm":
+            s_ach = s_bytes / (scan_ms * 1e-3) / 1e9
+            survey = {"bound": "hbm", "work": s_bytes, "work_unit": "B", "achieved": s_ach, "peak": HBM_PEAK_GBS,
+                      "unit": "GB/s", "frac": s_ach / HBM_PEAK_GBS}
+        else:
+            s_ach = s_flops / (scan_ms * 1e-3) / 1e12
+            survey = {"bound": "mfma_fp32", "work": s_flops, "work_unit": "FLOP", "achieved": s_ach,
+                      "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": s_ach / FP32_MFMA_PEAK_TFLOPS}
+        survey["note"] = ("SURVEY.md §8(d) work per launch (fp32: 2BND flops, 4 B/element; c3: bf16 corpus); "
+                          "frac > 1 = the fp32-equivalent work done in split-bf16 MFMAs with an exact fp64 rerank")
         traffic = None
         traffic_src = None
         cands = [args.pmc_json] if args.pmc_json else sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc.json")))
@@ -544,7 +591,7 @@ def main():
             "ms_per_step": elapsed / args.steps * 1e3,
             "p50_ms": p50 * 1e3,
             "higher_is_better": True,
-            "scaling": args.scaling if world > 1 else "weak",
+            "scaling": scaling if world > 1 else "weak",
             "vs_baseline": None,
             "dtype": {"fp32": "f32", "bf16x3": "f32 (bf16x3 split MFMA candidates, fp64 exact rerank)",
                       "bf16": "f32 (bf16 corpus x split query MFMA candidates, fp64 exact rerank)"}[prec],
@@ -553,7 +600,8 @@ def main():
                        "batch_per_gpu_equiv": B, "k": k,
                        "metric": metric, "parallelism": f"row-shard x{world}" if world > 1 else "single GPU",
                        "rows_per_gpu": n_local},
-            "roofline": dict(roof, traffic=traffic, kernel="scan2_kernel" if prec != "fp32" else "scan_topk", precision=prec,
+            "roofline": dict(roof, traffic=traffic, kernel="scan2_kernel" if prec != "fp32" else "scan_topk",
+                             survey_8d=survey, precision=prec,
                              precision_requested=args.precision, searches_by_precision=by_prec,
                              traffic_source=traffic_src, algorithmic_bytes=hbm_bytes, algorithmic_flops=mfma_flops,
                              avg_launch_ms=scan_ms, hbm_gbs=achieved_gbs, mfma_tflops=achieved_tf,

@@ -22,10 +22,13 @@
  *     stream) and return without waiting: the results are in device memory
  *     once the stream reaches that point (the exactness certificate is
  *     checked and any fallback queued on the device, see vdb_index_search).
- *     Host-memory calls run on `stream` or, if NULL, the index's own stream
- *     and return when the results are in host memory.
+ *     Host-memory calls run on `stream` or, if NULL, on a stream of the
+ *     per-search workspace they take (so concurrent host-memory searches from
+ *     several threads overlap on the device) and return when the results are
+ *     in host memory.
  *   - The library never frees caller memory.  An index owns its device-resident
- *     corpus (tiled fp32 layout) and a per-call workspace pool.
+ *     corpus (row-major fp32 rows + a split-bf16 candidate copy in MFMA operand
+ *     tiles) and a per-call workspace pool.
  *   - All entry points are thread-safe; searches on one index may run from
  *     several threads at once (the reference serves from a 4-thread executor,
  *     api/routes/vectors.py:43).
@@ -76,12 +79,15 @@ enum { VDB_MEM_HOST = 0, VDB_MEM_DEVICE = 1 };
  *                    d the normalised mean row of the first add, M the largest
  *                    |d.(x - bf16(x))|, c = q.d, so it is wider
  *                    and takes a larger candidate margin.
- *   VDB_PREC_AUTO    (default) BF16 while its certificate holds; after a search in
- *                    which any query was not certified, BF16X3 until the index's rows
- *                    change (add / clear; same split copy, so switching costs nothing).
- *                    A host-memory search reruns such a batch in BF16X3 at once; a
- *                    device-memory search sees the counts a search or more late (no
- *                    host sync) and its flagged queries take the exact path. */
+ *   VDB_PREC_AUTO    (default) BF16, per batch.  A host-memory search re-passes its
+ *                    uncertified queries (at most 1/8 of the batch, at most 64) in BF16X3
+ *                    as one gathered sub-search and stays BF16; more than that reruns the
+ *                    batch in BF16X3 and starts a HOLD: the next 16 searches run BF16X3,
+ *                    doubling per failed BF16 probe up to 2048 (reset by 64 certified BF16
+ *                    searches, or when the rows change).  A device-memory search sees its
+ *                    fallback counts a search or more late (no host sync): its flagged
+ *                    queries take the device-gated exact path and the next search starts
+ *                    the hold.  Stats "repass_queries", "auto_hold". */
 enum { VDB_PREC_FP32 = 0, VDB_PREC_BF16X3 = 1, VDB_PREC_BF16 = 2, VDB_PREC_AUTO = 3 };
 
 typedef struct vdb_index vdb_index;

@@ -89,6 +89,10 @@ struct Workspace {
     bool busy = false;
     bool used = false;
     hipStream_t last_st = nullptr;  // stream of the last search that used it
+    // host-memory searches without a caller stream run on their workspace's own stream, so
+    // concurrent host searches (the reference's 4-thread executor, api/routes/vectors.py:43)
+    // overlap on the device instead of queueing on one index stream
+    hipStream_t own = nullptr;
 };
 
 }  // namespace
@@ -119,12 +123,16 @@ struct vdb_index {
     int n_cu = 256;
     // knobs
     int64_t precision = VDB_PREC_AUTO;
-    // VDB_PREC_AUTO: set when a BF16 search left more than 1/64 of its queries uncertified;
-    // BF16X3 from then on, until the rows change (add / clear).  (Periodic BF16 retries cost a
-    // device-memory search the exact scan of most of its batch: C4 93 ms instead of 4.4.)
+    // VDB_PREC_AUTO: BF16 by default; a BF16 search whose uncertified queries are
+    // too many for a re-pass (host memory: more than 1/8 of the batch; device memory: any, seen
+    // lagged through h_totals) starts a HOLD of BF16X3 searches, 16 << (fails - 1) of them
+    // (exponential backoff up to 2048 while probes keep failing; `fails` resets after 64 BF16
+    // searches without a new failure, and hold and fails reset when the rows change).  So one
+    // near-duplicate query no longer pins the index to BF16X3, and a corpus that never certifies
+    // in BF16 pays a probe only once per 2048 searches.
+    std::atomic<int> auto_hold{0}, auto_fails{0}, auto_ok{0};
     // The device-gated fallback total last seen: pinned mirror of d_totals[0], written by the
     // gated exact kernel of a device-memory search and read by the next search.
-    std::atomic<bool> auto_b3{false};
     std::atomic<unsigned long long> auto_seen{0};
     unsigned long long* h_totals = nullptr;
     int64_t margin = -1;  // -1 = default
@@ -149,13 +157,16 @@ struct vdb_index {
     int64_t gate_div = 1;         // gated exact fallback: n_cu / gate_div row ranges, one query slot each when > 1
     int64_t finish_split = 1;  // workgroups per query in the finish kernel (tuning)
     // stats
-    std::atomic<int64_t> n_searches{0}, n_queries{0}, n_fallback{0}, n_overflow{0};
+    std::atomic<int64_t> n_searches{0}, n_queries{0}, n_fallback{0}, n_overflow{0}, n_repass{0};
     std::atomic<int64_t> n_by_prec[3] = {{0}, {0}, {0}};  // candidate passes per PREC_* (VDB_PREC_AUTO's choices)
     std::atomic<int64_t> scan_ns{0}, pipe_ns{0}, n_timed{0};
     unsigned long long* d_totals = nullptr;  // device: flagged / overflowed / flagged-in-bf16 queries of device-gated searches
     std::shared_mutex mu;  // add/clear/reserve exclusive; search shared
     std::mutex ws_mu;
     std::vector<Workspace*> pool;
+    // last work queued on each caller stream by searches without a workspace (graph searches):
+    // wait_idle() waits for these and the workspaces' events instead of the whole device
+    std::unordered_map<hipStream_t, hipEvent_t> uses;
 };
 
 namespace {
@@ -174,6 +185,8 @@ void free_workspace_memory(Workspace* w) {
     w->dev_bytes = w->exact_bytes = 0;
 }
 
+int wait_idle(vdb_index* ix);
+
 // The candidate copy of rows [row0, row0 + n) from the row-major rows (whole row tiles).
 hipError_t build_candidate_rows(const vdb_index* ix, const float* X, const float* inv32, int64_t row0, int64_t n,
                                 float* Xs, hipStream_t st) {
@@ -183,6 +196,10 @@ hipError_t build_candidate_rows(const vdb_index* ix, const float* X, const float
 
 int ensure_capacity(vdb_index* ix, int64_t rows) {
     if (rows <= ix->cap_rows) return VDB_OK;
+    if (ix->X) {  // every search that might read the old buffers is done (callers hold the write lock)
+        const int wr = wait_idle(ix);
+        if (wr) return wr;
+    }
     int64_t cap = std::max<int64_t>(ix->cap_rows * 2, kRowAlign);
     while (cap < rows) cap *= 2;
     cap = round_up(cap, kRowAlign);
@@ -220,8 +237,6 @@ int ensure_capacity(vdb_index* ix, int64_t rows) {
     CAP_TRY(hipMemsetAsync(i32, 0, cap * sizeof(float), ix->stream));
     CAP_TRY(hipMemsetAsync(s32, 0, cap * sizeof(float), ix->stream));
     if (ix->X) {
-        // all searches that might read the old buffers must be finished
-        CAP_TRY(hipDeviceSynchronize());
         const int64_t used_tiles = round_up(ix->count, 128) / 32;  // whole super tiles (prefix of the layout)
         CAP_TRY(hipMemcpyAsync(X, ix->X, (size_t)ix->count * ix->Dp * sizeof(float), hipMemcpyDeviceToDevice,
                                ix->stream));
@@ -259,13 +274,15 @@ int ensure_capacity(vdb_index* ix, int64_t rows) {
 // serialising on one workspace.
 constexpr size_t kMaxWs = 16;
 
-Workspace* acquire_ws(vdb_index* ix, hipStream_t st) {
+// own = a host-memory search that runs on the workspace's own stream: any free workspace
+// whose last search has finished (or a new one) serves.
+Workspace* acquire_ws(vdb_index* ix, hipStream_t st, bool own = false) {
     std::lock_guard<std::mutex> g(ix->ws_mu);
     Workspace* idle = nullptr;
     Workspace* any = nullptr;
     for (Workspace* w : ix->pool) {
         if (w->busy) continue;
-        if (!w->used || w->last_st == st) {
+        if (!w->used || (!own && w->last_st == st)) {
             w->busy = true;
             return w;
         }
@@ -288,6 +305,31 @@ void release_ws(vdb_index* ix, Workspace* w, hipStream_t st) {
     w->last_st = st;
     std::lock_guard<std::mutex> g(ix->ws_mu);
     w->busy = false;
+}
+
+// Remember the last work a search without a workspace queued on `st` (wait_idle).
+int note_use(vdb_index* ix, hipStream_t st) {
+    std::lock_guard<std::mutex> g(ix->ws_mu);
+    hipEvent_t& e = ix->uses[st];
+    if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(e, st));
+    return VDB_OK;
+}
+
+// Every search queued on this index (any stream) and its own stream are done: what a resize,
+// a rebuild of the candidate copy or a clear needs before touching the buffers searches read.
+// Waits on this index's events only, not on the whole device (other indexes keep running).
+int wait_idle(vdb_index* ix) {
+    std::vector<hipEvent_t> evs;
+    {
+        std::lock_guard<std::mutex> g(ix->ws_mu);
+        for (Workspace* w : ix->pool)
+            if (w->used && w->done) evs.push_back(w->done);
+        for (auto& kv : ix->uses) evs.push_back(kv.second);
+    }
+    for (hipEvent_t e : evs) HIP_TRY(hipEventSynchronize(e));
+    HIP_TRY(hipStreamSynchronize(ix->stream));
+    return VDB_OK;
 }
 
 // Accumulate the timing events of a search whose host side returned without
@@ -470,10 +512,11 @@ int32_t vdb_index_destroy(vdb_index* ix) {
         g_indices.erase(ix);
     }
     (void)hipSetDevice(ix->device);
-    (void)hipDeviceSynchronize();
+    (void)wait_idle(ix);
     for (Workspace* w : ix->pool) {
         free_workspace_memory(w);
         if (w->done) (void)hipEventDestroy(w->done);
+        if (w->own) (void)hipStreamDestroy(w->own);
         for (int r = 0; r < Workspace::kTRing; ++r)
             for (int e = 0; e < 4; ++e)
                 if (w->tring[r][e]) (void)hipEventDestroy(w->tring[r][e]);
@@ -489,6 +532,7 @@ int32_t vdb_index_destroy(vdb_index* ix) {
     if (ix->d_dir) (void)hipFree(ix->d_dir);
     if (ix->d_totals) (void)hipFree(ix->d_totals);
     if (ix->h_totals) (void)hipHostFree(ix->h_totals);
+    for (auto& kv : ix->uses) (void)hipEventDestroy(kv.second);
     if (ix->stream) (void)hipStreamDestroy(ix->stream);
     delete ix;
     return VDB_OK;
@@ -513,7 +557,8 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
         HIP_TRY(hipSetDevice(ix->device));
         std::unique_lock<std::shared_mutex> g(ix->mu);
         if (value == ix->precision) return VDB_OK;
-        HIP_TRY(hipDeviceSynchronize());
+        const int wr = wait_idle(ix);  // queued searches read the candidate copy
+        if (wr) return wr;
         const bool rebuild = (value == VDB_PREC_FP32) != (ix->precision == VDB_PREC_FP32);
         ix->precision = value;
         if (rebuild && ix->Xs && ix->count > 0) {  // fp32 tiles <-> split tiles
@@ -580,7 +625,8 @@ int32_t vdb_index_get_stat(const vdb_index* cix, const char* name, int64_t* valu
     unsigned long long dt[2] = {0, 0};
     if ((n == "fallback_queries" || n == "overflow_queries") && ix->d_totals) {
         HIP_TRY(hipSetDevice(ix->device));
-        HIP_TRY(hipDeviceSynchronize());
+        const int wr = wait_idle(ix);  // device-memory searches queued on caller streams
+        if (wr) return wr;
         HIP_TRY(hipMemcpy(dt, ix->d_totals, sizeof(dt), hipMemcpyDeviceToHost));
     }
     if (n == "scan_ns" || n == "pipeline_ns" || n == "timed_searches") {
@@ -591,6 +637,8 @@ int32_t vdb_index_get_stat(const vdb_index* cix, const char* name, int64_t* valu
     if (n == "searches") *value = ix->n_searches.load();
     else if (n == "queries") *value = ix->n_queries.load();
     else if (n == "fallback_queries") *value = ix->n_fallback.load() + (int64_t)dt[0];
+    else if (n == "repass_queries") *value = ix->n_repass.load();
+    else if (n == "auto_hold") *value = ix->auto_hold.load();
     else if (n == "overflow_queries") *value = ix->n_overflow.load() + (int64_t)dt[1];
     else if (n == "capacity") *value = ix->cap_rows;
     else if (n == "scan_ns") *value = ix->scan_ns.load();
@@ -698,7 +746,8 @@ int32_t vdb_index_add(vdb_index* ix, const float* vectors, int64_t n, int32_t me
     ix->xres_abs = xm[2];
     ix->xres_dir = xm[3];
     ix->count += n;
-    ix->auto_b3 = false;  // new rows: VDB_PREC_AUTO tries BF16 again
+    ix->auto_hold = 0;  // new rows: VDB_PREC_AUTO tries BF16 again
+    ix->auto_fails = 0;
     return VDB_OK;
 }
 
@@ -712,7 +761,10 @@ int32_t vdb_index_clear(vdb_index* ix) {
     if (!ix) return set_error(VDB_ERR_INVALID, "index is NULL");
     HIP_TRY(hipSetDevice(ix->device));
     std::unique_lock<std::shared_mutex> g(ix->mu);
-    HIP_TRY(hipDeviceSynchronize());
+    {
+        const int wr = wait_idle(ix);
+        if (wr) return wr;
+    }
     if (ix->X) {
         HIP_TRY(hipMemsetAsync(ix->X, 0, (size_t)(ix->cap_rows / 32) * ix->G * BLOCK_FLOATS * sizeof(float),
                                ix->stream));
@@ -724,7 +776,8 @@ int32_t vdb_index_clear(vdb_index* ix) {
     HIP_TRY(hipMemsetAsync(ix->d_xmax, 0, 64, ix->stream));
     HIP_TRY(hipStreamSynchronize(ix->stream));
     ix->count = 0;
-    ix->auto_b3 = false;
+    ix->auto_hold = 0;
+    ix->auto_fails = 0;
     ix->xmax = 0.0;
     ix->xres_rel = ix->xres_abs = 0.0;
     ix->dir_set = false;  // the next add picks a new direction (xres_dir's bits were cleared above)
@@ -766,6 +819,47 @@ int32_t vdb_index_get_vectors(vdb_index* ix, int64_t start, int64_t n, float* ou
 // host-memory search: nothing was written, the caller runs the search again in bf16x3 (two
 // candidate passes cost far less than the exact scan of most of the batch)
 constexpr int32_t kRetryBf16x3 = 1 << 20;
+// A host-memory bf16 search re-passes its uncertified queries in bf16x3 (gathered into one
+// device-memory sub-search) when they are at most 1/8 of the batch and at most this many.
+constexpr int kRepassMax = 64;
+
+// VDB_PREC_AUTO bookkeeping (vdb_index::auto_hold): a bf16 failure too large for a re-pass
+// starts a hold of bf16x3 searches, doubling per failed probe (16 .. 2048).
+void auto_fail(vdb_index* ix) {
+    const int f = std::min(8, ix->auto_fails.load() + 1);
+    ix->auto_fails = f;
+    ix->auto_ok = 0;
+    ix->auto_hold = 16 << (f - 1);
+}
+
+// The precision class of the next auto search: bf16x3 while a hold lasts.
+bool auto_take_hold(vdb_index* ix) {
+    int h = ix->auto_hold.load();
+    while (h > 0)
+        if (ix->auto_hold.compare_exchange_weak(h, h - 1)) return true;
+    if (++ix->auto_ok >= 64) ix->auto_fails = 0;  // probes have been certifying for a while
+    return false;
+}
+
+static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int32_t k, const uint32_t* row_mask,
+                             int32_t mem, float* out_scores, int64_t* out_indices, double* out_keys,
+                             int64_t index_offset, void* stream, const int64_t* row_ids, struct SearchOpts opt);
+
+// The uncertified queries flag_list[0..n) (device) of a bf16 search, gathered into a
+// device-memory bf16x3 sub-search on the same stream (its own certificate and gated exact
+// fallback), whose result rows are scattered back into the batch's outputs.
+static int repass_flagged(vdb_index* ix, const float* Qd, const int* flag_list, int n, int k, const uint32_t* md,
+                          float* out_s, int64_t* out_i, double* out_k, int64_t index_offset, const int64_t* row_ids,
+                          hipStream_t st);
+
+struct SearchOpts {
+    bool force_b3 = false;  // VDB_PREC_AUTO: this search runs bf16x3 (retry / re-pass)
+    bool repass = false;    // an internal sub-search of a re-pass (no search / query counts)
+};
+
+static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int32_t k, const uint32_t* row_mask,
+                             int32_t mem, float* out_scores, int64_t* out_indices, double* out_keys,
+                             int64_t index_offset, void* stream, const int64_t* row_ids, SearchOpts opt);
 
 static int32_t search_impl(vdb_index* ix, const float* queries, int32_t B, int32_t k, const uint32_t* row_mask,
                            int32_t mem, float* out_scores, int64_t* out_indices, double* out_keys,
@@ -775,34 +869,78 @@ static int32_t search_impl(vdb_index* ix, const float* queries, int32_t B, int32
     if (k <= 0 || k > 1024) return set_error(VDB_ERR_INVALID, "k must be in [1, 1024], got %d", k);
     if (!queries || !out_scores || !out_indices) return set_error(VDB_ERR_INVALID, "NULL query/output pointer");
     if (mem != VDB_MEM_HOST && mem != VDB_MEM_DEVICE) return set_error(VDB_ERR_INVALID, "bad mem kind %d", mem);
-    const int D = ix->dim;
-    if (mem == VDB_MEM_HOST && !all_finite(queries, (int64_t)B * D))
+    if (mem == VDB_MEM_HOST && !all_finite(queries, (int64_t)B * ix->dim))
         return set_error(VDB_ERR_NONFINITE, "query contains NaN or Inf");
     HIP_TRY(hipSetDevice(ix->device));
     std::shared_lock<std::shared_mutex> g(ix->mu);
+    SearchOpts opt;
+    opt.force_b3 = force_b3;
+    return search_locked(ix, queries, B, k, row_mask, mem, out_scores, out_indices, out_keys, index_offset, stream,
+                         row_ids, opt);
+}
+
+static int repass_flagged(vdb_index* ix, const float* Qd, const int* flag_list, int n, int k, const uint32_t* md,
+                          float* out_s, int64_t* out_i, double* out_k, int64_t index_offset, const int64_t* row_ids,
+                          hipStream_t st) {
+    const int D = ix->dim;
+    const size_t qb = round_up((int64_t)n * D * 4, 256), sb = round_up((int64_t)n * k * 4, 256),
+                 lb = round_up((int64_t)n * k * 8, 256);
+    char* buf = nullptr;
+    HIP_TRY(hipMallocAsync((void**)&buf, qb + sb + 2 * lb, st));
+    float* Qs = (float*)buf;
+    float* ss = (float*)(buf + qb);
+    int64_t* si = (int64_t*)(buf + qb + sb);
+    double* sk = (double*)(buf + qb + sb + lb);
+    hipError_t e = launch_gather_rows(Qd, D, flag_list, n, Qs, st);
+    int rc = e == hipSuccess ? VDB_OK : set_error(VDB_ERR_HIP, "re-pass gather: %s", hipGetErrorString(e));
+    if (rc == VDB_OK) {
+        SearchOpts o;
+        o.force_b3 = true;
+        o.repass = true;
+        rc = search_locked(ix, Qs, n, k, md, VDB_MEM_DEVICE, ss, si, sk, index_offset, st, row_ids, o);
+    }
+    if (rc == VDB_OK) {
+        e = launch_scatter_results(flag_list, n, k, ss, si, sk, out_s, out_i, out_k, st);
+        if (e != hipSuccess) rc = set_error(VDB_ERR_HIP, "re-pass scatter: %s", hipGetErrorString(e));
+    }
+    (void)hipFreeAsync(buf, st);
+    ix->n_repass += n;
+    return rc;
+}
+
+// The search itself (the caller holds the index's shared lock).
+static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int32_t k, const uint32_t* row_mask,
+                             int32_t mem, float* out_scores, int64_t* out_indices, double* out_keys,
+                             int64_t index_offset, void* stream, const int64_t* row_ids, SearchOpts opt) {
+    const int D = ix->dim;
     // device memory: the caller's stream, NULL = the null stream (ordered with the caller's
-    // default-stream work, e.g. PyTorch's); host memory: NULL = the index's own stream
-    hipStream_t st = (stream || mem == VDB_MEM_DEVICE) ? (hipStream_t)stream : ix->stream;
+    // default-stream work, e.g. PyTorch's); host memory: the caller's stream, or (NULL) the
+    // stream of the workspace this search takes, so concurrent host searches overlap
+    const bool own_stream = mem == VDB_MEM_HOST && !stream;
+    hipStream_t st = own_stream ? nullptr : (hipStream_t)stream;
     const int64_t N = ix->count;
-    ix->n_searches++;
-    ix->n_queries += B;
+    if (!opt.repass) {
+        ix->n_searches++;
+        ix->n_queries += B;
+    }
 
     // ---- sizes ----------------------------------------------------------------
     // candidates beyond k: the certificate needs a gap of 2 eps between the k-th and the
     // KP-th approximate score; bf16x3's bound grows with D (3D additions), so large D
     // gets a wider margin (1M x 1536 uniform: KP = 32 left ~1.5% of queries uncertified)
     const bool auto_prec = ix->precision == VDB_PREC_AUTO;
-    if (auto_prec && ix->h_totals) {  // fallbacks of earlier device-memory searches (lagged)
+    if (auto_prec && ix->h_totals && !opt.repass) {  // fallbacks of earlier device-memory searches (lagged)
         const unsigned long long seen = ix->h_totals[0];
         const unsigned long long prev = ix->auto_seen.exchange(seen);
-        if (seen > prev) ix->auto_b3 = true;
+        if (seen > prev) auto_fail(ix);
     }
+    const bool approx = N > 0 && !(ix->force_exact || k > kMaxApproxK);
     const int prec_req = !ix->Xs ? PREC_FP32
                          : ix->precision == VDB_PREC_BF16X3 ? PREC_BF16X3
                          : ix->precision == VDB_PREC_BF16 ? PREC_BF16
-                         : auto_prec ? (force_b3 || ix->auto_b3.load() ? PREC_BF16X3 : PREC_BF16)
+                         : auto_prec ? (opt.force_b3 || (approx && auto_take_hold(ix)) ? PREC_BF16X3 : PREC_BF16)
                                      : PREC_FP32;
-    if (N > 0 && !(ix->force_exact || k > kMaxApproxK)) ix->n_by_prec[prec_req]++;
+    if (approx) ix->n_by_prec[prec_req]++;
 
     int margin_def = std::max(16, k / 4);
     if (prec_req == PREC_BF16X3 && D >= 1024) margin_def = std::max(margin_def, 48);
@@ -841,7 +979,18 @@ static int32_t search_impl(vdb_index* ix, const float* queries, int32_t B, int32
     // profiles/r02_ab/).
     const int publish = (ix->scan_publish >= 0 ? (int)ix->scan_publish : spw >= 16) | (int)(ix->scan_realign << 8);
 
-    Workspace* w = acquire_ws(ix, st);
+    Workspace* w = acquire_ws(ix, st, own_stream);
+    if (own_stream) {
+        if (!w->own) {
+            const hipError_t e = hipStreamCreateWithFlags(&w->own, hipStreamNonBlocking);
+            if (e != hipSuccess) {
+                std::lock_guard<std::mutex> lg(ix->ws_mu);
+                w->busy = false;
+                return set_error(VDB_ERR_HIP, "workspace stream: %s", hipGetErrorString(e));
+            }
+        }
+        st = w->own;
+    }
     struct Releaser {
         vdb_index* ix; Workspace* w; hipStream_t st;
         ~Releaser() { release_ws(ix, w, st); }
@@ -941,10 +1090,9 @@ static int32_t search_impl(vdb_index* ix, const float* queries, int32_t B, int32
     }
 
     if (N == 0) {
-        // empty store: every slot "no result" (reference returns ([],[],[]), :117)
-        HIP_TRY(hipMemsetAsync(out_i, 0xFF, (size_t)B * k * 8, st));
-        HIP_TRY(hipMemsetAsync(out_s, 0, (size_t)B * k * 4, st));
-        if (out_k) HIP_TRY(hipMemsetAsync(out_k, 0, (size_t)B * k * 8, st));
+        // empty store: every slot "no result" (reference returns ([],[],[]), :117), keys -inf
+        // like every other invalid entry, so an empty shard's lists rank last in a merge
+        HIP_TRY(launch_empty_results((int64_t)B * k, out_s, out_i, out_k, st));
     } else {
         HIP_TRY(launch_prep_queries(Qd, B, Bp, D, ix->G, ix->metric, prec == PREC_FP32 ? Qt : nullptr,
                                     prec == PREC_FP32 ? nullptr : Qt, qn64, flags, gthr, gslots, gl_cnt, done, st));
@@ -1042,9 +1190,23 @@ static int32_t search_impl(vdb_index* ix, const float* queries, int32_t B, int32
             HIP_TRY(hipStreamSynchronize(st));
             n_flag = w->host_flag[0];
             ix->n_overflow += w->host_flag[1];
-            if (auto_prec && prec == PREC_BF16 && n_flag > 0) {
-                ix->auto_b3 = true;
-                if (!ix->no_fallback) return kRetryBf16x3;
+            if (auto_prec && prec == PREC_BF16 && n_flag > 0 && !ix->no_fallback) {
+                if (n_flag <= std::max(1, B / 8) && n_flag <= kRepassMax) {
+                    // a few uncertified queries: re-pass just those in bf16x3 (the index stays bf16)
+                    if (timed) {
+                        const int frc = flush_timing(ix, w);
+                        if (frc) return frc;
+                    }
+                    rc = repass_flagged(ix, Qd, flags + 1, n_flag, k, md, out_s, out_i, out_k, index_offset,
+                                        row_ids, st);
+                    if (rc) return rc;
+                    n_flag = 0;
+                } else {
+                    auto_fail(ix);
+                    ix->n_searches--;  // the retry counts this search (no double count)
+                    ix->n_queries -= B;
+                    return kRetryBf16x3;
+                }
             }
             if (timed) {
                 const int frc = flush_timing(ix, w);
@@ -1081,7 +1243,10 @@ int32_t vdb_shutdown(void) {
     for (vdb_index* ix : live) {
         HIP_TRY(hipSetDevice(ix->device));
         devices.insert(ix->device);
-        HIP_TRY(hipDeviceSynchronize());  // every queued search of this device is done
+        {
+            const int wr = wait_idle(ix);  // every queued search of this index is done
+            if (wr) return wr;
+        }
         const int frc = flush_all_timing(ix);
         if (frc) return frc;
         std::lock_guard<std::mutex> g(ix->ws_mu);
@@ -1114,8 +1279,12 @@ namespace vdb {
 int32_t index_search_rows(vdb_index* ix, const float* queries, int32_t B, int32_t k, const uint32_t* row_mask,
                           float* out_scores, int64_t* out_indices, double* out_keys, void* stream,
                           const int64_t* row_ids) {
-    return search_impl(ix, queries, B, k, row_mask, VDB_MEM_DEVICE, out_scores, out_indices, out_keys, 0, stream,
-                       row_ids);
+    int32_t rc = search_impl(ix, queries, B, k, row_mask, VDB_MEM_DEVICE, out_scores, out_indices, out_keys, 0,
+                             stream, row_ids);
+    if (rc == kRetryBf16x3)  // a batch too large for the device-gated fallback: rerun in bf16x3
+        rc = search_impl(ix, queries, B, k, row_mask, VDB_MEM_DEVICE, out_scores, out_indices, out_keys, 0, stream,
+                         row_ids, true);
+    return rc;
 }
 // Drop rows past `rows` (undo of a partial multi-shard add; rows past count are never read).
 int32_t index_truncate(vdb_index* ix, int64_t rows) {
@@ -1468,7 +1637,10 @@ int32_t vdb_graph_add(vdb_graph* g) {
             (void)hipFree(nb);
             return set_error(VDB_ERR_HIP, "graph grow: %s", hipGetErrorString(e));
         }
-        HIP_TRY(hipDeviceSynchronize());  // searches that read the old array are done
+        {
+            const int wr = wait_idle(ix);  // graph searches that read the old array are done
+            if (wr) return wr;
+        }
         (void)hipFree(g->nbr);
         g->nbr = nb;
         g->cap = cap;
@@ -1580,6 +1752,10 @@ int32_t vdb_graph_search(vdb_graph* g, const float* queries, int32_t nq, int32_t
     }
     if (tmp) HIP_TRY(hipFreeAsync(tmp, st));
     if (mem == VDB_MEM_HOST) HIP_TRY(hipStreamSynchronize(st));
+    else {
+        const int nr = note_use(ix, st);  // a later resize of the index waits for this search
+        if (nr) return nr;
+    }
     return VDB_OK;
 }
 
@@ -1613,7 +1789,7 @@ int32_t vdb_graph_stat(const vdb_graph* g, const char* name, int64_t* value) {
 int32_t vdb_graph_destroy(vdb_graph* g) {
     if (!g) return VDB_OK;
     (void)hipSetDevice(g->ix->device);
-    (void)hipDeviceSynchronize();
+    (void)wait_idle(g->ix);
     (void)hipFree(g->nbr);
     (void)hipFree(g->entries);
     (void)hipFree(g->d_stats);

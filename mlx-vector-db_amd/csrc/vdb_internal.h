@@ -192,6 +192,13 @@ hipError_t launch_finalize_u32(int metric, const double* sk, const uint32_t* si,
                                hipStream_t st, const int* qcount = nullptr, const int64_t* row_ids = nullptr);
 hipError_t launch_finalize_i64(int metric, const double* sk, const int64_t* si, int KP, int nq, const int* qmap,
                                int k, float* out_s, int64_t* out_i, double* out_k, hipStream_t st);
+// out[r] = Q[list[r]] (rows of D floats), r < n
+hipError_t launch_gather_rows(const float* Q, int D, const int* list, int n, float* out, hipStream_t st);
+// o*[list[r]][e] = s*[r][e] for r < n, e < k (ok may be NULL)
+hipError_t launch_scatter_results(const int* list, int n, int k, const float* ss, const int64_t* si, const double* sk,
+                                  float* os, int64_t* oi, double* ok, hipStream_t st);
+// n "no result" entries: score 0, row -1, key -inf (as write_result's invalid entries)
+hipError_t launch_empty_results(int64_t n, float* out_s, int64_t* out_i, double* out_k, hipStream_t st);
 
 // Graph search (vdb_graph.hip): one workgroup per query, beam of ef over a [N][R]
 // int32 neighbour array (-1 = none), started from the best of n_entries entry rows.

@@ -66,6 +66,61 @@ __global__ void __launch_bounds__(256) finalize_kernel(int metric, const double*
                  out_s + o, out_i + o, out_k ? out_k + o : nullptr);
 }
 
+// "No result" in every slot: what write_result stores for an invalid entry (score 0, row -1,
+// key -inf), so a search of an empty index (or an empty shard of a row-sharded corpus) ranks
+// below every real row in a later merge by key.
+__global__ void __launch_bounds__(256) empty_results_kernel(int64_t n, float* __restrict__ out_s,
+                                                            int64_t* __restrict__ out_i, double* __restrict__ out_k) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= n) return;
+    write_result(0, 0.0, 0, false, out_s + t, out_i + t, out_k ? out_k + t : nullptr);
+}
+
+hipError_t launch_empty_results(int64_t n, float* out_s, int64_t* out_i, double* out_k, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(empty_results_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, n, out_s, out_i,
+                       out_k);
+    return hipGetLastError();
+}
+
+// Re-pass plumbing (vdb_api.cpp repass_flagged): the listed query rows gathered into a dense
+// block, and the sub-search's result rows scattered back to those rows.
+__global__ void __launch_bounds__(256) gather_rows_kernel(const float* __restrict__ Q, int D,
+                                                          const int* __restrict__ list, int n, float* __restrict__ out) {
+    const int r = blockIdx.y;
+    const int b = list[r];
+    for (int d = blockIdx.x * 256 + threadIdx.x; d < D; d += gridDim.x * 256) out[(size_t)r * D + d] = Q[(size_t)b * D + d];
+}
+
+hipError_t launch_gather_rows(const float* Q, int D, const int* list, int n, float* out, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)std::min(8, (D + 255) / 256), (unsigned)n), dim3(256), 0, st,
+                       Q, D, list, n, out);
+    return hipGetLastError();
+}
+
+__global__ void __launch_bounds__(256) scatter_results_kernel(const int* __restrict__ list, int n, int k,
+                                                              const float* __restrict__ ss, const int64_t* __restrict__ si,
+                                                              const double* __restrict__ sk, float* __restrict__ os,
+                                                              int64_t* __restrict__ oi, double* __restrict__ ok) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= (int64_t)n * k) return;
+    const int r = (int)(t / k), e = (int)(t % k);
+    const size_t o = (size_t)list[r] * k + e;
+    os[o] = ss[t];
+    oi[o] = si[t];
+    if (ok) ok[o] = sk[t];
+}
+
+hipError_t launch_scatter_results(const int* list, int n, int k, const float* ss, const int64_t* si, const double* sk,
+                                  float* os, int64_t* oi, double* ok, hipStream_t st) {
+    const int64_t m = (int64_t)n * k;
+    if (m <= 0) return hipSuccess;
+    hipLaunchKernelGGL(scatter_results_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, list, n, k, ss, si,
+                       sk, os, oi, ok);
+    return hipGetLastError();
+}
+
 hipError_t launch_finalize_u32(int metric, const double* sk, const uint32_t* si, int KP, int nq, const int* qmap,
                                int k, int64_t index_offset, float* out_s, int64_t* out_i, double* out_k,
                                hipStream_t st, const int* qcount, const int64_t* row_ids) {

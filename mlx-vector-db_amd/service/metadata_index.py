@@ -82,8 +82,11 @@ class MetadataIndex:
 
     def _pair_rows(self, key: Any, value: Any, n: int) -> np.ndarray:
         """Sorted rows < n with ``meta.get(key) == value``."""
+        # rows past the metadata list (the reference allows fewer metadata entries than vectors;
+        # persistence pads them with {} on reload) have no keys: get(key) is None
+        m_rows = min(n, len(self._rows))
         if not _hashable(value):
-            return np.fromiter((i for i in range(n) if isinstance(self._rows[i], dict)
+            return np.fromiter((i for i in range(m_rows) if isinstance(self._rows[i], dict)
                                 and self._rows[i].get(key) == value), dtype=np.int64)
         lst = self._post.get(key, {}).get(value) if _hashable(key) else None
         rows = np.frombuffer(lst, dtype=np.int64) if lst is not None else np.zeros(0, np.int64)
@@ -93,7 +96,7 @@ class MetadataIndex:
             for vals in (self._post.get(key, {}) if _hashable(key) else {}).values():
                 a = np.frombuffer(vals, dtype=np.int64)
                 has[a[a < n]] = True
-            for i in range(n):  # rows holding the key with an unhashable value
+            for i in range(m_rows):  # rows holding the key with an unhashable value
                 m = self._rows[i]
                 if isinstance(m, dict) and key in m and not _hashable(m[key]):
                     has[i] = True

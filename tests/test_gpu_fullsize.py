@@ -6,17 +6,20 @@ queries across all query blocks is checked exactly (indices and fp64 keys) again
 oracle (oracle/ref_cpu.exact_search, which keys only a prefiltered candidate set, so it
 finishes in seconds at these sizes).
 
-  C2  1M x 768 cosine, B=64, k=10 (bf16x3 default): the exact-vs-MLX-fp32 question
-      (north_star: indices "bit-exact" with the fp32 reference): the numpy restatement of
-      the reference's fp32 batched path (reference_batch_search = performance/mlx_optimized.py:217-248)
-      is run on the same queries, and every place its order differs from the returned one
-      must be a near tie -- exact keys closer than the fp32 error bound of the reference's
-      own arithmetic.  The count goes to $VDB_TEST_REPORT_DIR/c2_fp32_ref.json.
+The exact-vs-reference-fp32 question (north_star: indices "bit-exact" with the MLX fp32
+reference): on the same queries the numpy restatement of the reference's own fp32 path
+(cosine: reference_batch_search = performance/mlx_optimized.py:217-248; L2: the store's
+per-query operator, service/optimized_vector_store.py:43-48 + :176-178) is run, and every
+place its order differs from the returned one must be a near tie -- exact keys closer than
+twice the fp32 error bound of the reference's own arithmetic.  The counts go to
+$VDB_TEST_REPORT_DIR/<config>_fp32_ref.json.
+
+  C2  1M x 768 cosine, B=64, k=10: all 64 queries exact and against the fp32 order.
   C3  1M x 1536 cosine, B=256, k=10 (4 query blocks).
   C4  10M x 128 L2, B=512, k=100 (8 query blocks), both step-end modes of the scan.
-  C3 and C4 run the default precision (VDB_PREC_AUTO) twice: its first, bf16 pass does not
-  certify these configurations and falls back (results still exact), after which the index
-  runs bf16x3, which must certify (<= 2% fallbacks); both searches are checked.
+  C6  10M x 128 cosine, B=64, k=10 (the metric's 8-GPU workload, on one GPU).
+  C3 / C4 / C6 run the default precision (VDB_PREC_AUTO) twice; both searches are checked
+  and the second must certify (<= 2% fallbacks; a fallback is still exact, only slower).
   C5  5M x 384 graph (M=16 -> degree 32, efSearch=128), batch 1: hnswlib's distance
       conventions (performance/hnsw_index.py:35,101) checked against exact keys of the
       returned rows, recall@10 against the exact path on 100 queries.
@@ -59,6 +62,44 @@ def _properties(s, i, metric, N):
         assert np.unique(row).size == row.size
 
 
+def _fp32_order(Q, V, i, sub, k, metric):
+    """Positions where the reference's fp32 order differs from ours, each checked to be a near
+    tie of the exact keys (< 2x the fp32 bound); returns the report fields."""
+    D = V.shape[1]
+    if metric == "cosine":
+        ri, rs = ref_cpu.reference_batch_search(Q[sub], V, k)
+        # one fp32 cosine: D additions + the normalisation roundings, relative to |q||x| = 1
+        eps32 = 1.01 * (D + 8) * 2.0 ** -24
+    else:
+        ri, rs = [], []
+        for b in sub:
+            d = ref_cpu.reference_euclidean_distances(Q[b], V)
+            top = ref_cpu.reference_topk_indices(d, k, metric)
+            ri.append(top)
+            rs.append(d[top])
+        ri, rs = np.array(ri), np.array(rs)
+        eps32 = None  # per query below: (D + 3) 2^-24 of the largest squared distance compared
+    pos_diff, set_diff, worst, bound = 0, 0, 0.0, 0.0
+    for r, b in enumerate(sub):
+        ours, ref = i[b].tolist(), ri[r].tolist()
+        pairs = [(a, c) for a, c in zip(ours, ref) if a != c]
+        pos_diff += len(pairs)
+        set_diff += len(set(ref) - set(ours))
+        rows = sorted(set(ours) | set(ref))
+        kx = ref_cpu.exact_keys(Q[b], V[rows], metric)
+        key = dict(zip(rows, kx))
+        e2 = 2 * eps32 if eps32 is not None else 2 * 1.01 * (D + 3) * 2.0 ** -24 * float(np.max(-kx))
+        bound = max(bound, e2)
+        for a, c in pairs:
+            gap = abs(key[a] - key[c])
+            worst = max(worst, gap)
+            assert gap < e2, (b, a, c, gap, e2)
+        for c in set(ref) - set(ours):  # a reference row we left out ties with our k-th
+            assert abs(key[ours[-1]] - key[c]) < e2
+    return {"queries": len(sub), "k": k, "positions_differing": pos_diff, "rows_differing": set_diff,
+            "max_exact_key_gap_of_a_swap": worst, "fp32_bound_2eps": bound}, rs
+
+
 def test_c2_exact_vs_reference_fp32_order(vdb):
     N, D, B, k = 1_000_000, 768, 64, 10
     V = np.random.default_rng(0).random((N, D), dtype=np.float32)
@@ -73,31 +114,12 @@ def test_c2_exact_vs_reference_fp32_order(vdb):
     es, ei, ek = ref_cpu.exact_search(Q[sub], V, k, "cosine")
     np.testing.assert_array_equal(i[sub], ei)
     np.testing.assert_array_equal(kk[sub], ek)
-    # the reference's own fp32 arithmetic (normalise, fp32 matmul, stable argsort)
-    ri, rs = ref_cpu.reference_batch_search(Q[sub], V, k)
-    # rigorous bound of one fp32 cosine: D additions + normalisation roundings, relative to |q||x| = 1
-    eps32 = 1.01 * (D + 8) * 2.0 ** -24
-    pos_diff, set_diff, worst = 0, 0, 0.0
-    for r, b in enumerate(sub):
-        ours, ref = i[b].tolist(), ri[r].tolist()
-        pairs = [(a, c) for a, c in zip(ours, ref) if a != c]
-        pos_diff += len(pairs)
-        set_diff += len(set(ref) - set(ours))
-        rows = sorted(set(ours) | set(ref))
-        key = dict(zip(rows, ref_cpu.exact_keys(Q[b], V[rows], "cosine")))
-        for a, c in pairs:
-            gap = abs(key[a] - key[c])
-            worst = max(worst, gap)
-            assert gap < 2 * eps32, (b, a, c, gap)
-        for c in set(ref) - set(ours):  # a reference row we left out ties with our k-th
-            assert key[ours[-1]] - key[c] < 2 * eps32
+    rep, rs = _fp32_order(Q, V, i, sub, k, "cosine")
     np.testing.assert_allclose(s[sub], rs, atol=1e-4, rtol=0)
     assert ix.stat("fallback_queries") == 0
-    _report("c2_fp32_ref.json", {"queries": len(sub), "k": k, "positions_differing": pos_diff,
-                                 "rows_differing": set_diff, "max_exact_key_gap_of_a_swap": worst,
-                                 "fp32_bound_2eps": 2 * eps32, "precision": ix.precision,
-                                 "searches_by_precision": {p: ix.stat(f"searches_{p}")
-                                                           for p in ("bf16", "bf16x3", "fp32")}})
+    rep.update(precision=ix.precision,
+               searches_by_precision={p: ix.stat(f"searches_{p}") for p in ("bf16", "bf16x3", "fp32")})
+    _report("c2_fp32_ref.json", rep)
 
 
 def test_c3_1m_x_1536_b256(vdb):
@@ -125,6 +147,9 @@ def test_c3_1m_x_1536_b256(vdb):
         np.testing.assert_array_equal(kk[sub], ek)
     by_prec = {p: ix.stat(f"searches_{p}") for p in ("bf16", "bf16x3", "fp32")}
     _report("c3.json", {"fallback_queries_per_search": fbs, "host_search_s": dts, "searches_by_precision": by_prec})
+    rep, rs = _fp32_order(Q, V, i, sub, k, "cosine")
+    np.testing.assert_allclose(s[sub], rs, atol=1e-4, rtol=0)
+    _report("c3_fp32_ref.json", rep)
     assert fbs[-1] <= B // 50  # certified by the candidate pass (a fallback is still exact, only slower)
 
 
@@ -156,6 +181,43 @@ def test_c4_10m_x_128_l2_b512_top100(vdb, sync):
     by_prec = {p: ix.stat(f"searches_{p}") for p in ("bf16", "bf16x3", "fp32")}
     _report(f"c4_sync{sync}.json", {"fallback_queries_per_search": fbs, "searches_by_precision": by_prec})
     assert fbs[-1] <= B // 50
+    if sync == 0:
+        rep, rs = _fp32_order(Q, V, i, sub, k, "euclidean")
+        np.testing.assert_allclose(s[sub], rs, atol=1e-4, rtol=1e-5)
+        _report("c4_fp32_ref.json", rep)
+
+
+def test_c6_10m_x_128_cosine_b64_top10(vdb):
+    """The metric's 8-GPU workload (BASELINE.json metric: cosine top-10 batch=64, 10M x 128)
+    on one GPU: properties on every query, exact on a spread, fp32-order report."""
+    N, D, B, k = 10_000_000, 128, 64, 10
+    V = np.random.default_rng(9).random((N, D), dtype=np.float32)
+    Q = np.random.default_rng(10).random((B, D), dtype=np.float32)
+    plant = {0: 9_999_999, 31: 0, 32: 5_555_555, 63: 123_456}
+    for b, r in plant.items():
+        Q[b] = V[r]
+    ix = vdb.NativeIndex(D, "cosine")
+    ix.reserve(N)
+    for s0 in range(0, N, 1 << 21):
+        ix.add(V[s0:s0 + (1 << 21)])
+    sub = list(range(0, B, 4))
+    es, ei, ek = ref_cpu.exact_search(Q[sub], V, k, "cosine")
+    fbs = []
+    for _ in range(2):
+        fb0 = ix.stat("fallback_queries")
+        s, i, kk = ix.search(Q, k, with_keys=True)
+        fbs.append(ix.stat("fallback_queries") - fb0)
+        _properties(s, i, "cosine", N)
+        for b, r in plant.items():
+            assert i[b, 0] == r and s[b, 0] > 0.9999
+        np.testing.assert_array_equal(i[sub], ei)
+        np.testing.assert_array_equal(kk[sub], ek)
+    by_prec = {p: ix.stat(f"searches_{p}") for p in ("bf16", "bf16x3", "fp32")}
+    _report("c6.json", {"fallback_queries_per_search": fbs, "searches_by_precision": by_prec})
+    assert fbs[-1] <= max(1, B // 50)
+    rep, rs = _fp32_order(Q, V, i, sub, k, "cosine")
+    np.testing.assert_allclose(s[sub], rs, atol=1e-4, rtol=0)
+    _report("c6_fp32_ref.json", rep)
 
 
 @pytest.mark.timeout(600)

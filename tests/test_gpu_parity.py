@@ -239,6 +239,54 @@ def test_auto_precision_switches_on_fallbacks(vdb, mem):
             assert ix.stat("searches_bf16x3") == 0 and ix.stat("fallback_queries") == 0
 
 
+def test_auto_repass_keeps_bf16_for_a_few_uncertified_queries(vdb):
+    """One near-duplicate query in a batch of ordinary ones: its bf16 certificate fails, it
+    alone is re-passed in bf16x3 (host memory), and the index stays bf16: the next batch
+    runs bf16 again (one query no longer pins the index to bf16x3)."""
+    rng = np.random.default_rng(41)
+    D, N, B, k = 256, 20000, 32, 10
+    V = rng.random((N, D), dtype=np.float32)
+    base = rng.random(D, dtype=np.float32)
+    V[:400] = (base + 1e-4 * rng.standard_normal((400, D))).astype(np.float32)  # a tight cluster
+    Q = rng.random((B, D), dtype=np.float32)
+    Q[7] = base  # the near-duplicate query: its top-10 sit inside the cluster
+    ix = vdb.NativeIndex(D, "cosine")
+    ix.add(V)
+    es, ei, ek = ref_cpu.exact_search(Q, V, k, "cosine")
+    for _ in range(3):
+        s, i, kk = ix.search(Q, k, with_keys=True)
+        np.testing.assert_array_equal(i, ei)
+        np.testing.assert_array_equal(kk, ek)
+    assert ix.stat("searches") == 3 and ix.stat("queries") == 3 * B
+    assert ix.stat("repass_queries") >= 3  # query 7, every search
+    assert ix.stat("searches_bf16") == 3  # never switched
+    assert ix.stat("auto_hold") == 0
+
+
+def test_auto_hold_expires(vdb):
+    """A failure too large for a re-pass starts a hold of 16 bf16x3 searches; after it the
+    index probes bf16 again (and, on data that still fails, holds twice as long)."""
+    rng = np.random.default_rng(43)
+    D, N, B, k = 128, 6000, 16, 10
+    base = rng.random(D, dtype=np.float32)
+    near = (base + 1e-4 * rng.standard_normal((N, D))).astype(np.float32)
+    Q = (near[rng.integers(0, N, B)] + 1e-5 * rng.standard_normal((B, D))).astype(np.float32)
+    ix = vdb.NativeIndex(D, "cosine")
+    ix.add(near)
+    es, ei, ek = ref_cpu.exact_search(Q, near, k, "cosine")
+    s, i, kk = ix.search(Q, k, with_keys=True)  # bf16 fails for most queries -> rerun in bf16x3
+    np.testing.assert_array_equal(i, ei)
+    assert ix.stat("searches_bf16") == 1 and ix.stat("auto_hold") == 16
+    for _ in range(16):
+        s, i, kk = ix.search(Q, k, with_keys=True)
+        np.testing.assert_array_equal(kk, ek)
+    assert ix.stat("searches_bf16") == 1 and ix.stat("auto_hold") == 0
+    s, i, kk = ix.search(Q, k, with_keys=True)  # the probe: bf16 again, fails again -> hold 32
+    np.testing.assert_array_equal(i, ei)
+    assert ix.stat("searches_bf16") == 2 and ix.stat("auto_hold") == 32
+    assert ix.stat("searches") == 18 and ix.stat("queries") == 18 * B
+
+
 def test_duplicates_force_certificate_fallback(vdb):
     """50 copies of the nearest row: the candidate list cannot certify the top-k,
     so the exact scan must take over and keep the lower-index-first order."""

@@ -148,6 +148,27 @@ def test_multi_device_shards_equal_one_index(store_mod, metric):
         sh.close()
 
 
+@pytest.mark.parametrize("metric", ["cosine", "euclidean"])
+def test_shards_with_empty_shards(store_mod, metric):
+    """Fewer rows than shards: the empty shards' lists carry key -inf, so they rank
+    below every real row in the merge (an L2 key is -d^2 <= 0, a cosine score may be negative)."""
+    from service import _vdb
+    rng = np.random.default_rng(46)
+    V = rng.standard_normal((3, 24)).astype(np.float32)
+    Q = np.concatenate([V[[2, 0]], rng.standard_normal((2, 24)).astype(np.float32)])
+    for rows in (1, 3):
+        sh = _vdb.NativeShards(24, metric, [0, 0, 0, 0])
+        sh.add(V[:rows])
+        assert sorted(sh.shard_counts()) == [0] * (4 - rows) + [1] * rows
+        for k in (1, 5):
+            s, i, kk = sh.search(Q, k, with_keys=True)
+            es, ei, ek = ref_cpu.exact_search(Q, V[:rows], k, metric)
+            np.testing.assert_array_equal(i, ei)
+            np.testing.assert_array_equal(kk, ek)
+            assert ((i >= 0).sum(axis=1) == min(k, rows)).all()
+        sh.close()
+
+
 def test_store_over_devices_list(store_mod, tmp_path):
     """MLXVectorStoreConfig(devices=[0, 0]): the store API over the shard set."""
     rng = np.random.default_rng(45)

@@ -53,6 +53,20 @@ def test_bitmap_equals_reference_scan(filt):
         assert words.size == (n + 31) // 32
 
 
+@pytest.mark.parametrize("filt", [{"kind": None}, {"tags": ["x", "y"]}, {"missing": None}, {"hash": 3}])
+def test_fewer_metadata_rows_than_vectors(filt):
+    """Rows past the metadata list count as {}: no IndexError for None or
+    unhashable filter values."""
+    rng = np.random.default_rng(1)
+    meta = _meta(rng, 50)
+    ix = MetadataIndex()
+    ix.extend(meta)
+    n = 80  # 30 vectors without metadata
+    words, cnt = ix.bitmap(filt, n)
+    want = _scan(meta + [{}] * 30, filt, n)
+    assert _rows_of(words, n) == want and cnt == len(want)
+
+
 def test_cache_invalidated_by_adds():
     ix = MetadataIndex()
     ix.extend([{"a": 1}, {"a": 2}])
