@@ -137,6 +137,49 @@ def cpu_baseline(V, Q, k, metric="cosine", budget_s=10.0):
     return res
 
 
+def serving_stats(V, metric, k, device, n_queries=400, threads=4):
+    """The reference's live path: single-vector `store.query` calls from a 4-thread executor
+    (api/routes/vectors.py:43, :226-234 -> service/optimized_vector_store.py:116-192), here
+    through the drop-in store (host memory in and out) over the same corpus: batch-1 latency
+    (one caller at a time) and the 4-thread throughput with and without the store's query
+    coalescer (concurrent callers joining one device search)."""
+    import shutil
+    import tempfile
+    from concurrent.futures import ThreadPoolExecutor
+    from service.optimized_vector_store import MLXVectorStore, MLXVectorStoreConfig
+    N, D = V.shape
+    tmp = tempfile.mkdtemp(prefix="vdb_bench_store_")
+    try:
+        st = MLXVectorStore(tmp, MLXVectorStoreConfig(dimension=D, metric=metric, persist=False, device=device))
+        st.add_vectors(V, [{}] * N)
+        Qs = np.random.default_rng(2).random((n_queries, D), dtype=np.float32)
+        for q in Qs[:5]:
+            st.query(q, k)
+        lat = []
+        for q in Qs[:100]:
+            t0 = time.perf_counter()
+            st.query(q, k)
+            lat.append(time.perf_counter() - t0)
+        out = {"batch1_p50_ms": float(np.median(lat)) * 1e3, "batch1_p99_ms": float(np.percentile(lat, 99)) * 1e3,
+               "threads": threads, "queries": n_queries}
+        for mode in (True, False):
+            st.config.coalesce = mode
+            b0, q0 = st._coalescer.batches, st._coalescer.queries
+            with ThreadPoolExecutor(threads) as ex:
+                t0 = time.perf_counter()
+                list(ex.map(lambda q: st.query(q, k), Qs))
+                dt = time.perf_counter() - t0
+            key = "coalesced" if mode else "direct"
+            out[f"store_query_{threads}threads_qps_{key}"] = n_queries / dt
+            if mode:
+                nb = st._coalescer.batches - b0
+                out["coalesced_mean_batch"] = (st._coalescer.queries - q0) / max(nb, 1)
+        st._index.close()
+        return out
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
 def cpu_graph_baseline(V, nbr, entries, Q, k, ef, metric, gt, budget_s=15.0):
     """The graph search restated on the CPU (oracle/ref_cpu.graph_search, hnswlib's
     searchBaseLayerST) over the same neighbour array: queries one at a time until
@@ -341,6 +384,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-serving", action="store_true",
+                    help="c1/c2 at N=1: skip the store-API serving numbers (batch-1 p50, 4-thread QPS)")
     ap.add_argument("--scaling", default=None, choices=["weak", "strong"],
                     help="N>1: weak = global batch B*N (fixed work per GPU), strong = global batch B "
                          "(default: strong for c4 / c6, whose BASELINE batch is sharded, weak otherwise)")
@@ -616,6 +661,8 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             V = np.concatenate(host_parts) if len(host_parts) > 1 else host_parts[0]
             del host_parts
+            if args.config in ("c1", "c2") and not args.no_serving:
+                rec["serving"] = serving_stats(V, metric, k, local)
             rec["cpu_baseline"] = cpu_baseline(V, Q, k, metric)
         print(json.dumps(rec), flush=True)
     if world > 1:

@@ -134,7 +134,9 @@ int32_t vdb_index_get_stat(const vdb_index* idx, const char* name, int64_t* valu
  * (service/optimized_vector_store.py:96-106; mlx_optimized.py:127-137).
  * Appends n rows of `dim` fp32 (row-major) in place (capacity doubling), packs
  * them into the MFMA-tiled layout and computes the per-row norms once.
- * Non-finite input -> VDB_ERR_NONFINITE and nothing is appended. */
+ * Non-finite input -> VDB_ERR_NONFINITE and nothing is appended.  Device-memory rows
+ * (mem = VDB_MEM_DEVICE) are read after the work queued on `stream` so far (NULL = the
+ * null stream); the call returns when the rows are ingested (the source may be reused). */
 int32_t vdb_index_add(vdb_index* idx, const float* vectors, int64_t n, int32_t mem, void* stream);
 int32_t vdb_index_count(const vdb_index* idx, int64_t* n);
 /* Replaces MLXVectorStore.clear (service/optimized_vector_store.py:198-209). */
@@ -260,6 +262,17 @@ int32_t vdb_shards_shard_count(const vdb_shards* s, int32_t shard, int64_t* n);
 /* row_mask: NULL or ceil(count/32) host words over GLOBAL rows (as vdb_index_search) */
 int32_t vdb_shards_search(vdb_shards* s, const float* queries_host, int32_t n_queries, int32_t k,
                           const uint32_t* row_mask, float* out_scores, int64_t* out_indices, double* out_keys);
+/* Stream-ordered form (no host wait): queries [n_queries, dim], row_mask (NULL or
+ * ceil(count/32) words over GLOBAL rows) and the outputs are device memory on devices[0];
+ * the search is ordered after the work queued on `stream` (a stream of devices[0], NULL = its
+ * null stream) and the outputs are ready when `stream` reaches the merge, so batches can be
+ * queued back to back.  Per shard: peer copies of the queries (and the mask, whose shard-local
+ * bitmap is built on the shard's device), the shard's device search, a peer copy of its lists
+ * to devices[0]; the merge runs on `stream`.  vdb_shards_search is the host-memory form of
+ * the same path.  Reference constraint: one process serving every device (main.py:395). */
+int32_t vdb_shards_search_device(vdb_shards* s, const float* queries, int32_t n_queries, int32_t k,
+                                 const uint32_t* row_mask, float* out_scores, int64_t* out_indices,
+                                 double* out_keys, void* stream);
 int32_t vdb_shards_get_vectors(vdb_shards* s, int64_t start, int64_t n, float* out_host);
 int32_t vdb_shards_clear(vdb_shards* s);
 int32_t vdb_shards_reserve(vdb_shards* s, int64_t rows);

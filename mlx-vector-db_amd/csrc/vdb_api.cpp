@@ -700,6 +700,16 @@ int32_t vdb_index_add(vdb_index* ix, const float* vectors, int64_t n, int32_t me
     int rc = ensure_capacity(ix, ix->count + n);
     if (rc) return rc;
     HIP_TRY(hipMemsetAsync(ix->d_nonfinite, 0, sizeof(int), st));
+    if (mem == VDB_MEM_DEVICE) {
+        // the rows may still be being written on the caller's stream (NULL = the null stream):
+        // ingest (on the index's own stream) starts after that work
+        hipEvent_t ready = nullptr;
+        HIP_TRY(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+        hipError_t e = hipEventRecord(ready, (hipStream_t)stream);
+        if (e == hipSuccess) e = hipStreamWaitEvent(st, ready, 0);
+        (void)hipEventDestroy(ready);
+        HIP_TRY(e);
+    }
     const int D = ix->dim;
     const int64_t chunk = std::max<int64_t>(1, (int64_t)(256ll << 20) / ((int64_t)D * 4));
     float* staging = nullptr;
@@ -726,8 +736,7 @@ int32_t vdb_index_add(vdb_index* ix, const float* vectors, int64_t n, int32_t me
             HIP_TRY(residual_direction(ix, ix->count + r, m, st));
         }
     }
-    if (staging) (void)hipFree(staging);
-    (void)stream;  // ingest always runs on the index's own stream (serialised with growth)
+    if (staging) (void)hipFree(staging);  // ingest runs on the index's own stream (serialised with growth)
     int nonfinite = 0;
     unsigned long long xb[4] = {0, 0, 0, 0};
     HIP_TRY(hipMemcpyAsync(&nonfinite, ix->d_nonfinite, sizeof(int), hipMemcpyDeviceToHost, st));
@@ -1368,6 +1377,10 @@ struct vdb_graph {
     int teams = 1;               // workgroups per query (vdb_graph_set_param "teams")
     unsigned long long* d_stats = nullptr;
     std::atomic<int64_t> n_queries{0};
+    int device = 0;  // the index's device (the graph may outlive an explicitly closed index)
+    // last search queued on each stream (device memory): vdb_graph_destroy waits for these only
+    std::mutex use_mu;
+    std::unordered_map<hipStream_t, hipEvent_t> uses;
 };
 
 namespace {
@@ -1376,6 +1389,7 @@ int graph_upload(vdb_index* ix, int R, int64_t n, const int32_t* nbr_host, const
                  vdb_graph** out) {
     vdb_graph* g = new vdb_graph();
     g->ix = ix;
+    g->device = ix->device;
     g->R = R;
     g->knn = R;
     g->n = n;
@@ -1755,6 +1769,10 @@ int32_t vdb_graph_search(vdb_graph* g, const float* queries, int32_t nq, int32_t
     else {
         const int nr = note_use(ix, st);  // a later resize of the index waits for this search
         if (nr) return nr;
+        std::lock_guard<std::mutex> lg(g->use_mu);  // and so does the graph's destroy
+        hipEvent_t& ev = g->uses[st];
+        if (!ev) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(ev, st));
     }
     return VDB_OK;
 }
@@ -1788,8 +1806,11 @@ int32_t vdb_graph_stat(const vdb_graph* g, const char* name, int64_t* value) {
 
 int32_t vdb_graph_destroy(vdb_graph* g) {
     if (!g) return VDB_OK;
-    (void)hipSetDevice(g->ix->device);
-    (void)wait_idle(g->ix);
+    (void)hipSetDevice(g->device);
+    for (auto& kv : g->uses) {  // its own searches only: the index may already be closed
+        (void)hipEventSynchronize(kv.second);
+        (void)hipEventDestroy(kv.second);
+    }
     (void)hipFree(g->nbr);
     (void)hipFree(g->entries);
     (void)hipFree(g->d_stats);

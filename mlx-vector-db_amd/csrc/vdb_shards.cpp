@@ -77,21 +77,6 @@ int next_pow2(int v) {
     return p;
 }
 
-// bits [src0, src0 + n) of `src` -> bits [dst0, dst0 + n) of `dst` (dst zeroed beforehand)
-void copy_bits(const uint32_t* src, int64_t src0, uint32_t* dst, int64_t dst0, int64_t n) {
-    for (int64_t i = 0; i < n;) {
-        const int64_t s = src0 + i, d = dst0 + i;
-        if ((s & 31) == 0 && (d & 31) == 0 && n - i >= 32) {  // whole aligned words
-            const int64_t w = (n - i) / 32;
-            std::memcpy(dst + d / 32, src + s / 32, (size_t)w * 4);
-            i += w * 32;
-            continue;
-        }
-        if ((src[s >> 5] >> (s & 31)) & 1u) dst[d >> 5] |= 1u << (d & 31);
-        ++i;
-    }
-}
-
 }  // namespace
 
 struct vdb_shards {
@@ -239,6 +224,139 @@ int32_t vdb_shards_add(vdb_shards* s, const float* vectors, int64_t n) {
     return VDB_OK;
 }
 
+}  // extern "C"
+
+namespace {
+
+// The shard-local bitmap of a global one: bit l <- bit gid[l] of the global mask (both on the
+// shard's device); one thread per local word.
+__global__ void __launch_bounds__(256) shard_mask_kernel(const uint32_t* __restrict__ gmask,
+                                                         const int64_t* __restrict__ gid, int64_t n,
+                                                         uint32_t* __restrict__ lmask) {
+    const int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (w >= (n + 31) / 32) return;
+    uint32_t bits = 0;
+    for (int b = 0; b < 32; ++b) {
+        const int64_t l = w * 32 + b;
+        if (l < n) {
+            const int64_t g = gid[l];
+            bits |= ((gmask[g >> 5] >> (g & 31)) & 1u) << b;
+        }
+    }
+    lmask[w] = bits;
+}
+
+// The search of every shard, queued without a host wait: queries, mask and outputs on
+// devices[0], ordered after the work queued on `st` (a stream of devices[0]) so far; the
+// outputs are ready once `st` reaches the merge.  Each shard: peer copy of the queries (and
+// of the global mask, then its local bitmap built on its device) on the shard's stream, the
+// shard's device search (candidate pass + exact rerank, global ids, fp64 keys), peer copy of
+// its [B, k] lists into slot g of the root's gather buffers; the root waits for every shard
+// on `st` and merges there.  Scratch is stream-ordered (hipMallocAsync / hipFreeAsync).
+int shards_search_dev(vdb_shards* s, const float* q_root, int32_t B, int32_t k, const uint32_t* mask_root,
+                      float* out_scores, int64_t* out_indices, double* out_keys, hipStream_t st) {
+    const int G = (int)s->sh.size();
+    const int D = s->dim;
+    const size_t qb = (size_t)B * D * 4, lb = (size_t)B * k;
+    const int root = s->sh[0].device;
+    const int64_t gmw = (s->count + 31) / 32;
+    SH_TRY(hipSetDevice(root));
+    const int KP = std::max(32, next_pow2(k));
+    const size_t r_keys = (size_t)G * lb * 8, r_ids = r_keys, m_bytes = (size_t)B * KP * 16;
+    char* rb = nullptr;
+    SH_TRY(hipMallocAsync((void**)&rb, r_keys + r_ids + m_bytes + 1024, st));
+    double* g_keys = (double*)rb;
+    int64_t* g_ids = (int64_t*)(rb + r_keys);
+    double* m_keys = (double*)(rb + r_keys + r_ids);
+    int64_t* m_ids = (int64_t*)(rb + r_keys + r_ids + (size_t)B * KP * 8);
+    hipEvent_t go = nullptr;
+    SH_TRY(hipEventCreateWithFlags(&go, hipEventDisableTiming));
+    hipError_t e = hipEventRecord(go, st);  // queries / mask written, gather buffers allocated
+    int rc = VDB_OK;
+    int queued = 0;  // shards whose work (and done event) is queued
+    for (int g = 0; g < G && e == hipSuccess && rc == VDB_OK; ++g) {
+        Shard& sd = s->sh[g];
+        e = hipSetDevice(sd.device);
+        if (e == hipSuccess) e = hipStreamWaitEvent(sd.st, go, 0);
+        const int64_t mw = (sd.count + 31) / 32;
+        const bool masked = mask_root && sd.count > 0;
+        const size_t off_m = (qb + 255) & ~size_t(255);
+        const size_t off_gm = off_m + (((size_t)(mw + 1) * 4 + 255) & ~size_t(255));
+        const size_t off_o = off_gm + (masked && sd.device != root ? (((size_t)gmw * 4 + 255) & ~size_t(255)) : 0);
+        char* b = nullptr;
+        if (e == hipSuccess) e = hipMallocAsync((void**)&b, off_o + lb * 20 + 1024, sd.st);
+        if (e != hipSuccess) break;
+        float* q = (float*)b;
+        uint32_t* lm = (uint32_t*)(b + off_m);
+        float* ls = (float*)(b + off_o);
+        int64_t* li = (int64_t*)(b + off_o + lb * 4);
+        double* lk = (double*)(b + off_o + lb * 12);
+        e = hipMemcpyPeerAsync(q, sd.device, q_root, root, qb, sd.st);
+        const uint32_t* md = nullptr;
+        if (e == hipSuccess && masked) {
+            const uint32_t* gm = mask_root;
+            if (sd.device != root) {
+                uint32_t* gcopy = (uint32_t*)(b + off_gm);
+                e = hipMemcpyPeerAsync(gcopy, sd.device, mask_root, root, (size_t)gmw * 4, sd.st);
+                gm = gcopy;
+            }
+            if (e == hipSuccess) {
+                hipLaunchKernelGGL(shard_mask_kernel, dim3((unsigned)((mw + 255) / 256)), dim3(256), 0, sd.st, gm, sd.gid,
+                                   sd.count, lm);
+                e = hipGetLastError();
+            }
+            md = lm;
+        }
+        if (e == hipSuccess) rc = index_search_rows(sd.ix, q, B, k, md, ls, li, lk, sd.st, sd.gid);
+        // gather this shard's (key, global id) lists into slot g of the root buffers
+        if (e == hipSuccess && rc == VDB_OK) {
+            e = hipMemcpyPeerAsync(g_keys + (size_t)g * lb, root, lk, sd.device, lb * 8, sd.st);
+            if (e == hipSuccess) e = hipMemcpyPeerAsync(g_ids + (size_t)g * lb, root, li, sd.device, lb * 8, sd.st);
+        }
+        (void)hipFreeAsync(b, sd.st);  // after this shard's copies (stream order)
+        if (e == hipSuccess && rc == VDB_OK) e = hipEventRecord(sd.done, sd.st);
+        if (e == hipSuccess && rc == VDB_OK) ++queued;
+    }
+    (void)hipSetDevice(root);
+    // the root waits for every shard that queued work (also on failure, so the gather buffers
+    // are freed after the last peer copy into them)
+    for (int g = 0; g < queued; ++g) (void)hipStreamWaitEvent(st, s->sh[g].done, 0);
+    if (queued < G) {  // a shard failed part-way: its stream may still copy into the buffers
+        for (int g = queued; g < G; ++g) {
+            (void)hipSetDevice(s->sh[g].device);
+            (void)hipStreamSynchronize(s->sh[g].st);
+        }
+        (void)hipSetDevice(root);
+    }
+    if (e == hipSuccess && rc == VDB_OK) {
+        // list j of query q at j * B * k + q * k
+        e = launch_merge_f64_i64(KP, g_keys, g_ids, G, k, k, (int64_t)lb, B, m_keys, m_ids, st);
+        if (e == hipSuccess)
+            e = launch_finalize_i64(s->metric, m_keys, m_ids, KP, B, nullptr, k, out_scores, out_indices, out_keys, st);
+    }
+    (void)hipFreeAsync(rb, st);
+    (void)hipEventDestroy(go);
+    if (rc != VDB_OK) return rc;
+    if (e != hipSuccess)
+        return fail(e == hipErrorOutOfMemory ? VDB_ERR_OOM : VDB_ERR_HIP,
+                    std::string("shard search: ") + hipGetErrorString(e));
+    return VDB_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t vdb_shards_search_device(vdb_shards* s, const float* queries, int32_t B, int32_t k, const uint32_t* row_mask,
+                                 float* out_scores, int64_t* out_indices, double* out_keys, void* stream) {
+    if (!s) return fail(VDB_ERR_INVALID, "shard set is NULL");
+    if (B <= 0) return fail(VDB_ERR_INVALID, "n_queries must be >= 1");
+    if (k <= 0 || k > 1024) return fail(VDB_ERR_INVALID, "k must be in [1, 1024]");
+    if (!queries || !out_scores || !out_indices) return fail(VDB_ERR_INVALID, "NULL query/output pointer");
+    std::shared_lock<std::shared_mutex> lk(s->mu);
+    return shards_search_dev(s, queries, B, k, row_mask, out_scores, out_indices, out_keys, (hipStream_t)stream);
+}
+
 int32_t vdb_shards_search(vdb_shards* s, const float* queries, int32_t B, int32_t k, const uint32_t* row_mask,
                           float* out_scores, int64_t* out_indices, double* out_keys) {
     if (!s) return fail(VDB_ERR_INVALID, "shard set is NULL");
@@ -248,93 +366,38 @@ int32_t vdb_shards_search(vdb_shards* s, const float* queries, int32_t B, int32_
     for (int64_t i = 0; i < (int64_t)B * s->dim; ++i)
         if (!std::isfinite(queries[i])) return fail(VDB_ERR_NONFINITE, "query contains NaN or Inf");
     std::shared_lock<std::shared_mutex> lk(s->mu);
-    const int G = (int)s->sh.size();
-    const int D = s->dim;
-    const size_t qb = (size_t)B * D * 4, lb = (size_t)B * k;
+    // host memory: staged on devices[0] and run through the stream-ordered path on a stream of
+    // this call, waited for once at the end
     const int root = s->sh[0].device;
-    hipStream_t rst = s->sh[0].st;
-    struct Buf {
-        char* p = nullptr;
-        int dev = 0;
-        hipStream_t st = nullptr;
-    };
-    std::vector<Buf> bufs;
-    bool queued_ok = false;
-    auto release = [&]() {
-        if (!queued_ok)  // an error part-way: peer copies into the root buffers may be queued
-            for (Shard& sd : s->sh) {
-                (void)hipSetDevice(sd.device);
-                (void)hipStreamSynchronize(sd.st);
-            }
-        for (Buf& b : bufs) {
-            (void)hipSetDevice(b.dev);
-            (void)hipFreeAsync(b.p, b.st);
-        }
-        bufs.clear();
-    };
-    struct Guard {
-        std::function<void()> f;
-        ~Guard() { f(); }
-    } guard{release};
-    auto take = [&](int dev, hipStream_t st, size_t bytes, char** p) -> hipError_t {
-        hipError_t e = hipSetDevice(dev);
-        if (e == hipSuccess) e = hipMallocAsync((void**)p, bytes, st);
-        if (e == hipSuccess) bufs.push_back({*p, dev, st});
-        return e;
-    };
-    // root: gathered [G][B][k] keys + ids, merged [B][KP], outputs [B][k]
-    const int KP = std::max(32, next_pow2(k));
-    char* rb = nullptr;
-    const size_t r_keys = (size_t)G * lb * 8, r_ids = r_keys, m_bytes = (size_t)B * KP * 16, o_bytes = lb * 20;
-    SH_TRY(take(root, rst, r_keys + r_ids + m_bytes + o_bytes + 4096, &rb));
-    double* g_keys = (double*)rb;
-    int64_t* g_ids = (int64_t*)(rb + r_keys);
-    double* m_keys = (double*)(rb + r_keys + r_ids);
-    int64_t* m_ids = (int64_t*)(rb + r_keys + r_ids + (size_t)B * KP * 8);
-    char* ob = rb + r_keys + r_ids + m_bytes;
-    float* o_s = (float*)ob;
-    int64_t* o_i = (int64_t*)(ob + lb * 4);
-    double* o_k = (double*)(ob + lb * 12);
-    std::vector<uint32_t> lmask;
-    for (int g = 0; g < G; ++g) {
-        Shard& sd = s->sh[g];
-        const int64_t mw = (sd.count + 31) / 32;
-        char* b = nullptr;
-        SH_TRY(take(sd.device, sd.st, qb + (size_t)(mw + 1) * 4 + lb * 20 + 1024, &b));
-        float* q = (float*)b;
-        uint32_t* m = (uint32_t*)(b + qb);
-        char* o = b + qb + (size_t)(mw + 1) * 4;
-        o = (char*)(((uintptr_t)o + 255) & ~(uintptr_t)255);
-        float* ls = (float*)o;
-        int64_t* li = (int64_t*)(o + lb * 4);
-        double* lk2 = (double*)(o + lb * 12);
-        SH_TRY(hipMemcpyAsync(q, queries, qb, hipMemcpyHostToDevice, sd.st));
-        const uint32_t* md = nullptr;
-        if (row_mask && sd.count > 0) {
-            lmask.assign((size_t)mw, 0u);
-            for (const Piece& pc : sd.pieces) copy_bits(row_mask, pc.g0, lmask.data(), pc.l0, pc.n);
-            SH_TRY(hipMemcpyAsync(m, lmask.data(), (size_t)mw * 4, hipMemcpyHostToDevice, sd.st));
-            SH_TRY(hipStreamSynchronize(sd.st));  // lmask is reused by the next shard
-            md = m;
-        }
-        const int rc = index_search_rows(sd.ix, q, B, k, md, ls, li, lk2, sd.st, sd.gid);
-        if (rc != VDB_OK) return rc;
-        // gather this shard's (key, global id) lists into slot g of the root buffers
-        SH_TRY(hipMemcpyPeerAsync(g_keys + (size_t)g * lb, root, lk2, sd.device, lb * 8, sd.st));
-        SH_TRY(hipMemcpyPeerAsync(g_ids + (size_t)g * lb, root, li, sd.device, lb * 8, sd.st));
-        SH_TRY(hipEventRecord(sd.done, sd.st));
-    }
     SH_TRY(hipSetDevice(root));
-    for (int g = 0; g < G; ++g) SH_TRY(hipStreamWaitEvent(rst, s->sh[g].done, 0));
-    queued_ok = true;  // root work is ordered after every shard's copies from here on
-    // list j of query q at j * B * k + q * k
-    SH_TRY(launch_merge_f64_i64(KP, g_keys, g_ids, G, k, k, (int64_t)lb, B, m_keys, m_ids, rst));
-    SH_TRY(launch_finalize_i64(s->metric, m_keys, m_ids, KP, B, nullptr, k, o_s, o_i, o_k, rst));
-    SH_TRY(hipMemcpyAsync(out_scores, o_s, lb * 4, hipMemcpyDeviceToHost, rst));
-    SH_TRY(hipMemcpyAsync(out_indices, o_i, lb * 8, hipMemcpyDeviceToHost, rst));
-    if (out_keys) SH_TRY(hipMemcpyAsync(out_keys, o_k, lb * 8, hipMemcpyDeviceToHost, rst));
-    SH_TRY(hipStreamSynchronize(rst));
-    // the shard streams' buffers are freed stream-ordered after their peer copies
+    hipStream_t st = nullptr;
+    SH_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    const size_t qb = (size_t)B * s->dim * 4, lb = (size_t)B * k, mb = row_mask ? (size_t)((s->count + 31) / 32) * 4 : 0;
+    char* buf = nullptr;
+    hipError_t e = hipMallocAsync((void**)&buf, qb + mb + lb * 20 + 1024, st);
+    int rc = VDB_OK;
+    if (e == hipSuccess) {
+        float* q = (float*)buf;
+        uint32_t* m = row_mask ? (uint32_t*)(buf + ((qb + 255) & ~size_t(255))) : nullptr;
+        char* o = buf + ((qb + 255) & ~size_t(255)) + ((mb + 255) & ~size_t(255));
+        float* os = (float*)o;
+        int64_t* oi = (int64_t*)(o + lb * 4);
+        double* ok = (double*)(o + lb * 12);
+        e = hipMemcpyAsync(q, queries, qb, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess && m && mb) e = hipMemcpyAsync(m, row_mask, mb, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess) rc = shards_search_dev(s, q, B, k, m, os, oi, ok, st);
+        if (e == hipSuccess && rc == VDB_OK) e = hipMemcpyAsync(out_scores, os, lb * 4, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess && rc == VDB_OK) e = hipMemcpyAsync(out_indices, oi, lb * 8, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess && rc == VDB_OK && out_keys)
+            e = hipMemcpyAsync(out_keys, ok, lb * 8, hipMemcpyDeviceToHost, st);
+        (void)hipFreeAsync(buf, st);
+    }
+    const hipError_t e2 = hipStreamSynchronize(st);
+    (void)hipStreamDestroy(st);
+    if (rc != VDB_OK) return rc;
+    if (e == hipSuccess) e = e2;
+    if (e != hipSuccess)
+        return fail(e == hipErrorOutOfMemory ? VDB_ERR_OOM : VDB_ERR_HIP, std::string("shard search: ") + hipGetErrorString(e));
     return VDB_OK;
 }
 

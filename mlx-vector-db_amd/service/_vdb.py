@@ -44,7 +44,7 @@ EXPORTED_SYMBOLS = (
     "vdb_graph_build", "vdb_graph_import", "vdb_graph_export", "vdb_graph_add", "vdb_graph_info", "vdb_graph_search",
     "vdb_graph_stat", "vdb_graph_set_param", "vdb_graph_destroy",
     "vdb_shards_create", "vdb_shards_destroy", "vdb_shards_add", "vdb_shards_count", "vdb_shards_shard_count",
-    "vdb_shards_search", "vdb_shards_get_vectors", "vdb_shards_clear", "vdb_shards_reserve",
+    "vdb_shards_search", "vdb_shards_search_device", "vdb_shards_get_vectors", "vdb_shards_clear", "vdb_shards_reserve",
     "vdb_shards_set_param", "vdb_shards_get_stat", "vdb_shutdown",
 )
 
@@ -117,6 +117,7 @@ def load_library():
             "vdb_shards_count": (c_i32, [c_vp, p_i64]),
             "vdb_shards_shard_count": (c_i32, [c_vp, c_i32, p_i64]),
             "vdb_shards_search": (c_i32, [c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp]),
+            "vdb_shards_search_device": (c_i32, [c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
             "vdb_shards_get_vectors": (c_i32, [c_vp, c_i64, c_i64, c_vp]),
             "vdb_shards_clear": (c_i32, [c_vp]),
             "vdb_shards_reserve": (c_i32, [c_vp, c_i64]),
@@ -357,6 +358,18 @@ class NativeShards:
         _check(self._lib.vdb_shards_search(self._h, _ptr(q), B, k, mask_p, _ptr(scores), _ptr(idx),
                                            _ptr(keys) if keys is not None else None))
         return (scores, idx, keys) if with_keys else (scores, idx)
+
+
+def _shards_search_device(self, q_ptr: int, n_queries: int, k: int, out_scores_ptr: int, out_idx_ptr: int,
+                          out_keys_ptr: int = 0, mask_ptr: int = 0, stream: int = 0) -> None:
+    """Stream-ordered search of every shard (all pointers on devices[0], no host wait)."""
+    _check(self._lib.vdb_shards_search_device(
+        self._h, ctypes.c_void_p(q_ptr), int(n_queries), int(k), ctypes.c_void_p(mask_ptr or None),
+        ctypes.c_void_p(out_scores_ptr), ctypes.c_void_p(out_idx_ptr), ctypes.c_void_p(out_keys_ptr or None),
+        ctypes.c_void_p(stream or None)))
+
+
+NativeShards.search_device = _shards_search_device
 
 
 def shutdown() -> None:

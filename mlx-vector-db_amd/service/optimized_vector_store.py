@@ -56,6 +56,9 @@ class MLXVectorStoreConfig:
     # searched on every shard at once and the per-shard top-k lists are gathered and merged
     # on the first device (service/_vdb.py NativeShards); None = the single `device`
     devices: Optional[List[int]] = None
+    # concurrent single-vector queries (the REST executor's 4 threads, api/routes/vectors.py:43)
+    # join one batched device search instead of one corpus scan each (_QueryCoalescer)
+    coalesce: bool = True
 
 
 def _as_matrix(vectors: Any) -> np.ndarray:
@@ -125,6 +128,63 @@ class _Write(_Read):
         self.lk.release_write()
 
 
+class _QueryCoalescer:
+    """Continuous batching of concurrent single-vector queries.
+
+    The reference serves /vectors/query one vector per request from a 4-thread executor
+    (api/routes/vectors.py:43, :226-234): each call is a full scan of the corpus
+    (service/optimized_vector_store.py:149-192).  A scan costs about the same for 1 query as
+    for 64 (the corpus read dominates), so while one batch runs on the device the
+    queries that arrive meanwhile wait and then run together as the next batch: no artificial
+    delay when a query arrives alone, up to ``max_batch`` queries per scan under load.  Each
+    caller gets its own row; k differs per caller, the batch runs max(k) (the exact order
+    makes every caller's top-k the prefix of the batch's).  Callers hold the store's read
+    lock while they wait, so every query of a batch sees the same rows."""
+
+    def __init__(self, run, max_batch: int = 64):
+        self._run = run            # run(Q [B, D], k) -> [(indices, scores, metadata)] * B
+        self._max = max_batch
+        self._cv = threading.Condition(threading.Lock())
+        self._pending: List[list] = []
+        self._running = False
+        self.batches = 0
+        self.queries = 0
+
+    def query(self, q: np.ndarray, k: int):
+        req = [q, int(k), None, None]  # query, k, result, error
+        self._cv.acquire()
+        try:
+            self._pending.append(req)
+            # wait for a result; whenever no batch is running, lead the next one (FIFO, so this
+            # caller's own query is in one of the batches it leads)
+            while req[2] is None and req[3] is None:
+                if self._running:
+                    self._cv.wait()
+                    continue
+                self._running = True
+                batch, self._pending = self._pending[:self._max], self._pending[self._max:]
+                self._cv.release()
+                try:
+                    kmax = max(r[1] for r in batch)
+                    res = self._run(np.stack([r[0] for r in batch]), kmax)
+                    for r, (ix, sc, md) in zip(batch, res):
+                        r[2] = (ix[:r[1]], sc[:r[1]], md[:r[1]])
+                except BaseException as e:  # every caller of the batch sees the failure
+                    for r in batch:
+                        r[3] = e
+                finally:
+                    self._cv.acquire()
+                    self._running = False
+                    self.batches += 1
+                    self.queries += len(batch)
+                    self._cv.notify_all()
+        finally:
+            self._cv.release()
+        if req[3] is not None:
+            raise req[3]
+        return req[2]
+
+
 class MLXVectorStore:
     """service/optimized_vector_store.py:59-242, MI355X-native."""
 
@@ -143,6 +203,7 @@ class MLXVectorStore:
         self._vector_count = 0
         self._hnsw_index = None
         self._files = StoreFiles(self.store_path)
+        self._coalescer = _QueryCoalescer(lambda Q, k: self._brute_force_search(Q, k, None))
         if self.config.enable_hnsw:  # service/optimized_vector_store.py:72-78
             from performance.hnsw_index import ProductionHNSWIndex
             self._hnsw_index = ProductionHNSWIndex(self.config.dimension, self.store_path, self.config.metric,
@@ -261,6 +322,10 @@ class MLXVectorStore:
                     return list(fi), list(fd), list(fm)
                 except Exception as e:
                     logger.warning("HNSW-Suche fehlgeschlagen, falle auf Brute-Force zurück: %s", e)
+            if self.config.coalesce and not filter_metadata and self._compiled_similarity_fn and int(k) > 0:
+                if q.shape[0] != self._dim:
+                    raise ValueError(f"Dimension mismatch: query has {q.shape[0]} dims, store holds {self._dim}")
+                return self._coalescer.query(q, k)
             return self._brute_force_search(q[None, :], k, filter_metadata)[0]
 
     def batch_query(self, query_vectors: Union[np.ndarray, Any], k: int = 10,

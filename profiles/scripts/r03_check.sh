@@ -7,7 +7,7 @@ TAG=${1:-a}; K=${2:-}; shift 2; CONFIGS="$@"
 O=gpurun_out/$TAG; mkdir -p $O
 if [ "$K" != "skip" ]; then
   if [ -n "$K" ]; then KARG=(-k "$K"); else KARG=(); fi
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${KARG[@]}" > $O/pytest_gpu.log 2>&1 || { echo "pytest failed"; grep -E "FAIL|Error" $O/pytest_gpu.log | head -20; tail -40 $O/pytest_gpu.log; exit 1; }
+  timeout -k 10 900 python -u -m pytest tests -m "${MARK:-gpu}" -x -v --timeout 300 --timeout-method thread "${KARG[@]}" > $O/pytest_gpu.log 2>&1 || { echo "pytest failed"; grep -E "FAIL|Error" $O/pytest_gpu.log | head -20; tail -40 $O/pytest_gpu.log; exit 1; }
   tail -1 $O/pytest_gpu.log
 fi
 for c in $CONFIGS; do

@@ -84,3 +84,39 @@ def test_device_tensors_stay_on_device(mo):
                                atol=1e-4, rtol=0)
     idx = mo.fast_top_k_indices(out[0], 7)
     assert idx.is_cuda and idx.cpu().tolist() == ref_cpu.reference_topk_indices(out[0].cpu().numpy(), 7).tolist()
+
+
+def test_batch_search_device_corpus_no_host_copy(mo, monkeypatch):
+    """optimized_batch_similarity_search (performance/mlx_optimized.py:217-248) on torch CUDA
+    tensors at 200K rows: the corpus goes device to device into a cached index (no .cpu() of
+    any tensor during the calls, checked by a patched Tensor.cpu), results stay on device and
+    match the exact oracle; the reference's fp32 scores within 1e-4; an in-place write to the
+    corpus (version bump) is seen by the next call."""
+    import torch
+    rng = np.random.default_rng(53)
+    Vh = rng.random((200_000, 128), dtype=np.float32)
+    Qh = rng.random((48, 128), dtype=np.float32)
+    Qh[5] = Vh[199_999]
+    V, Q = torch.from_numpy(Vh).cuda(), torch.from_numpy(Qh).cuda()
+    es, ei, _ = ref_cpu.exact_search(Qh, Vh, 10, "cosine")
+    ri, rs = ref_cpu.reference_batch_search(Qh, Vh, 10)
+    real_cpu = torch.Tensor.cpu
+    copies = []
+
+    def guarded_cpu(self, *a, **kw):
+        copies.append(tuple(self.shape))
+        return real_cpu(self, *a, **kw)
+    monkeypatch.setattr(torch.Tensor, "cpu", guarded_cpu)
+    outs = [mo.optimized_batch_similarity_search(Q, V, 10) for _ in range(3)]
+    i1, s1 = mo.optimized_similarity_search(Q[5], V, 4)
+    torch.cuda.synchronize()
+    assert copies == []  # nothing moved to the host inside the mirror
+    monkeypatch.setattr(torch.Tensor, "cpu", real_cpu)
+    for i, s in outs:
+        assert i.is_cuda and s.is_cuda and tuple(i.shape) == (48, 10)
+        np.testing.assert_array_equal(i.cpu().numpy(), ei)
+        np.testing.assert_allclose(s.cpu().numpy(), rs, atol=1e-4, rtol=0)
+    assert i1.is_cuda and i1.cpu().tolist() == ei[5, :4].tolist()
+    V[123] = Q[7]  # in place: the cached index must not serve the old rows
+    i2, _ = mo.optimized_batch_similarity_search(Q[7:8], V, 1)
+    assert i2.cpu().tolist() == [[123]]

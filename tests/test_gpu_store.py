@@ -188,3 +188,38 @@ def test_store_over_devices_list(store_mod, tmp_path):
     from service import _vdb
     _vdb.shutdown()  # idle workspaces released; the stores keep working
     assert st.query(V[10], k=1)[0] == [10]
+
+
+@pytest.mark.parametrize("metric", ["cosine", "euclidean"])
+def test_shards_search_device_queued_back_to_back(store_mod, metric):
+    """vdb_shards_search_device (include/vdb.h): three batches queued on one stream of
+    devices[0] without a host wait (device masks included), each equal to exact_search."""
+    import torch
+    from service import _vdb
+    rng = np.random.default_rng(47)
+    V = rng.random((40_003, 48), dtype=np.float32)
+    sh = _vdb.NativeShards(48, metric, [0, 0, 0])
+    for a, b in ((0, 10_000), (10_000, 40_003)):
+        sh.add(V[a:b])
+    mask = rng.random(V.shape[0]) < 0.5
+    bits = np.zeros(((V.shape[0] + 31) // 32) * 32, bool)
+    bits[:V.shape[0]] = mask
+    words = torch.from_numpy(np.packbits(bits, bitorder="little").view("<u4").astype(np.int32)).cuda()
+    st = torch.cuda.Stream()
+    batches = [rng.random((B, 48), dtype=np.float32) for B in (17, 64, 5)]
+    outs = []
+    with torch.cuda.stream(st):
+        for j, Qh in enumerate(batches):
+            q = torch.from_numpy(Qh).cuda()
+            s_ = torch.empty((q.shape[0], 12), dtype=torch.float32, device="cuda")
+            i_ = torch.empty((q.shape[0], 12), dtype=torch.int64, device="cuda")
+            k_ = torch.empty((q.shape[0], 12), dtype=torch.float64, device="cuda")
+            sh.search_device(q.data_ptr(), q.shape[0], 12, s_.data_ptr(), i_.data_ptr(), k_.data_ptr(),
+                             mask_ptr=words.data_ptr() if j == 1 else 0, stream=st.cuda_stream)
+            outs.append((q, s_, i_, k_))
+    st.synchronize()
+    for j, (Qh, (_, s_, i_, k_)) in enumerate(zip(batches, outs)):
+        es, ei, ek = ref_cpu.exact_search(Qh, V, 12, metric, row_mask=mask if j == 1 else None)
+        np.testing.assert_array_equal(i_.cpu().numpy(), ei)
+        np.testing.assert_array_equal(k_.cpu().numpy(), ek)
+    sh.close()
