@@ -156,8 +156,9 @@ struct vdb_index {
     int64_t scan_qring = 0;       // split pass, global query operand: query chunks through an LDS ring
     int64_t gate_div = 1;         // gated exact fallback: n_cu / gate_div row ranges, one query slot each when > 1
     int64_t finish_split = 1;  // workgroups per query in the finish kernel (tuning)
+    int64_t scan3 = 0;         // large-batch candidate pass: -1 auto (B >= 128), 0 off, 1 always (vdb_scan3_kernel.h)
     // stats
-    std::atomic<int64_t> n_searches{0}, n_queries{0}, n_fallback{0}, n_overflow{0}, n_repass{0};
+    std::atomic<int64_t> n_searches{0}, n_queries{0}, n_fallback{0}, n_overflow{0}, n_repass{0}, n_scan3{0};
     std::atomic<int64_t> n_by_prec[3] = {{0}, {0}, {0}};  // candidate passes per PREC_* (VDB_PREC_AUTO's choices)
     std::atomic<int64_t> scan_ns{0}, pipe_ns{0}, n_timed{0};
     unsigned long long* d_totals = nullptr;  // device: flagged / overflowed / flagged-in-bf16 queries of device-gated searches
@@ -489,6 +490,8 @@ int32_t vdb_index_create(int32_t dim, int32_t metric, int32_t device, vdb_index*
     // start value of the scan_qring parameter (A/B runs of whole test suites)
     if (const char* qr = std::getenv("VDB_SCAN_QRING")) ix->scan_qring = std::atoi(qr) != 0;
     if (const char* gd = std::getenv("VDB_GATE_DIV")) ix->gate_div = std::min(64, std::max(1, std::atoi(gd)));
+    // start value of the scan3 parameter (A/B runs of whole suites): -1 auto, 0 off, 1 always
+    if (const char* s3 = std::getenv("VDB_SCAN3")) ix->scan3 = std::min(1, std::max(-1, std::atoi(s3)));
     hipError_t e = hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMalloc(&ix->d_xmax, 64);
     if (e == hipSuccess) e = hipMemset(ix->d_xmax, 0, 64);
@@ -593,6 +596,9 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
     } else if (n == "finish_split") {
         if (value < 1 || value > 8) return set_error(VDB_ERR_INVALID, "finish_split must be in [1, 8]");
         ix->finish_split = value;
+    } else if (n == "scan3") {
+        if (value < -1 || value > 1) return set_error(VDB_ERR_INVALID, "scan3 must be -1, 0 or 1");
+        ix->scan3 = value;
     } else if (n == "gate_div") {
         if (value < 1 || value > 64) return set_error(VDB_ERR_INVALID, "gate_div must be in [1, 64]");
         ix->gate_div = value;
@@ -638,6 +644,7 @@ int32_t vdb_index_get_stat(const vdb_index* cix, const char* name, int64_t* valu
     else if (n == "queries") *value = ix->n_queries.load();
     else if (n == "fallback_queries") *value = ix->n_fallback.load() + (int64_t)dt[0];
     else if (n == "repass_queries") *value = ix->n_repass.load();
+    else if (n == "searches_scan3") *value = ix->n_scan3.load();
     else if (n == "auto_hold") *value = ix->auto_hold.load();
     else if (n == "overflow_queries") *value = ix->n_overflow.load() + (int64_t)dt[1];
     else if (n == "capacity") *value = ix->cap_rows;
@@ -987,6 +994,16 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     // steps 1, 2, 4, 8 cost more than the pilot's bound leaves to gain (measured: stamps,
     // profiles/r02_ab/).
     const int publish = (ix->scan_publish >= 0 ? (int)ix->scan_publish : spw >= 16) | (int)(ix->scan_realign << 8);
+    // The large-batch pass (vdb_scan3_kernel.h): 256 queries per workgroup sharing each row
+    // group through LDS.  Auto: B >= 128 and enough workgroups per query block that no
+    // workgroup is likely to hold more than its KW = 32 best of a query's top k.
+    const int n_qb3 = (B + 255) / 256;
+    const int64_t steps3 = std::max<int64_t>(1, round_up(N, scan3_rows_per_step()) / scan3_rows_per_step());
+    const int wg3_target = ix->n_wg_override > 0 ? (int)ix->n_wg_override : std::max(1, ix->n_cu / n_qb3);
+    const int spw3 = (int)std::max<int64_t>(1, (steps3 + wg3_target - 1) / wg3_target);
+    const int n_wg3 = (int)((steps3 + spw3 - 1) / spw3);
+    const bool use_s3 = split_pass && !exact_all &&
+                        (ix->scan3 == 1 || (ix->scan3 < 0 && B >= 128 && n_wg3 >= std::max(8, 4 * k / 32)));
 
     Workspace* w = acquire_ws(ix, st, own_stream);
     if (own_stream) {
@@ -1024,7 +1041,8 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     const bool priv = !exact_all && !split_pass && scan_priv(prec, variant, KP);
     // global per-query candidate lists: at most 512 entries per workgroup and query
     // (the largest LDS buffer of any variant; 4 x 64 for the wave-private one)
-    const int64_t gl_cap = exact_all ? 0 : (int64_t)((n_wg + 7) / 8 * 8) * 512;
+    const int64_t gl_cap = exact_all ? 0 : use_s3 ? (int64_t)((n_wg3 + 7) / 8 * 8) * 64
+                                              : (int64_t)((n_wg + 7) / 8 * 8) * 512;
     bytes += (size_t)B * gl_cap * 8 + (size_t)Bp * 4 + 768;
     // Pilot sample: 512 row tiles, more for large k (its bound then saves more insert work than
     // the sample costs: C4, k = 100, 512 -> 4096 tiles: 89.5 K -> 96.4 K QPS, profiles/r02_ab).
@@ -1127,7 +1145,7 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
                 if (split_pass) {
                     HIP_TRY(launch_pilot2(prec, ix->metric, pilot_rank, Xscan, ix->rinit32, md, Qt, Gs, N, B,
                                           n_qblocks, QB, n_pilot, pslots, gthr, st));
-                    if (!ix->pilot_fused) HIP_TRY(launch_pilot_bound(pslots, B, pilot_rank, gthr, st));
+                    if (!ix->pilot_fused || use_s3) HIP_TRY(launch_pilot_bound(pslots, B, pilot_rank, gthr, st));
                 }
                 else
                     HIP_TRY(launch_pilot(prec, ix->metric, pilot_rank, Xscan, rowscale, md, Qt, Gs, N, B,
@@ -1136,7 +1154,11 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
             // scan_ns times the scan kernel alone (the roofline's kernel); pipeline_ns
             // everything from the pilot to the rerank
             if (timed) HIP_TRY(hipEventRecord(tev[0], st));
-            if (split_pass)
+            if (use_s3) ix->n_scan3++;
+            if (use_s3)
+                HIP_TRY(launch_scan3(prec, ix->metric, Xscan, ix->rinit32, md, Qt, Gs, N, B, n_qb3, steps3, n_wg3, spw3,
+                                     gl_s, gl_i, gl_cnt, gl_cap, gthr, st));
+            else if (split_pass)
                 HIP_TRY(launch_scan2(prec, ix->metric, KP, Xscan, ix->rinit32, md, Qt, Gs, N, B, n_qblocks, n_steps,
                                      n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, pslots,
                                      n_pilot > 0 && ix->pilot_fused ? pilot_rank : 0, lockstep, publish, (int)ix->scan_qring,

@@ -1,6 +1,7 @@
 // vdb_scan2.hip — the split-bf16 candidate pass (PREC_BF16X3, the default, and PREC_BF16):
 // pilot kernel, dispatch to the instantiation units (kernel: vdb_scan2_kernel.h).
 #include "vdb_scan2_kernel.h"
+#include "vdb_scan3_kernel.h"
 
 namespace vdb {
 
@@ -125,6 +126,17 @@ hipError_t launch_pilot2(int prec, int metric, int KP, const float* Xs, const fl
 // Dispatch
 // =============================================================================
 int scan2_rows_per_step() { return S2_ROWS; }
+int scan3_rows_per_step() { return S3_ROWS; }
+
+hipError_t launch_scan3(int prec, int metric, const float* Xs, const float* rinit, const uint32_t* mask,
+                        const float* Qs, int G, int64_t N, int B, int n_qb, int64_t n_steps, int n_wg, int spw,
+                        float* gl_s, uint32_t* gl_i, uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr, hipStream_t st) {
+    auto* unit = prec == PREC_BF16X3 ? (metric == 0 ? launch_scan3_b3c : launch_scan3_b3l)
+                 : prec == PREC_BF16 ? (metric == 0 ? launch_scan3_b1c : launch_scan3_b1l)
+                                     : nullptr;
+    if (!unit || metric < 0 || metric > 1) return hipErrorInvalidValue;
+    return unit(Xs, rinit, mask, Qs, G, N, B, n_qb, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, st);
+}
 
 hipError_t launch_scan2(int prec, int metric, int KP, const float* Xs, const float* rinit, const uint32_t* mask,
                         const float* Qs, int G, int64_t N, int B, int n_qblocks, int64_t n_steps, int n_wg, int spw,

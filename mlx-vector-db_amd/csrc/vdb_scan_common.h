@@ -13,7 +13,7 @@ namespace vdb {
 // compaction costs ~32 ballot rounds instead of a sort network.
 template <int KP, int CAP>
 __device__ __forceinline__ void compact_query(float* sc, uint32_t* ix, int* cnt, float* thr, uint32_t* gslot) {
-    constexpr int E = CAP / 64;
+    constexpr int E = (CAP + 63) / 64;  // CAP need not be a multiple of 64 (scan3: 48)
     const int lane = threadIdx.x & 63;
     const int n = *cnt < CAP ? *cnt : CAP;
     if (n <= KP) return;

@@ -518,3 +518,49 @@ def test_full_size_c2_subset(vdb, precision):
     es, ei, ek = ref_cpu.exact_search(Q[sub], V, k, "cosine")
     np.testing.assert_array_equal(i[sub], ei)
     np.testing.assert_allclose(s[sub], es, atol=1e-6, rtol=0)
+
+
+@pytest.mark.parametrize("metric", ["cosine", "euclidean"])
+@pytest.mark.parametrize("precision", ["bf16", "bf16x3"])
+def test_scan3_large_batch_pass(vdb, metric, precision):
+    """The large-batch candidate pass (vdb_scan3_kernel.h, knob "scan3" = 1): query blocks of 256
+    over rows shared through LDS, KW = 32 kept per query and workgroup.  Bit-exact vs the oracle
+    for ragged batches (1, 64, 300: two blocks, the second partial), k up to 100, D in {128 (the
+    compile-time group count), 200 (ragged), 768}, a filter mask, and a corpus whose clustered
+    rows put more than KW of a query's top k into one workgroup (the drop bound then sends that
+    query to the exact path, still exact)."""
+    rng = np.random.default_rng(61)
+    for D, N in ((128, 70_000), (200, 30_011), (768, 20_000)):
+        V = rng.random((N, D), dtype=np.float32)
+        Q = rng.random((300, D), dtype=np.float32)
+        Q[7], Q[299] = V[N - 1], V[12345]
+        ix = vdb.NativeIndex(D, metric, precision=precision)
+        ix.set_param("scan3", 1)
+        ix.add(V)
+        for B, k in ((300, 10), (64, 100), (1, 5)):
+            s, i, kk = ix.search(Q[:B], k, with_keys=True)
+            es, ei, ek = ref_cpu.exact_search(Q[:B], V, k, metric)
+            np.testing.assert_array_equal(i, ei)
+            np.testing.assert_array_equal(kk, ek)
+        mask = rng.random(N) < 0.3
+        bits = np.zeros(((N + 31) // 32) * 32, bool)
+        bits[:N] = mask
+        words = np.packbits(bits, bitorder="little").view("<u4").astype(np.uint32)
+        s, i, kk = ix.search(Q[:260], 16, row_mask=words, with_keys=True)
+        es, ei, ek = ref_cpu.exact_search(Q[:260], V, 16, metric, row_mask=mask)
+        np.testing.assert_array_equal(i, ei)
+        np.testing.assert_array_equal(kk, ek)
+        assert ix.stat("searches_scan3") == 4
+        ix.close()
+    # 40 near copies of one row inside one workgroup's range: > KW of the query's top 50 there
+    V = rng.random((40_000, 96), dtype=np.float32)
+    V[20_000:20_040] = (V[5] + 1e-3 * rng.random((40, 96))).astype(np.float32)
+    Q = np.concatenate([V[5:6], rng.random((199, 96), dtype=np.float32)])
+    ix = vdb.NativeIndex(96, metric, precision=precision)
+    ix.set_param("scan3", 1)
+    ix.add(V)
+    s, i, kk = ix.search(Q, 50, with_keys=True)
+    es, ei, ek = ref_cpu.exact_search(Q, V, 50, metric)
+    np.testing.assert_array_equal(i, ei)
+    np.testing.assert_array_equal(kk, ek)
+    ix.close()
