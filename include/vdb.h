@@ -79,7 +79,8 @@ enum { VDB_MEM_HOST = 0, VDB_MEM_DEVICE = 1 };
  *                    d the normalised mean row of the first add, M the largest
  *                    |d.(x - bf16(x))|, c = q.d, so it is wider
  *                    and takes a larger candidate margin.
- *   VDB_PREC_AUTO    (default) BF16, per batch.  A host-memory search re-passes its
+ *   VDB_PREC_AUTO    (default) BF16X3 for k > 16 (BF16 would need 256 candidates per query
+ *                    there, a slower pass); otherwise BF16, per batch.  A host-memory search re-passes its
  *                    uncertified queries (at most 1/8 of the batch, at most 64) in BF16X3
  *                    as one gathered sub-search and stays BF16; more than that reruns the
  *                    batch in BF16X3 and starts a HOLD: the next 16 searches run BF16X3,

@@ -838,6 +838,8 @@ constexpr int32_t kRetryBf16x3 = 1 << 20;
 // A host-memory bf16 search re-passes its uncertified queries in bf16x3 (gathered into one
 // device-memory sub-search) when they are at most 1/8 of the batch and at most this many.
 constexpr int kRepassMax = 64;
+// VDB_PREC_AUTO uses the bf16 pass up to this k (its KP = next_pow2(k + 112) stays 128)
+constexpr int kAutoBf16MaxK = 16;
 
 // VDB_PREC_AUTO bookkeeping (vdb_index::auto_hold): a bf16 failure too large for a re-pass
 // starts a hold of bf16x3 searches, doubling per failed probe (16 .. 2048).
@@ -951,10 +953,16 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
         if (seen > prev) auto_fail(ix);
     }
     const bool approx = N > 0 && !(ix->force_exact || k > kMaxApproxK);
+    // AUTO takes bf16x3 directly where bf16's wider certificate needs KP = 256 (k > 16): that
+    // pass runs 32-query blocks at twice the query-operand traffic and measured 3x slower than
+    // bf16x3 (C4, k = 100: 13 vs 3.9 ms, profiles/r02s_ab/s4_c4_str2.json), and in device memory
+    // its uncertified queries cost the exact path
+    const bool auto_b16 = k <= kAutoBf16MaxK;
     const int prec_req = !ix->Xs ? PREC_FP32
                          : ix->precision == VDB_PREC_BF16X3 ? PREC_BF16X3
                          : ix->precision == VDB_PREC_BF16 ? PREC_BF16
-                         : auto_prec ? (opt.force_b3 || (approx && auto_take_hold(ix)) ? PREC_BF16X3 : PREC_BF16)
+                         : auto_prec ? (opt.force_b3 || !auto_b16 || (approx && auto_take_hold(ix)) ? PREC_BF16X3
+                                                                                                : PREC_BF16)
                                      : PREC_FP32;
     if (approx) ix->n_by_prec[prec_req]++;
 

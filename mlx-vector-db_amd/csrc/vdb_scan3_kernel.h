@@ -73,7 +73,7 @@ scan3_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
     constexpr size_t GSTEP = 8 * BLOCK_FLOATS;  // query: consecutive groups of one super tile
     constexpr size_t PLANE = 4 * BLOCK_FLOATS;  // query: lo plane after hi
     const int G = GC > 0 ? GC : G_arg;
-    const size_t XGSTEP = corpus_gstep(), XPLANE = corpus_plane(G);
+    const size_t XPLANE = corpus_plane(G);
 
     __shared__ __attribute__((aligned(16))) float s_x[2][PIECES * 256];  // corpus slots (group parity)
     __shared__ float s_sc[NW][64 * CAP];
