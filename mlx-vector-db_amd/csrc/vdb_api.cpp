@@ -157,8 +157,9 @@ struct vdb_index {
     int64_t gate_div = 1;         // gated exact fallback: n_cu / gate_div row ranges, one query slot each when > 1
     int64_t finish_split = 1;  // workgroups per query in the finish kernel (tuning)
     int64_t scan3 = 0;         // large-batch candidate pass: -1 auto (B >= 128), 0 off, 1 always (vdb_scan3_kernel.h)
+    int64_t scan_q4 = 0;       // split pass 128-query shape (D <= 128, KP = 128, B >= 256): -1 auto, 0 off, 1 on
     // stats
-    std::atomic<int64_t> n_searches{0}, n_queries{0}, n_fallback{0}, n_overflow{0}, n_repass{0}, n_scan3{0};
+    std::atomic<int64_t> n_searches{0}, n_queries{0}, n_fallback{0}, n_overflow{0}, n_repass{0}, n_scan3{0}, n_q4{0};
     std::atomic<int64_t> n_by_prec[3] = {{0}, {0}, {0}};  // candidate passes per PREC_* (VDB_PREC_AUTO's choices)
     std::atomic<int64_t> scan_ns{0}, pipe_ns{0}, n_timed{0};
     unsigned long long* d_totals = nullptr;  // device: flagged / overflowed / flagged-in-bf16 queries of device-gated searches
@@ -492,6 +493,7 @@ int32_t vdb_index_create(int32_t dim, int32_t metric, int32_t device, vdb_index*
     if (const char* gd = std::getenv("VDB_GATE_DIV")) ix->gate_div = std::min(64, std::max(1, std::atoi(gd)));
     // start value of the scan3 parameter (A/B runs of whole suites): -1 auto, 0 off, 1 always
     if (const char* s3 = std::getenv("VDB_SCAN3")) ix->scan3 = std::min(1, std::max(-1, std::atoi(s3)));
+    if (const char* q4 = std::getenv("VDB_SCAN_Q4")) ix->scan_q4 = std::min(1, std::max(-1, std::atoi(q4)));
     hipError_t e = hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMalloc(&ix->d_xmax, 64);
     if (e == hipSuccess) e = hipMemset(ix->d_xmax, 0, 64);
@@ -596,6 +598,9 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
     } else if (n == "finish_split") {
         if (value < 1 || value > 8) return set_error(VDB_ERR_INVALID, "finish_split must be in [1, 8]");
         ix->finish_split = value;
+    } else if (n == "scan_q4") {
+        if (value < -1 || value > 1) return set_error(VDB_ERR_INVALID, "scan_q4 must be -1, 0 or 1");
+        ix->scan_q4 = value;
     } else if (n == "scan3") {
         if (value < -1 || value > 1) return set_error(VDB_ERR_INVALID, "scan3 must be -1, 0 or 1");
         ix->scan3 = value;
@@ -645,6 +650,7 @@ int32_t vdb_index_get_stat(const vdb_index* cix, const char* name, int64_t* valu
     else if (n == "fallback_queries") *value = ix->n_fallback.load() + (int64_t)dt[0];
     else if (n == "repass_queries") *value = ix->n_repass.load();
     else if (n == "searches_scan3") *value = ix->n_scan3.load();
+    else if (n == "searches_q4") *value = ix->n_q4.load();
     else if (n == "auto_hold") *value = ix->auto_hold.load();
     else if (n == "overflow_queries") *value = ix->n_overflow.load() + (int64_t)dt[1];
     else if (n == "capacity") *value = ix->cap_rows;
@@ -976,16 +982,22 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     int KP = std::max(32, next_pow2(k + margin));
     const bool exact_all = ix->force_exact || k > kMaxApproxK || KP > 256;
     if (KP > 256) KP = 256;
-    const int QB = KP == 256 ? 32 : 64;
-    const int Bp = (int)round_up(B, 128);  // whole query super tiles (tiled layout)
-    const int n_qblocks = (B + QB - 1) / QB;
     const int prec = prec_req;
     const int Gs = prec == PREC_FP32 ? ix->G : ix->G / 2;  // scan groups (8 or 16 dims)
     // fp32: vdb_scan.hip (variants); split-bf16 (bf16x3, bf16): vdb_scan2.hip
     const bool split_pass = prec != PREC_FP32;
+    // The split pass's 128-query shape (vdb_scan2_kernel.h, q4): short rows whose query block
+    // fits LDS at 128 queries (D <= 128), KP = 128, batches of >= 256: half the query blocks, so
+    // each row range is re-read from L2 by half as many workgroups (C4: 8 -> 4 blocks)
+    const bool q4 = split_pass && !exact_all && KP == 128 && B >= 256 && Gs <= 8 &&
+                    (ix->scan_q4 == 1 || (ix->scan_q4 < 0));
+    const int QB = q4 ? 128 : KP == 256 ? 32 : 64;
+    const int QB_pilot = KP == 256 ? 32 : 64;  // the pilot's own query blocks (pilot2 instantiations)
+    const int Bp = (int)round_up(B, 128);  // whole query super tiles (tiled layout)
+    const int n_qblocks = (B + QB - 1) / QB;
     int variant = split_pass ? 0 : (int)ix->scan_variant;
     if (!split_pass && !scan_variant_ok(prec, variant, Gs)) variant = 0;  // e.g. PX=8 needs Dp % 128 == 0
-    const int64_t step_rows = split_pass ? scan2_rows_per_step() : scan_rows_per_step(prec, variant);
+    const int64_t step_rows = split_pass ? scan2_rows_per_step(q4) : scan_rows_per_step(prec, variant);
     const int64_t n_steps = std::max<int64_t>(1, round_up(N, step_rows) / step_rows);
     // one 4-wave workgroup per CU (1 wave per SIMD, all of its 512 registers):
     // measured faster than two per CU, whose top-k epilogues then overlap (profiles/)
@@ -1152,8 +1164,8 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
             if (n_pilot > 0) {
                 if (split_pass) {
                     HIP_TRY(launch_pilot2(prec, ix->metric, pilot_rank, Xscan, ix->rinit32, md, Qt, Gs, N, B,
-                                          n_qblocks, QB, n_pilot, pslots, gthr, st));
-                    if (!ix->pilot_fused || use_s3) HIP_TRY(launch_pilot_bound(pslots, B, pilot_rank, gthr, st));
+                                          (B + QB_pilot - 1) / QB_pilot, QB_pilot, n_pilot, pslots, gthr, st));
+                    if (!ix->pilot_fused || use_s3 || q4) HIP_TRY(launch_pilot_bound(pslots, B, pilot_rank, gthr, st));
                 }
                 else
                     HIP_TRY(launch_pilot(prec, ix->metric, pilot_rank, Xscan, rowscale, md, Qt, Gs, N, B,
@@ -1163,14 +1175,15 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
             // everything from the pilot to the rerank
             if (timed) HIP_TRY(hipEventRecord(tev[0], st));
             if (use_s3) ix->n_scan3++;
+            if (q4 && !use_s3) ix->n_q4++;
             if (use_s3)
                 HIP_TRY(launch_scan3(prec, ix->metric, Xscan, ix->rinit32, md, Qt, Gs, N, B, n_qb3, steps3, n_wg3, spw3,
                                      gl_s, gl_i, gl_cnt, gl_cap, gthr, st));
             else if (split_pass)
                 HIP_TRY(launch_scan2(prec, ix->metric, KP, Xscan, ix->rinit32, md, Qt, Gs, N, B, n_qblocks, n_steps,
                                      n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, pslots,
-                                     n_pilot > 0 && ix->pilot_fused ? pilot_rank : 0, lockstep, publish, (int)ix->scan_qring,
-                                     st));
+                                     n_pilot > 0 && ix->pilot_fused && !q4 ? pilot_rank : 0, lockstep, publish,
+                                     (int)ix->scan_qring, st, q4));
             else if (priv)
                 HIP_TRY(launch_scan_topk_priv(prec, ix->metric, KP, Xscan, rowscale, md, Qt, Gs, N, B, n_qblocks,
                                               n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, st));

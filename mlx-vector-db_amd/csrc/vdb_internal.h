@@ -103,13 +103,15 @@ hipError_t launch_pilot_bound(uint32_t* pslots, int B, int KP, uint32_t* gthr, h
 // Split-bf16 candidate pass (vdb_scan2.hip; PREC_BF16X3 / PREC_BF16): Xs = the split copy
 // (cosine: of the NORMALISED rows), rinit = -|x|^2/2 per row (L2 accumulator start), Qs =
 // split query tiles (prep_queries), G = 16-dim groups.  Steps of scan2_rows_per_step() rows.
-int scan2_rows_per_step();
+int scan2_rows_per_step(bool q4 = false);
 int scan2_qb(int KP);
+// q4: the 128-query shape of the split pass (query block in LDS: D <= 128; KP = 128; 2 row
+// tiles per wave, steps of scan2_rows_per_step(true) rows; a workgroup keeps 48 per query)
 hipError_t launch_scan2(int prec, int metric, int KP, const float* Xs, const float* rinit, const uint32_t* mask,
                         const float* Qs, int G, int64_t N, int B, int n_qblocks, int64_t n_steps, int n_wg, int spw,
                         float* gl_s, uint32_t* gl_i, uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr,
                         uint32_t* gslots, const uint32_t* pslots, int prank, int lockstep, int publish, int qring,
-                        hipStream_t st);
+                        hipStream_t st, bool q4 = false);
 // The large-batch split pass (vdb_scan3_kernel.h): 256 queries per workgroup (n_qb blocks), row
 // groups shared by the waves through LDS, KW = 32 kept per query and workgroup (drop bound ->
 // gthr).  Steps of scan3_rows_per_step() rows; same inputs / outputs as launch_scan2.

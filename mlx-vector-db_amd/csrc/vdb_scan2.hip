@@ -125,7 +125,7 @@ hipError_t launch_pilot2(int prec, int metric, int KP, const float* Xs, const fl
 // =============================================================================
 // Dispatch
 // =============================================================================
-int scan2_rows_per_step() { return S2_ROWS; }
+int scan2_rows_per_step(bool q4) { return q4 ? 2 * S2_NW * 32 : S2_ROWS; }
 int scan3_rows_per_step() { return S3_ROWS; }
 
 hipError_t launch_scan3(int prec, int metric, const float* Xs, const float* rinit, const uint32_t* mask,
@@ -142,8 +142,9 @@ hipError_t launch_scan2(int prec, int metric, int KP, const float* Xs, const flo
                         const float* Qs, int G, int64_t N, int B, int n_qblocks, int64_t n_steps, int n_wg, int spw,
                         float* gl_s, uint32_t* gl_i, uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr,
                         uint32_t* gslots, const uint32_t* pslots, int prank, int lockstep, int publish, int qring,
-                        hipStream_t st) {
-    const bool ql = scan2_qlds(G, KP);
+                        hipStream_t st, bool q4) {
+    const bool ql = scan2_qlds(G, KP, q4);
+    if (q4 && (!ql || KP != 128)) return hipErrorInvalidValue;
     const bool fs = !lockstep;
     const bool qch = qring && !ql && !fs && G % S2_QCG == 0;
     const bool nt = !ql && n_qblocks == 1;
@@ -152,7 +153,7 @@ hipError_t launch_scan2(int prec, int metric, int KP, const float* Xs, const flo
                                      : nullptr;
     if (!unit || metric < 0 || metric > 1) return hipErrorInvalidValue;
     return unit(KP, Xs, rinit, mask, Qs, G, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr,
-                gslots, pslots, prank, nt, ql, fs, qch, publish, st);
+                gslots, pslots, prank, nt, ql, fs, qch, q4, publish, st);
 }
 
 }  // namespace vdb

@@ -132,15 +132,21 @@ __device__ __forceinline__ uint32_t pilot_slot_rank(uint32_t (&v)[PILOT_E], int 
 // loaded once per workgroup instead of once per wave (lockstep step ends only: one workgroup
 // barrier per chunk, which every wave reaches since all run the same steps).
 constexpr int S2_QCG = 4;
+// RT row tiles per wave (the default S2_RT = 4; the 128-query shape QT = 4 takes 2, so the
+// accumulators stay at 128 registers).  KW < KP: a workgroup keeps only its KW best per query
+// (smaller LDS buffers, which the 128-query blocks need); its compactions then do not raise
+// gthr (a workgroup's KW-th best is no bound of the global KP-th) and at its end it raises gthr
+// to its drop bound (its KW-th best), which keeps the certificate's invariant (rows outside the
+// lists score <= max(a_KP, final gthr)); the finish then certifies as usual.
 template <int PREC, int METRIC, int QT, int PX, int KP, int CAP, bool NT, bool QLDS, bool FLAGSYNC, int GC = 0,
-          bool QCH = false>
+          bool QCH = false, int RT_ = S2_RT, int KW = KP>
 __global__ void __launch_bounds__(64 * S2_NW, 1)
 scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, const uint32_t* __restrict__ mask,
              const float* __restrict__ Qs, int G_arg, int64_t N, int B, int64_t n_steps, int steps_per_wg, int n_qb,
              float* __restrict__ gl_s, uint32_t* __restrict__ gl_i, uint32_t* __restrict__ gl_cnt, int64_t gl_cap,
              uint32_t* __restrict__ gthr, uint32_t* __restrict__ gslots, const uint32_t* __restrict__ pslots,
              int prank, int publish) {
-    constexpr int RT = S2_RT, NW = S2_NW;
+    constexpr int RT = RT_, NW = S2_NW;
     constexpr int QB = 32 * QT;
     constexpr int XPL = Planes<PREC>::XPL, QPL = 2;
     const int G = GC > 0 ? GC : G_arg;
@@ -252,8 +258,10 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
     constexpr int LPQ = 64 / QPW;
     constexpr int SL = KP / LPQ;
     constexpr int SLV = SL / 4 > 0 ? SL / 4 : 1;
+    // publishing needs a lane group of >= NW lanes per query (QB <= 64); the 128-query shape
+    // runs without it (its bound: the pilot's, the compactions' own thresholds)
+    constexpr bool PUB = LPQ >= NW && KW == KP;
     static_assert(SL % 4 == 0, "slots per lane must be whole uint4 loads");
-    static_assert(LPQ >= NW, "a lane group publishes one best per wave");
     const int pq_r = lane % LPQ;
     const int pq = wv + NW * (lane / LPQ);
     const int pqg = qb * QB + pq;
@@ -502,8 +510,8 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
             }
             for (int q = wv; q < QB; q += NW)
                 if (s_cnt[q] >= CAP)
-                    compact_query<KP, CAP>(s_sc + q * CAP, s_ix + q * CAP, s_cnt + q, s_thr + q,
-                                           qb * QB + q < B ? gthr + qb * QB + q : nullptr);
+                    compact_query<KW, CAP>(s_sc + q * CAP, s_ix + q * CAP, s_cnt + q, s_thr + q,
+                                           KW == KP && qb * QB + q < B ? gthr + qb * QB + q : nullptr);
             if (FLAGSYNC && threadIdx.x == 0) *(volatile int*)&s_need = 0;
             __syncthreads();  // B2
             any_left = 0;
@@ -539,7 +547,7 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
 #ifdef VDB_S2_NO_PUBLISH
         if (false) {
 #else
-        if ((publish & 1) && ((sd & (sd - 1)) == 0 || s + 1 == s_end)) {
+        if (PUB && (publish & 1) && ((sd & (sd - 1)) == 0 || s + 1 == s_end)) {
 #endif
             int improved = 0;
             if (pq_r < NW && pqg < B) {
@@ -584,8 +592,8 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
         if (__builtin_amdgcn_readfirstlane(*(volatile int*)&s_done) == NW) break;
         for (int q = wv; q < QB; q += NW)
             if (s_cnt[q] >= CAP)
-                compact_query<KP, CAP>(s_sc + q * CAP, s_ix + q * CAP, s_cnt + q, s_thr + q,
-                                       qb * QB + q < B ? gthr + qb * QB + q : nullptr);
+                compact_query<KW, CAP>(s_sc + q * CAP, s_ix + q * CAP, s_cnt + q, s_thr + q,
+                                       KW == KP && qb * QB + q < B ? gthr + qb * QB + q : nullptr);
         if (threadIdx.x == 0) *(volatile int*)&s_need = 0;
         __syncthreads();  // B2
     }
@@ -593,7 +601,15 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
     // ---- flush: entries above the shared bound -> global per-query lists ----
     __syncthreads();
     uint32_t tkey = 0;
-    if (lane < QPW && qb * QB + wv + NW * lane < B) tkey = max(gthr[qb * QB + wv + NW * lane], s_sh[wv + NW * lane]);
+    if (lane < QPW && qb * QB + wv + NW * lane < B) {
+        const int q = wv + NW * lane;
+        uint32_t dk = 0;
+        if (KW < KP && s_begin < s_end) {  // this workgroup's drop bound (its KW-th best, once compacted)
+            dk = s_thr[q] == -INFINITY ? 0u : order_key(s_thr[q]);
+            if (dk) atomicMax(gthr + qb * QB + q, dk);
+        }
+        tkey = max(max(gthr[qb * QB + q], s_sh[q]), dk);
+    }
     append_flush<CAP>(s_sc, s_ix, s_cnt, wv, NW, QPW, qb * QB, B, tkey, gl_s, gl_i, gl_cnt, gl_cap);
 #ifdef VDB_STAMP
     {
@@ -618,15 +634,19 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
 // ---- launch templates ----
 inline int scan2_qb(int KP) { return KP == 256 ? 32 : 64; }
 
-// The query block goes to LDS when it is small (C4: 64 queries x 128 dims = 32 KiB).
-inline bool scan2_qlds(int G16, int KP) { return (size_t)G16 * 2 * (scan2_qb(KP) / 32) * 1024 <= 32 * 1024; }
+// The query block goes to LDS when it is small (C4: 64 queries x 128 dims = 32 KiB; the
+// 128-query shape: 64 KiB).
+inline bool scan2_qlds(int G16, int KP, bool q4 = false) {
+    return (size_t)G16 * 2 * (q4 ? 4 : scan2_qb(KP) / 32) * 1024 <= (q4 ? 64 : 32) * 1024;
+}
 
-template <int P, int M, int QT, int PX, int KP, int CAP, bool NT, bool QL, bool FS, int GC, bool QC = false>
+template <int P, int M, int QT, int PX, int KP, int CAP, bool NT, bool QL, bool FS, int GC, bool QC = false,
+          int RT_ = S2_RT, int KW = KP>
 static hipError_t scan2_launch_g(const float* Xs, const float* rinit, const uint32_t* mask, const float* Qs, int G,
                                  int64_t N, int B, int n_qblocks, int64_t n_steps, int n_wg, int spw, float* gl_s,
                                  uint32_t* gl_i, uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr, uint32_t* gslots,
                                  const uint32_t* pslots, int prank, int publish, hipStream_t st) {
-    auto k = scan2_kernel<P, M, QT, PX, KP, CAP, NT, QL, FS, GC, QC>;
+    auto k = scan2_kernel<P, M, QT, PX, KP, CAP, NT, QL, FS, GC, QC, RT_, KW>;
     const size_t lds = QL ? (size_t)G * 2 * QT * 1024 : QC ? (size_t)2 * S2_QCG * 2 * QT * 1024 : 0;
     if (QL || QC) {
         // the dynamic part (query block) plus the static top-k buffers must fit the 160 KiB of a
@@ -648,20 +668,20 @@ static hipError_t scan2_launch_g(const float* Xs, const float* rinit, const uint
 
 // query block in LDS (short rows): the common short row (D = 128 -> 8 groups) gets its own
 // instantiation with the group count built in
-template <int P, int M, int QT, int PX, int KP, int CAP, bool NT, bool QL, bool FS>
+template <int P, int M, int QT, int PX, int KP, int CAP, bool NT, bool QL, bool FS, int RT_ = S2_RT, int KW = KP>
 static hipError_t scan2_launch(const float* Xs, const float* rinit, const uint32_t* mask, const float* Qs, int G,
                                int64_t N, int B, int n_qblocks, int64_t n_steps, int n_wg, int spw, float* gl_s,
                                uint32_t* gl_i, uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr, uint32_t* gslots,
                                const uint32_t* pslots, int prank, int publish, hipStream_t st) {
     if constexpr (QL) {
         if (G == 8)
-            return scan2_launch_g<P, M, QT, PX, KP, CAP, NT, QL, FS, 8>(Xs, rinit, mask, Qs, G, N, B, n_qblocks, n_steps,
-                                                                        n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr,
-                                                                        gslots, pslots, prank, publish, st);
+            return scan2_launch_g<P, M, QT, PX, KP, CAP, NT, QL, FS, 8, false, RT_, KW>(
+                Xs, rinit, mask, Qs, G, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots,
+                pslots, prank, publish, st);
     }
-    return scan2_launch_g<P, M, QT, PX, KP, CAP, NT, QL, FS, 0>(Xs, rinit, mask, Qs, G, N, B, n_qblocks, n_steps, n_wg,
-                                                                spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, pslots,
-                                                                prank, publish, st);
+    return scan2_launch_g<P, M, QT, PX, KP, CAP, NT, QL, FS, 0, false, RT_, KW>(
+        Xs, rinit, mask, Qs, G, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, pslots,
+        prank, publish, st);
 }
 
 // The argument list of one (precision, metric) unit's launcher (launch_scan2 dispatches).
@@ -669,12 +689,16 @@ static hipError_t scan2_launch(const float* Xs, const float* rinit, const uint32
     int KP, const float *Xs, const float *rinit, const uint32_t *mask, const float *Qs, int G, int64_t N, int B,    \
         int n_qblocks, int64_t n_steps, int n_wg, int spw, float *gl_s, uint32_t *gl_i, uint32_t *gl_cnt,          \
         int64_t gl_cap, uint32_t *gthr, uint32_t *gslots, const uint32_t *pslots, int prank, bool nt, bool ql,     \
-        bool fs, bool qch, int publish, hipStream_t st
+        bool fs, bool qch, bool q4, int publish, hipStream_t st
 #define S2_ARGS Xs, rinit, mask, Qs, G, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, \
                 pslots, prank, publish, st
 #define S2_ONE(P, M, KPV, QTV, PXV, CAPV, NTV, QLV, FSV)                 \
-    if (KP == KPV && nt == NTV && ql == QLV && fs == FSV && !qch)       \
+    if (KP == KPV && nt == NTV && ql == QLV && fs == FSV && !qch && !q4) \
         return scan2_launch<P, M, QTV, PXV, KPV, CAPV, NTV, QLV, FSV>(S2_ARGS);
+// the 128-query shape (query block in LDS, 2 row tiles per wave, KW = 48 kept of KP = 128)
+#define S2_ONE4(P, M, PXV, FSV)                                               \
+    if (KP == 128 && ql && fs == FSV && !qch && q4)                           \
+        return scan2_launch<P, M, 4, PXV, 128, 64, false, true, FSV, 2, 48>(S2_ARGS);
 // query ring variants (global query operand, lockstep step ends)
 #define S2_ONEQ(P, M, KPV, QTV, PXV, CAPV, NTV)                                      \
     if (KP == KPV && nt == NTV && !ql && !fs && qch)                                \
@@ -693,7 +717,8 @@ static hipError_t scan2_launch(const float* Xs, const float* rinit, const uint32
     S2_KP(P, M, PXV, false, false, false) S2_KP(P, M, PXV, true, false, false)     \
     S2_KP(P, M, PXL, false, true, false) S2_KP(P, M, PXL, false, true, true)       \
     S2_KP(P, M, PXV, false, false, true) S2_KP(P, M, PXV, true, false, true)       \
-    S2_KPQ(P, M, PXV, false) S2_KPQ(P, M, PXV, true)
+    S2_KPQ(P, M, PXV, false) S2_KPQ(P, M, PXV, true)                              \
+    S2_ONE4(P, M, PXL, false) S2_ONE4(P, M, PXL, true)
 #ifndef VDB_S2_QLDS_PX
 #define VDB_S2_QLDS_PX 2
 #endif

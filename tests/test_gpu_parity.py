@@ -564,3 +564,47 @@ def test_scan3_large_batch_pass(vdb, metric, precision):
     np.testing.assert_array_equal(i, ei)
     np.testing.assert_array_equal(kk, ek)
     ix.close()
+
+
+@pytest.mark.parametrize("metric", ["cosine", "euclidean"])
+def test_scan2_q4_shape(vdb, metric):
+    """The split pass's 128-query shape (knob "scan_q4" = 1; D <= 128, KP = 128, B >= 256):
+    query block of 128 in LDS, 2 row tiles per wave, 48 kept per query and workgroup with the
+    drop bound raising gthr at the end.  Bit-exact vs the oracle for bf16 (k = 10) and bf16x3
+    (k = 100), compile-time (D = 128) and runtime (D = 64) group counts, ragged batches, a mask,
+    and clustered rows that put more than 48 of a query's top 100 into one workgroup."""
+    rng = np.random.default_rng(67)
+    for D, N in ((128, 120_000), (64, 50_003)):
+        V = rng.random((N, D), dtype=np.float32)
+        Q = rng.random((520, D), dtype=np.float32)
+        Q[3], Q[519] = V[N - 1], V[777]
+        for prec, k in (("bf16", 10), ("bf16x3", 100)):
+            ix = vdb.NativeIndex(D, metric, precision=prec)
+            ix.set_param("scan_q4", 1)
+            ix.add(V)
+            for B in (520, 256):
+                s, i, kk = ix.search(Q[:B], k, with_keys=True)
+                es, ei, ek = ref_cpu.exact_search(Q[:B], V, k, metric)
+                np.testing.assert_array_equal(i, ei)
+                np.testing.assert_array_equal(kk, ek)
+            mask = rng.random(N) < 0.4
+            bits = np.zeros(((N + 31) // 32) * 32, bool)
+            bits[:N] = mask
+            words = np.packbits(bits, bitorder="little").view("<u4").astype(np.uint32)
+            s, i, kk = ix.search(Q[:300], k, row_mask=words, with_keys=True)
+            es, ei, ek = ref_cpu.exact_search(Q[:300], V, k, metric, row_mask=mask)
+            np.testing.assert_array_equal(i, ei)
+            np.testing.assert_array_equal(kk, ek)
+            assert ix.stat("searches_q4") == 3
+            ix.close()
+    V = rng.random((60_000, 128), dtype=np.float32)
+    V[30_000:30_070] = (V[9] + 1e-3 * rng.random((70, 128))).astype(np.float32)
+    Q = np.concatenate([V[9:10], rng.random((299, 128), dtype=np.float32)])
+    ix = vdb.NativeIndex(128, metric, precision="bf16x3")
+    ix.set_param("scan_q4", 1)
+    ix.add(V)
+    s, i, kk = ix.search(Q, 100, with_keys=True)
+    es, ei, ek = ref_cpu.exact_search(Q, V, 100, metric)
+    np.testing.assert_array_equal(i, ei)
+    np.testing.assert_array_equal(kk, ek)
+    ix.close()
