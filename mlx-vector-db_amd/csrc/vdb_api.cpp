@@ -157,7 +157,7 @@ struct vdb_index {
     int64_t gate_div = 1;         // gated exact fallback: n_cu / gate_div row ranges, one query slot each when > 1
     int64_t finish_split = 1;  // workgroups per query in the finish kernel (tuning)
     int64_t scan3 = 0;         // large-batch candidate pass: -1 auto (B >= 128), 0 off, 1 always (vdb_scan3_kernel.h)
-    int64_t scan_q4 = 0;       // split pass 128-query shape (D <= 128, KP = 128, B >= 256): -1 auto, 0 off, 1 on
+    int64_t scan_q4 = -1;      // split pass 128-query shape (D <= 128, KP = 128, B >= 256): -1 auto, 0 off, 1 on
     // stats
     std::atomic<int64_t> n_searches{0}, n_queries{0}, n_fallback{0}, n_overflow{0}, n_repass{0}, n_scan3{0}, n_q4{0};
     std::atomic<int64_t> n_by_prec[3] = {{0}, {0}, {0}};  // candidate passes per PREC_* (VDB_PREC_AUTO's choices)
