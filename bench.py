@@ -1,26 +1,31 @@
 #!/usr/bin/env python3
 """Headline benchmark: brute-force cosine / L2 top-k on MI355X (BASELINE.json).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c1|c3|c4] [--scaling weak|strong]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1|c2|c3|c4|c5|c6] [--scaling weak|strong]
 
 One "step" = one batch of queries searched against the whole corpus (fused
 MFMA candidate scan + exact fp64 rerank; queries, corpus and outputs resident
-in HBM).  N=1 runs BASELINE.json configs[1] (C2: 1M x 768 fp32 cosine, batch
-64, top-10).  N>1 (torchrun, one rank per GPU, RCCL) row-shards the corpus over
-the ranks (service/sharded.py): each rank searches its shard, the per-shard
-top-k lists (fp64 keys + global row ids) are all-gathered over xGMI and merged
-on device, bit-identical to one GPU.  Default "weak" scaling keeps the work per
-GPU fixed: the global batch is B x N queries against the same corpus (each rank:
-B x N queries x N_rows/N rows); "strong" keeps the batch at B.
+in HBM).  The default run measures BASELINE.json's metric, both halves:
+  * the line itself: configs[1] (C2: 1M x 768 cosine top-10, batch 64) -- at
+    N > 1 row-sharded with the batch per GPU fixed ("weak": global batch 64 N);
+  * "metric_workload_10m_x_128": the metric's "10M x 128D @8 GPU" workload (c6:
+    cosine top-10, batch 64, row-sharded with the global batch fixed at 64).
+N>1 (torchrun, one rank per GPU, RCCL; or --gpus N alone, which spawns the
+ranks) row-shards the corpus over the ranks (service/sharded.py): each rank
+searches its shard, the per-shard top-k lists (fp64 keys + global row ids) are
+all-gathered over xGMI and merged on device, bit-identical to one GPU.
+--config c4 / c6 default to "strong" scaling (BASELINE's fixed global batch),
+the others to "weak".
 
 Throughput (`value`): the K timed batches are queued back to back on the stream
 (device-memory searches return without a host wait) between two synchronises;
 latency (`p50_ms`) comes from a separate loop that waits for every batch.
 Rank 0 prints one JSON line: QPS (whole job), p50 batch latency, the roofline
 of the dominant kernel (the scan kernel, HIP-event timed inside the library on
-the stream it runs on) and, at N=1, the CPU baseline: the reference's batched
-path (performance/mlx_optimized.py:217-248) restated in numpy
-(oracle/ref_cpu.py), timed on this host on one bounded sample.
+the stream it runs on; named against the implementation's own work and against
+SURVEY.md §8(d)'s) and, at N=1, the CPU baseline: the reference's paths restated
+in numpy (oracle/ref_cpu.py), timed on this host on a bounded sample, and for
+c1/c2 the store-API serving numbers (batch-1 p50, 4-thread query QPS).
 """
 import argparse
 import glob
@@ -382,7 +387,10 @@ def main():
     # profiles/r02s_ab/s15/); the timed region is still ~30 ms
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default=None, choices=sorted(CONFIGS),
+                    help="default: c2 (BASELINE.json configs[1]) plus the metric's 8-GPU workload c6 as a sub-record")
+    ap.add_argument("--no-metric-workload", action="store_true",
+                    help="default run: skip the c6 sub-record (the metric's 10M x 128 workload)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-serving", action="store_true",
                     help="c1/c2 at N=1: skip the store-API serving numbers (batch-1 p50, 4-thread QPS)")
@@ -397,6 +405,8 @@ def main():
                     help="candidate-pass step end: 1 lockstep barrier, 2 flag-gated rounds (tuning; default by D)")
     ap.add_argument("--gate-div", type=int, default=None, help="gated fallback: n_cu / d workgroups (tuning)")
     ap.add_argument("--scan-qring", type=int, default=None, help="1: query operand through an LDS ring (tuning)")
+    ap.add_argument("--scan-qlds", type=int, default=None, help="0: query block never in LDS (tuning)")
+    ap.add_argument("--scan-q4", type=int, default=None, help="128-query shape: -1 auto, 0 off, 1 on (tuning)")
     ap.add_argument("--scan-realign", type=int, default=None,
                     help="flag-gated step ends: a workgroup barrier every n steps (tuning)")
     ap.add_argument("--dir-bound", type=int, default=None,
@@ -443,14 +453,39 @@ def main():
     if args.config == "c5":
         return main_graph(args, world, rank, local, dev)
 
-    N, D, B, k, metric, desc = CONFIGS[args.config]
-    N = args.rows or N
-    scaling = args.scaling or DEFAULT_SCALING.get(args.config, "weak")
+    cfg = args.config or "c2"
+    rec = bench_brute(cfg, args, world, rank, local, dev, primary=True)
+    if args.config is None and not args.no_metric_workload:
+        # the default run also measures the second half of BASELINE.json's metric, "10M x 128D @8
+        # GPU" (c6: cosine top-10, batch 64, row-sharded over the ranks with the batch fixed), on
+        # the same ranks: the driver's N = 1, 2, 4, 8 series then carries both workloads
+        sub = bench_brute("c6", args, world, rank, local, dev, primary=False)
+        if rank == 0:
+            rec["metric_workload_10m_x_128"] = {
+                k_: sub[k_] for k_ in ("value", "unit", "n_gpus", "steps", "ms_per_step", "p50_ms", "scaling", "dtype",
+                                       "config", "fallback_queries_timed")}
+            rec["metric_workload_10m_x_128"]["roofline"] = {
+                k_: sub["roofline"][k_] for k_ in ("bound", "achieved", "peak", "unit", "frac", "avg_launch_ms",
+                                                   "precision", "basis", "survey_8d")}
+    if rank == 0:
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def bench_brute(cfg, args, world, rank, local, dev, primary=True):
+    """One brute-force config: this rank's shard, the timed loop, the record (rank 0; None
+    elsewhere).  primary=False: the compact secondary line (no CPU baseline / serving)."""
+    rec = None
+    N, D, B, k, metric, desc = CONFIGS[cfg]
+    N = (args.rows if primary else None) or N
+    scaling = args.scaling or DEFAULT_SCALING.get(cfg, "weak")
     lo, hi = shard_bounds(N, world, rank)
     n_local = hi - lo
 
     # ---- data: this rank's shard of the corpus, replicated queries -------------------
-    keep_host = world == 1 and rank == 0 and not args.no_cpu_baseline
+    keep_host = primary and world == 1 and rank == 0 and not args.no_cpu_baseline
     ix = _vdb.NativeIndex(D, metric, local, precision=args.precision)
     if args.scan_variant is not None:
         ix.set_param("scan_variant" if args.precision == "fp32" else "scan_variant_bf16x3", args.scan_variant)
@@ -466,6 +501,10 @@ def main():
         ix.set_param("gate_div", args.gate_div)
     if args.scan_qring is not None:
         ix.set_param("scan_qring", args.scan_qring)
+    if args.scan_qlds is not None:
+        ix.set_param("scan_qlds", args.scan_qlds)
+    if args.scan_q4 is not None:
+        ix.set_param("scan_q4", args.scan_q4)
     if args.dir_bound is not None:
         ix.set_param("dir_bound", args.dir_bound)
     if args.scan_publish is not None:
@@ -600,9 +639,9 @@ def main():
         roof["basis"] = (f"implementation: {elem} B per corpus element read once + queries; "
                          f"{ {'fp32': 1, 'bf16x3': 3, 'bf16': 2}[prec]} MFMA product(s) per fp32 product "
                          f"({'fp32' if prec == 'fp32' else 'bf16'} peak)")
-        s_bound = SURVEY_BOUND.get(args.config, "mfma_fp32")
+        s_bound = SURVEY_BOUND.get(cfg, "mfma_fp32")
         s_flops = 2.0 * Bg * n_local * D
-        s_bytes = n_local * D * (2 if args.config == "c3" else 4) + 4 * n_local + 4 * Bg * D + 12 * Bg * k
+        s_bytes = n_local * D * (2 if cfg == "c3" else 4) + 4 * n_local + 4 * Bg * D + 12 * Bg * k
         if s_bound == "hbm":
             s_ach = s_bytes / (scan_ms * 1e-3) / 1e9
             survey = {"bound": "hbm", "work": s_bytes, "work_unit": "B", "achieved": s_ach, "peak": HBM_PEAK_GBS,
@@ -615,13 +654,13 @@ def main():
                           "frac > 1 = the fp32-equivalent work done in split-bf16 MFMAs with an exact fp64 rerank")
         traffic = None
         traffic_src = None
-        cands = [args.pmc_json] if args.pmc_json else sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc.json")))
+        cands = [args.pmc_json] if (args.pmc_json and primary) else sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc.json")))
         for path in reversed(cands):
             try:
                 pm = json.load(open(path))
             except (OSError, ValueError):
                 continue
-            if (pm.get("config") == args.config and pm.get("n_gpus") == world and "hbm_bytes_per_launch" in pm
+            if (pm.get("config") == cfg and pm.get("n_gpus") == world and "hbm_bytes_per_launch" in pm
                     and pm.get("precision", "fp32") == prec):
                 traffic = pm["hbm_bytes_per_launch"]
                 traffic_src = os.path.relpath(path, ROOT)
@@ -641,7 +680,7 @@ def main():
             "dtype": {"fp32": "f32", "bf16x3": "f32 (bf16x3 split MFMA candidates, fp64 exact rerank)",
                       "bf16": "f32 (bf16 corpus x split query MFMA candidates, fp64 exact rerank)"}[prec],
             "data": "synthetic uniform [0,1) fp32 (numpy PCG64, corpus seed 0 per 65536-row chunk, queries seed 1)",
-            "config": {"workload": f"{args.config}: {desc}", "n_rows": N, "dim": D, "global_batch": Bg,
+            "config": {"workload": f"{cfg}: {desc}", "n_rows": N, "dim": D, "global_batch": Bg,
                        "batch_per_gpu_equiv": B, "k": k,
                        "metric": metric, "parallelism": f"row-shard x{world}" if world > 1 else "single GPU",
                        "rows_per_gpu": n_local},
@@ -661,13 +700,13 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             V = np.concatenate(host_parts) if len(host_parts) > 1 else host_parts[0]
             del host_parts
-            if args.config in ("c1", "c2") and not args.no_serving:
+            if cfg in ("c1", "c2") and not args.no_serving:
                 rec["serving"] = serving_stats(V, metric, k, local)
             rec["cpu_baseline"] = cpu_baseline(V, Q, k, metric)
-        print(json.dumps(rec), flush=True)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+    ix.close()
+    return rec
+
+
 
 
 if __name__ == "__main__":

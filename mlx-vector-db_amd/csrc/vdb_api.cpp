@@ -157,6 +157,7 @@ struct vdb_index {
     int64_t gate_div = 1;         // gated exact fallback: n_cu / gate_div row ranges, one query slot each when > 1
     int64_t finish_split = 1;  // workgroups per query in the finish kernel (tuning)
     int64_t scan3 = 0;         // large-batch candidate pass: -1 auto (B >= 128), 0 off, 1 always (vdb_scan3_kernel.h)
+    int64_t scan_qlds = -1;    // split pass: query block in LDS when it fits (-1 auto), 0 never
     int64_t scan_q4 = -1;      // split pass 128-query shape (D <= 128, KP = 128, B >= 256): -1 auto, 0 off, 1 on
     // stats
     std::atomic<int64_t> n_searches{0}, n_queries{0}, n_fallback{0}, n_overflow{0}, n_repass{0}, n_scan3{0}, n_q4{0};
@@ -598,6 +599,9 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
     } else if (n == "finish_split") {
         if (value < 1 || value > 8) return set_error(VDB_ERR_INVALID, "finish_split must be in [1, 8]");
         ix->finish_split = value;
+    } else if (n == "scan_qlds") {
+        if (value < -1 || value > 0) return set_error(VDB_ERR_INVALID, "scan_qlds must be -1 or 0");
+        ix->scan_qlds = value;
     } else if (n == "scan_q4") {
         if (value < -1 || value > 1) return set_error(VDB_ERR_INVALID, "scan_q4 must be -1, 0 or 1");
         ix->scan_q4 = value;
@@ -1183,7 +1187,7 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
                 HIP_TRY(launch_scan2(prec, ix->metric, KP, Xscan, ix->rinit32, md, Qt, Gs, N, B, n_qblocks, n_steps,
                                      n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, pslots,
                                      n_pilot > 0 && ix->pilot_fused && !q4 ? pilot_rank : 0, lockstep, publish,
-                                     (int)ix->scan_qring, st, q4));
+                                     (int)ix->scan_qring, st, q4, (int)ix->scan_qlds));
             else if (priv)
                 HIP_TRY(launch_scan_topk_priv(prec, ix->metric, KP, Xscan, rowscale, md, Qt, Gs, N, B, n_qblocks,
                                               n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, st));

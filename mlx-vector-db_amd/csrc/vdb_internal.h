@@ -111,7 +111,7 @@ hipError_t launch_scan2(int prec, int metric, int KP, const float* Xs, const flo
                         const float* Qs, int G, int64_t N, int B, int n_qblocks, int64_t n_steps, int n_wg, int spw,
                         float* gl_s, uint32_t* gl_i, uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr,
                         uint32_t* gslots, const uint32_t* pslots, int prank, int lockstep, int publish, int qring,
-                        hipStream_t st, bool q4 = false);
+                        hipStream_t st, bool q4 = false, int qlds = -1);
 // The large-batch split pass (vdb_scan3_kernel.h): 256 queries per workgroup (n_qb blocks), row
 // groups shared by the waves through LDS, KW = 32 kept per query and workgroup (drop bound ->
 // gthr).  Steps of scan3_rows_per_step() rows; same inputs / outputs as launch_scan2.
