@@ -697,7 +697,7 @@ def bench_brute(cfg, args, world, rank, local, dev, primary=True):
             "fallback_queries_timed": fb_timed,  # (auto's bf16 probe falls back in warm-up at C3 / C4)
             "fallback_list_overflow": overflow,
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if keep_host:
             V = np.concatenate(host_parts) if len(host_parts) > 1 else host_parts[0]
             del host_parts
             if cfg in ("c1", "c2") and not args.no_serving:

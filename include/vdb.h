@@ -114,8 +114,10 @@ int32_t vdb_index_reserve(vdb_index* idx, int64_t rows);
  * "scan_variant" / "scan_variant_bf16x3" (0..2, kernel tiling variants),
  * "scan_sync" (candidate-pass step end: 0 auto by dimension, 1 per-step barrier,
  * 2 flag-gated compaction rounds; results identical, speed differs),
- * "scan_publish" (split pass slot publishing: -1 auto = on with >= 16 steps per
- * workgroup, 0 off, 1 on), "scan_qring" (split pass, lockstep step ends: 1 = the
+ * "scan_publish" (split pass slot publishing: -1 auto = off (round 3 measurement), 0 off,
+ * 1 on), "scan_q4" (split pass 128-query shape for D <= 128, KP = 128, B >= 256: -1 auto = on,
+ * 0 off, 1 on where it applies), "scan_qlds" (-1 auto: query block in LDS when it fits, 0 never),
+ * "scan3" (large-batch shape, vdb_scan3_kernel.h: 0 default off, 1 on, -1 auto), "scan_qring" (split pass, lockstep step ends: 1 = the
  * query operand through a per-workgroup LDS ring; start value from the environment
  * variable VDB_SCAN_QRING, default 0), "gate_div" (1..64: the device-gated exact
  * fallback runs on n_cu / gate_div row ranges, one query slot each when > 1; start value

@@ -150,7 +150,7 @@ struct vdb_index {
     // bound kernel.  Measured (profiles/r02_ab, C2): the prologue costs the scan ~25 us (bf16)
     // / ~30 us (bf16x3) against ~5 us for the kernel, so 0 is the default.
     int64_t pilot_fused = 0;
-    int64_t scan_publish = -1;    // split pass slot publishing: -1 auto (>= 16 steps per workgroup), 0 off, 1 on
+    int64_t scan_publish = -1;    // split pass slot publishing: -1 auto (= off since round 3), 0 off, 1 on
     bool no_dir_bound = false;    // diagnostics: PREC_BF16 certificate with Cauchy-Schwarz only
     int64_t scan_realign = 0;     // flag-gated step ends: a workgroup barrier every n steps (0 none)
     int64_t scan_qring = 0;       // split pass, global query operand: query chunks through an LDS ring
@@ -1013,11 +1013,13 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     // groups per step, the epilogue ~half of it) gain from dropping the per-step workgroup barrier
     // (C4 scan 7.58 -> 6.22 ms); long steps lose (C2 0.57 -> 0.65 ms, C3 2.62 -> 2.90 ms), measured.
     const int lockstep = ix->scan_sync == 0 ? (ix->Dp > 128) : ix->scan_sync == 1;
-    // Slot publishing (shared bound from the workgroups' own bests, vdb_scan2.hip) pays off
-    // over many steps (C4: 610 per workgroup); with few (C2: 8) its global round trips at
-    // steps 1, 2, 4, 8 cost more than the pilot's bound leaves to gain (measured: stamps,
-    // profiles/r02_ab/).
-    const int publish = (ix->scan_publish >= 0 ? (int)ix->scan_publish : spw >= 16) | (int)(ix->scan_realign << 8);
+    // Slot publishing (shared bound from the workgroups' own bests, vdb_scan2.hip): round 2 found it
+    // paying off over many steps (C4: 610 per workgroup) and not over few (C2: 8, profiles/r02_ab/).
+    // Measured again in round 3 (profiles/r03_ab/publish): off is as fast or faster everywhere --
+    // C6 (10M x 128, one 64-query block, 77 steps per workgroup: 256 workgroups' same-address slot
+    // atomics for the same 64 queries) 0.92 -> 0.47 ms, C2 0.30 -> 0.29, C3 / C4 equal -- so auto
+    // is off (the knob stays for A/B)
+    const int publish = (ix->scan_publish >= 0 ? (int)ix->scan_publish : 0) | (int)(ix->scan_realign << 8);
     // The large-batch pass (vdb_scan3_kernel.h): 256 queries per workgroup sharing each row
     // group through LDS.  Auto: B >= 128 and enough workgroups per query block that no
     // workgroup is likely to hold more than its KW = 32 best of a query's top k.
