@@ -69,6 +69,7 @@ SURVEY_BOUND = {"c1": "hbm", "c2": "mfma_fp32", "c3": "hbm", "c4": "mfma_fp32", 
 GRAPH_M, GRAPH_EF = 16, 128
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md, Peak FP32 (matrix)
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md, Peak BF16 MFMA, dense
+I8_MFMA_PEAK_TOPS = 5000.0      # MI355X_MICROARCH.md, I8 MFMA: 2x BF16 per clock (2x the K), dense
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md, HBM3E peak (spec)
 CHUNK_ROWS = 1 << 16
 
@@ -397,7 +398,7 @@ def main():
     ap.add_argument("--scaling", default=None, choices=["weak", "strong"],
                     help="N>1: weak = global batch B*N (fixed work per GPU), strong = global batch B "
                          "(default: strong for c4 / c6, whose BASELINE batch is sharded, weak otherwise)")
-    ap.add_argument("--precision", default="auto", choices=["auto", "bf16x3", "bf16", "fp32"],
+    ap.add_argument("--precision", default="auto", choices=["auto", "bf16x3", "bf16", "fp32", "i8", "i8x3"],
                     help="candidate-pass arithmetic (results identical; DESIGN.md §3)")
     ap.add_argument("--scan-variant", type=int, default=None, help="candidate-pass kernel variant (tuning)")
     ap.add_argument("--n-wg", type=int, default=None, help="candidate-pass workgroups (tuning)")
@@ -558,7 +559,7 @@ def bench_brute(cfg, args, world, rank, local, dev, primary=True):
     ev_in_loop = bool(args.timing) and n_str == 1
     ix.set_param("timing", int(ev_in_loop))
     scan0, pipe0, n0 = ix.stat("scan_ns"), ix.stat("pipeline_ns"), ix.stat("timed_searches")
-    by_prec0 = {p: ix.stat(f"searches_{p}") for p in ("fp32", "bf16x3", "bf16")}
+    by_prec0 = {p: ix.stat(f"searches_{p}") for p in ("fp32", "bf16x3", "bf16", "i8", "i8x3")}
     fb0 = ix.stat("fallback_queries")
     if world > 1:
         dist.barrier()
@@ -611,21 +612,23 @@ def bench_brute(cfg, args, world, rank, local, dev, primary=True):
         # Two rooflines of the scan kernel, each named:
         # (1) "implementation" (the top-level fields): the work the kernel's own arithmetic must do
         #     per launch -- every corpus row read once at the element size of the candidate copy it
-        #     scans (bf16: the hi plane, 2 B; bf16x3 / fp32: 4 B), the L2 row start values, the
-        #     queries; its own MFMA count (fp32: 2BND on the FP32 peak; bf16 2x and bf16x3 3x the
-        #     products on the bf16 peak) -- bound by whichever floor is longer;
+        #     scans (i8: the hi plane, 1 B; bf16 / i8x3: 2 B; bf16x3 / fp32: 4 B), the L2 row start
+        #     values, the queries; its own MFMA count (fp32: 2BND on the FP32 peak; bf16 2x and
+        #     bf16x3 3x the products on the bf16 peak; i8 2x and i8x3 3x on the int8 peak) -- bound
+        #     by whichever floor is longer;
         # (2) "survey_8d": SURVEY.md §8(d)'s algorithmic work for the config (fp32 arithmetic:
         #     2BND flops, 4 B per element; C3 names the bf16 corpus, 2 B) on the roofline §8(d) calls
         #     binding.  frac > 1 there means the kernel does that fp32-equivalent work in cheaper
         #     MFMAs (split bf16) than §8(d)'s FP32-MFMA roofline assumes; exactness comes from the
         #     fp64 rerank + certificate.
         Dp = (D + 63) // 64 * 64
-        elem = 2 if prec == "bf16" else 4
-        hbm_bytes = n_local * Dp * elem + (n_local * 4 if metric == "euclidean" else 0) + Bg * Dp * 4
-        if prec == "fp32":
-            mfma_flops, mfma_peak = 2.0 * Bg * n_local * D, FP32_MFMA_PEAK_TFLOPS
-        else:
-            mfma_flops, mfma_peak = (3 if prec == "bf16x3" else 2) * 2.0 * Bg * n_local * D, BF16_MFMA_PEAK_TFLOPS
+        elem = {"i8": 1, "i8x3": 2, "bf16": 2}.get(prec, 4)
+        q_elem = 2 if prec in ("i8", "i8x3") else 4  # query tiles (int8: two 1-byte planes)
+        hbm_bytes = n_local * Dp * elem + (n_local * 4 if metric == "euclidean" else 0) + Bg * Dp * q_elem
+        n_mfma = {"fp32": 1, "bf16x3": 3, "bf16": 2, "i8": 2, "i8x3": 3}[prec]
+        mfma_flops = n_mfma * 2.0 * Bg * n_local * D
+        mfma_peak = {"fp32": FP32_MFMA_PEAK_TFLOPS, "bf16x3": BF16_MFMA_PEAK_TFLOPS, "bf16": BF16_MFMA_PEAK_TFLOPS,
+                     "i8": I8_MFMA_PEAK_TOPS, "i8x3": I8_MFMA_PEAK_TOPS}[prec]
         t_hbm = hbm_bytes / (HBM_PEAK_GBS * 1e9)
         t_mfma = mfma_flops / (mfma_peak * 1e12)
         achieved_gbs = hbm_bytes / (scan_ms * 1e-3) / 1e9
@@ -637,8 +640,8 @@ def bench_brute(cfg, args, world, rank, local, dev, primary=True):
             roof = {"bound": "mfma", "achieved": achieved_tf, "peak": mfma_peak, "unit": "TFLOP/s",
                     "frac": achieved_tf / mfma_peak}
         roof["basis"] = (f"implementation: {elem} B per corpus element read once + queries; "
-                         f"{ {'fp32': 1, 'bf16x3': 3, 'bf16': 2}[prec]} MFMA product(s) per fp32 product "
-                         f"({'fp32' if prec == 'fp32' else 'bf16'} peak)")
+                         f"{n_mfma} MFMA product(s) per fp32 product "
+                         f"({ {'fp32': 'fp32', 'i8': 'int8', 'i8x3': 'int8'}.get(prec, 'bf16')} peak)")
         s_bound = SURVEY_BOUND.get(cfg, "mfma_fp32")
         s_flops = 2.0 * Bg * n_local * D
         s_bytes = n_local * D * (2 if cfg == "c3" else 4) + 4 * n_local + 4 * Bg * D + 12 * Bg * k
@@ -651,7 +654,7 @@ def bench_brute(cfg, args, world, rank, local, dev, primary=True):
             survey = {"bound": "mfma_fp32", "work": s_flops, "work_unit": "FLOP", "achieved": s_ach,
                       "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": s_ach / FP32_MFMA_PEAK_TFLOPS}
         survey["note"] = ("SURVEY.md §8(d) work per launch (fp32: 2BND flops, 4 B/element; c3: bf16 corpus); "
-                          "frac > 1 = the fp32-equivalent work done in split-bf16 MFMAs with an exact fp64 rerank")
+                          "frac > 1 = the fp32-equivalent work done in split-bf16 / int8 MFMAs with an exact fp64 rerank")
         traffic = None
         traffic_src = None
         cands = [args.pmc_json] if (args.pmc_json and primary) else sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc.json")))
@@ -678,13 +681,16 @@ def bench_brute(cfg, args, world, rank, local, dev, primary=True):
             "scaling": scaling if world > 1 else "weak",
             "vs_baseline": None,
             "dtype": {"fp32": "f32", "bf16x3": "f32 (bf16x3 split MFMA candidates, fp64 exact rerank)",
-                      "bf16": "f32 (bf16 corpus x split query MFMA candidates, fp64 exact rerank)"}[prec],
+                      "bf16": "f32 (bf16 corpus x split query MFMA candidates, fp64 exact rerank)",
+                      "i8": "f32 (int8 centred corpus x 16-bit query integer-MFMA candidates, fp64 exact rerank)",
+                      "i8x3": "f32 (16-bit fixed-point corpus x query integer-MFMA candidates, fp64 exact rerank)"}[prec],
             "data": "synthetic uniform [0,1) fp32 (numpy PCG64, corpus seed 0 per 65536-row chunk, queries seed 1)",
             "config": {"workload": f"{cfg}: {desc}", "n_rows": N, "dim": D, "global_batch": Bg,
                        "batch_per_gpu_equiv": B, "k": k,
                        "metric": metric, "parallelism": f"row-shard x{world}" if world > 1 else "single GPU",
                        "rows_per_gpu": n_local},
-            "roofline": dict(roof, traffic=traffic, kernel="scan2_kernel" if prec != "fp32" else "scan_topk",
+            "roofline": dict(roof, traffic=traffic,
+                             kernel={"fp32": "scan_topk", "i8": "scan8_kernel", "i8x3": "scan8_kernel"}.get(prec, "scan2_kernel"),
                              survey_8d=survey, precision=prec,
                              precision_requested=args.precision, searches_by_precision=by_prec,
                              traffic_source=traffic_src, algorithmic_bytes=hbm_bytes, algorithmic_flops=mfma_flops,

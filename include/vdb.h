@@ -79,17 +79,30 @@ enum { VDB_MEM_HOST = 0, VDB_MEM_DEVICE = 1 };
  *                    d the normalised mean row of the first add, M the largest
  *                    |d.(x - bf16(x))|, c = q.d, so it is wider
  *                    and takes a larger candidate margin.
- *   VDB_PREC_AUTO    (default) BF16X3 for k > 16 (BF16 would need 256 candidates per query
- *                    there, a slower pass); otherwise BF16, per batch.  A host-memory search re-passes its
- *                    uncertified queries (at most 1/8 of the batch, at most 64) in BF16X3
- *                    as one gathered sub-search and stays BF16; more than that reruns the
- *                    batch in BF16X3 and starts a HOLD: the next 16 searches run BF16X3,
+ *   VDB_PREC_I8      an int8 copy of the CENTRED rows z = y - mu (y the scored row, mu the
+ *                    mean row of the first add), 16-bit fixed point in two planes
+ *                    z ~ s_x (xh + xl/256); the query 16-bit fixed point per batch.  I8
+ *                    reads the hi plane only (1 byte per element, a quarter of the fp32
+ *                    copy): x.q ~ s_x s_q (xh.qh + xh.ql/256) on v_mfma_i32_32x32x32_i8
+ *                    (exact integer sums, twice the K of a bf16 MFMA per cycle); the
+ *                    certificate adds the measured row rounding (as BF16: Cauchy-Schwarz or
+ *                    along d) and each query's own rounding (vdb_scan8_kernel.h).
+ *   VDB_PREC_I8X3    both planes (2 bytes per element): xh.qh + (xh.ql + xl.qh)/256, an
+ *                    error bound of bf16x3's order at half its bytes and MFMA cycles.
+ *   VDB_PREC_AUTO    (default) the x3 precision for k > 16 (the one-plane ones would need 256
+ *                    candidates per query there, a slower pass); otherwise the one-plane one,
+ *                    per batch: I8 / I8X3 on the int8 copy (knob "auto_int8" = 1, the default;
+ *                    start value from VDB_AUTO_I8), BF16 / BF16X3 on the split copy (0).
+ *                    A host-memory search re-passes its
+ *                    uncertified queries (at most 1/8 of the batch, at most 64) in the x3 one
+ *                    as one gathered sub-search and stays one-plane; more than that reruns the
+ *                    batch in x3 and starts a HOLD: the next 16 searches run x3,
  *                    doubling per failed BF16 probe up to 2048 (reset by 64 certified BF16
  *                    searches, or when the rows change).  A device-memory search sees its
  *                    fallback counts a search or more late (no host sync): its flagged
  *                    queries take the device-gated exact path and the next search starts
  *                    the hold.  Stats "repass_queries", "auto_hold". */
-enum { VDB_PREC_FP32 = 0, VDB_PREC_BF16X3 = 1, VDB_PREC_BF16 = 2, VDB_PREC_AUTO = 3 };
+enum { VDB_PREC_FP32 = 0, VDB_PREC_BF16X3 = 1, VDB_PREC_BF16 = 2, VDB_PREC_AUTO = 3, VDB_PREC_I8 = 4, VDB_PREC_I8X3 = 5 };
 
 typedef struct vdb_index vdb_index;
 
@@ -127,8 +140,8 @@ int32_t vdb_index_reserve(vdb_index* idx, int64_t rows);
  * "timing" (0/1: HIP events around the candidate pass; stats "scan_ns",
  * "pipeline_ns", "timed_searches").  Stats also: "searches", "queries",
  * "fallback_queries", "overflow_queries", "capacity", "count", "device_bytes", "precision",
- * "searches_fp32" / "searches_bf16x3" / "searches_bf16" (candidate passes run in each; with
- * VDB_PREC_AUTO these show its choices). */
+ * "searches_fp32" / "searches_bf16x3" / "searches_bf16" / "searches_i8" / "searches_i8x3"
+ * (candidate passes run in each; with VDB_PREC_AUTO these show its choices), "auto_int8". */
 int32_t vdb_index_set_param(vdb_index* idx, const char* name, int64_t value);
 int32_t vdb_index_get_stat(const vdb_index* idx, const char* name, int64_t* value);
 

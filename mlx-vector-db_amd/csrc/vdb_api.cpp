@@ -119,6 +119,18 @@ struct vdb_index {
     float* d_dir = nullptr;  // [Dp], zero padded
     bool dir_set = false;
     double xres_dir = 0.0;
+    // The int8 pass (PREC_I8 / PREC_I8X3, vdb_scan8.hip): the candidate copy holds z = y - mu,
+    // mu [Dp] the mean of the first add's candidate rows (set with dir, frozen until clear()),
+    // quantised with step sx = 1.25 max |z| / 127 (over those rows; later rows past the range
+    // clip, which the residual statistics then show); d_i8 [0..6) the running row statistics of
+    // quant_rows (fp64 bits), [6] max |z| (float bits) at setup; i8st = their host copies.
+    float* d_mu = nullptr;
+    float sx = 0.0f;
+    int64_t dir_rows = 0;  // rows dir / mu / sx were derived from (re-derived as the index doubles, up to kDirRows)
+    unsigned long long* d_i8 = nullptr;
+    double i8st[6] = {0, 0, 0, 0, 0, 0};
+    // VDB_PREC_AUTO's candidate copy: the int8 one (I8 / I8X3) when set, else the split-bf16 one
+    bool auto_i8 = true;
     hipStream_t stream = nullptr;
     int n_cu = 256;
     // knobs
@@ -161,7 +173,7 @@ struct vdb_index {
     int64_t scan_q4 = -1;      // split pass 128-query shape (D <= 128, KP = 128, B >= 256): -1 auto, 0 off, 1 on
     // stats
     std::atomic<int64_t> n_searches{0}, n_queries{0}, n_fallback{0}, n_overflow{0}, n_repass{0}, n_scan3{0}, n_q4{0};
-    std::atomic<int64_t> n_by_prec[3] = {{0}, {0}, {0}};  // candidate passes per PREC_* (VDB_PREC_AUTO's choices)
+    std::atomic<int64_t> n_by_prec[N_PREC] = {{0}, {0}, {0}, {0}, {0}};  // candidate passes per PREC_* (VDB_PREC_AUTO's choices)
     std::atomic<int64_t> scan_ns{0}, pipe_ns{0}, n_timed{0};
     unsigned long long* d_totals = nullptr;  // device: flagged / overflowed / flagged-in-bf16 queries of device-gated searches
     std::shared_mutex mu;  // add/clear/reserve exclusive; search shared
@@ -190,11 +202,34 @@ void free_workspace_memory(Workspace* w) {
 
 int wait_idle(vdb_index* ix);
 
-// The candidate copy of rows [row0, row0 + n) from the row-major rows (whole row tiles).
+// The candidate copy a precision setting uses: fp32 tiles, split-bf16 tiles or the int8 copy.
+enum CopyClass { kCopyFp32 = 0, kCopySplit = 1, kCopyInt8 = 2 };
+int copy_class(int64_t precision, bool auto_i8) {
+    if (precision == VDB_PREC_FP32) return kCopyFp32;
+    if (precision == VDB_PREC_I8 || precision == VDB_PREC_I8X3 || (precision == VDB_PREC_AUTO && auto_i8))
+        return kCopyInt8;
+    return kCopySplit;
+}
+
+// The candidate copy of rows [row0, row0 + n) from the row-major rows (whole row tiles; the int8
+// copy row by row, its statistics into d_i8).
 hipError_t build_candidate_rows(const vdb_index* ix, const float* X, const float* inv32, int64_t row0, int64_t n,
                                 float* Xs, hipStream_t st) {
-    if (ix->precision == VDB_PREC_FP32) return launch_tile_rows(X, ix->G, row0, n, Xs, st);
-    return launch_split_rows(X, ix->G, row0, n, ix->metric == VDB_METRIC_COSINE ? inv32 : nullptr, Xs, st);
+    const float* inv = ix->metric == VDB_METRIC_COSINE ? inv32 : nullptr;
+    switch (copy_class(ix->precision, ix->auto_i8)) {
+        case kCopyFp32: return launch_tile_rows(X, ix->G, row0, n, Xs, st);
+        case kCopyInt8: return launch_quant_rows(X, inv, ix->d_mu, ix->d_dir, ix->sx, row0, n, ix->G, Xs, ix->d_i8, st);
+        default: return launch_split_rows(X, ix->G, row0, n, inv, Xs, st);
+    }
+}
+
+// Host copies of the int8 copy's row statistics (after the kernels that update them).
+hipError_t read_i8_stats(vdb_index* ix, hipStream_t st) {
+    unsigned long long b[6];
+    hipError_t e = hipMemcpyAsync(b, ix->d_i8, sizeof(b), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e == hipSuccess) std::memcpy(ix->i8st, b, sizeof(b));
+    return e;
 }
 
 int ensure_capacity(vdb_index* ix, int64_t rows) {
@@ -495,9 +530,12 @@ int32_t vdb_index_create(int32_t dim, int32_t metric, int32_t device, vdb_index*
     // start value of the scan3 parameter (A/B runs of whole suites): -1 auto, 0 off, 1 always
     if (const char* s3 = std::getenv("VDB_SCAN3")) ix->scan3 = std::min(1, std::max(-1, std::atoi(s3)));
     if (const char* q4 = std::getenv("VDB_SCAN_Q4")) ix->scan_q4 = std::min(1, std::max(-1, std::atoi(q4)));
+    if (const char* a8 = std::getenv("VDB_AUTO_I8")) ix->auto_i8 = std::atoi(a8) != 0;
     hipError_t e = hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMalloc(&ix->d_xmax, 64);
     if (e == hipSuccess) e = hipMemset(ix->d_xmax, 0, 64);
+    if (e == hipSuccess) e = hipMalloc(&ix->d_i8, 64);
+    if (e == hipSuccess) e = hipMemset(ix->d_i8, 0, 64);
     if (e != hipSuccess) {
         delete ix;
         return set_error(VDB_ERR_HIP, "index setup failed: %s", hipGetErrorString(e));
@@ -536,6 +574,8 @@ int32_t vdb_index_destroy(vdb_index* ix) {
     if (ix->rinit32) (void)hipFree(ix->rinit32);
     if (ix->d_xmax) (void)hipFree(ix->d_xmax);
     if (ix->d_dir) (void)hipFree(ix->d_dir);
+    if (ix->d_mu) (void)hipFree(ix->d_mu);
+    if (ix->d_i8) (void)hipFree(ix->d_i8);
     if (ix->d_totals) (void)hipFree(ix->d_totals);
     if (ix->h_totals) (void)hipHostFree(ix->h_totals);
     for (auto& kv : ix->uses) (void)hipEventDestroy(kv.second);
@@ -556,20 +596,36 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
     if (!ix || !name) return set_error(VDB_ERR_INVALID, "NULL argument");
     std::string n(name);
     if (n == "precision") {
-        if (value != VDB_PREC_FP32 && value != VDB_PREC_BF16X3 && value != VDB_PREC_BF16 && value != VDB_PREC_AUTO)
+        if (value != VDB_PREC_FP32 && value != VDB_PREC_BF16X3 && value != VDB_PREC_BF16 && value != VDB_PREC_AUTO &&
+            value != VDB_PREC_I8 && value != VDB_PREC_I8X3)
             return set_error(VDB_ERR_INVALID,
-                             "precision must be %d (fp32), %d (bf16x3), %d (bf16) or %d (auto), got %lld",
-                             VDB_PREC_FP32, VDB_PREC_BF16X3, VDB_PREC_BF16, VDB_PREC_AUTO, (long long)value);
+                             "precision must be %d (fp32), %d (bf16x3), %d (bf16), %d (auto), %d (i8) or %d (i8x3), "
+                             "got %lld",
+                             VDB_PREC_FP32, VDB_PREC_BF16X3, VDB_PREC_BF16, VDB_PREC_AUTO, VDB_PREC_I8, VDB_PREC_I8X3,
+                             (long long)value);
         HIP_TRY(hipSetDevice(ix->device));
         std::unique_lock<std::shared_mutex> g(ix->mu);
         if (value == ix->precision) return VDB_OK;
         const int wr = wait_idle(ix);  // queued searches read the candidate copy
         if (wr) return wr;
-        const bool rebuild = (value == VDB_PREC_FP32) != (ix->precision == VDB_PREC_FP32);
+        const bool rebuild = copy_class(value, ix->auto_i8) != copy_class(ix->precision, ix->auto_i8);
         ix->precision = value;
-        if (rebuild && ix->Xs && ix->count > 0) {  // fp32 tiles <-> split tiles
+        if (rebuild && ix->Xs && ix->count > 0) {  // fp32 tiles / split tiles / int8 copy
             HIP_TRY(build_candidate_rows(ix, ix->X, ix->inv32, 0, ix->count, ix->Xs, ix->stream));
-            HIP_TRY(hipStreamSynchronize(ix->stream));
+            HIP_TRY(read_i8_stats(ix, ix->stream));
+        }
+    } else if (n == "auto_int8") {  // VDB_PREC_AUTO's candidate copy: 1 int8, 0 split-bf16
+        HIP_TRY(hipSetDevice(ix->device));
+        std::unique_lock<std::shared_mutex> g(ix->mu);
+        const bool v = value != 0;
+        if (v == ix->auto_i8) return VDB_OK;
+        const int wr = wait_idle(ix);
+        if (wr) return wr;
+        const bool rebuild = copy_class(ix->precision, v) != copy_class(ix->precision, ix->auto_i8);
+        ix->auto_i8 = v;
+        if (rebuild && ix->Xs && ix->count > 0) {
+            HIP_TRY(build_candidate_rows(ix, ix->X, ix->inv32, 0, ix->count, ix->Xs, ix->stream));
+            HIP_TRY(read_i8_stats(ix, ix->stream));
         }
     } else if (n == "margin") {
         ix->margin = value;
@@ -666,6 +722,9 @@ int32_t vdb_index_get_stat(const vdb_index* cix, const char* name, int64_t* valu
     else if (n == "searches_fp32") *value = ix->n_by_prec[PREC_FP32].load();
     else if (n == "searches_bf16x3") *value = ix->n_by_prec[PREC_BF16X3].load();
     else if (n == "searches_bf16") *value = ix->n_by_prec[PREC_BF16].load();
+    else if (n == "searches_i8") *value = ix->n_by_prec[PREC_I8].load();
+    else if (n == "searches_i8x3") *value = ix->n_by_prec[PREC_I8X3].load();
+    else if (n == "auto_int8") *value = ix->auto_i8 ? 1 : 0;
     else if (n == "device_bytes")
         *value = (int64_t)(ix->cap_rows / 32) * ix->G * BLOCK_FLOATS * 4 * 2 + ix->cap_rows * 20;
     else return set_error(VDB_ERR_INVALID, "unknown stat '%s'", name);
@@ -677,31 +736,52 @@ int32_t vdb_index_get_stat(const vdb_index* cix, const char* name, int64_t* valu
 // index); then the maximum of |dir . (y - bf16(y))| over these rows (d_xmax[3]).
 constexpr int64_t kDirRows = 65536;
 
+// On the first add also the int8 copy's centring row mu (the mean of the same rows) and its
+// quantisation step sx = 1.25 max |y - mu| / 127 over them (vdb_scan8.hip): this runs before
+// the candidate copy of the first rows is built.
+static hipError_t setup_direction(vdb_index* ix, int64_t row0, int64_t n, hipStream_t st) {
+    if (ix->dir_set) return hipSuccess;
+    const float* inv = ix->metric == VDB_METRIC_COSINE ? ix->inv32 : nullptr;
+    const int D = ix->dim;
+    const int64_t m = std::min(n, kDirRows);
+    hipError_t e = hipSuccess;
+    if (!ix->d_dir) e = hipMalloc(&ix->d_dir, (size_t)ix->Dp * sizeof(float));
+    if (e == hipSuccess && !ix->d_mu) e = hipMalloc(&ix->d_mu, (size_t)ix->Dp * sizeof(float));
+    double* sums = nullptr;
+    if (e == hipSuccess) e = hipMalloc(&sums, (size_t)D * sizeof(double));
+    if (e == hipSuccess) e = hipMemsetAsync(sums, 0, (size_t)D * sizeof(double), st);
+    if (e == hipSuccess) e = launch_dir_sum(ix->X, inv, row0, m, D, ix->G, sums, st);
+    std::vector<double> h(D);
+    if (e == hipSuccess) e = hipMemcpyAsync(h.data(), sums, (size_t)D * sizeof(double), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (sums) (void)hipFree(sums);
+    if (e != hipSuccess) return e;
+    double nn = 0.0;
+    for (double v : h) nn += v * v;
+    std::vector<float> dir(ix->Dp, 0.0f), mu(ix->Dp, 0.0f);
+    if (nn > 0.0 && std::isfinite(nn))
+        for (int d = 0; d < D; ++d) dir[d] = (float)(h[d] / std::sqrt(nn));
+    for (int d = 0; d < D; ++d) mu[d] = (float)(h[d] / (double)std::max<int64_t>(m, 1));
+    e = hipMemcpyAsync(ix->d_dir, dir.data(), (size_t)ix->Dp * sizeof(float), hipMemcpyHostToDevice, st);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(ix->d_mu, mu.data(), (size_t)ix->Dp * sizeof(float), hipMemcpyHostToDevice, st);
+    uint32_t zb = 0;
+    uint32_t* dz = reinterpret_cast<uint32_t*>(ix->d_i8 + 6);
+    if (e == hipSuccess) e = hipMemsetAsync(dz, 0, sizeof(uint32_t), st);
+    if (e == hipSuccess) e = launch_zmax(ix->X, inv, ix->d_mu, row0, m, D, ix->G, dz, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(&zb, dz, sizeof(zb), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);  // dir / mu are stack buffers
+    if (e != hipSuccess) return e;
+    float zmax = 0.0f;
+    std::memcpy(&zmax, &zb, sizeof(zmax));
+    ix->sx = zmax > 0.0f && std::isfinite(zmax) ? 1.25f * zmax / 127.0f : 1.0f;
+    ix->dir_rows = m;
+    ix->dir_set = true;
+    return hipSuccess;
+}
+
 static hipError_t residual_direction(vdb_index* ix, int64_t row0, int64_t n, hipStream_t st) {
     const float* inv = ix->metric == VDB_METRIC_COSINE ? ix->inv32 : nullptr;
-    if (!ix->dir_set) {
-        const int D = ix->dim;
-        hipError_t e = hipSuccess;
-        if (!ix->d_dir) e = hipMalloc(&ix->d_dir, (size_t)ix->Dp * sizeof(float));
-        double* sums = nullptr;
-        if (e == hipSuccess) e = hipMalloc(&sums, (size_t)D * sizeof(double));
-        if (e == hipSuccess) e = hipMemsetAsync(sums, 0, (size_t)D * sizeof(double), st);
-        if (e == hipSuccess) e = launch_dir_sum(ix->X, inv, row0, std::min(n, kDirRows), D, ix->G, sums, st);
-        std::vector<double> h(D);
-        if (e == hipSuccess) e = hipMemcpyAsync(h.data(), sums, (size_t)D * sizeof(double), hipMemcpyDeviceToHost, st);
-        if (e == hipSuccess) e = hipStreamSynchronize(st);
-        if (sums) (void)hipFree(sums);
-        if (e != hipSuccess) return e;
-        double nn = 0.0;
-        for (double v : h) nn += v * v;
-        std::vector<float> dir(ix->Dp, 0.0f);
-        if (nn > 0.0 && std::isfinite(nn))
-            for (int d = 0; d < D; ++d) dir[d] = (float)(h[d] / std::sqrt(nn));
-        e = hipMemcpyAsync(ix->d_dir, dir.data(), (size_t)ix->Dp * sizeof(float), hipMemcpyHostToDevice, st);
-        if (e == hipSuccess) e = hipStreamSynchronize(st);  // dir is a stack buffer
-        if (e != hipSuccess) return e;
-        ix->dir_set = true;
-    }
     return launch_resid_dir(ix->X, inv, row0, n, ix->dim, ix->G, ix->d_dir, ix->d_xmax + 3, st);
 }
 
@@ -739,6 +819,7 @@ int32_t vdb_index_add(vdb_index* ix, const float* vectors, int64_t n, int32_t me
             if (e == hipSuccess)
                 e = launch_pack_rows(staging, m, D, ix->G, ix->X, ix->count + r, ix->nrm64, ix->inv32, ix->sq32,
                                      ix->rinit32, ix->metric == VDB_METRIC_COSINE, ix->d_xmax, ix->d_nonfinite, st);
+            if (e == hipSuccess) e = setup_direction(ix, ix->count + r, m, st);
             if (e == hipSuccess) e = build_candidate_rows(ix, ix->X, ix->inv32, ix->count + r, m, ix->Xs, st);
             if (e == hipSuccess) e = residual_direction(ix, ix->count + r, m, st);
             if (e == hipSuccess) e = hipStreamSynchronize(st);  // staging reuse
@@ -749,6 +830,7 @@ int32_t vdb_index_add(vdb_index* ix, const float* vectors, int64_t n, int32_t me
         } else {
             HIP_TRY(launch_pack_rows(src, m, D, ix->G, ix->X, ix->count + r, ix->nrm64, ix->inv32, ix->sq32,
                                      ix->rinit32, ix->metric == VDB_METRIC_COSINE, ix->d_xmax, ix->d_nonfinite, st));
+            HIP_TRY(setup_direction(ix, ix->count + r, m, st));
             HIP_TRY(build_candidate_rows(ix, ix->X, ix->inv32, ix->count + r, m, ix->Xs, st));
             HIP_TRY(residual_direction(ix, ix->count + r, m, st));
         }
@@ -758,12 +840,35 @@ int32_t vdb_index_add(vdb_index* ix, const float* vectors, int64_t n, int32_t me
     unsigned long long xb[4] = {0, 0, 0, 0};
     HIP_TRY(hipMemcpyAsync(&nonfinite, ix->d_nonfinite, sizeof(int), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(xb, ix->d_xmax, sizeof(xb), hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
+    HIP_TRY(read_i8_stats(ix, st));
     if (nonfinite) {
-        // rows past `count` are never read; the next add overwrites them
-        const int64_t used_tiles = round_up(ix->count + n, 32) / 32;
-        (void)used_tiles;
+        // rows past `count` are never read; the next add overwrites them.  A rejected first add
+        // leaves no direction / centring row behind (they would hold its non-finite values).
+        if (ix->count == 0) {
+            ix->dir_set = false;
+            ix->dir_rows = 0;
+            HIP_TRY(hipMemsetAsync(ix->d_xmax, 0, 32, st));
+            HIP_TRY(hipMemsetAsync(ix->d_i8, 0, 64, st));
+            HIP_TRY(hipStreamSynchronize(st));
+            std::memset(ix->i8st, 0, sizeof(ix->i8st));
+        }
         return set_error(VDB_ERR_NONFINITE, "%d row(s) contain NaN or Inf; nothing was added", nonfinite);
+    }
+    // Direction, centring row and quantisation step from a few rows (a store filled one REST add
+    // at a time) would stay poor for good: while they came from fewer than kDirRows rows, they
+    // are derived again from all rows each time the index doubles, and the int8 copy and the
+    // residual maxima along dir are rebuilt (O(kDirRows) work in total).
+    if (ix->dir_rows < kDirRows && ix->count + n >= 2 * ix->dir_rows) {
+        const int64_t all = ix->count + n;
+        ix->dir_set = false;
+        HIP_TRY(hipMemsetAsync(ix->d_xmax + 3, 0, 8, st));
+        HIP_TRY(hipMemsetAsync(ix->d_i8, 0, 64, st));
+        HIP_TRY(setup_direction(ix, 0, all, st));
+        if (copy_class(ix->precision, ix->auto_i8) == kCopyInt8)
+            HIP_TRY(build_candidate_rows(ix, ix->X, ix->inv32, 0, all, ix->Xs, st));
+        HIP_TRY(residual_direction(ix, 0, all, st));
+        HIP_TRY(hipMemcpyAsync(xb, ix->d_xmax, sizeof(xb), hipMemcpyDeviceToHost, st));
+        HIP_TRY(read_i8_stats(ix, st));
     }
     double xm[4];
     std::memcpy(xm, xb, sizeof(xm));
@@ -800,13 +905,16 @@ int32_t vdb_index_clear(vdb_index* ix) {
                                    ix->stream));
     }
     HIP_TRY(hipMemsetAsync(ix->d_xmax, 0, 64, ix->stream));
+    HIP_TRY(hipMemsetAsync(ix->d_i8, 0, 64, ix->stream));
     HIP_TRY(hipStreamSynchronize(ix->stream));
+    std::memset(ix->i8st, 0, sizeof(ix->i8st));
     ix->count = 0;
     ix->auto_hold = 0;
     ix->auto_fails = 0;
     ix->xmax = 0.0;
     ix->xres_rel = ix->xres_abs = 0.0;
     ix->dir_set = false;  // the next add picks a new direction (xres_dir's bits were cleared above)
+    ix->dir_rows = 0;
     ix->xres_dir = 0.0;
     return VDB_OK;
 }
@@ -968,28 +1076,35 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     // bf16x3 (C4, k = 100: 13 vs 3.9 ms, profiles/r02s_ab/s4_c4_str2.json), and in device memory
     // its uncertified queries cost the exact path
     const bool auto_b16 = k <= kAutoBf16MaxK;
+    // AUTO on the int8 copy: I8 / I8X3 where the split copy would run BF16 / BF16X3 (same rules)
+    const bool a8 = ix->auto_i8;
+    const bool auto_x3 = auto_prec && (opt.force_b3 || !auto_b16 || (approx && auto_take_hold(ix)));
     const int prec_req = !ix->Xs ? PREC_FP32
                          : ix->precision == VDB_PREC_BF16X3 ? PREC_BF16X3
                          : ix->precision == VDB_PREC_BF16 ? PREC_BF16
-                         : auto_prec ? (opt.force_b3 || !auto_b16 || (approx && auto_take_hold(ix)) ? PREC_BF16X3
-                                                                                                : PREC_BF16)
+                         : ix->precision == VDB_PREC_I8X3 ? PREC_I8X3
+                         : ix->precision == VDB_PREC_I8 ? PREC_I8
+                         : auto_prec ? (auto_x3 ? (a8 ? PREC_I8X3 : PREC_BF16X3) : (a8 ? PREC_I8 : PREC_BF16))
                                      : PREC_FP32;
     if (approx) ix->n_by_prec[prec_req]++;
+    // the "one plane" precisions (a wide certificate: KP = 128 for small k) and their re-pass
+    const bool one_plane = prec_req == PREC_BF16 || prec_req == PREC_I8;
 
     int margin_def = std::max(16, k / 4);
-    if (prec_req == PREC_BF16X3 && D >= 1024) margin_def = std::max(margin_def, 48);
+    if ((prec_req == PREC_BF16X3 || prec_req == PREC_I8X3) && D >= 1024) margin_def = std::max(margin_def, 48);
     // bf16 (hi plane only): eps ~ the rows' bf16 residual (~1.5e-3 relative on uniform data),
     // ~30x bf16x3's: 1M x 768 uniform needs KP = 128 for k = 10 (KP = 64 left 26% of the
     // queries uncertified; KP = 128: none of 2560)
-    if (prec_req == PREC_BF16) margin_def = std::max(16, std::min(std::max(112, k / 2), 256 - k));
+    if (one_plane) margin_def = std::max(16, std::min(std::max(112, k / 2), 256 - k));
     const int margin = ix->margin >= 0 ? (int)ix->margin : margin_def;
     int KP = std::max(32, next_pow2(k + margin));
     const bool exact_all = ix->force_exact || k > kMaxApproxK || KP > 256;
     if (KP > 256) KP = 256;
     const int prec = prec_req;
-    const int Gs = prec == PREC_FP32 ? ix->G : ix->G / 2;  // scan groups (8 or 16 dims)
+    const bool i8_pass = prec_is_i8(prec);  // vdb_scan8.hip
+    const int Gs = prec == PREC_FP32 ? ix->G : i8_pass ? ix->G / 4 : ix->G / 2;  // scan groups (8, 32 or 16 dims)
     // fp32: vdb_scan.hip (variants); split-bf16 (bf16x3, bf16): vdb_scan2.hip
-    const bool split_pass = prec != PREC_FP32;
+    const bool split_pass = prec == PREC_BF16X3 || prec == PREC_BF16;
     // The split pass's 128-query shape (vdb_scan2_kernel.h, q4): short rows whose query block
     // fits LDS at 128 queries (D <= 128), KP = 128, batches of >= 256: half the query blocks, so
     // each row range is re-read from L2 by half as many workgroups (C4: 8 -> 4 blocks)
@@ -999,9 +1114,10 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     const int QB_pilot = KP == 256 ? 32 : 64;  // the pilot's own query blocks (pilot2 instantiations)
     const int Bp = (int)round_up(B, 128);  // whole query super tiles (tiled layout)
     const int n_qblocks = (B + QB - 1) / QB;
-    int variant = split_pass ? 0 : (int)ix->scan_variant;
-    if (!split_pass && !scan_variant_ok(prec, variant, Gs)) variant = 0;  // e.g. PX=8 needs Dp % 128 == 0
-    const int64_t step_rows = split_pass ? scan2_rows_per_step(q4) : scan_rows_per_step(prec, variant);
+    int variant = split_pass || i8_pass ? 0 : (int)ix->scan_variant;
+    if (!split_pass && !i8_pass && !scan_variant_ok(prec, variant, Gs)) variant = 0;  // e.g. PX=8 needs Dp % 128 == 0
+    const int64_t step_rows = i8_pass ? scan8_rows_per_step(prec, ix->metric)
+                              : split_pass ? scan2_rows_per_step(q4) : scan_rows_per_step(prec, variant);
     const int64_t n_steps = std::max<int64_t>(1, round_up(N, step_rows) / step_rows);
     // one 4-wave workgroup per CU (1 wave per SIMD, all of its 512 registers):
     // measured faster than two per CU, whose top-k epilogues then overlap (profiles/)
@@ -1064,7 +1180,8 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     bytes += fin_split > 1 ? (size_t)B * fin_split * (KP_MAX * 16 + 4) + 1024 : 0;
     bytes += (size_t)Bp * 4 + 256;                          // shared thresholds
     bytes += (size_t)Bp * (KP_MAX + PILOT_SLOTS) * 4 + 256;  // shared threshold slots + pilot slots
-    const bool priv = !exact_all && !split_pass && scan_priv(prec, variant, KP);
+    bytes += (size_t)Bp * 12 + 1024;                          // int8 pass: qmax, lsl, qerr [Bp]; qscal
+    const bool priv = !exact_all && !split_pass && !i8_pass && scan_priv(prec, variant, KP);
     // global per-query candidate lists: at most 512 entries per workgroup and query
     // (the largest LDS buffer of any variant; 4 x 64 for the wave-private one)
     const int64_t gl_cap = exact_all ? 0 : use_s3 ? (int64_t)((n_wg3 + 7) / 8 * 8) * 64
@@ -1124,6 +1241,10 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     uint32_t* fx_ck = fin_split > 1 ? c.take<uint32_t>((size_t)B * fin_split * KP_MAX) : nullptr;
     uint32_t* fx_cr = fin_split > 1 ? c.take<uint32_t>((size_t)B * fin_split * KP_MAX) : nullptr;
     int* fx_n = fin_split > 1 ? c.take<int>((size_t)B * fin_split) : nullptr;
+    float* q8max = c.take<float>(Bp);
+    float* q8lsl = c.take<float>(Bp);
+    float* q8err = c.take<float>(Bp);
+    float* q8scal = c.take<float>(64);
 
     const float* Qd = queries;
     const uint32_t* md = row_mask;
@@ -1148,7 +1269,16 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
         HIP_TRY(launch_empty_results((int64_t)B * k, out_s, out_i, out_k, st));
     } else {
         HIP_TRY(launch_prep_queries(Qd, B, Bp, D, ix->G, ix->metric, prec == PREC_FP32 ? Qt : nullptr,
-                                    prec == PREC_FP32 ? nullptr : Qt, qn64, flags, gthr, gslots, gl_cnt, done, st));
+                                    split_pass ? Qt : nullptr, qn64, flags, gthr, gslots, gl_cnt, done, st,
+                                    i8_pass ? q8max : nullptr));
+        if (i8_pass && !exact_all) {
+            Int8Consts c8;
+            c8.sx = ix->sx;
+            c8.zmax_h = ix->i8st[4];
+            c8.xl_max = ix->i8st[5];
+            c8.rmax_half = 0.5 * ix->xmax * ix->xmax;
+            HIP_TRY(launch_prep8(Qd, qn64, q8max, B, Bp, D, Gs, ix->metric, prec, c8, Qt, q8lsl, q8err, q8scal, st));
+        }
         int n_flag = 0;
         if (!exact_all) {
             const bool timed = ix->timing != 0;
@@ -1168,7 +1298,11 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
             const float* rowscale = ix->metric == 0 ? ix->inv32 : ix->sq32;
             const float* Xscan = ix->Xs;  // fp32 or split tiles, per the precision class
             if (n_pilot > 0) {
-                if (split_pass) {
+                if (i8_pass) {
+                    HIP_TRY(launch_pilot8(prec, ix->metric, Xscan, ix->rinit32, md, Qt, q8scal, Gs, N, B,
+                                          (B + QB_pilot - 1) / QB_pilot, QB_pilot, n_pilot, pslots, st));
+                    HIP_TRY(launch_pilot_bound(pslots, B, pilot_rank, gthr, st));
+                } else if (split_pass) {
                     HIP_TRY(launch_pilot2(prec, ix->metric, pilot_rank, Xscan, ix->rinit32, md, Qt, Gs, N, B,
                                           (B + QB_pilot - 1) / QB_pilot, QB_pilot, n_pilot, pslots, gthr, st));
                     if (!ix->pilot_fused || use_s3 || q4) HIP_TRY(launch_pilot_bound(pslots, B, pilot_rank, gthr, st));
@@ -1182,7 +1316,11 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
             if (timed) HIP_TRY(hipEventRecord(tev[0], st));
             if (use_s3) ix->n_scan3++;
             if (q4 && !use_s3) ix->n_q4++;
-            if (use_s3)
+            if (i8_pass)
+                HIP_TRY(launch_scan8(prec, ix->metric, KP, Xscan, ix->rinit32, md, Qt, q8lsl, q8scal, Gs, N, B,
+                                     n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, lockstep,
+                                     (int)ix->scan_qlds, st));
+            else if (use_s3)
                 HIP_TRY(launch_scan3(prec, ix->metric, Xscan, ix->rinit32, md, Qt, Gs, N, B, n_qb3, steps3, n_wg3, spw3,
                                      gl_s, gl_i, gl_cnt, gl_cap, gthr, st));
             else if (split_pass)
@@ -1207,7 +1345,9 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
             //   bf16:   2D additions + the query split (2^-16) + the same 8, plus xres: the
             //           corpus rounding |q.(x - bf16(x))| <= |q| |x - bf16(x)|, bounded by the
             //           largest row residual measured at ingest (relative for cosine)
-            fa.eps_rel = prec == PREC_FP32 ? 1.01 * (double)(D + 8) * std::ldexp(1.0, -24)
+            // int8: exact integer sums; 8 roundings (normalisation, centring, the fp32 combination)
+            fa.eps_rel = i8_pass ? 1.01 * 8.0 * std::ldexp(1.0, -24)
+                         : prec == PREC_FP32 ? 1.01 * (double)(D + 8) * std::ldexp(1.0, -24)
                          : prec == PREC_BF16X3
                              ? 1.01 * (3.0 * D * std::ldexp(1.0, -23) + 3.1 * std::ldexp(1.0, -16) +
                                        8.0 * std::ldexp(1.0, -24))
@@ -1217,6 +1357,13 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
             fa.xres = prec != PREC_BF16 ? 0.0 : 1.01 * (ix->metric == 0 ? ix->xres_rel : ix->xres_abs);
             fa.dir = prec == PREC_BF16 && ix->dir_set && !ix->no_dir_bound ? ix->d_dir : nullptr;
             fa.dres = 1.01 * ix->xres_dir;
+            if (i8_pass) {  // the int8 copy's rounding of the centred rows (absolute: cosine rows are unit)
+                fa.xres = 1.01 * ix->i8st[prec == PREC_I8 ? 0 : 2] + 1e-300;
+                fa.dir = ix->dir_set && !ix->no_dir_bound ? ix->d_dir : nullptr;
+                fa.dres = 1.01 * ix->i8st[prec == PREC_I8 ? 1 : 3];
+                fa.qerr = q8err;
+                fa.mu = ix->d_mu;
+            }
             fa.out_s = out_s; fa.out_i = out_i; fa.out_k = out_k; fa.index_offset = index_offset;
             fa.row_ids = row_ids;
             fa.flag_count = flags; fa.flag_list = flags + 1; fa.gthr = gthr; fa.overflow_count = flags + B + 1;
@@ -1240,7 +1387,7 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
                     }
                 }
                 rc = run_exact(ix, w, Qd, qn64, flags + 1, B, k, md, out_s, out_i, out_k, index_offset, row_ids, st,
-                               flags, flags + B + 1, done, auto_prec && prec == PREC_BF16 ? ix->h_totals : nullptr);
+                               flags, flags + B + 1, done, auto_prec && one_plane ? ix->h_totals : nullptr);
                 return rc;
             }
             HIP_TRY(hipMemcpyAsync(w->host_flag, flags, sizeof(int), hipMemcpyDeviceToHost, st));
@@ -1248,7 +1395,7 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
             HIP_TRY(hipStreamSynchronize(st));
             n_flag = w->host_flag[0];
             ix->n_overflow += w->host_flag[1];
-            if (auto_prec && prec == PREC_BF16 && n_flag > 0 && !ix->no_fallback) {
+            if (auto_prec && one_plane && n_flag > 0 && !ix->no_fallback) {
                 if (n_flag <= std::max(1, B / 8) && n_flag <= kRepassMax) {
                     // a few uncertified queries: re-pass just those in bf16x3 (the index stays bf16)
                     if (timed) {

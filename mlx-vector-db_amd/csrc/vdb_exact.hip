@@ -459,7 +459,22 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
     // bf16 corpus rounding: |q.(y - bf16(y))| <= bq, Cauchy-Schwarz |q| R or, along the index's
     // residual direction, |q - c dir| R + |c| M with c = q.dir (vdb_ingest.hip resid_dir_kernel);
     // cosine on the unit query
-    __shared__ double s_bq;
+    __shared__ double s_bq, s_shift;
+    if (wv == 1) {
+        // exact = approx + shift, per query: the candidate passes score 2 q.x - |x|^2 for L2
+        // (-|q|^2 to the exact key), the int8 pass leaves out mu.q' (cosine) / 2 mu.q (L2) as
+        // the same constant for every row (vdb_scan8_kernel.h).  The approximate certificate
+        // and the rerank cut only compare approximate scores with each other; the exact-key
+        // test compares an exact key with them.
+        double mq = 0.0;
+        if (a.mu) {
+            const float* qq = a.Q + (int64_t)b * a.D;
+            const double qs = METRIC == 0 ? 1.0 / fmax(qn, 1e-8) : 1.0;
+            for (int d = lane; d < a.D; d += 64) mq += (double)qq[d] * qs * (double)a.mu[d];
+            mq = wave_sum_butterfly(mq);
+        }
+        if (lane == 0) s_shift = METRIC == 0 ? mq : 2.0 * mq - qn * qn;
+    }
     if (wv == 0) {
         double bq = 0.0;
         if (a.xres > 0.0) {
@@ -484,38 +499,57 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
         if (lane == 0) s_bq = bq;
     }
     __shared__ double s_cut;
+    // the exact-key certificate (one workgroup per query): when the approximate one fails, the
+    // query is still certified if the exact k-th best of the reranked candidates beats every
+    // row outside them, e_k > acut + eps (those score <= acut + eps).  The rerank set holds
+    // every candidate that can be in the exact top k (approx >= a_k - 2 eps), so e_k >= a_k -
+    // eps: this never fails where the approximate test (a_k - eps > acut + eps) passes, and
+    // needs one eps of gap instead of two.  s_bar = acut + eps, or +inf where it cannot apply.
+    __shared__ double s_bar, s_ekk;
+    __shared__ int s_ok1;  // 0 = deferred to the exact-key test
     __syncthreads();
     if (tid == 0) {
         const bool full = m == KP;
         const double T = (double)key_to_float(a.gthr[b]);
         const bool have_k = m >= a.k;
         const double ak = have_k ? (double)key_to_float(s_ak) : -INFINITY;
+        const double qe = a.qerr ? (double)a.qerr[b] : 0.0;  // the int8 pass's per-query share
         bool ok = true;
         double eps = 0.0;
         if (full || T > -INFINITY) {
             const double akp = full ? (double)key_to_float(s_akp) : -INFINITY;
             const double acut = fmax(akp, T);
             if (METRIC == 0) {
-                eps = a.eps_rel + s_bq;
+                eps = a.eps_rel + s_bq + qe;
             } else {
                 eps = a.eps_rel * (2.0 * qn * a.xmax + a.xmax * a.xmax) + 2.0 * s_bq +
-                      2.4e-7 * fmax(fabs(ak), fabs(acut));
+                      2.4e-7 * fmax(fabs(ak), fabs(acut)) + qe;
             }
             ok = have_k && acut + eps < ak - eps;
         } else if (have_k) {  // the list holds every eligible row: only the rerank cut needs eps
-            eps = METRIC == 0 ? a.eps_rel + s_bq
+            eps = METRIC == 0 ? a.eps_rel + s_bq + qe
                               : a.eps_rel * (2.0 * qn * a.xmax + a.xmax * a.xmax) + 2.0 * s_bq +
-                                    2.4e-7 * fabs(ak);
+                                    2.4e-7 * fabs(ak) + qe;
         }
-        if (!ok && sp == 0) {
+        const bool defer = S == 1 && have_k && !ok;  // decided after the exact keys
+        if (!ok && !defer && sp == 0) {
             const int pos = atomicAdd(a.flag_count, 1);
             a.flag_list[pos] = b;
+        }
+        s_ok1 = defer ? 0 : 1;  // 0: the exact-key test decides the flag
+        s_ekk = -INFINITY;
+        if (defer) {
+            const double akp = full ? (double)key_to_float(s_akp) : -INFINITY;
+            s_bar = fmax(akp, T) + eps;
+        } else {
+            s_bar = INFINITY;
         }
         // Rerank cut: the k best approx rows score (exact) >= a_k - eps, so the exact k-th best
         // is >= a_k - eps, and a row with approx < a_k - 2 eps scores (exact) < a_k - eps:
         // only candidates with approx >= a_k - 2 eps can be in the exact top k (2.001: the L2
-        // bound's rounding term grows with |approx| below a_k).
-        s_cut = ok && have_k ? ak - 2.001 * eps : -INFINITY;
+        // bound's rounding term grows with |approx| below a_k).  Valid whether or not the
+        // approximate certificate passed (it only compares candidates with each other).
+        s_cut = (ok || defer) && have_k ? ak - 2.001 * eps : -INFINITY;
     }
     __syncthreads();
     if (s_cut > -INFINITY) {
@@ -667,6 +701,7 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
         for (int off = 1; off < TPC; off <<= 1) er += __shfl_xor(er, off, 64);
         if (sub != 0) continue;
         if (j < m) {
+            if (er == a.k - 1) s_ekk = ek;
             if (er < a.k) {
                 const size_t o = (size_t)b * a.k + er;
                 write_result(METRIC, ek, global_row(a.row_ids, r, a.index_offset), true, a.out_s + o, a.out_i + o,
@@ -680,6 +715,15 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
     for (int j = KP + tid; j < a.k; j += 64 * FIN_WAVES) {  // k > KP cannot happen on this path; defensive
         const size_t o = (size_t)b * a.k + j;
         write_result(METRIC, -INFINITY, 0, false, a.out_s + o, a.out_i + o, a.out_k ? a.out_k + o : nullptr);
+    }
+    if (S == 1) {
+        __syncthreads();
+        const double ekk = s_ekk - s_shift;  // the exact k-th best in approximate units (+ fp64 rounding)
+        const double tol = 4e-16 * (fabs(s_ekk) + fabs(s_shift));
+        if (tid == 0 && !s_ok1 && !(ekk - tol > s_bar)) {  // neither certificate: the exact path rewrites it
+            const int pos = atomicAdd(a.flag_count, 1);
+            a.flag_list[pos] = b;
+        }
     }
     FIN_STAMP(4);
     FIN_STAMP(5);

@@ -245,7 +245,7 @@ __global__ void __launch_bounds__(256) prep_queries_kernel(const float* __restri
                                                            double* __restrict__ qn64, int* __restrict__ flag_count,
                                                            uint32_t* __restrict__ gthr,
                                                            uint32_t* __restrict__ gslots, uint32_t* __restrict__ gl_cnt,
-                                                           int* __restrict__ done) {
+                                                           int* __restrict__ done, float* __restrict__ qmax) {
     const int lane = threadIdx.x & 63;
     const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (b == 0 && lane == 0 && flag_count) {
@@ -277,6 +277,13 @@ __global__ void __launch_bounds__(256) prep_queries_kernel(const float* __restri
     if (lane == 0) qn64[b] = nq;
     // cosine: the candidate pass works on q/max(|q|,1e-8) rounded to fp32.
     const float scale = metric == 0 ? (float)(1.0 / fmax(nq, 1e-8)) : 1.0f;
+    if (qmax && real) {  // the int8 pass's batch scale (vdb_scan8.hip prep8)
+        float m = 0.0f;
+        for (int d = lane; d < D; d += 64) m = fmaxf(m, fabsf(q[d] * scale));
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+        if (lane == 0) qmax[b] = m;
+    }
     if (Qt) {
         const int GQ = G + QG_EXTRA;
         for (int p = lane; 4 * p < Dp + 8 * QG_EXTRA; p += 64) {
@@ -314,9 +321,9 @@ __global__ void __launch_bounds__(256) prep_queries_kernel(const float* __restri
 
 hipError_t launch_prep_queries(const float* Q, int B, int Bp, int D, int G, int metric, float* Qt, float* Qs,
                                double* qn64, int* flag_count, uint32_t* gthr, uint32_t* gslots, uint32_t* gl_cnt,
-                               int* done, hipStream_t st) {
+                               int* done, hipStream_t st, float* qmax) {
     hipLaunchKernelGGL(prep_queries_kernel, dim3((Bp + 3) / 4), dim3(256), 0, st, Q, B, Bp, D, G, metric, Qt, Qs,
-                       qn64, flag_count, gthr, gslots, gl_cnt, done);
+                       qn64, flag_count, gthr, gslots, gl_cnt, done, qmax);
     return hipGetLastError();
 }
 }  // namespace vdb

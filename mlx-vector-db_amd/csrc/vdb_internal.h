@@ -22,6 +22,40 @@ constexpr int PREC_BF16X3 = 1;
 //               x.q ~ xh.qh + xh.ql, two v_mfma_f32_32x32x16_bf16 per 16-dim group; bounded by the
 //               index's largest row residual |x - bf16(x)| (pack_rows)
 constexpr int PREC_BF16 = 2;
+//   PREC_I8     int8 copy of the centred rows (vdb_scan8_kernel.h): x ~ s_x xh (1 byte per element),
+//               query s_q qh (8 bits): one v_mfma_i32_32x32x32_i8 per 32-dim group
+//   PREC_I8X3   both planes of the int8 copy, x ~ s_x (xh + xl/256), query 16 bits: three per group
+constexpr int PREC_I8 = 3;
+constexpr int PREC_I8X3 = 4;
+constexpr int N_PREC = 5;
+inline bool prec_is_i8(int p) { return p == PREC_I8 || p == PREC_I8X3; }
+
+// Per-index constants of the int8 pass (vdb_api.cpp): the quantisation step s_x of the centred
+// rows, max |s_x xh| and max |s_x xl / 256| over the rows (row norms), max |x|^2 / 2 (L2 start)
+struct Int8Consts {
+    float sx;
+    double zmax_h, xl_max, rmax_half;
+};
+// max |y - mu| of rows [row0, row0 + n) as float bits (atomicMax into *out)
+hipError_t launch_zmax(const float* X, const float* inv32, const float* mu, int64_t row0, int64_t n, int D, int G,
+                       uint32_t* out, hipStream_t st);
+// rows [row0, row0 + n) -> the int8 copy Xq (two planes, 32-dim groups, the split layout's block
+// order); stats[0..6) running maxima (fp64 bits): |z - s_x xh|, |dir.(z - s_x xh)|, |z - z~|,
+// |dir.(z - z~)|, |s_x xh|, |s_x xl / 256|
+hipError_t launch_quant_rows(const float* X, const float* inv32, const float* mu, const float* dir, float sx,
+                             int64_t row0, int64_t n, int G, float* Xq, unsigned long long* stats, hipStream_t st);
+// queries -> int8 tiles Qq (G8 + QG_EXTRA groups), per query lsl / qerr, per batch qscal[3]
+hipError_t launch_prep8(const float* Q, const double* qn64, const float* qmax, int B, int Bp, int D, int G8,
+                        int metric, int prec, const Int8Consts& c, float* Qq, float* lsl, float* qerr, float* qscal,
+                        hipStream_t st);
+hipError_t launch_pilot8(int prec, int metric, const float* Xq, const float* rinit, const uint32_t* mask,
+                         const float* Qq, const float* qscal, int G8, int64_t N, int B, int n_qblocks, int QB,
+                         int n_sample, uint32_t* pslots, hipStream_t st);
+int scan8_rows_per_step(int prec, int metric);
+hipError_t launch_scan8(int prec, int metric, int KP, const float* Xq, const float* rinit, const uint32_t* mask,
+                        const float* Qq, const float* lsl, const float* qscal, int G8, int64_t N, int B,
+                        int n_qblocks, int64_t n_steps, int n_wg, int spw, float* gl_s, uint32_t* gl_i,
+                        uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr, int lockstep, int qlds, hipStream_t st);
 
 // Ingest: row-major fp32 [n][D] (device) -> the index's row-major fp32 copy X [cap][Dp]
 // (zero padded to Dp = 8 G; read by the exact paths, export and the graph) rows [row0, row0+n),
@@ -63,9 +97,11 @@ constexpr int PILOT_SLOTS = 256;  // pilot bound slots per query (pslots [Bp][PI
 // fp32; zero padding written) and/or the split-bf16 tiles Qs (G/2 + QG_EXTRA
 // groups, same wrap), canonical fp64 norms [Bp]; resets *flag_count and done[Bp] (the
 // gated fallback's per-query counters, ExactTail).
+// qmax (optional, the int8 pass): per query max |q'| over its dims (q' cosine-normalised).
 hipError_t launch_prep_queries(const float* Q, int B, int Bp, int D, int G, int metric,
                                float* Qt, float* Qs, double* qn64, int* flag_count, uint32_t* gthr,
-                               uint32_t* gslots, uint32_t* gl_cnt, int* done, hipStream_t st);
+                               uint32_t* gslots, uint32_t* gl_cnt, int* done, hipStream_t st,
+                               float* qmax = nullptr);
 
 // Candidate pass: MFMA fp32 scores fused with a per-workgroup top-KP.
 // Output lists cand_[s|i][B][n_wg][KP], each sorted best first.
@@ -150,6 +186,11 @@ struct FinishArgs {
     // bound per query becomes min(|q| R, |q - c dir| R + |c| M), c = q.dir (R = xres)
     const float* dir = nullptr;
     double dres = 0.0;
+    // the int8 pass, optional: the query's own share of eps per query (prep8: query rounding,
+    // dropped terms, L2 start rounding), added to the certificate's eps
+    const float* qerr = nullptr;
+    // the int8 pass's centring row (its scores leave out mu.q; the exact-key certificate adds it)
+    const float* mu = nullptr;
     float* out_s; int64_t* out_i; double* out_k; int64_t index_offset;
     int* flag_count; int* flag_list; const uint32_t* gthr;
     int* overflow_count;  // lists longer than the finish kernel holds (they take the exact path)

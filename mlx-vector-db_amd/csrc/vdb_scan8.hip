@@ -1,0 +1,344 @@
+// vdb_scan8.hip — the int8 candidate pass (PREC_I8 / PREC_I8X3, kernel: vdb_scan8_kernel.h):
+// the corpus quantisation at ingest, the per-batch query quantisation, the pilot with the same
+// arithmetic, and the dispatch to the instantiation units.
+#include "vdb_scan8_kernel.h"
+
+namespace vdb {
+
+// =============================================================================
+// Ingest: the 16-bit fixed-point copy of the centred rows
+// =============================================================================
+// max |y - mu| over rows [row0, row0 + n) (y = x * inv32 for cosine), as float bits into *out
+// (non-negative floats order like their bits): the index's quantisation step s_x derives from it
+// at the first add (vdb_api.cpp setup_direction).
+__global__ void __launch_bounds__(256) zmax_kernel(const float* __restrict__ X, const float* __restrict__ inv32,
+                                                   const float* __restrict__ mu, int64_t row0, int64_t n, int D, int G,
+                                                   uint32_t* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    float m = 0.0f;
+    if (i < n) {
+        const uint64_t r = (uint64_t)(row0 + i);
+        const float iv = inv32 ? inv32[r] : 1.0f;
+        for (int d = lane; d < D; d += 64) {
+            const float x = X[row_piece_offset(r, d >> 2, G) + (d & 3)];
+            m = fmaxf(m, fabsf((inv32 ? x * iv : x) - mu[d]));
+        }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+    if (lane == 0 && i < n) atomicMax(out, __float_as_uint(m));
+}
+
+hipError_t launch_zmax(const float* X, const float* inv32, const float* mu, int64_t row0, int64_t n, int D, int G,
+                       uint32_t* out, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(zmax_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, X, inv32, mu, row0, n, D, G, out);
+    return hipGetLastError();
+}
+
+// 16 values -> 16 int8 (byte j = element j) in one f32x4
+__device__ __forceinline__ f32x4 pack_i8x16(const int (&v)[16]) {
+    f32x4 o;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const uint32_t u = (uint32_t)(v[4 * w] & 255) | ((uint32_t)(v[4 * w + 1] & 255) << 8) |
+                           ((uint32_t)(v[4 * w + 2] & 255) << 16) | ((uint32_t)(v[4 * w + 3] & 255) << 24);
+        o[w] = __uint_as_float(u);
+    }
+    return o;
+}
+
+// t -> (hi, lo) with t ~ hi + lo / 256, |hi|, |lo| <= 127 (values past the range clip; the
+// residual the statistics measure then shows it)
+__device__ __forceinline__ void split_i8(float t, int& hi, int& lo) {
+    hi = (int)fminf(fmaxf(rintf(t), -127.0f), 127.0f);
+    lo = (int)fminf(fmaxf(rintf((t - (float)hi) * 256.0f), -127.0f), 127.0f);
+}
+
+// One wave per row: z = y - mu, xh / xl planes of the int8 copy (block (tile, 32-dim group g,
+// plane) lane i + 32 h holds dims 32 g + 16 h .. + 15 of row 32 t + i), and the row statistics
+// (fp64 bits, running maxima) stats[0] |z - s_x xh|, [1] |dir.(z - s_x xh)|, [2] |z - z~|,
+// [3] |dir.(z - z~)| (z~ = s_x (xh + xl/256)), [4] |s_x xh|, [5] |s_x xl / 256|.
+__global__ void __launch_bounds__(256) quant_rows_kernel(const float* __restrict__ X, const float* __restrict__ inv32,
+                                                         const float* __restrict__ mu, const float* __restrict__ dir,
+                                                         float sx, int64_t row0, int64_t n, int G,
+                                                         float* __restrict__ Xq, unsigned long long* __restrict__ stats) {
+    const int lane = threadIdx.x & 63;
+    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= n) return;
+    const uint64_t r = (uint64_t)(row0 + i);
+    const float iv = inv32 ? inv32[r] : 1.0f;
+    const float isx = 1.0f / sx;
+    const int G8 = G >> 2;
+    const int nc = 2 * G8;  // 16-dim chunks
+    double s_r8 = 0.0, s_d8 = 0.0, s_r16 = 0.0, s_d16 = 0.0, s_h = 0.0, s_l = 0.0;
+    for (int c = lane; c < nc; c += 64) {
+        const float* src = X + (size_t)r * (size_t)(8 * G) + 16 * c;
+        int hv[16], lv[16];
+#pragma unroll
+        for (int j4 = 0; j4 < 4; ++j4) {
+            const f32x4 xv = *(const f32x4*)(src + 4 * j4);
+            const f32x4 mv = *(const f32x4*)(mu + 16 * c + 4 * j4);
+            const f32x4 dv = *(const f32x4*)(dir + 16 * c + 4 * j4);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float z = (inv32 ? xv[j] * iv : xv[j]) - mv[j];
+                int h, l;
+                split_i8(z * isx, h, l);
+                hv[4 * j4 + j] = h;
+                lv[4 * j4 + j] = l;
+                const double zh = (double)sx * h, zl = (double)sx * l / 256.0;
+                const double r8 = (double)z - zh, r16 = r8 - zl;
+                s_r8 += r8 * r8;
+                s_r16 += r16 * r16;
+                s_d8 += (double)dv[j] * r8;
+                s_d16 += (double)dv[j] * r16;
+                s_h += zh * zh;
+                s_l += zl * zl;
+            }
+        }
+        const uint64_t t = r >> 5;
+        float* dst = Xq + corpus_block(t, c >> 1, 0, G8) + (size_t)((r & 31) + 32 * (c & 1)) * 4;
+        *(f32x4*)dst = pack_i8x16(hv);
+        *(f32x4*)(dst + corpus_plane(G8)) = pack_i8x16(lv);
+    }
+    s_r8 = wave_sum_butterfly(s_r8);
+    s_d8 = wave_sum_butterfly(s_d8);
+    s_r16 = wave_sum_butterfly(s_r16);
+    s_d16 = wave_sum_butterfly(s_d16);
+    s_h = wave_sum_butterfly(s_h);
+    s_l = wave_sum_butterfly(s_l);
+    if (lane == 0) {
+        const double v[6] = {sqrt(s_r8), fabs(s_d8), sqrt(s_r16), fabs(s_d16), sqrt(s_h), sqrt(s_l)};
+        bool fin = true;  // a non-finite row (the whole add is rejected) leaves no statistics
+#pragma unroll
+        for (int k = 0; k < 6; ++k) fin = fin && isfinite(v[k]);
+#pragma unroll
+        for (int k = 0; k < 6 && fin; ++k) {
+            const unsigned long long b = (unsigned long long)__double_as_longlong(v[k]);
+            if (b > __atomic_load_n(stats + k, __ATOMIC_RELAXED)) atomicMax(stats + k, b);
+        }
+    }
+}
+
+hipError_t launch_quant_rows(const float* X, const float* inv32, const float* mu, const float* dir, float sx,
+                             int64_t row0, int64_t n, int G, float* Xq, unsigned long long* stats, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(quant_rows_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, X, inv32, mu, dir, sx, row0,
+                       n, G, Xq, stats);
+    return hipGetLastError();
+}
+
+// =============================================================================
+// Queries: one scale per batch, s_q = max |q'| / 127 (q' the fp32 query the other passes use:
+// cosine normalised), 16-bit fixed point in two int8 planes, tiles as the split layout
+// (s2_blk, G8 + QG_EXTRA groups, the leading ones repeated).  Per query: lsl = the prefilter's
+// slack (bound of the L term), qerr = the query's share of the certificate's eps.
+// =============================================================================
+__global__ void __launch_bounds__(256) prep8_kernel(const float* __restrict__ Q, const double* __restrict__ qn64,
+                                                    const float* __restrict__ qmax, int B, int Bp, int D, int G8,
+                                                    int metric, int prec, Int8Consts c, float* __restrict__ Qq,
+                                                    float* __restrict__ lsl, float* __restrict__ qerr,
+                                                    float* __restrict__ qscal) {
+    const int lane = threadIdx.x & 63;
+    const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (b >= Bp) return;
+    float m = 0.0f;
+    for (int j = lane; j < B; j += 64) m = fmaxf(m, qmax[j]);
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+    float sq = m > 0.0f ? m / 127.0f : 1.0f;
+    // L2: H starts at -|x|^2 / 2 / (s_x s_q), which must stay well inside int32 (with the
+    // products' own range): a coarser query scale where it would not (eps follows, qerr)
+    if (metric == 1) sq = fmaxf(sq, (float)(c.rmax_half / ((double)c.sx * 1.0e9)));
+    const float uH = c.sx * sq;
+    if (b == 0 && lane == 0) {
+        qscal[0] = uH;
+        qscal[1] = uH * (1.0f / 256.0f);
+        qscal[2] = 1.0f / uH;
+    }
+    const bool real = b < B;
+    const double nq = real ? qn64[b] : 0.0;
+    const float scale = metric == 0 ? (float)(1.0 / fmax(nq, 1e-8)) : 1.0f;
+    const float* q = Q + (int64_t)(real ? b : 0) * D;
+    const float isq = 1.0f / sq;
+    const int GQ = G8 + QG_EXTRA;
+    double s_rq = 0.0, s_r8 = 0.0, s_ql = 0.0, s_qh = 0.0;
+    for (int cc = lane; cc < 2 * GQ; cc += 64) {
+        const int g = cc >> 1, h = cc & 1;
+        const int d0 = 32 * (g % G8) + 16 * h;
+        int hv[16], lv[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int d = d0 + j;
+            const float qv = (real && d < D) ? q[d] * scale : 0.0f;
+            split_i8(qv * isq, hv[j], lv[j]);
+            if (g < G8) {
+                const double qh = (double)sq * hv[j], ql = (double)sq * lv[j] / 256.0;
+                const double r8 = (double)qv - qh, rq = r8 - ql;
+                s_rq += rq * rq;
+                s_r8 += r8 * r8;
+                s_ql += ql * ql;
+                s_qh += qh * qh;
+            }
+        }
+        float* dst = Qq + s2_blk((uint64_t)(b >> 5), g, GQ) + (size_t)((b & 31) + 32 * h) * 4;
+        *(f32x4*)dst = pack_i8x16(hv);
+        *(f32x4*)(dst + 4 * BLOCK_FLOATS) = pack_i8x16(lv);
+    }
+    s_rq = wave_sum_butterfly(s_rq);
+    s_r8 = wave_sum_butterfly(s_r8);
+    s_ql = wave_sum_butterfly(s_ql);
+    s_qh = wave_sum_butterfly(s_qh);
+    if (lane == 0) {
+        const bool x3 = prec == PREC_I8X3;
+        const double za = c.zmax_h + (x3 ? c.xl_max : 0.0);  // bound of |z~|
+        // I8X3: |L uL| <= |s_x xh| |s_q ql / 256| + |s_x xl / 256| |s_q qh| (I8 has no L)
+        const double sl = x3 ? c.zmax_h * sqrt(s_ql) + c.xl_max * sqrt(s_qh) : 0.0;
+        // approx - z.q' = -(z - z~).q' (the corpus term, finish) - z~.(q' - q~) (q~ = s_q qh for
+        // I8, s_q (qh + ql / 256) for I8X3) - [I8X3: the dropped s_x s_q xl.ql / 65536] (+ L2: the
+        // rounding of H's start, <= 0.5 uH, 1 uH with the fp32 product before it)
+        double e = za * sqrt(x3 ? s_rq : s_r8) + (x3 ? c.xl_max * sqrt(s_ql) : 0.0) + (metric == 1 ? (double)uH : 0.0);
+        e = 1.01 * (metric == 0 ? e : 2.0 * e);
+        lsl[b] = real ? (float)(1.01 * sl) * (1.0f + 1e-5f) + 1e-30f : 0.0f;
+        qerr[b] = real ? (float)e * (1.0f + 1e-5f) : 0.0f;
+    }
+}
+
+hipError_t launch_prep8(const float* Q, const double* qn64, const float* qmax, int B, int Bp, int D, int G8,
+                        int metric, int prec, const Int8Consts& c, float* Qq, float* lsl, float* qerr, float* qscal,
+                        hipStream_t st) {
+    hipLaunchKernelGGL(prep8_kernel, dim3((Bp + 3) / 4), dim3(256), 0, st, Q, qn64, qmax, B, Bp, D, G8, metric, prec, c,
+                       Qq, lsl, qerr, qscal);
+    return hipGetLastError();
+}
+
+// =============================================================================
+// Pilot (vdb_scan2.hip pilot2 with the int8 arithmetic): best fp32 (half-)score per sampled
+// tile and query into the pilot slots; L2 adds the exact fp32 start value per row.
+// =============================================================================
+constexpr int PILOT8_WAVES = 4;
+__host__ __device__ inline int pilot8_w(int G8) { return G8 >= 8 ? 4 : G8 >= 3 ? 2 : 1; }
+
+template <int PREC, int METRIC, int QT>
+__global__ void __launch_bounds__(64 * PILOT8_WAVES)
+pilot8_scores_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, const uint32_t* __restrict__ mask,
+                     const float* __restrict__ Qq, const float* __restrict__ qscal, int G, int64_t N, int B,
+                     int64_t n_tiles, int n_sample, uint32_t* __restrict__ pslots) {
+    constexpr int QB = 32 * QT;
+    constexpr int XPL = Planes8<PREC>::XPL;
+    constexpr size_t GSTEP = 8 * BLOCK_FLOATS, PLANE = 4 * BLOCK_FLOATS;
+    __shared__ int s_part[PILOT8_WAVES][2][QT][16][64];
+    const int lane = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6;
+    const int W = pilot8_w(G);
+    const int part = wv % W;
+    const int i = blockIdx.x * (PILOT8_WAVES / W) + wv / W;
+    const int qb = blockIdx.y;
+    const bool live = i < n_sample;
+    const uint64_t t = live ? (uint64_t)((int64_t)i * n_tiles / n_sample) : 0;
+    const float* xs = Xq + corpus_block(t, 0, 0, G) + lane * 4;
+    const size_t XGSTEP = corpus_gstep(), XPLANE = corpus_plane(G);
+    const float* qs = Qq + s2_blk((uint64_t)(qb * QT), 0, G + QG_EXTRA) + lane * 4;
+    i32x16 aH[1][QT], aL[1][QT];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) aH[0][qt][v] = aL[0][qt][v] = 0;
+    for (int g = part; g < G; g += W) {
+        constexpr int QPL = Planes8<PREC>::QPL;
+        f32x4 xr[1][XPL], qr[QT][QPL];
+#pragma unroll
+        for (int pl = 0; pl < XPL; ++pl) xr[0][pl] = *(const f32x4*)(xs + g * XGSTEP + pl * XPLANE);
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+            for (int pl = 0; pl < QPL; ++pl) qr[qt][pl] = *(const f32x4*)(qs + g * GSTEP + pl * PLANE + qt * BLOCK_FLOATS);
+        group_mfma8<PREC, 1, QT>(xr, qr, aH, aL);
+    }
+    if (part > 0) {
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+                s_part[wv][0][qt][v][lane] = aH[0][qt][v];
+                s_part[wv][1][qt][v][lane] = aL[0][qt][v];
+            }
+    }
+    __syncthreads();
+    if (part > 0 || !live) return;
+    for (int w = 1; w < W; ++w)
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+                aH[0][qt][v] += s_part[wv + w][0][qt][v][lane];
+                aL[0][qt][v] += s_part[wv + w][1][qt][v][lane];
+            }
+    const float uH = qscal[0], uL = qscal[1];
+    const uint32_t valid = tile_valid16(mask, (int64_t)t, N, lane);
+    float rr[16];
+#pragma unroll
+    for (int v = 0; v < 16; ++v)
+        rr[v] = METRIC == 1 ? rinit[t * 32 + (v & 3) + 8 * (v >> 2) + 4 * (lane >> 5)] : 0.0f;
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+        const int q = qb * QB + qt * 32 + (lane & 31);
+        float best = -INFINITY;
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+            const float sv = fmaf((float)aH[0][qt][v], uH, (float)aL[0][qt][v] * uL) + rr[v];
+            best = ((valid >> v) & 1u) ? fmaxf(best, sv) : best;
+        }
+        if (METRIC == 1) best = 2.0f * best;
+        if (q < B && best != -INFINITY)
+            atomicMax(pslots + (size_t)q * PILOT_SLOTS + (i % PILOT_SLOTS), order_key(best));
+    }
+}
+
+hipError_t launch_pilot8(int prec, int metric, const float* Xq, const float* rinit, const uint32_t* mask,
+                         const float* Qq, const float* qscal, int G8, int64_t N, int B, int n_qblocks, int QB,
+                         int n_sample, uint32_t* pslots, hipStream_t st) {
+    const int64_t n_tiles = (N + 31) / 32;
+    if (n_sample > n_tiles) n_sample = (int)n_tiles;
+    if (n_sample <= 0) return hipSuccess;
+    const int tpb = PILOT8_WAVES / pilot8_w(G8);
+    const dim3 grid((n_sample + tpb - 1) / tpb, n_qblocks);
+    bool launched = false;
+#define VDB_PILOT8(P, M, QTV)                                                                                    \
+    if (!launched && prec == P && metric == M && QB == 32 * QTV) {                                               \
+        hipLaunchKernelGGL((pilot8_scores_kernel<P, M, QTV>), grid, dim3(64 * PILOT8_WAVES), 0, st, Xq, rinit,   \
+                           mask, Qq, qscal, G8, N, B, n_tiles, n_sample, pslots);                                \
+        launched = true;                                                                                         \
+    }
+    VDB_PILOT8(PREC_I8, 0, 2) VDB_PILOT8(PREC_I8, 1, 2) VDB_PILOT8(PREC_I8, 0, 1) VDB_PILOT8(PREC_I8, 1, 1)
+    VDB_PILOT8(PREC_I8X3, 0, 2) VDB_PILOT8(PREC_I8X3, 1, 2) VDB_PILOT8(PREC_I8X3, 0, 1) VDB_PILOT8(PREC_I8X3, 1, 1)
+#undef VDB_PILOT8
+    if (!launched) return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+// =============================================================================
+// Dispatch
+// =============================================================================
+int scan8_rows_per_step(int prec, int metric) { return scan8_rows(prec, metric); }
+
+hipError_t launch_scan8(int prec, int metric, int KP, const float* Xq, const float* rinit, const uint32_t* mask,
+                        const float* Qq, const float* lsl, const float* qscal, int G8, int64_t N, int B,
+                        int n_qblocks, int64_t n_steps, int n_wg, int spw, float* gl_s, uint32_t* gl_i,
+                        uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr, int lockstep, int qlds, hipStream_t st) {
+    // the query block in LDS: auto when it fits (qlds < 0), never with 0 -- except for rows of
+    // fewer 32-dim groups than the global-operand variants keep in flight (PX = 4)
+    const bool ql = (qlds != 0 && scan8_qlds(G8, KP)) || G8 < 4;
+    const bool fs = !lockstep;
+    const bool nt = !ql && n_qblocks == 1;
+    auto* unit = prec == PREC_I8X3 ? (metric == 0 ? launch_scan8_i3c : launch_scan8_i3l)
+                 : prec == PREC_I8 ? (metric == 0 ? launch_scan8_i1c : launch_scan8_i1l)
+                                   : nullptr;
+    if (!unit || metric < 0 || metric > 1) return hipErrorInvalidValue;
+    return unit(KP, Xq, rinit, mask, Qq, lsl, qscal, G8, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt,
+                gl_cap, gthr, nt, ql, fs, st);
+}
+
+}  // namespace vdb

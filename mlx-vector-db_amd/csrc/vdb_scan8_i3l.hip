@@ -1,0 +1,7 @@
+// vdb_scan8_i3l.hip — instantiation unit of the int8 candidate pass: int8 x3 (two planes), L2
+// (every KP / load policy / step-end variant; kernel in vdb_scan8_kernel.h).
+#include "vdb_scan8_kernel.h"
+
+namespace vdb {
+S8_UNIT(launch_scan8_i3l, PREC_I8X3, 1, 2, 2)
+}  // namespace vdb

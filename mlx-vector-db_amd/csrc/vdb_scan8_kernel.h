@@ -1,0 +1,464 @@
+// vdb_scan8_kernel.h — the int8 candidate pass (PREC_I8 / PREC_I8X3) and its launch templates
+// (included by vdb_scan8.hip and the per-(precision, metric) instantiation units
+// vdb_scan8_{i1,i3}{c,l}.hip, which the build compiles in parallel).
+//
+// Arithmetic.  The candidate copy holds the CENTRED rows z = y - mu (y the row the pass scores:
+// cosine the normalised row, L2 the row; mu the mean row of the first add, vdb_api.cpp) as
+// 16-bit fixed point in two int8 planes, z ~ s_x (xh + xl / 256) (vdb_scan8.hip quant_rows).
+// The query block q (cosine: normalised) is quantised the same way per batch, q ~ s_q (qh + ql /
+// 256) (vdb_scan8.hip prep8).  Per 32-dim group and (row tile, query tile) the pass issues
+//   PREC_I8    xh.qh -> H                                   1 v_mfma_i32_32x32x32_i8
+//   PREC_I8X3  xh.qh -> H, xh.ql + xl.qh -> L               3 v_mfma_i32_32x32x32_i8
+// and the (half-)score is H s_x s_q (+ L s_x s_q / 256): integer sums are exact, an i8 MFMA does
+// twice the K of a bf16 one in the same cycles, and the I8 pass reads one byte per element
+// (half of the bf16 hi plane) and one accumulator set (scan2's register shape: 4 row tiles per
+// wave).  Its error bound is the wider one (the query's 8-bit rounding |z~.(q - s_q qh)| adds
+// to the corpus term), which the finish's exact-key certificate (vdb_exact.hip: the exact k-th
+// best candidate against acut + eps, one eps instead of two) absorbs at C2 / C6's gaps; where
+// it does not, auto re-passes the query in I8X3.  Ranking by z.q instead of y.q drops mu.q, the same for every
+// row of a query, so candidates, bounds and the certificate (all differences of approximate
+// scores) are unchanged by it.  L2 scores q.x - |x|^2/2 = q.mu + q.z - |x|^2/2: H starts at
+// rint(-|x|^2 / 2 / (s_x s_q)) per row, so the pass ends at score / 2 (up to q.mu).
+// Error vs the exact score (finish_kernel's eps, vdb_api.cpp): the corpus rounding
+// |q.(z - z~)| (the measured row residuals, Cauchy-Schwarz or along the residual direction, as
+// for bf16), the query rounding |z~.(q - q~)| and for I8X3 the dropped xl.ql term (per query,
+// prep8 -> qerr), the L2 start rounding, and fp32 rounding of the final combination.
+//
+// Shape: scan2's (4 waves, one per SIMD, a shared query block of QT tiles, RT row tiles per
+// wave and step -- I8 4, I8X3 2: two accumulator sets per tile --, PX corpus groups in flight in
+// registers, the query block from L2 or, for short rows, LDS).  Epilogue: a tile passes when its
+// largest H clears the query's threshold in H units (I8X3: minus the largest |L| term, lsl per
+// query), then the fp32 score of each register is compared and appended.
+#pragma once
+#include "vdb_scan2_kernel.h"
+
+namespace vdb {
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int S8_NW = 4;  // waves per workgroup
+// row tiles per wave per step: I8 cosine 4 (one accumulator set, 128 registers), I8X3 2 (two
+// sets), I8 L2 2 (its per-row start values, prefetched a step ahead, would spill at 4)
+#ifndef VDB_S8_RT1
+#define VDB_S8_RT1 4
+#endif
+#ifndef VDB_S8_RT3
+#define VDB_S8_RT3 2
+#endif
+constexpr int scan8_rt(int prec, int metric) { return prec == PREC_I8X3 || metric == 1 ? VDB_S8_RT3 : VDB_S8_RT1; }
+constexpr int scan8_rows(int prec, int metric) { return scan8_rt(prec, metric) * S8_NW * 32; }
+
+template <int PREC>
+struct Planes8 {
+    static constexpr int XPL = PREC == PREC_I8X3 ? 2 : 1;  // corpus planes read
+    static constexpr int QPL = PREC == PREC_I8X3 ? 2 : 1;  // query planes read
+    static constexpr bool L = PREC == PREC_I8X3;  // the L accumulator set
+};
+
+template <int PREC, int RT, int QT>
+__device__ __forceinline__ void group_mfma8(const f32x4 (&x)[RT][Planes8<PREC>::XPL],
+                                            const f32x4 (&q)[QT][Planes8<PREC>::QPL], i32x16 (&aH)[RT][QT],
+                                            i32x16 (&aL)[RT][QT]) {
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) {
+            const i32x4 xh = __builtin_bit_cast(i32x4, x[rt][0]);
+            const i32x4 qh = __builtin_bit_cast(i32x4, q[qt][0]);
+            aH[rt][qt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(xh, qh, aH[rt][qt], 0, 0, 0);
+            if constexpr (PREC == PREC_I8X3) {
+                const i32x4 ql = __builtin_bit_cast(i32x4, q[qt][Planes8<PREC>::QPL - 1]);
+                aL[rt][qt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(xh, ql, aL[rt][qt], 0, 0, 0);
+                aL[rt][qt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(__builtin_bit_cast(i32x4, x[rt][Planes8<PREC>::XPL - 1]),
+                                                                   qh, aL[rt][qt], 0, 0, 0);
+            }
+        }
+}
+
+__device__ __forceinline__ int imax16(const i32x16& a) {
+    int m = max(max(a[0], a[1]), a[2]);
+#pragma unroll
+    for (int v = 3; v < 15; v += 2) m = max(max(m, a[v]), a[v + 1]);
+    return max(m, a[15]);
+}
+
+// The smallest H that can still pass threshold th (half units) given |L uL| <= slack, minus a
+// margin for the fp32 evaluation: H <= the result means the tile's scores are all <= th.
+__device__ __forceinline__ int h_floor(float th, float slack, float invU) {
+    if (!(th > -INFINITY)) return INT_MIN;
+    const float t = (th - slack) * invU;
+    const float m = t - fabsf(t) * 1e-5f - 4.0f;
+    if (m <= -2.0e9f) return INT_MIN;
+    if (m >= 2.0e9f) return 2000000000;
+    return (int)floorf(m);
+}
+
+// Per-batch scalars written by prep8 (device): [0] uH = s_x s_q, [1] uL = uH / 256, [2] 1 / uH.
+template <int PREC, int METRIC, int QT, int PX, int KP, int CAP, bool NT, bool QLDS, bool FLAGSYNC, int GC = 0,
+          int RT_ = scan8_rt(PREC, METRIC), int KW = KP>
+__global__ void __launch_bounds__(64 * S8_NW, 1)
+scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, const uint32_t* __restrict__ mask,
+             const float* __restrict__ Qq, const float* __restrict__ lsl, const float* __restrict__ qscal, int G_arg,
+             int64_t N, int B, int64_t n_steps, int steps_per_wg, int n_qb, float* __restrict__ gl_s,
+             uint32_t* __restrict__ gl_i, uint32_t* __restrict__ gl_cnt, int64_t gl_cap, uint32_t* __restrict__ gthr) {
+    constexpr int RT = RT_, NW = S8_NW;
+    constexpr int QB = 32 * QT;
+    constexpr int XPL = Planes8<PREC>::XPL, QPL = Planes8<PREC>::QPL;
+    constexpr bool HL = Planes8<PREC>::L;
+    const int G = GC > 0 ? GC : G_arg;
+    constexpr int PQ = QLDS ? 1 : PX;
+    constexpr size_t GSTEP = 8 * BLOCK_FLOATS;  // query: consecutive groups of one super tile
+    constexpr size_t PLANE = 4 * BLOCK_FLOATS;  // query: lo plane after hi
+    constexpr size_t XGSTEP = corpus_gstep();
+    const size_t XPLANE = corpus_plane(G);
+    static_assert(PX <= QG_EXTRA, "query prefetch deeper than the duplicated groups");
+    __shared__ float s_sc[QB * CAP];
+    __shared__ uint32_t s_ix[QB * CAP];
+    __shared__ int s_cnt[QB];
+    __shared__ float s_thr[QB];
+    __shared__ int s_need, s_done;
+    extern __shared__ __attribute__((aligned(16))) float s_q[];  // QLDS: [G][plane][QT][256]
+
+    const int lane = threadIdx.x & 63;
+    const int lane4 = lane * 4;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    int wg, qb;
+    xcd_map(n_qb, wg, qb);
+    if (threadIdx.x == 0) {
+        s_need = 0;
+        s_done = 0;
+    }
+    for (int i = threadIdx.x; i < QB; i += 64 * NW) {
+        s_cnt[i] = 0;
+        s_thr[i] = -INFINITY;
+    }
+    const float uH = qscal[0], uL = qscal[1], invU = qscal[2];
+    float qsl[QT];  // per query: bound of |L uL| (the prefilter's slack)
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+        const int qg = qb * QB + qt * 32 + (lane & 31);
+        qsl[qt] = qg < B ? lsl[qg] : 0.0f;
+    }
+    const float* Qbase = Qq + s2_blk((uint64_t)(qb * QT), 0, G + QG_EXTRA);
+    if constexpr (QLDS) {
+        for (int e = threadIdx.x; e < G * 2 * QT * 64; e += 64 * NW) {
+            const int l = e & 63, qt = (e >> 6) % QT, pl = (e / (64 * QT)) & 1, g = e / (128 * QT);
+            *(f32x4*)(s_q + (size_t)e * 4) = *(const f32x4*)(Qbase + g * GSTEP + pl * PLANE + qt * BLOCK_FLOATS + 4 * l);
+        }
+    }
+    __syncthreads();
+
+    constexpr int QPW = QB / NW;
+    const int64_t s_begin = (int64_t)wg * steps_per_wg;
+    const int64_t s_end = s_begin + steps_per_wg < n_steps ? s_begin + steps_per_wg : n_steps;
+
+    f32x4 xr[PX][RT][XPL];
+    f32x4 qr[PQ][QT][QPL];
+    auto q_lds = [&](int g, f32x4 (&q)[QT][QPL]) {
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+            for (int pl = 0; pl < QPL; ++pl) q[qt][pl] = *(const f32x4*)(s_q + ((size_t)(g * 2 + pl) * QT + qt) * 256 + lane4);
+    };
+    if (s_begin < s_end) {
+        const float* xs = Xq + corpus_block((uint64_t)((s_begin * NW + wv) * RT), 0, 0, G);
+#pragma unroll
+        for (int p = 0; p < PX; ++p)
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+                for (int pl = 0; pl < XPL; ++pl)
+                    xr[p][rt][pl] = corpus_ld<NT>(xs + p * XGSTEP + pl * XPLANE + rt * BLOCK_FLOATS + lane4);
+        if constexpr (!QLDS) {
+#pragma unroll
+            for (int p = 0; p < PQ; ++p)
+#pragma unroll
+                for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+                    for (int pl = 0; pl < QPL; ++pl)
+                        qr[p][qt][pl] = *(const f32x4*)(Qbase + p * GSTEP + pl * PLANE + qt * BLOCK_FLOATS + lane4);
+        } else {
+            q_lds(0, qr[0]);
+        }
+    }
+    // the next step's shared bounds and (L2) start values, loaded one step ahead: lane half h
+    // holds -|x|^2/2 of rows 32 t + 8 a + 4 h + b (a, b = 0..3) of each tile, the rows of its
+    // accumulator registers 4 a + b
+    constexpr int NRI = METRIC == 1 ? RT : 1;
+    auto load_epi = [&](int64_t st_, uint32_t (&g_)[QT], f32x4 (&r_)[NRI][4]) {
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) {
+            const int qg = qb * QB + qt * 32 + (lane & 31);
+            g_[qt] = qg < B ? gthr[qg] : 0u;
+        }
+        if constexpr (METRIC == 1) {
+            const int64_t tt = (st_ * NW + wv) * RT;
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+                for (int a = 0; a < 4; ++a)
+                    r_[rt][a] = *(const f32x4*)(rinit + (tt + rt) * 32 + 8 * a + 4 * (lane >> 5));
+        }
+    };
+    uint32_t gkn[QT];
+    f32x4 rin[NRI][4];
+    if (s_begin < s_end) load_epi(s_begin, gkn, rin);
+
+    for (int64_t s = s_begin; s < s_end; ++s) {
+        const int64_t t0 = (s * NW + wv) * RT;
+        const float* xs = Xq + corpus_block((uint64_t)t0, 0, 0, G);
+        const float* xn = (s + 1 < s_end) ? Xq + corpus_block((uint64_t)(t0 + NW * RT), 0, 0, G) : xs;
+        i32x16 aH[RT][QT], aL[RT][QT];
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+            i32x16 init;
+#pragma unroll
+            for (int v = 0; v < 16; ++v) init[v] = 0;
+            if constexpr (METRIC == 1) {
+#pragma unroll
+                for (int a = 0; a < 4; ++a)
+#pragma unroll
+                    for (int b2 = 0; b2 < 4; ++b2) init[4 * a + b2] = __float2int_rn(rin[METRIC == 1 ? rt : 0][a][b2] * invU);
+            }
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt) {
+                aH[rt][qt] = init;
+#pragma unroll
+                for (int v = 0; v < 16; ++v) aL[rt][qt][v] = 0;
+            }
+        }
+        uint32_t gk[QT];
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) gk[qt] = gkn[qt];
+
+        auto group = [&](const int p, const int g, const float* xsrc, const float* qsrc) {
+            if constexpr (QLDS) {
+                f32x4 qn[1][QT][QPL];
+                q_lds(g + 1 < G ? g + 1 : 0, qn[0]);
+                group_mfma8<PREC, RT, QT>(xr[p], qr[0], aH, aL);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+                    for (int pl = 0; pl < XPL; ++pl)
+                        xr[p][rt][pl] = corpus_ld<NT>(xsrc + pl * XPLANE + rt * BLOCK_FLOATS + lane4);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+                    for (int pl = 0; pl < QPL; ++pl) qr[0][qt][pl] = qn[0][qt][pl];
+                (void)qsrc;
+            } else {
+                group_mfma8<PREC, RT, QT>(xr[p], qr[p % PQ], aH, aL);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+                    for (int pl = 0; pl < XPL; ++pl)
+                        xr[p][rt][pl] = corpus_ld<NT>(xsrc + pl * XPLANE + rt * BLOCK_FLOATS + lane4);
+#pragma unroll
+                for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+                    for (int pl = 0; pl < QPL; ++pl)
+                        qr[p % PQ][qt][pl] = *(const f32x4*)(qsrc + pl * PLANE + qt * BLOCK_FLOATS + lane4);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        };
+        int gb = 0;
+        for (; gb < G - PX; gb += PX) {
+#pragma unroll
+            for (int p = 0; p < PX; ++p)
+                group(p, gb + p, xs + (size_t)(gb + p + PX) * XGSTEP, Qbase + (size_t)(gb + p + PQ) * GSTEP);
+        }
+        if (s + 1 < s_end) load_epi(s + 1, gkn, rin);
+#pragma unroll
+        for (int p = 0; p < PX; ++p)
+            group(p, gb + p, xn + (size_t)p * XGSTEP, Qbase + (size_t)(gb + p + PQ) * GSTEP);
+
+        // ---- epilogue ----
+        float thh[QT];
+        int thi[QT];
+        bool qok[QT];
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) {
+            const int ql = qt * 32 + (lane & 31);
+            const float thr = fmaxf(s_thr[ql], key_to_float(gk[qt]));
+            thh[qt] = METRIC == 0 ? thr : 0.5f * thr;
+            thi[qt] = h_floor(thh[qt], qsl[qt], invU);
+            qok[qt] = qb * QB + ql < B;
+        }
+        // register by register (v_cmp + a wave-uniform branch), as scan2: the fp32 (half-)score
+        // H uH + L uL of each candidate register; lanes whose score passes append
+        auto insert_pass = [&](int rt, int qt, float th, uint32_t cand) -> uint32_t {
+            const int ql = qt * 32 + (lane & 31);
+            uint32_t left = 0;
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+                const float sv = HL ? fmaf((float)aH[rt][qt][v], uH, (float)aL[rt][qt][v] * uL)
+                                    : (float)aH[rt][qt][v] * uH;
+                const bool p = ((cand >> v) & 1u) && sv > th;
+                if (__any(p)) {
+                    if (p) {
+                        float a_ = sv;
+                        uint32_t rb = (uint32_t)((t0 + rt) * 32) + 4u * (uint32_t)(lane >> 5);
+                        asm volatile("" : "+v"(a_), "+v"(rb));
+                        const float sc = METRIC == 0 ? a_ : 2.0f * a_;
+                        const int pos = atomicAdd(&s_cnt[ql], 1);
+                        if (pos < CAP) {
+                            s_sc[ql * CAP + pos] = sc;
+                            s_ix[ql * CAP + pos] = rb + (uint32_t)((v & 3) + 8 * (v >> 2));
+                        } else {
+                            left |= 1u << v;
+                        }
+                    }
+                }
+            }
+            return left;
+        };
+        uint32_t pend[RT][QT];
+        uint32_t any_left = 0;
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt) {
+                pend[rt][qt] = 0u;
+                if (__any(qok[qt] && imax16(aH[rt][qt]) > thi[qt])) {
+                    const uint32_t valid = qok[qt] ? tile_valid16(mask, t0 + rt, N, lane) : 0u;
+                    pend[rt][qt] = insert_pass(rt, qt, thh[qt], valid);
+                    any_left |= pend[rt][qt];
+                }
+            }
+        // compaction rounds (as scan2): lockstep = a workgroup barrier per step; FLAGSYNC = a wave
+        // with leftovers raises s_need and the others join at their step end
+        for (bool joined = false;; joined = true) {
+            if constexpr (!FLAGSYNC) {
+                if (!__syncthreads_or(any_left != 0)) break;
+            } else {
+                const bool mine = __any(any_left != 0);
+                if (mine && lane == 0) *(volatile int*)&s_need = 1;
+                if (!mine && (joined || !__builtin_amdgcn_readfirstlane(*(volatile int*)&s_need))) break;
+                __syncthreads();  // B1
+            }
+            for (int q = wv; q < QB; q += NW)
+                if (s_cnt[q] >= CAP)
+                    compact_query<KW, CAP>(s_sc + q * CAP, s_ix + q * CAP, s_cnt + q, s_thr + q,
+                                           KW == KP && qb * QB + q < B ? gthr + qb * QB + q : nullptr);
+            if (FLAGSYNC && threadIdx.x == 0) *(volatile int*)&s_need = 0;
+            __syncthreads();  // B2
+            any_left = 0;
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+                for (int qt = 0; qt < QT; ++qt) {
+                    if (!__any(pend[rt][qt] != 0)) continue;
+                    const int ql = qt * 32 + (lane & 31);
+                    const float thr = fmaxf(s_thr[ql], key_to_float(gk[qt]));
+                    pend[rt][qt] = insert_pass(rt, qt, METRIC == 0 ? thr : 0.5f * thr, pend[rt][qt]);
+                    any_left |= pend[rt][qt];
+                }
+        }
+    }
+
+    // FLAGSYNC: keep answering compaction rounds until every wave is past its last step
+    if (FLAGSYNC && lane == 0) atomicAdd(&s_done, 1);
+    for (; FLAGSYNC;) {
+        if (lane == 0) *(volatile int*)&s_need = 1;
+        __syncthreads();  // B1
+        if (__builtin_amdgcn_readfirstlane(*(volatile int*)&s_done) == NW) break;
+        for (int q = wv; q < QB; q += NW)
+            if (s_cnt[q] >= CAP)
+                compact_query<KW, CAP>(s_sc + q * CAP, s_ix + q * CAP, s_cnt + q, s_thr + q,
+                                       KW == KP && qb * QB + q < B ? gthr + qb * QB + q : nullptr);
+        if (threadIdx.x == 0) *(volatile int*)&s_need = 0;
+        __syncthreads();  // B2
+    }
+
+    // ---- flush: entries above the shared bound -> global per-query lists ----
+    __syncthreads();
+    uint32_t tkey = 0;
+    if (lane < QPW && qb * QB + wv + NW * lane < B) {
+        const int q = wv + NW * lane;
+        uint32_t dk = 0;
+        if (KW < KP && s_begin < s_end) {  // this workgroup's drop bound (its KW-th best, once compacted)
+            dk = s_thr[q] == -INFINITY ? 0u : order_key(s_thr[q]);
+            if (dk) atomicMax(gthr + qb * QB + q, dk);
+        }
+        tkey = max(gthr[qb * QB + q], dk);
+    }
+    append_flush<CAP>(s_sc, s_ix, s_cnt, wv, NW, QPW, qb * QB, B, tkey, gl_s, gl_i, gl_cnt, gl_cap);
+}
+
+// ---- launch templates ----
+template <int P, int M, int QT, int PX, int KP, int CAP, bool NT, bool QL, bool FS, int GC, int RT_ = scan8_rt(P, M),
+          int KW = KP>
+static hipError_t scan8_launch_g(const float* Xq, const float* rinit, const uint32_t* mask, const float* Qq,
+                                 const float* lsl, const float* qscal, int G, int64_t N, int B, int n_qblocks,
+                                 int64_t n_steps, int n_wg, int spw, float* gl_s, uint32_t* gl_i, uint32_t* gl_cnt,
+                                 int64_t gl_cap, uint32_t* gthr, hipStream_t st) {
+    auto k = scan8_kernel<P, M, QT, PX, KP, CAP, NT, QL, FS, GC, RT_, KW>;
+    const size_t lds = QL ? (size_t)G * 2 * QT * 1024 : 0;
+    if (QL) {
+        static std::atomic<size_t> lds_set{0};
+        size_t cur = lds_set.load();
+        while (lds > cur) {
+            hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (e != hipSuccess) return e;
+            if (lds_set.compare_exchange_weak(cur, lds)) break;
+        }
+    }
+    const int n_wg8 = (n_wg + 7) / 8 * 8;
+    hipLaunchKernelGGL(k, dim3(n_wg8 * n_qblocks), dim3(64 * S8_NW), lds, st, Xq, rinit, mask, Qq, lsl, qscal, G, N, B,
+                       n_steps, spw, n_qblocks, gl_s, gl_i, gl_cnt, gl_cap, gthr);
+    return hipGetLastError();
+}
+
+template <int P, int M, int QT, int PX, int KP, int CAP, bool NT, bool QL, bool FS>
+static hipError_t scan8_launch(const float* Xq, const float* rinit, const uint32_t* mask, const float* Qq,
+                               const float* lsl, const float* qscal, int G, int64_t N, int B, int n_qblocks,
+                               int64_t n_steps, int n_wg, int spw, float* gl_s, uint32_t* gl_i, uint32_t* gl_cnt,
+                               int64_t gl_cap, uint32_t* gthr, hipStream_t st) {
+    if constexpr (QL) {
+        if (G == 4)  // D = 128: the group loop unrolls, and the whole next step is in flight
+            return scan8_launch_g<P, M, QT, 4, KP, CAP, NT, QL, FS, 4>(Xq, rinit, mask, Qq, lsl, qscal, G, N, B,
+                                                                        n_qblocks, n_steps, n_wg, spw, gl_s, gl_i,
+                                                                        gl_cnt, gl_cap, gthr, st);
+    }
+    return scan8_launch_g<P, M, QT, PX, KP, CAP, NT, QL, FS, 0>(Xq, rinit, mask, Qq, lsl, qscal, G, N, B, n_qblocks,
+                                                                n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr,
+                                                                st);
+}
+
+// The query block goes to LDS when it is small (short rows: 64 queries x 128 dims x 2 planes =
+// 16 KiB).
+inline bool scan8_qlds(int G8, int KP) { return (size_t)G8 * 2 * (KP == 256 ? 1 : 2) * 1024 <= 32 * 1024; }
+
+#define S8_UNIT_PARAMS                                                                                             \
+    int KP, const float *Xq, const float *rinit, const uint32_t *mask, const float *Qq, const float *lsl,          \
+        const float *qscal, int G, int64_t N, int B, int n_qblocks, int64_t n_steps, int n_wg, int spw,           \
+        float *gl_s, uint32_t *gl_i, uint32_t *gl_cnt, int64_t gl_cap, uint32_t *gthr, bool nt, bool ql, bool fs, \
+        hipStream_t st
+#define S8_ARGS Xq, rinit, mask, Qq, lsl, qscal, G, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, st
+#define S8_ONE(P, M, KPV, QTV, PXV, CAPV, NTV, QLV, FSV) \
+    if (KP == KPV && nt == NTV && ql == QLV && fs == FSV)  \
+        return scan8_launch<P, M, QTV, PXV, KPV, CAPV, NTV, QLV, FSV>(S8_ARGS);
+#define S8_KP(P, M, PXV, NTV, QLV, FSV)          \
+    S8_ONE(P, M, 32, 2, PXV, 128, NTV, QLV, FSV)  \
+    S8_ONE(P, M, 64, 2, PXV, 128, NTV, QLV, FSV)  \
+    S8_ONE(P, M, 128, 2, PXV, 192, NTV, QLV, FSV) \
+    S8_ONE(P, M, 256, 1, PXV, 320, NTV, QLV, FSV)
+#define S8_MODES(P, M, PXV, PXL)                                               \
+    S8_KP(P, M, PXV, false, false, false) S8_KP(P, M, PXV, true, false, false) \
+    S8_KP(P, M, PXL, false, true, false) S8_KP(P, M, PXL, false, true, true)   \
+    S8_KP(P, M, PXV, false, false, true) S8_KP(P, M, PXV, true, false, true)
+#define S8_UNIT(NAME, P, M, PXV, PXL)  \
+    hipError_t NAME(S8_UNIT_PARAMS) {  \
+        S8_MODES(P, M, PXV, PXL)       \
+        return hipErrorInvalidValue;   \
+    }
+hipError_t launch_scan8_i1c(S8_UNIT_PARAMS);
+hipError_t launch_scan8_i1l(S8_UNIT_PARAMS);
+hipError_t launch_scan8_i3c(S8_UNIT_PARAMS);
+hipError_t launch_scan8_i3l(S8_UNIT_PARAMS);
+
+}  // namespace vdb

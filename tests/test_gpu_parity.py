@@ -31,7 +31,7 @@ def _mask_words(mask_bool):
     return np.packbits(bits, bitorder="little").view("<u4").astype(np.uint32)
 
 
-PRECISIONS = ["bf16x3", "bf16", "fp32", "auto"]
+PRECISIONS = ["bf16x3", "bf16", "fp32", "auto", "i8", "i8x3"]
 
 
 def _check(vdb, V, Q, k, metric, mask=None, force_exact=False, margin=None, chunked_add=False, precision="bf16x3",
@@ -108,6 +108,7 @@ def test_finish_split(vdb, split, metric):
     Q = rng.random((40, 200), dtype=np.float32)
     _check(vdb, V, Q, 25, metric, params={"finish_split": split})
     _check(vdb, V, Q, 25, metric, precision="bf16", params={"finish_split": split})
+    _check(vdb, V, Q, 25, metric, precision="i8", params={"finish_split": split})
 
 
 @pytest.mark.parametrize("precision", ["bf16x3", "bf16"])
@@ -161,15 +162,22 @@ def test_precision_switch_keeps_results(vdb):
     b = ix.search(Q, 17, with_keys=True)
     ix.set_precision("bf16")
     c = ix.search(Q, 17, with_keys=True)
+    ix.set_precision("i8")
+    d = ix.search(Q, 17, with_keys=True)
+    ix.set_precision("i8x3")
+    e = ix.search(Q, 17, with_keys=True)
+    ix.set_precision("bf16")
+    f = ix.search(Q, 17, with_keys=True)
     es, ei, ek = ref_cpu.exact_search(Q, V, 17, "euclidean")
-    for s, i, kk in (a, b, c):
+    for s, i, kk in (a, b, c, d, e, f):
         np.testing.assert_array_equal(i, ei)
         np.testing.assert_array_equal(kk, ek)
     assert ix.stat("fallback_queries") == 0
 
 
+@pytest.mark.parametrize("precision", ["bf16", "i8"])
 @pytest.mark.parametrize("metric", ["cosine", "euclidean"])
-def test_bf16_directional_residual_bound(vdb, metric):
+def test_bf16_directional_residual_bound(vdb, metric, precision):
     """bf16 certificate with the corpus-rounding bound taken along the rows' mean direction
     (|q - c dir| R + |c| M): on uniform rows (one shared direction) it certifies the queries
     that Cauchy-Schwarz's |q| R leaves uncertified; results are exact either way."""
@@ -180,7 +188,7 @@ def test_bf16_directional_residual_bound(vdb, metric):
     es, ei, ek = ref_cpu.exact_search(Q, V, k, metric)
     fb = {}
     for dirb in (1, 0):
-        ix = vdb.NativeIndex(D, metric, precision="bf16")
+        ix = vdb.NativeIndex(D, metric, precision=precision)
         ix.set_param("dir_bound", dirb)
         ix.add(V)
         s, i, kk = ix.search(Q, k, with_keys=True)
@@ -188,14 +196,25 @@ def test_bf16_directional_residual_bound(vdb, metric):
         np.testing.assert_array_equal(kk, ek)
         fb[dirb] = ix.stat("fallback_queries")
         ix.close()
-    print(f"{metric}: bf16 fallbacks with the directional bound {fb[1]}, Cauchy-Schwarz {fb[0]} of {B}")
+    print(f"{metric}: {precision} fallbacks with the directional bound {fb[1]}, Cauchy-Schwarz {fb[0]} of {B}")
     assert fb[1] <= fb[0], fb
-    if metric == "cosine":  # (1M x 1536, B = 256: 0 vs every query, profiles/r02s_ab/s4_c3_bf16*.json)
-        assert fb[1] == 0, fb
+    if metric == "cosine" and precision == "bf16":  # (1M x 1536, B = 256: 0 vs every query,
+        assert fb[1] == 0, fb                          # profiles/r02s_ab/s4_c3_bf16*.json)
+    # i8 (8-bit query: a wider bound) leaves a few of these 1536-dim queries to auto's re-pass
 
 
+def _auto_index(vdb, D, a8):
+    """An auto-precision index on the int8 copy (a8 = 1: one-plane I8, x3 I8X3) or the split
+    copy (0: BF16 / BF16X3); returns it and the stat names of its one-plane / x3 passes."""
+    ix = vdb.NativeIndex(D, "cosine")
+    ix.set_param("auto_int8", a8)
+    assert ix.precision == "auto" and ix.stat("auto_int8") == a8
+    return ix, ("searches_i8", "searches_i8x3") if a8 else ("searches_bf16", "searches_bf16x3")
+
+
+@pytest.mark.parametrize("a8", [1, 0])
 @pytest.mark.parametrize("mem", ["host", "device"])
-def test_auto_precision_switches_on_fallbacks(vdb, mem):
+def test_auto_precision_switches_on_fallbacks(vdb, mem, a8):
     """VDB_PREC_AUTO runs the bf16 pass while it certifies; rows closer together than the
     bf16 residual bound leave most queries uncertified, after which the index runs bf16x3
     until its rows change (host memory: the batch itself is rerun in bf16x3; device memory:
@@ -208,8 +227,7 @@ def test_auto_precision_switches_on_fallbacks(vdb, mem):
     near = (base + 1e-4 * rng.standard_normal((N, D))).astype(np.float32)
     for V, expect_switch in ((far, False), (near, True)):
         Q = (V[rng.integers(0, N, B)] + 1e-5 * rng.standard_normal((B, D))).astype(np.float32)
-        ix = vdb.NativeIndex(D, "cosine")
-        assert ix.precision == "auto"
+        ix, (one, x3) = _auto_index(vdb, D, a8)
         ix.add(V)
         es, ei, ek = ref_cpu.exact_search(Q, V, k, "cosine")
         for _ in range(2):
@@ -225,21 +243,22 @@ def test_auto_precision_switches_on_fallbacks(vdb, mem):
                 i, kk = idd.cpu().numpy(), kd.cpu().numpy()
             np.testing.assert_array_equal(i, ei)
             np.testing.assert_array_equal(kk, ek)
-        assert ix.stat("searches_bf16") >= 1
+        assert ix.stat(one) >= 1
         if expect_switch:
-            assert ix.stat("fallback_queries") * 64 > B  # bf16x3 cannot separate these rows either
-            # host memory: the uncertified bf16 pass is rerun at once in bf16x3, then the second
-            # search runs bf16x3; device memory: the first search falls back, the second runs bf16x3
-            assert ix.stat("searches_bf16x3") == (2 if mem == "host" else 1)
-            assert ix.stat("searches_bf16") == 1
-            ix.add(V[:1])  # new rows: bf16 gets another chance
+            assert ix.stat("fallback_queries") * 64 > B  # the x3 pass cannot separate these rows either
+            # host memory: the uncertified one-plane pass is rerun at once in x3, then the second
+            # search runs x3; device memory: the first search falls back, the second runs x3
+            assert ix.stat(x3) == (2 if mem == "host" else 1)
+            assert ix.stat(one) == 1
+            ix.add(V[:1])  # new rows: the one-plane pass gets another chance
             ix.search(Q, k)
-            assert ix.stat("searches_bf16") == 2
+            assert ix.stat(one) == 2
         else:
-            assert ix.stat("searches_bf16x3") == 0 and ix.stat("fallback_queries") == 0
+            assert ix.stat(x3) == 0 and ix.stat("fallback_queries") == 0
 
 
-def test_auto_repass_keeps_bf16_for_a_few_uncertified_queries(vdb):
+@pytest.mark.parametrize("a8", [1, 0])
+def test_auto_repass_keeps_bf16_for_a_few_uncertified_queries(vdb, a8):
     """One near-duplicate query in a batch of ordinary ones: its bf16 certificate fails, it
     alone is re-passed in bf16x3 (host memory), and the index stays bf16: the next batch
     runs bf16 again (one query no longer pins the index to bf16x3)."""
@@ -250,7 +269,7 @@ def test_auto_repass_keeps_bf16_for_a_few_uncertified_queries(vdb):
     V[:400] = (base + 1e-4 * rng.standard_normal((400, D))).astype(np.float32)  # a tight cluster
     Q = rng.random((B, D), dtype=np.float32)
     Q[7] = base  # the near-duplicate query: its top-10 sit inside the cluster
-    ix = vdb.NativeIndex(D, "cosine")
+    ix, (one, x3) = _auto_index(vdb, D, a8)
     ix.add(V)
     es, ei, ek = ref_cpu.exact_search(Q, V, k, "cosine")
     for _ in range(3):
@@ -259,11 +278,12 @@ def test_auto_repass_keeps_bf16_for_a_few_uncertified_queries(vdb):
         np.testing.assert_array_equal(kk, ek)
     assert ix.stat("searches") == 3 and ix.stat("queries") == 3 * B
     assert ix.stat("repass_queries") >= 3  # query 7, every search
-    assert ix.stat("searches_bf16") == 3  # never switched
+    assert ix.stat(one) == 3  # never switched
     assert ix.stat("auto_hold") == 0
 
 
-def test_auto_hold_expires(vdb):
+@pytest.mark.parametrize("a8", [1, 0])
+def test_auto_hold_expires(vdb, a8):
     """A failure too large for a re-pass starts a hold of 16 bf16x3 searches; after it the
     index probes bf16 again (and, on data that still fails, holds twice as long)."""
     rng = np.random.default_rng(43)
@@ -271,19 +291,19 @@ def test_auto_hold_expires(vdb):
     base = rng.random(D, dtype=np.float32)
     near = (base + 1e-4 * rng.standard_normal((N, D))).astype(np.float32)
     Q = (near[rng.integers(0, N, B)] + 1e-5 * rng.standard_normal((B, D))).astype(np.float32)
-    ix = vdb.NativeIndex(D, "cosine")
+    ix, (one, x3) = _auto_index(vdb, D, a8)
     ix.add(near)
     es, ei, ek = ref_cpu.exact_search(Q, near, k, "cosine")
-    s, i, kk = ix.search(Q, k, with_keys=True)  # bf16 fails for most queries -> rerun in bf16x3
+    s, i, kk = ix.search(Q, k, with_keys=True)  # one-plane fails for most queries -> rerun in x3
     np.testing.assert_array_equal(i, ei)
-    assert ix.stat("searches_bf16") == 1 and ix.stat("auto_hold") == 16
+    assert ix.stat(one) == 1 and ix.stat("auto_hold") == 16
     for _ in range(16):
         s, i, kk = ix.search(Q, k, with_keys=True)
         np.testing.assert_array_equal(kk, ek)
-    assert ix.stat("searches_bf16") == 1 and ix.stat("auto_hold") == 0
-    s, i, kk = ix.search(Q, k, with_keys=True)  # the probe: bf16 again, fails again -> hold 32
+    assert ix.stat(one) == 1 and ix.stat("auto_hold") == 0
+    s, i, kk = ix.search(Q, k, with_keys=True)  # the probe: one-plane again, fails again -> hold 32
     np.testing.assert_array_equal(i, ei)
-    assert ix.stat("searches_bf16") == 2 and ix.stat("auto_hold") == 32
+    assert ix.stat(one) == 2 and ix.stat("auto_hold") == 32
     assert ix.stat("searches") == 18 and ix.stat("queries") == 18 * B
 
 
@@ -608,3 +628,68 @@ def test_scan2_q4_shape(vdb, metric):
     np.testing.assert_array_equal(i, ei)
     np.testing.assert_array_equal(kk, ek)
     ix.close()
+
+
+@pytest.mark.parametrize("precision", ["i8", "i8x3"])
+@pytest.mark.parametrize("metric", ["cosine", "euclidean"])
+def test_i8_quantisation_edges(vdb, metric, precision):
+    """The int8 copy (vdb_scan8_kernel.h): centring row and quantisation step come from the
+    first add, are derived again as a small index doubles, and rows past the step's range
+    clip (their residual enters the certificate); L2 rows far from the origin push the query
+    scale up (int32 range of H's start value).  Every result stays exact."""
+    rng = np.random.default_rng(77)
+    D, k = 200, 12
+    cases = []
+    V = rng.random((9000, D), dtype=np.float32)
+    cases.append(("tiny first add", V, [1, 2, 5, 40, 952, 8000]))
+    W = rng.random((9000, D), dtype=np.float32)
+    W[5000:] *= 10.0  # past the range fixed by the first 5000 rows... until the re-derivation
+    cases.append(("outliers after the setup", W, [5000, 4000]))
+    W2 = rng.random((70000, 64), dtype=np.float32)
+    W2[66000:] = W2[66000:] * 30.0 - 15.0  # past kDirRows: the setup stays, these rows clip
+    cases.append(("outliers past kDirRows", W2, [66000, 4000]))
+    F = (1000.0 + rng.random((6000, D), dtype=np.float32)).astype(np.float32)
+    cases.append(("far from the origin", F, [6000]))
+    Z = rng.random((3000, D), dtype=np.float32)
+    Z[100:110] = 0.0
+    cases.append(("zero rows", Z, [3000]))
+    for name, V, pieces in cases:
+        Dv = V.shape[1]
+        Q = rng.random((11, Dv), dtype=np.float32) * (V.max() - V.min()) + V.min()
+        Q[0] = V[123]
+        if name == "zero rows":
+            Q[1] = 0.0
+        ix = vdb.NativeIndex(Dv, metric, precision=precision)
+        r = 0
+        for p in pieces:
+            ix.add(V[r:r + p])
+            r += p
+        s, i, kk = ix.search(Q, k, with_keys=True)
+        es, ei, ek = ref_cpu.exact_search(Q, V, k, metric)
+        np.testing.assert_array_equal(i, ei, err_msg=name)
+        valid = ei >= 0
+        np.testing.assert_array_equal(kk[valid], ek[valid], err_msg=name)
+        print(f"{metric} {precision} {name}: fallbacks {ix.stat('fallback_queries')} of {Q.shape[0]}")
+        ix.close()
+
+
+@pytest.mark.parametrize("metric", ["cosine", "euclidean"])
+def test_i8_store_filled_one_add_at_a_time(vdb, metric):
+    """A store filled by many small adds (the REST path: one vector per request) gets a
+    usable int8 setup: after the re-derivations the int8 pass certifies the batch."""
+    rng = np.random.default_rng(5)
+    D, k = 96, 10
+    V = rng.random((3000, D), dtype=np.float32)
+    ix = vdb.NativeIndex(D, metric, precision="i8")
+    r = 0
+    while r < V.shape[0]:
+        n = int(rng.integers(1, 8))
+        ix.add(V[r:r + n])
+        r += n
+    Q = rng.random((16, D), dtype=np.float32)
+    s, i, kk = ix.search(Q, k, with_keys=True)
+    es, ei, ek = ref_cpu.exact_search(Q, V, k, metric)
+    np.testing.assert_array_equal(i, ei)
+    np.testing.assert_array_equal(kk, ek)
+    assert ix.stat("searches_i8") == 1
+    assert ix.stat("fallback_queries") <= 2, ix.stat("fallback_queries")
