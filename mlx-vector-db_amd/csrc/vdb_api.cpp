@@ -105,6 +105,7 @@ struct vdb_index {
     float* X = nullptr;   // row-major fp32 [cap_rows][Dp] (rerank, exact scan, export, graph)
     float* Xs = nullptr;  // the candidate pass's copy, same bytes: split-bf16 tiles (PREC_BF16X3 / BF16 /
                           // AUTO) or fp32 tiles (PREC_FP32), rebuilt from X when the precision class changes
+    float* Xq = nullptr;  // the int8 copy (PREC_I8 / I8X3, AUTO with auto_i8): half the bytes of X
     double* nrm64 = nullptr;
     float* inv32 = nullptr;
     float* sq32 = nullptr;
@@ -143,6 +144,13 @@ struct vdb_index {
     // near-duplicate query no longer pins the index to BF16X3, and a corpus that never certifies
     // in BF16 pays a probe only once per 2048 searches.
     std::atomic<int> auto_hold{0}, auto_fails{0}, auto_ok{0};
+    // With auto_i8, the one-plane pass is I8 (the int8 copy); an I8 failure too large for a
+    // re-pass holds BF16 (the split copy) instead for 16 << (fails8 - 1) searches (up to 2048;
+    // fails8 resets after 64 I8 searches without a new failure, both when the rows change), so
+    // data where the 8-bit query's wider bound does not certify (1M x 1536) runs BF16 and probes
+    // I8 rarely.  last_i8: the last one-plane pass was I8 (device-memory failures arrive late).
+    std::atomic<int> auto_hold8{0}, auto_fails8{0}, auto_ok8{0};
+    std::atomic<bool> last_i8{false};
     // The device-gated fallback total last seen: pinned mirror of d_totals[0], written by the
     // gated exact kernel of a device-memory search and read by the next search.
     std::atomic<unsigned long long> auto_seen{0};
@@ -202,25 +210,30 @@ void free_workspace_memory(Workspace* w) {
 
 int wait_idle(vdb_index* ix);
 
-// The candidate copy a precision setting uses: fp32 tiles, split-bf16 tiles or the int8 copy.
-enum CopyClass { kCopyFp32 = 0, kCopySplit = 1, kCopyInt8 = 2 };
-int copy_class(int64_t precision, bool auto_i8) {
-    if (precision == VDB_PREC_FP32) return kCopyFp32;
-    if (precision == VDB_PREC_I8 || precision == VDB_PREC_I8X3 || (precision == VDB_PREC_AUTO && auto_i8))
-        return kCopyInt8;
-    return kCopySplit;
+// The candidate copies a precision setting keeps: Xs holds fp32 tiles (FP32), split-bf16 tiles
+// (BF16 / BF16X3 / AUTO) or nothing (I8 / I8X3); Xq the int8 copy (I8 / I8X3, AUTO with auto_i8:
+// AUTO keeps both and picks per batch, vdb_index_search).
+enum XsKind { kXsNone = -1, kXsFp32 = 0, kXsSplit = 1 };
+int xs_kind(int64_t precision) {
+    if (precision == VDB_PREC_FP32) return kXsFp32;
+    if (precision == VDB_PREC_I8 || precision == VDB_PREC_I8X3) return kXsNone;
+    return kXsSplit;
+}
+bool needs_i8(int64_t precision, bool auto_i8) {
+    return precision == VDB_PREC_I8 || precision == VDB_PREC_I8X3 || (precision == VDB_PREC_AUTO && auto_i8);
 }
 
-// The candidate copy of rows [row0, row0 + n) from the row-major rows (whole row tiles; the int8
-// copy row by row, its statistics into d_i8).
-hipError_t build_candidate_rows(const vdb_index* ix, const float* X, const float* inv32, int64_t row0, int64_t n,
-                                float* Xs, hipStream_t st) {
-    const float* inv = ix->metric == VDB_METRIC_COSINE ? inv32 : nullptr;
-    switch (copy_class(ix->precision, ix->auto_i8)) {
-        case kCopyFp32: return launch_tile_rows(X, ix->G, row0, n, Xs, st);
-        case kCopyInt8: return launch_quant_rows(X, inv, ix->d_mu, ix->d_dir, ix->sx, row0, n, ix->G, Xs, ix->d_i8, st);
-        default: return launch_split_rows(X, ix->G, row0, n, inv, Xs, st);
-    }
+// The candidate copies of rows [row0, row0 + n) from the row-major rows (tiles: whole row tiles;
+// the int8 copy row by row, its statistics into d_i8).  xs / xq: which copies to build.
+hipError_t build_candidate_rows(const vdb_index* ix, int64_t row0, int64_t n, hipStream_t st, bool xs = true,
+                                bool xq = true) {
+    const float* inv = ix->metric == VDB_METRIC_COSINE ? ix->inv32 : nullptr;
+    hipError_t e = hipSuccess;
+    if (xs && xs_kind(ix->precision) == kXsFp32) e = launch_tile_rows(ix->X, ix->G, row0, n, ix->Xs, st);
+    if (xs && xs_kind(ix->precision) == kXsSplit) e = launch_split_rows(ix->X, ix->G, row0, n, inv, ix->Xs, st);
+    if (e == hipSuccess && xq && needs_i8(ix->precision, ix->auto_i8))
+        e = launch_quant_rows(ix->X, inv, ix->d_mu, ix->d_dir, ix->sx, row0, n, ix->G, ix->Xq, ix->d_i8, st);
+    return e;
 }
 
 // Host copies of the int8 copy's row statistics (after the kernels that update them).
@@ -245,6 +258,7 @@ int ensure_capacity(vdb_index* ix, int64_t rows) {
     const size_t x_bytes = (size_t)(cap / 32) * tile_floats * sizeof(float);
     float* X = nullptr;
     float* Xs = nullptr;
+    float* Xq = nullptr;
     double* n64 = nullptr;
     float *i32 = nullptr, *s32 = nullptr, *r32 = nullptr;
     // All new buffers are allocated and filled before the index switches to them; on
@@ -252,7 +266,7 @@ int ensure_capacity(vdb_index* ix, int64_t rows) {
     // and the index keeps its current buffers, so a later retry sees the same HBM.
     auto fail = [&](hipError_t e, const char* what) {
         (void)hipStreamSynchronize(ix->stream);
-        for (void* p : {(void*)X, (void*)Xs, (void*)n64, (void*)i32, (void*)s32, (void*)r32})
+        for (void* p : {(void*)X, (void*)Xs, (void*)Xq, (void*)n64, (void*)i32, (void*)s32, (void*)r32})
             if (p) (void)hipFree(p);
         return set_error(e == hipErrorOutOfMemory ? VDB_ERR_OOM : VDB_ERR_HIP,
                          "growing the index to %lld rows: %s failed: %s", (long long)cap, what, hipGetErrorString(e));
@@ -265,6 +279,8 @@ int ensure_capacity(vdb_index* ix, int64_t rows) {
     CAP_TRY(hipMalloc(&X, x_bytes));
     CAP_TRY(hipMalloc(&Xs, x_bytes));
     CAP_TRY(hipMemsetAsync(Xs, 0, x_bytes, ix->stream));
+    CAP_TRY(hipMalloc(&Xq, x_bytes / 2));
+    CAP_TRY(hipMemsetAsync(Xq, 0, x_bytes / 2, ix->stream));
     CAP_TRY(hipMalloc(&n64, cap * sizeof(double)));
     CAP_TRY(hipMalloc(&i32, cap * sizeof(float)));
     CAP_TRY(hipMalloc(&s32, cap * sizeof(float)));
@@ -280,6 +296,8 @@ int ensure_capacity(vdb_index* ix, int64_t rows) {
                                ix->stream));
         CAP_TRY(hipMemcpyAsync(Xs, ix->Xs, (size_t)used_tiles * tile_floats * sizeof(float), hipMemcpyDeviceToDevice,
                                ix->stream));
+        CAP_TRY(hipMemcpyAsync(Xq, ix->Xq, (size_t)used_tiles * tile_floats * sizeof(float) / 2,
+                               hipMemcpyDeviceToDevice, ix->stream));
         CAP_TRY(hipMemcpyAsync(n64, ix->nrm64, ix->count * sizeof(double), hipMemcpyDeviceToDevice, ix->stream));
         CAP_TRY(hipMemcpyAsync(i32, ix->inv32, ix->count * sizeof(float), hipMemcpyDeviceToDevice, ix->stream));
         CAP_TRY(hipMemcpyAsync(s32, ix->sq32, ix->count * sizeof(float), hipMemcpyDeviceToDevice, ix->stream));
@@ -290,6 +308,7 @@ int ensure_capacity(vdb_index* ix, int64_t rows) {
     if (ix->X) {
         (void)hipFree(ix->X);
         if (ix->Xs) (void)hipFree(ix->Xs);
+        if (ix->Xq) (void)hipFree(ix->Xq);
         (void)hipFree(ix->nrm64);
         (void)hipFree(ix->inv32);
         (void)hipFree(ix->sq32);
@@ -297,6 +316,7 @@ int ensure_capacity(vdb_index* ix, int64_t rows) {
     }
     ix->X = X;
     ix->Xs = Xs;
+    ix->Xq = Xq;
     ix->nrm64 = n64;
     ix->inv32 = i32;
     ix->sq32 = s32;
@@ -568,6 +588,7 @@ int32_t vdb_index_destroy(vdb_index* ix) {
     }
     if (ix->X) (void)hipFree(ix->X);
     if (ix->Xs) (void)hipFree(ix->Xs);
+    if (ix->Xq) (void)hipFree(ix->Xq);
     if (ix->nrm64) (void)hipFree(ix->nrm64);
     if (ix->inv32) (void)hipFree(ix->inv32);
     if (ix->sq32) (void)hipFree(ix->sq32);
@@ -608,10 +629,12 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
         if (value == ix->precision) return VDB_OK;
         const int wr = wait_idle(ix);  // queued searches read the candidate copy
         if (wr) return wr;
-        const bool rebuild = copy_class(value, ix->auto_i8) != copy_class(ix->precision, ix->auto_i8);
+        // rebuild a copy the new setting reads that the old one did not keep up to date
+        const bool xs = xs_kind(value) != kXsNone && xs_kind(value) != xs_kind(ix->precision);
+        const bool xq = needs_i8(value, ix->auto_i8) && !needs_i8(ix->precision, ix->auto_i8);
         ix->precision = value;
-        if (rebuild && ix->Xs && ix->count > 0) {  // fp32 tiles / split tiles / int8 copy
-            HIP_TRY(build_candidate_rows(ix, ix->X, ix->inv32, 0, ix->count, ix->Xs, ix->stream));
+        if ((xs || xq) && ix->Xs && ix->count > 0) {
+            HIP_TRY(build_candidate_rows(ix, 0, ix->count, ix->stream, xs, xq));
             HIP_TRY(read_i8_stats(ix, ix->stream));
         }
     } else if (n == "auto_int8") {  // VDB_PREC_AUTO's candidate copy: 1 int8, 0 split-bf16
@@ -621,10 +644,10 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
         if (v == ix->auto_i8) return VDB_OK;
         const int wr = wait_idle(ix);
         if (wr) return wr;
-        const bool rebuild = copy_class(ix->precision, v) != copy_class(ix->precision, ix->auto_i8);
+        const bool xq = needs_i8(ix->precision, v) && !needs_i8(ix->precision, ix->auto_i8);
         ix->auto_i8 = v;
-        if (rebuild && ix->Xs && ix->count > 0) {
-            HIP_TRY(build_candidate_rows(ix, ix->X, ix->inv32, 0, ix->count, ix->Xs, ix->stream));
+        if (xq && ix->Xs && ix->count > 0) {
+            HIP_TRY(build_candidate_rows(ix, 0, ix->count, ix->stream, false, true));
             HIP_TRY(read_i8_stats(ix, ix->stream));
         }
     } else if (n == "margin") {
@@ -712,6 +735,7 @@ int32_t vdb_index_get_stat(const vdb_index* cix, const char* name, int64_t* valu
     else if (n == "searches_scan3") *value = ix->n_scan3.load();
     else if (n == "searches_q4") *value = ix->n_q4.load();
     else if (n == "auto_hold") *value = ix->auto_hold.load();
+    else if (n == "auto_hold8") *value = ix->auto_hold8.load();
     else if (n == "overflow_queries") *value = ix->n_overflow.load() + (int64_t)dt[1];
     else if (n == "capacity") *value = ix->cap_rows;
     else if (n == "scan_ns") *value = ix->scan_ns.load();
@@ -726,7 +750,7 @@ int32_t vdb_index_get_stat(const vdb_index* cix, const char* name, int64_t* valu
     else if (n == "searches_i8x3") *value = ix->n_by_prec[PREC_I8X3].load();
     else if (n == "auto_int8") *value = ix->auto_i8 ? 1 : 0;
     else if (n == "device_bytes")
-        *value = (int64_t)(ix->cap_rows / 32) * ix->G * BLOCK_FLOATS * 4 * 2 + ix->cap_rows * 20;
+        *value = (int64_t)(ix->cap_rows / 32) * ix->G * BLOCK_FLOATS * 10 + ix->cap_rows * 20;  // X, Xs, Xq
     else return set_error(VDB_ERR_INVALID, "unknown stat '%s'", name);
     return VDB_OK;
 }
@@ -820,7 +844,7 @@ int32_t vdb_index_add(vdb_index* ix, const float* vectors, int64_t n, int32_t me
                 e = launch_pack_rows(staging, m, D, ix->G, ix->X, ix->count + r, ix->nrm64, ix->inv32, ix->sq32,
                                      ix->rinit32, ix->metric == VDB_METRIC_COSINE, ix->d_xmax, ix->d_nonfinite, st);
             if (e == hipSuccess) e = setup_direction(ix, ix->count + r, m, st);
-            if (e == hipSuccess) e = build_candidate_rows(ix, ix->X, ix->inv32, ix->count + r, m, ix->Xs, st);
+            if (e == hipSuccess) e = build_candidate_rows(ix, ix->count + r, m, st);
             if (e == hipSuccess) e = residual_direction(ix, ix->count + r, m, st);
             if (e == hipSuccess) e = hipStreamSynchronize(st);  // staging reuse
             if (e != hipSuccess) {
@@ -831,7 +855,7 @@ int32_t vdb_index_add(vdb_index* ix, const float* vectors, int64_t n, int32_t me
             HIP_TRY(launch_pack_rows(src, m, D, ix->G, ix->X, ix->count + r, ix->nrm64, ix->inv32, ix->sq32,
                                      ix->rinit32, ix->metric == VDB_METRIC_COSINE, ix->d_xmax, ix->d_nonfinite, st));
             HIP_TRY(setup_direction(ix, ix->count + r, m, st));
-            HIP_TRY(build_candidate_rows(ix, ix->X, ix->inv32, ix->count + r, m, ix->Xs, st));
+            HIP_TRY(build_candidate_rows(ix, ix->count + r, m, st));
             HIP_TRY(residual_direction(ix, ix->count + r, m, st));
         }
     }
@@ -864,8 +888,7 @@ int32_t vdb_index_add(vdb_index* ix, const float* vectors, int64_t n, int32_t me
         HIP_TRY(hipMemsetAsync(ix->d_xmax + 3, 0, 8, st));
         HIP_TRY(hipMemsetAsync(ix->d_i8, 0, 64, st));
         HIP_TRY(setup_direction(ix, 0, all, st));
-        if (copy_class(ix->precision, ix->auto_i8) == kCopyInt8)
-            HIP_TRY(build_candidate_rows(ix, ix->X, ix->inv32, 0, all, ix->Xs, st));
+        if (needs_i8(ix->precision, ix->auto_i8)) HIP_TRY(build_candidate_rows(ix, 0, all, st, false, true));
         HIP_TRY(residual_direction(ix, 0, all, st));
         HIP_TRY(hipMemcpyAsync(xb, ix->d_xmax, sizeof(xb), hipMemcpyDeviceToHost, st));
         HIP_TRY(read_i8_stats(ix, st));
@@ -877,8 +900,12 @@ int32_t vdb_index_add(vdb_index* ix, const float* vectors, int64_t n, int32_t me
     ix->xres_abs = xm[2];
     ix->xres_dir = xm[3];
     ix->count += n;
-    ix->auto_hold = 0;  // new rows: VDB_PREC_AUTO tries BF16 again
+    ix->auto_hold = 0;  // new rows: VDB_PREC_AUTO tries the one-plane passes again
     ix->auto_fails = 0;
+    ix->auto_hold8 = 0;
+    ix->auto_fails8 = 0;
+    // device-memory failures already landed belong to the old rows: they start no hold
+    if (ix->h_totals) ix->auto_seen = ix->h_totals[0];
     return VDB_OK;
 }
 
@@ -903,6 +930,9 @@ int32_t vdb_index_clear(vdb_index* ix) {
         if (ix->Xs)
             HIP_TRY(hipMemsetAsync(ix->Xs, 0, (size_t)(ix->cap_rows / 32) * ix->G * BLOCK_FLOATS * sizeof(float),
                                    ix->stream));
+        if (ix->Xq)
+            HIP_TRY(hipMemsetAsync(ix->Xq, 0, (size_t)(ix->cap_rows / 32) * ix->G * BLOCK_FLOATS * sizeof(float) / 2,
+                                   ix->stream));
     }
     HIP_TRY(hipMemsetAsync(ix->d_xmax, 0, 64, ix->stream));
     HIP_TRY(hipMemsetAsync(ix->d_i8, 0, 64, ix->stream));
@@ -911,6 +941,8 @@ int32_t vdb_index_clear(vdb_index* ix) {
     ix->count = 0;
     ix->auto_hold = 0;
     ix->auto_fails = 0;
+    ix->auto_hold8 = 0;
+    ix->auto_fails8 = 0;
     ix->xmax = 0.0;
     ix->xres_rel = ix->xres_abs = 0.0;
     ix->dir_set = false;  // the next add picks a new direction (xres_dir's bits were cleared above)
@@ -974,6 +1006,21 @@ bool auto_take_hold(vdb_index* ix) {
     while (h > 0)
         if (ix->auto_hold.compare_exchange_weak(h, h - 1)) return true;
     if (++ix->auto_ok >= 64) ix->auto_fails = 0;  // probes have been certifying for a while
+    return false;
+}
+
+// The same pair for the I8 -> BF16 hold (vdb_index::auto_hold8).
+void auto_fail8(vdb_index* ix) {
+    const int f = std::min(8, ix->auto_fails8.load() + 1);
+    ix->auto_fails8 = f;
+    ix->auto_ok8 = 0;
+    ix->auto_hold8 = 16 << (f - 1);
+}
+bool auto_take_hold8(vdb_index* ix) {
+    int h = ix->auto_hold8.load();
+    while (h > 0)
+        if (ix->auto_hold8.compare_exchange_weak(h, h - 1)) return true;
+    if (++ix->auto_ok8 >= 64) ix->auto_fails8 = 0;
     return false;
 }
 
@@ -1068,7 +1115,10 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     if (auto_prec && ix->h_totals && !opt.repass) {  // fallbacks of earlier device-memory searches (lagged)
         const unsigned long long seen = ix->h_totals[0];
         const unsigned long long prev = ix->auto_seen.exchange(seen);
-        if (seen > prev) auto_fail(ix);
+        if (seen > prev) {
+            if (ix->last_i8) auto_fail8(ix);
+            else auto_fail(ix);
+        }
     }
     const bool approx = N > 0 && !(ix->force_exact || k > kMaxApproxK);
     // AUTO takes bf16x3 directly where bf16's wider certificate needs KP = 256 (k > 16): that
@@ -1076,16 +1126,19 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     // bf16x3 (C4, k = 100: 13 vs 3.9 ms, profiles/r02s_ab/s4_c4_str2.json), and in device memory
     // its uncertified queries cost the exact path
     const bool auto_b16 = k <= kAutoBf16MaxK;
-    // AUTO on the int8 copy: I8 / I8X3 where the split copy would run BF16 / BF16X3 (same rules)
-    const bool a8 = ix->auto_i8;
+    // AUTO keeps both copies with auto_i8: the one-plane pass is I8 unless an I8 hold is on
+    // (then BF16); the x3 pass (k > 16, holds, re-passes, retries) is BF16X3 -- faster than I8X3,
+    // whose two accumulator sets per tile take half BF16X3's row tiles per wave
     const bool auto_x3 = auto_prec && (opt.force_b3 || !auto_b16 || (approx && auto_take_hold(ix)));
+    const bool auto_8 = auto_prec && !auto_x3 && ix->auto_i8 && !(approx && auto_take_hold8(ix));
     const int prec_req = !ix->Xs ? PREC_FP32
                          : ix->precision == VDB_PREC_BF16X3 ? PREC_BF16X3
                          : ix->precision == VDB_PREC_BF16 ? PREC_BF16
                          : ix->precision == VDB_PREC_I8X3 ? PREC_I8X3
                          : ix->precision == VDB_PREC_I8 ? PREC_I8
-                         : auto_prec ? (auto_x3 ? (a8 ? PREC_I8X3 : PREC_BF16X3) : (a8 ? PREC_I8 : PREC_BF16))
+                         : auto_prec ? (auto_x3 ? PREC_BF16X3 : auto_8 ? PREC_I8 : PREC_BF16)
                                      : PREC_FP32;
+    if (auto_prec && approx && !auto_x3) ix->last_i8 = auto_8;
     if (approx) ix->n_by_prec[prec_req]++;
     // the "one plane" precisions (a wide certificate: KP = 128 for small k) and their re-pass
     const bool one_plane = prec_req == PREC_BF16 || prec_req == PREC_I8;
@@ -1096,6 +1149,9 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     // ~30x bf16x3's: 1M x 768 uniform needs KP = 128 for k = 10 (KP = 64 left 26% of the
     // queries uncertified; KP = 128: none of 2560)
     if (one_plane) margin_def = std::max(16, std::min(std::max(112, k / 2), 256 - k));
+    // I8 (the 8-bit query's wider bound): KP = 256.  1M x 768 uniform, B = 64: KP = 128 left one
+    // query per batch uncertified; 256 none (profiles/r03_i8/c2_i8_kp*)
+    if (prec_req == PREC_I8) margin_def = std::max(16, 256 - k);
     const int margin = ix->margin >= 0 ? (int)ix->margin : margin_def;
     int KP = std::max(32, next_pow2(k + margin));
     const bool exact_all = ix->force_exact || k > kMaxApproxK || KP > 256;
@@ -1296,7 +1352,7 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
                 HIP_TRY(hipEventRecord(tev[3], st));
             }
             const float* rowscale = ix->metric == 0 ? ix->inv32 : ix->sq32;
-            const float* Xscan = ix->Xs;  // fp32 or split tiles, per the precision class
+            const float* Xscan = i8_pass ? ix->Xq : ix->Xs;  // the copy this pass reads
             if (n_pilot > 0) {
                 if (i8_pass) {
                     HIP_TRY(launch_pilot8(prec, ix->metric, Xscan, ix->rinit32, md, Qt, q8scal, Gs, N, B,
@@ -1407,7 +1463,8 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
                     if (rc) return rc;
                     n_flag = 0;
                 } else {
-                    auto_fail(ix);
+                    if (prec == PREC_I8) auto_fail8(ix);
+                    else auto_fail(ix);
                     ix->n_searches--;  // the retry counts this search (no double count)
                     ix->n_queries -= B;
                     return kRetryBf16x3;

@@ -204,12 +204,13 @@ def test_bf16_directional_residual_bound(vdb, metric, precision):
 
 
 def _auto_index(vdb, D, a8):
-    """An auto-precision index on the int8 copy (a8 = 1: one-plane I8, x3 I8X3) or the split
-    copy (0: BF16 / BF16X3); returns it and the stat names of its one-plane / x3 passes."""
+    """An auto-precision index with (a8 = 1, the default) or without the int8 copy: its
+    one-plane pass is I8 (BF16 during an I8 hold) or BF16; the x3 pass is BF16X3 either way.
+    Returns it and the stat names of its one-plane / x3 passes."""
     ix = vdb.NativeIndex(D, "cosine")
     ix.set_param("auto_int8", a8)
     assert ix.precision == "auto" and ix.stat("auto_int8") == a8
-    return ix, ("searches_i8", "searches_i8x3") if a8 else ("searches_bf16", "searches_bf16x3")
+    return ix, ("searches_i8" if a8 else "searches_bf16", "searches_bf16x3")
 
 
 @pytest.mark.parametrize("a8", [1, 0])
@@ -246,9 +247,15 @@ def test_auto_precision_switches_on_fallbacks(vdb, mem, a8):
         assert ix.stat(one) >= 1
         if expect_switch:
             assert ix.stat("fallback_queries") * 64 > B  # the x3 pass cannot separate these rows either
-            # host memory: the uncertified one-plane pass is rerun at once in x3, then the second
-            # search runs x3; device memory: the first search falls back, the second runs x3
-            assert ix.stat(x3) == (2 if mem == "host" else 1)
+            if a8:
+                # the I8 failure holds BF16 (host: the batch is rerun in BF16X3 at once); the
+                # second search runs BF16, fails too and (host) reruns in BF16X3
+                assert ix.stat("searches_bf16") == 1
+                assert ix.stat(x3) == (2 if mem == "host" else 0)
+            else:
+                # host memory: the uncertified one-plane pass is rerun at once in x3, then the second
+                # search runs x3; device memory: the first search falls back, the second runs x3
+                assert ix.stat(x3) == (2 if mem == "host" else 1)
             assert ix.stat(one) == 1
             ix.add(V[:1])  # new rows: the one-plane pass gets another chance
             ix.search(Q, k)
@@ -282,10 +289,35 @@ def test_auto_repass_keeps_bf16_for_a_few_uncertified_queries(vdb, a8):
     assert ix.stat("auto_hold") == 0
 
 
+def test_auto_hold8_holds_bf16_until_the_rows_change(vdb):
+    """With the int8 copy, an I8 failure too large for a re-pass holds BF16 (the split copy) for
+    16 searches instead of dropping to an x3 pass; new rows end the hold."""
+    rng = np.random.default_rng(43)
+    D, N, B, k = 128, 6000, 16, 10
+    base = rng.random(D, dtype=np.float32)
+    near = (base + 1e-4 * rng.standard_normal((N, D))).astype(np.float32)
+    Q = (near[rng.integers(0, N, B)] + 1e-5 * rng.standard_normal((B, D))).astype(np.float32)
+    ix, (one, x3) = _auto_index(vdb, D, 1)
+    ix.add(near)
+    es, ei, ek = ref_cpu.exact_search(Q, near, k, "cosine")
+    s, i, kk = ix.search(Q, k, with_keys=True)  # I8 fails for most queries -> rerun in BF16X3
+    np.testing.assert_array_equal(i, ei)
+    assert ix.stat("searches_i8") == 1 and ix.stat("auto_hold8") == 16
+    s, i, kk = ix.search(Q, k, with_keys=True)  # the hold: BF16
+    np.testing.assert_array_equal(kk, ek)
+    assert ix.stat("searches_i8") == 1 and ix.stat("searches_bf16") == 1 and ix.stat("auto_hold8") == 15
+    ix.add(near[:1])  # new rows: I8 again
+    assert ix.stat("auto_hold8") == 0
+    ix.search(Q, k)
+    assert ix.stat("searches_i8") == 2
+
+
 @pytest.mark.parametrize("a8", [1, 0])
 def test_auto_hold_expires(vdb, a8):
     """A failure too large for a re-pass starts a hold of 16 bf16x3 searches; after it the
-    index probes bf16 again (and, on data that still fails, holds twice as long)."""
+    index probes the one-plane pass again (and, on data that still fails, holds twice as long).
+    With the int8 copy (a8) the x3 hold is reached through BF16: the first search's I8 failure
+    holds BF16, whose own failure starts the x3 hold."""
     rng = np.random.default_rng(43)
     D, N, B, k = 128, 6000, 16, 10
     base = rng.random(D, dtype=np.float32)
@@ -294,6 +326,11 @@ def test_auto_hold_expires(vdb, a8):
     ix, (one, x3) = _auto_index(vdb, D, a8)
     ix.add(near)
     es, ei, ek = ref_cpu.exact_search(Q, near, k, "cosine")
+    if a8:  # I8 fails -> BF16 hold; then the BF16 pass is the one-plane pass probed below
+        s, i, kk = ix.search(Q, k, with_keys=True)
+        np.testing.assert_array_equal(i, ei)
+        assert ix.stat("searches_i8") == 1 and ix.stat("auto_hold8") == 16
+        one = "searches_bf16"
     s, i, kk = ix.search(Q, k, with_keys=True)  # one-plane fails for most queries -> rerun in x3
     np.testing.assert_array_equal(i, ei)
     assert ix.stat(one) == 1 and ix.stat("auto_hold") == 16
@@ -304,7 +341,8 @@ def test_auto_hold_expires(vdb, a8):
     s, i, kk = ix.search(Q, k, with_keys=True)  # the probe: one-plane again, fails again -> hold 32
     np.testing.assert_array_equal(i, ei)
     assert ix.stat(one) == 2 and ix.stat("auto_hold") == 32
-    assert ix.stat("searches") == 18 and ix.stat("queries") == 18 * B
+    n = 18 + a8
+    assert ix.stat("searches") == n and ix.stat("queries") == n * B
 
 
 def test_duplicates_force_certificate_fallback(vdb):
