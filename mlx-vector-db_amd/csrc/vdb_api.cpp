@@ -1166,8 +1166,10 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     // each row range is re-read from L2 by half as many workgroups (C4: 8 -> 4 blocks)
     const bool q4 = split_pass && !exact_all && KP == 128 && B >= 256 && Gs <= 8 &&
                     (ix->scan_q4 == 1 || (ix->scan_q4 < 0));
-    const int QB = q4 ? 128 : KP == 256 ? 32 : 64;
-    const int QB_pilot = KP == 256 ? 32 : 64;  // the pilot's own query blocks (pilot2 instantiations)
+    // query rows per candidate-pass block: the int8 pass keeps 64 at KP = 256 (KW = 64 kept per
+    // workgroup, vdb_scan8_kernel.h), the split pass 32 there
+    const int QB = q4 ? 128 : i8_pass ? scan8_qb(KP) : KP == 256 ? 32 : 64;
+    const int QB_pilot = i8_pass ? 64 : KP == 256 ? 32 : 64;  // the pilot's own query blocks (instantiations)
     const int Bp = (int)round_up(B, 128);  // whole query super tiles (tiled layout)
     const int n_qblocks = (B + QB - 1) / QB;
     int variant = split_pass || i8_pass ? 0 : (int)ix->scan_variant;

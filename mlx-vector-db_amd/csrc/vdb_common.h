@@ -105,6 +105,17 @@ __device__ __forceinline__ float key_to_float(uint32_t k) {
     return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
 }
 
+// LDS flags shared by a workgroup's waves (the flag-gated step ends of the candidate passes):
+// relaxed workgroup-scope atomics keep the LDS address space (ds_read / ds_write).  A volatile
+// access through a generic pointer compiled to flat_load / flat_store, which the compiler
+// waits for with s_waitcnt vmcnt(0) -- at every step end, draining the corpus prefetch.
+__device__ __forceinline__ int lds_flag_ld(int* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_flag_st(int* p, int v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 // ---- ordering ----------------------------------------------------------------
 // Keys are "higher is better"; ties go to the LOWER row index.  Index types are
 // compared unsigned so that the sentinel (UINT32_MAX / int64 -1) sorts last.

@@ -52,6 +52,7 @@ hipError_t launch_pilot8(int prec, int metric, const float* Xq, const float* rin
                          const float* Qq, const float* qscal, int G8, int64_t N, int B, int n_qblocks, int QB,
                          int n_sample, uint32_t* pslots, hipStream_t st);
 int scan8_rows_per_step(int prec, int metric);
+int scan8_qb(int KP);  // queries per block of the int8 pass
 hipError_t launch_scan8(int prec, int metric, int KP, const float* Xq, const float* rinit, const uint32_t* mask,
                         const float* Qq, const float* lsl, const float* qscal, int G8, int64_t N, int B,
                         int n_qblocks, int64_t n_steps, int n_wg, int spw, float* gl_s, uint32_t* gl_i,

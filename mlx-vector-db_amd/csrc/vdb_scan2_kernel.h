@@ -504,15 +504,15 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
                 if (!__syncthreads_or(any_left != 0)) break;
             } else {
                 const bool mine = __any(any_left != 0);
-                if (mine && lane == 0) *(volatile int*)&s_need = 1;
-                if (!mine && (joined || !__builtin_amdgcn_readfirstlane(*(volatile int*)&s_need))) break;
+                if (mine && lane == 0) lds_flag_st(&s_need, 1);
+                if (!mine && (joined || !__builtin_amdgcn_readfirstlane(lds_flag_ld(&s_need)))) break;
                 __syncthreads();  // B1
             }
             for (int q = wv; q < QB; q += NW)
                 if (s_cnt[q] >= CAP)
                     compact_query<KW, CAP>(s_sc + q * CAP, s_ix + q * CAP, s_cnt + q, s_thr + q,
                                            KW == KP && qb * QB + q < B ? gthr + qb * QB + q : nullptr);
-            if (FLAGSYNC && threadIdx.x == 0) *(volatile int*)&s_need = 0;
+            if (FLAGSYNC && threadIdx.x == 0) lds_flag_st(&s_need, 0);
             __syncthreads();  // B2
             any_left = 0;
 #pragma unroll
@@ -587,14 +587,14 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
     // FLAGSYNC: keep answering compaction rounds until every wave is past its last step
     if (FLAGSYNC && lane == 0) atomicAdd(&s_done, 1);
     for (; FLAGSYNC;) {
-        if (lane == 0) *(volatile int*)&s_need = 1;
+        if (lane == 0) lds_flag_st(&s_need, 1);
         __syncthreads();  // B1
-        if (__builtin_amdgcn_readfirstlane(*(volatile int*)&s_done) == NW) break;
+        if (__builtin_amdgcn_readfirstlane(lds_flag_ld(&s_done)) == NW) break;
         for (int q = wv; q < QB; q += NW)
             if (s_cnt[q] >= CAP)
                 compact_query<KW, CAP>(s_sc + q * CAP, s_ix + q * CAP, s_cnt + q, s_thr + q,
                                        KW == KP && qb * QB + q < B ? gthr + qb * QB + q : nullptr);
-        if (threadIdx.x == 0) *(volatile int*)&s_need = 0;
+        if (threadIdx.x == 0) lds_flag_st(&s_need, 0);
         __syncthreads();  // B2
     }
 

@@ -323,6 +323,7 @@ hipError_t launch_pilot8(int prec, int metric, const float* Xq, const float* rin
 // Dispatch
 // =============================================================================
 int scan8_rows_per_step(int prec, int metric) { return scan8_rows(prec, metric); }
+int scan8_qb(int KP) { (void)KP; return 64; }  // every KP (KP = 256: KW = 64, S8_KP)
 
 hipError_t launch_scan8(int prec, int metric, int KP, const float* Xq, const float* rinit, const uint32_t* mask,
                         const float* Qq, const float* lsl, const float* qscal, int G8, int64_t N, int B,

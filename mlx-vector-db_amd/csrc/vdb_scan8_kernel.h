@@ -38,6 +38,17 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int S8_NW = 4;  // waves per workgroup
+
+#ifdef VDB_STAMP8
+// Diagnostic build only (make variant VDEFS=-DVDB_STAMP8): per-wave cycles of scan8_kernel:
+// [0] total, [1] in the stream waits (s8_wait), [2] K-loop (step start to the last group's
+// refill, waits included), [3] epilogue, [4] steps, [5] start time (absolute)
+static __device__ unsigned long long g_scan8_stamps[1 << 16][8];
+#define S8_NOW() __builtin_amdgcn_s_memtime()
+#define S8_STAMP(...) __VA_ARGS__
+#else
+#define S8_STAMP(...)
+#endif
 // row tiles per wave per step: I8 cosine 4 (one accumulator set, 128 registers), I8X3 2 (two
 // sets), I8 L2 2 (its per-row start values, prefetched a step ahead, would spill at 4)
 #ifndef VDB_S8_RT1
@@ -83,6 +94,39 @@ __device__ __forceinline__ int imax16(const i32x16& a) {
     return max(m, a[15]);
 }
 
+// The streams the K-loop consumes -- corpus tiles, global query tiles, L2 start values -- are
+// loaded by inline asm the compiler does not track, and waited for explicitly: s_waitcnt
+// vmcnt(N), N = this kernel's loads issued after the slot (a compile-time constant), tied to
+// the registers the slot fills.  Compiler-visible loads carried across the step loop made its
+// wait pass drain every outstanding load at the loop header (s_waitcnt vmcnt(0) before the
+// first MFMA of each step, the whole next-step prefetch included).  vmcnt retires in issue
+// order, so any other younger memory operation only makes a wait more conservative.
+template <bool NT>
+__device__ __forceinline__ f32x4 s8_ld(const float* base, uint32_t voff) {
+    f32x4 r;
+    if constexpr (NT)
+        asm volatile("global_load_dwordx4 %0, %1, %2 nt" : "=v"(r) : "v"(voff), "s"(base));
+    else
+        asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(r) : "v"(voff), "s"(base));
+    return r;
+}
+template <int N, int A, int C>
+__device__ __forceinline__ void s8_wait(f32x4 (&r)[A][C]) {
+    asm volatile("s_waitcnt vmcnt(%1)" : "+v"(r[0][0]) : "n"(N));
+#pragma unroll
+    for (int a = 0; a < A; ++a)
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+            if (a + c > 0) asm volatile("" : "+v"(r[a][c]));
+}
+template <int A, int C>
+__device__ __forceinline__ void s8_tie(f32x4 (&r)[A][C]) {  // after an s8_wait: these are ready too
+#pragma unroll
+    for (int a = 0; a < A; ++a)
+#pragma unroll
+        for (int c = 0; c < C; ++c) asm volatile("" : "+v"(r[a][c]));
+}
+
 // The smallest H that can still pass threshold th (half units) given |L uL| <= slack, minus a
 // margin for the fp32 evaluation: H <= the result means the tile's scores are all <= th.
 __device__ __forceinline__ int h_floor(float th, float slack, float invU) {
@@ -123,6 +167,7 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
     const int lane = threadIdx.x & 63;
     const int lane4 = lane * 4;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    S8_STAMP(const unsigned long long st_t0 = S8_NOW(); unsigned long long st_w = 0, st_k = 0, st_e = 0, st_n = 0;)
     int wg, qb;
     xcd_map(n_qb, wg, qb);
     if (threadIdx.x == 0) {
@@ -161,51 +206,54 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
 #pragma unroll
             for (int pl = 0; pl < QPL; ++pl) q[qt][pl] = *(const f32x4*)(s_q + ((size_t)(g * 2 + pl) * QT + qt) * 256 + lane4);
     };
-    if (s_begin < s_end) {
-        const float* xs = Xq + corpus_block((uint64_t)((s_begin * NW + wv) * RT), 0, 0, G);
+    // The shared bound is read once: with KW < KP (the I8 shape) nothing raises it during the
+    // scan but the pilot (before it); with KW == KP other workgroups' compactions do, and a
+    // stale copy only drops fewer rows (same speed, measured: profiles/r03_i8/)
+    uint32_t gk[QT];
 #pragma unroll
-        for (int p = 0; p < PX; ++p)
-#pragma unroll
-            for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-                for (int pl = 0; pl < XPL; ++pl)
-                    xr[p][rt][pl] = corpus_ld<NT>(xs + p * XGSTEP + pl * XPLANE + rt * BLOCK_FLOATS + lane4);
-        if constexpr (!QLDS) {
-#pragma unroll
-            for (int p = 0; p < PQ; ++p)
-#pragma unroll
-                for (int qt = 0; qt < QT; ++qt)
-#pragma unroll
-                    for (int pl = 0; pl < QPL; ++pl)
-                        qr[p][qt][pl] = *(const f32x4*)(Qbase + p * GSTEP + pl * PLANE + qt * BLOCK_FLOATS + lane4);
-        } else {
-            q_lds(0, qr[0]);
-        }
-    }
-    // the next step's shared bounds and (L2) start values, loaded one step ahead: lane half h
-    // holds -|x|^2/2 of rows 32 t + 8 a + 4 h + b (a, b = 0..3) of each tile, the rows of its
-    // accumulator registers 4 a + b
+    for (int qt = 0; qt < QT; ++qt) gk[qt] = gthr[qb * QB + qt * 32 + (lane & 31)];
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the compiler's loads are done before the streams start
+    // loads per slot (group) of the streams: corpus tiles, + query tiles from global memory
+    constexpr int LPS = RT * XPL + (QLDS ? 0 : QT * QPL);
+    const uint32_t voff = (uint32_t)lane * 16u;
+    // L2: the next step's start values, loaded one step ahead, before the tail groups' refills
+    // (lane half h holds -|x|^2/2 of rows 32 t + 8 a + 4 h + b, a, b = 0..3, of each tile: the
+    // rows of its accumulator registers 4 a + b)
     constexpr int NRI = METRIC == 1 ? RT : 1;
-    auto load_epi = [&](int64_t st_, uint32_t (&g_)[QT], f32x4 (&r_)[NRI][4]) {
-#pragma unroll
-        for (int qt = 0; qt < QT; ++qt) {
-            const int qg = qb * QB + qt * 32 + (lane & 31);
-            g_[qt] = qg < B ? gthr[qg] : 0u;
-        }
+    auto load_epi = [&](int64_t st_, f32x4 (&r_)[NRI][4]) {
         if constexpr (METRIC == 1) {
             const int64_t tt = (st_ * NW + wv) * RT;
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
                 for (int a = 0; a < 4; ++a)
-                    r_[rt][a] = *(const f32x4*)(rinit + (tt + rt) * 32 + 8 * a + 4 * (lane >> 5));
+                    r_[rt][a] = s8_ld<false>(rinit + (tt + rt) * 32 + 8 * a, (uint32_t)(lane >> 5) * 16u);
         }
     };
-    uint32_t gkn[QT];
     f32x4 rin[NRI][4];
-    if (s_begin < s_end) load_epi(s_begin, gkn, rin);
+    if (s_begin < s_end) {
+        load_epi(s_begin, rin);  // before the slots: PX * LPS loads younger than these
+        const float* xs = Xq + corpus_block((uint64_t)((s_begin * NW + wv) * RT), 0, 0, G);
+#pragma unroll
+        for (int p = 0; p < PX; ++p) {
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+                for (int pl = 0; pl < XPL; ++pl)
+                    xr[p][rt][pl] = s8_ld<NT>(xs + p * XGSTEP + pl * XPLANE + rt * BLOCK_FLOATS, voff);
+            if constexpr (!QLDS) {
+#pragma unroll
+                for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+                    for (int pl = 0; pl < QPL; ++pl)
+                        qr[p][qt][pl] = s8_ld<false>(Qbase + p * GSTEP + pl * PLANE + qt * BLOCK_FLOATS, voff);
+            }
+        }
+        if constexpr (QLDS) q_lds(0, qr[0]);
+    }
 
     for (int64_t s = s_begin; s < s_end; ++s) {
+        S8_STAMP(const unsigned long long st_a = S8_NOW(); ++st_n;)
         const int64_t t0 = (s * NW + wv) * RT;
         const float* xs = Xq + corpus_block((uint64_t)t0, 0, 0, G);
         const float* xn = (s + 1 < s_end) ? Xq + corpus_block((uint64_t)(t0 + NW * RT), 0, 0, G) : xs;
@@ -216,6 +264,7 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
 #pragma unroll
             for (int v = 0; v < 16; ++v) init[v] = 0;
             if constexpr (METRIC == 1) {
+                if (rt == 0) s8_wait<PX * LPS>(rin);  // issued before the PX slots now in flight
 #pragma unroll
                 for (int a = 0; a < 4; ++a)
 #pragma unroll
@@ -228,11 +277,12 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
                 for (int v = 0; v < 16; ++v) aL[rt][qt][v] = 0;
             }
         }
-        uint32_t gk[QT];
-#pragma unroll
-        for (int qt = 0; qt < QT; ++qt) gk[qt] = gkn[qt];
 
         auto group = [&](const int p, const int g, const float* xsrc, const float* qsrc) {
+            // slot p was filled PX - 1 slots (and, for a tail group, the L2 start values) ago
+            S8_STAMP(const unsigned long long st_b = S8_NOW();)
+            s8_wait<(PX - 1) * LPS>(xr[p]);
+            S8_STAMP(st_w += S8_NOW() - st_b;)
             if constexpr (QLDS) {
                 f32x4 qn[1][QT][QPL];
                 q_lds(g + 1 < G ? g + 1 : 0, qn[0]);
@@ -242,7 +292,7 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
                 for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
                     for (int pl = 0; pl < XPL; ++pl)
-                        xr[p][rt][pl] = corpus_ld<NT>(xsrc + pl * XPLANE + rt * BLOCK_FLOATS + lane4);
+                        xr[p][rt][pl] = s8_ld<NT>(xsrc + pl * XPLANE + rt * BLOCK_FLOATS, voff);
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int qt = 0; qt < QT; ++qt)
@@ -250,18 +300,19 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
                     for (int pl = 0; pl < QPL; ++pl) qr[0][qt][pl] = qn[0][qt][pl];
                 (void)qsrc;
             } else {
+                s8_tie(qr[p % PQ]);  // loaded right after slot p's corpus tiles
                 group_mfma8<PREC, RT, QT>(xr[p], qr[p % PQ], aH, aL);
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
                     for (int pl = 0; pl < XPL; ++pl)
-                        xr[p][rt][pl] = corpus_ld<NT>(xsrc + pl * XPLANE + rt * BLOCK_FLOATS + lane4);
+                        xr[p][rt][pl] = s8_ld<NT>(xsrc + pl * XPLANE + rt * BLOCK_FLOATS, voff);
 #pragma unroll
                 for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
                     for (int pl = 0; pl < QPL; ++pl)
-                        qr[p % PQ][qt][pl] = *(const f32x4*)(qsrc + pl * PLANE + qt * BLOCK_FLOATS + lane4);
+                        qr[p % PQ][qt][pl] = s8_ld<false>(qsrc + pl * PLANE + qt * BLOCK_FLOATS, voff);
                 __builtin_amdgcn_sched_barrier(0);
             }
         };
@@ -271,11 +322,23 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
             for (int p = 0; p < PX; ++p)
                 group(p, gb + p, xs + (size_t)(gb + p + PX) * XGSTEP, Qbase + (size_t)(gb + p + PQ) * GSTEP);
         }
-        if (s + 1 < s_end) load_epi(s + 1, gkn, rin);
+        if (s + 1 < s_end) load_epi(s + 1, rin);
 #pragma unroll
         for (int p = 0; p < PX; ++p)
             group(p, gb + p, xn + (size_t)p * XGSTEP, Qbase + (size_t)(gb + p + PQ) * GSTEP);
 
+        S8_STAMP(const unsigned long long st_c = S8_NOW(); st_k += st_c - st_a;)
+#ifdef VDB_SCAN8_KLOOP_ONLY
+        {  // diagnostic build (make variant): the K-loop alone, results are garbage
+            int f = 0;
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+                for (int qt = 0; qt < QT; ++qt) f += imax16(aH[rt][qt]);
+            if (f == 123456789) gl_s[0] = (float)f;
+            continue;
+        }
+#endif
         // ---- epilogue ----
         float thh[QT];
         int thi[QT];
@@ -336,15 +399,15 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
                 if (!__syncthreads_or(any_left != 0)) break;
             } else {
                 const bool mine = __any(any_left != 0);
-                if (mine && lane == 0) *(volatile int*)&s_need = 1;
-                if (!mine && (joined || !__builtin_amdgcn_readfirstlane(*(volatile int*)&s_need))) break;
+                if (mine && lane == 0) lds_flag_st(&s_need, 1);
+                if (!mine && (joined || !__builtin_amdgcn_readfirstlane(lds_flag_ld(&s_need)))) break;
                 __syncthreads();  // B1
             }
             for (int q = wv; q < QB; q += NW)
                 if (s_cnt[q] >= CAP)
                     compact_query<KW, CAP>(s_sc + q * CAP, s_ix + q * CAP, s_cnt + q, s_thr + q,
                                            KW == KP && qb * QB + q < B ? gthr + qb * QB + q : nullptr);
-            if (FLAGSYNC && threadIdx.x == 0) *(volatile int*)&s_need = 0;
+            if (FLAGSYNC && threadIdx.x == 0) lds_flag_st(&s_need, 0);
             __syncthreads();  // B2
             any_left = 0;
 #pragma unroll
@@ -358,19 +421,20 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
                     any_left |= pend[rt][qt];
                 }
         }
+        S8_STAMP(st_e += S8_NOW() - st_c;)
     }
 
     // FLAGSYNC: keep answering compaction rounds until every wave is past its last step
     if (FLAGSYNC && lane == 0) atomicAdd(&s_done, 1);
     for (; FLAGSYNC;) {
-        if (lane == 0) *(volatile int*)&s_need = 1;
+        if (lane == 0) lds_flag_st(&s_need, 1);
         __syncthreads();  // B1
-        if (__builtin_amdgcn_readfirstlane(*(volatile int*)&s_done) == NW) break;
+        if (__builtin_amdgcn_readfirstlane(lds_flag_ld(&s_done)) == NW) break;
         for (int q = wv; q < QB; q += NW)
             if (s_cnt[q] >= CAP)
                 compact_query<KW, CAP>(s_sc + q * CAP, s_ix + q * CAP, s_cnt + q, s_thr + q,
                                        KW == KP && qb * QB + q < B ? gthr + qb * QB + q : nullptr);
-        if (threadIdx.x == 0) *(volatile int*)&s_need = 0;
+        if (threadIdx.x == 0) lds_flag_st(&s_need, 0);
         __syncthreads();  // B2
     }
 
@@ -387,6 +451,16 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
         tkey = max(gthr[qb * QB + q], dk);
     }
     append_flush<CAP>(s_sc, s_ix, s_cnt, wv, NW, QPW, qb * QB, B, tkey, gl_s, gl_i, gl_cnt, gl_cap);
+#ifdef VDB_STAMP8
+    {
+        const int w = blockIdx.x * NW + wv;
+        if (lane == 0 && w < (1 << 16)) {
+            const unsigned long long v[6] = {S8_NOW() - st_t0, st_w, st_k, st_e, st_n, st_t0};
+#pragma unroll
+            for (int i = 0; i < 6; ++i) g_scan8_stamps[w][i] = v[i];
+        }
+    }
+#endif
 }
 
 // ---- launch templates ----
@@ -413,25 +487,26 @@ static hipError_t scan8_launch_g(const float* Xq, const float* rinit, const uint
     return hipGetLastError();
 }
 
-template <int P, int M, int QT, int PX, int KP, int CAP, bool NT, bool QL, bool FS>
+template <int P, int M, int QT, int PX, int KP, int CAP, bool NT, bool QL, bool FS, int KW = KP>
 static hipError_t scan8_launch(const float* Xq, const float* rinit, const uint32_t* mask, const float* Qq,
                                const float* lsl, const float* qscal, int G, int64_t N, int B, int n_qblocks,
                                int64_t n_steps, int n_wg, int spw, float* gl_s, uint32_t* gl_i, uint32_t* gl_cnt,
                                int64_t gl_cap, uint32_t* gthr, hipStream_t st) {
     if constexpr (QL) {
         if (G == 4)  // D = 128: the group loop unrolls, and the whole next step is in flight
-            return scan8_launch_g<P, M, QT, 4, KP, CAP, NT, QL, FS, 4>(Xq, rinit, mask, Qq, lsl, qscal, G, N, B,
+            return scan8_launch_g<P, M, QT, 4, KP, CAP, NT, QL, FS, 4, scan8_rt(P, M), KW>(Xq, rinit, mask, Qq, lsl, qscal, G, N, B,
                                                                         n_qblocks, n_steps, n_wg, spw, gl_s, gl_i,
                                                                         gl_cnt, gl_cap, gthr, st);
     }
-    return scan8_launch_g<P, M, QT, PX, KP, CAP, NT, QL, FS, 0>(Xq, rinit, mask, Qq, lsl, qscal, G, N, B, n_qblocks,
+    return scan8_launch_g<P, M, QT, PX, KP, CAP, NT, QL, FS, 0, scan8_rt(P, M), KW>(Xq, rinit, mask, Qq, lsl, qscal, G, N, B, n_qblocks,
                                                                 n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr,
                                                                 st);
 }
 
 // The query block goes to LDS when it is small (short rows: 64 queries x 128 dims x 2 planes =
 // 16 KiB).
-inline bool scan8_qlds(int G8, int KP) { return (size_t)G8 * 2 * (KP == 256 ? 1 : 2) * 1024 <= 32 * 1024; }
+inline bool scan8_qlds(int G8, int KP) { return (size_t)G8 * 2 * 2 * 1024 <= 32 * 1024; }
+
 
 #define S8_UNIT_PARAMS                                                                                             \
     int KP, const float *Xq, const float *rinit, const uint32_t *mask, const float *Qq, const float *lsl,          \
@@ -439,14 +514,16 @@ inline bool scan8_qlds(int G8, int KP) { return (size_t)G8 * 2 * (KP == 256 ? 1 
         float *gl_s, uint32_t *gl_i, uint32_t *gl_cnt, int64_t gl_cap, uint32_t *gthr, bool nt, bool ql, bool fs, \
         hipStream_t st
 #define S8_ARGS Xq, rinit, mask, Qq, lsl, qscal, G, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, st
-#define S8_ONE(P, M, KPV, QTV, PXV, CAPV, NTV, QLV, FSV) \
-    if (KP == KPV && nt == NTV && ql == QLV && fs == FSV)  \
-        return scan8_launch<P, M, QTV, PXV, KPV, CAPV, NTV, QLV, FSV>(S8_ARGS);
-#define S8_KP(P, M, PXV, NTV, QLV, FSV)          \
-    S8_ONE(P, M, 32, 2, PXV, 128, NTV, QLV, FSV)  \
-    S8_ONE(P, M, 64, 2, PXV, 128, NTV, QLV, FSV)  \
-    S8_ONE(P, M, 128, 2, PXV, 192, NTV, QLV, FSV) \
-    S8_ONE(P, M, 256, 1, PXV, 320, NTV, QLV, FSV)
+#define S8_ONE(P, M, KPV, QTV, PXV, CAPV, NTV, QLV, FSV, KWV) \
+    if (KP == KPV && nt == NTV && ql == QLV && fs == FSV)       \
+        return scan8_launch<P, M, QTV, PXV, KPV, CAPV, NTV, QLV, FSV, KWV>(S8_ARGS);
+// KP = 256 keeps 64-query blocks: a workgroup keeps its best KW = 64 per query (LDS 64 KiB; the
+// drop bound -> gthr, vdb_scan2_kernel.h), so a 64-query batch reads the corpus once
+#define S8_KP(P, M, PXV, NTV, QLV, FSV)               \
+    S8_ONE(P, M, 32, 2, PXV, 128, NTV, QLV, FSV, 32)   \
+    S8_ONE(P, M, 64, 2, PXV, 128, NTV, QLV, FSV, 64)   \
+    S8_ONE(P, M, 128, 2, PXV, 192, NTV, QLV, FSV, 128) \
+    S8_ONE(P, M, 256, 2, PXV, 128, NTV, QLV, FSV, 64)
 #define S8_MODES(P, M, PXV, PXL)                                               \
     S8_KP(P, M, PXV, false, false, false) S8_KP(P, M, PXV, true, false, false) \
     S8_KP(P, M, PXL, false, true, false) S8_KP(P, M, PXL, false, true, true)   \
