@@ -1246,8 +1246,12 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
                                               : (int64_t)((n_wg + 7) / 8 * 8) * 512;
     bytes += (size_t)B * gl_cap * 8 + (size_t)Bp * 4 + 768;
     // Pilot sample: 512 row tiles, more for large k (its bound then saves more insert work than
-    // the sample costs: C4, k = 100, 512 -> 4096 tiles: 89.5 K -> 96.4 K QPS, profiles/r02_ab).
-    const int64_t pilot_def = std::min<int64_t>(4096, 512 * std::max(1, k / 12));
+    // the sample costs: C4, k = 100, 512 -> 4096 tiles: 89.5 K -> 96.4 K QPS, profiles/r02_ab),
+    // and at least 1/160 of the rows: the bound's global rank ~ r N / S sets how many entries
+    // each workgroup inserts (C6, 10 M rows, int8 pass: 512 -> 2048 tiles, scan 0.329 -> 0.259 ms,
+    // 200 K -> 250 K QPS; C2 / C3, 1 M rows: larger samples only add pilot time,
+    // profiles/r03_i8/pilot).
+    const int64_t pilot_def = std::min<int64_t>(4096, std::max<int64_t>(512 * std::max(1, k / 12), N / (32 * 160)));
     const int n_pilot = (int)std::min<int64_t>(ix->pilot_tiles >= 0 ? ix->pilot_tiles : pilot_def, round_up(N, 32) / 32);
     // Rank of the pilot's bound among its sampled scores.  The KP-th best sample is a
     // guaranteed lower bound of the global KP-th best but sits at global rank ~KP N / S (C2:

@@ -43,7 +43,7 @@ constexpr int S8_NW = 4;  // waves per workgroup
 // Diagnostic build only (make variant VDEFS=-DVDB_STAMP8): per-wave cycles of scan8_kernel:
 // [0] total, [1] in the stream waits (s8_wait), [2] K-loop (step start to the last group's
 // refill, waits included), [3] epilogue, [4] steps, [5] start time (absolute)
-static __device__ unsigned long long g_scan8_stamps[1 << 16][8];
+static __device__ unsigned long long g_scan8_stamps[1 << 16][10];
 #define S8_NOW() __builtin_amdgcn_s_memtime()
 #define S8_STAMP(...) __VA_ARGS__
 #else
@@ -162,12 +162,13 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
     __shared__ int s_cnt[QB];
     __shared__ float s_thr[QB];
     __shared__ int s_need, s_done;
+    __shared__ uint32_t s_pend[S8_NW][8][64];  // per wave and tile: each lane's entries left for a compaction round
     extern __shared__ __attribute__((aligned(16))) float s_q[];  // QLDS: [G][plane][QT][256]
 
     const int lane = threadIdx.x & 63;
     const int lane4 = lane * 4;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    S8_STAMP(const unsigned long long st_t0 = S8_NOW(); unsigned long long st_w = 0, st_k = 0, st_e = 0, st_n = 0;)
+    S8_STAMP(const unsigned long long st_t0 = S8_NOW(); unsigned long long st_w = 0, st_k = 0, st_e = 0, st_n = 0, st_x = 0, st_y = 0, st_z = 0;)
     int wg, qb;
     xcd_map(n_qb, wg, qb);
     if (threadIdx.x == 0) {
@@ -340,101 +341,106 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
         }
 #endif
         // ---- epilogue ----
-        float thh[QT];
         int thi[QT];
         bool qok[QT];
 #pragma unroll
         for (int qt = 0; qt < QT; ++qt) {
             const int ql = qt * 32 + (lane & 31);
             const float thr = fmaxf(s_thr[ql], key_to_float(gk[qt]));
-            thh[qt] = METRIC == 0 ? thr : 0.5f * thr;
-            thi[qt] = h_floor(thh[qt], qsl[qt], invU);
+            thi[qt] = h_floor(METRIC == 0 ? thr : 0.5f * thr, qsl[qt], invU);
             qok[qt] = qb * QB + ql < B;
         }
-        // register by register (v_cmp + a wave-uniform branch), as scan2: the fp32 (half-)score
-        // H uH + L uL of each candidate register; lanes whose score passes append
-        auto insert_pass = [&](int rt, int qt, float th, uint32_t cand) -> uint32_t {
-            const int ql = qt * 32 + (lane & 31);
-            uint32_t left = 0;
-#pragma unroll
-            for (int v = 0; v < 16; ++v) {
-                const float sv = HL ? fmaf((float)aH[rt][qt][v], uH, (float)aL[rt][qt][v] * uL)
-                                    : (float)aH[rt][qt][v] * uH;
-                const bool p = ((cand >> v) & 1u) && sv > th;
-                if (__any(p)) {
-                    if (p) {
-                        float a_ = sv;
-                        uint32_t rb = (uint32_t)((t0 + rt) * 32) + 4u * (uint32_t)(lane >> 5);
-                        asm volatile("" : "+v"(a_), "+v"(rb));
-                        const float sc = METRIC == 0 ? a_ : 2.0f * a_;
-                        const int pos = atomicAdd(&s_cnt[ql], 1);
-                        if (pos < CAP) {
-                            s_sc[ql * CAP + pos] = sc;
-                            s_ix[ql * CAP + pos] = rb + (uint32_t)((v & 3) + 8 * (v >> 2));
-                        } else {
-                            left |= 1u << v;
-                        }
-                    }
-                }
-            }
-            return left;
-        };
-        // Every tile is tested first (compact code: the hot path of the epilogue), the rare
-        // insertions follow in one cold section.  With each tile's unrolled insertion inline
-        // between the tests, the hot path spread over tens of KB of code and the epilogue took
-        // ~5x its instruction count (C6: 7.3 K of a step's 9.6 K cycles, stamp build VDB_STAMP8)
-        uint32_t tpass = 0;  // wave-uniform: bit rt * QT + qt = some lane of tile (rt, qt) passes
+        // The hot path: every tile's H maximum against the integer floor of its threshold
+        uint32_t todo = 0;  // wave-uniform: bit rt * QT + qt = some lane of tile (rt, qt) passes
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
             for (int qt = 0; qt < QT; ++qt)
-                tpass |= __any(qok[qt] && imax16(aH[rt][qt]) > thi[qt]) ? 1u << (rt * QT + qt) : 0u;
-        uint32_t pend[RT][QT];
-        uint32_t any_left = 0;
+                todo |= __any(qok[qt] && imax16(aH[rt][qt]) > thi[qt]) ? 1u << (rt * QT + qt) : 0u;
+        S8_STAMP(const unsigned long long st_d = S8_NOW(); st_z += st_d - st_c; st_x += (todo != 0u) + ((unsigned long long)__builtin_popcount(todo) << 20);)
+        // The rare insertions: one tile at a time through ONE copy of the insertion code (the tile's
+        // registers picked by a wave-uniform switch), lanes whose fp32 (half-)score H uH (+ L uL)
+        // passes append; entries that find the buffer full wait in s_pend for a compaction round.
+        // (With the insertion unrolled per tile, and again for the compaction rounds, the kernel
+        // was 68 KB and the compiler hoisted the score conversion of all 128 accumulators out of
+        // the cold blocks into every step: C6 7.6 K cycles per step in the epilogue.)
+        uint32_t pmask = 0;  // wave-uniform: tiles with entries left in s_pend
+        for (bool joined = false;; joined = true) {
+            while (todo != 0u) {
+                const int t = __builtin_amdgcn_readfirstlane(__builtin_ctz(todo));
+                todo &= todo - 1u;
+                i32x16 h, l;
+                switch (t) {
+#define S8_TILE_CASE(T_)                                                  \
+    case T_:                                                              \
+        if constexpr ((T_) < RT * QT) {                                   \
+            h = aH[(T_) / QT][(T_) % QT];                                 \
+            if constexpr (HL) l = aL[(T_) / QT][(T_) % QT];               \
+        }                                                                 \
+        break;
+                    S8_TILE_CASE(0) S8_TILE_CASE(1) S8_TILE_CASE(2) S8_TILE_CASE(3)
+                    S8_TILE_CASE(4) S8_TILE_CASE(5) S8_TILE_CASE(6) S8_TILE_CASE(7)
+#undef S8_TILE_CASE
+                    default: __builtin_unreachable();
+                }
+                static_assert(RT * QT <= 8, "tile switch covers 8 tiles");
+                const int rt = t / QT, qt = t - rt * QT;
+                const int ql = qt * 32 + (lane & 31);
+                uint32_t gkq = gk[0];
+                bool ok = qok[0];
 #pragma unroll
-        for (int rt = 0; rt < RT; ++rt)
+                for (int q2 = 1; q2 < QT; ++q2)
+                    if (qt == q2) {
+                        gkq = gk[q2];
+                        ok = qok[q2];
+                    }
+                const float thr = fmaxf(s_thr[ql], key_to_float(gkq));
+                const float th = METRIC == 0 ? thr : 0.5f * thr;
+                const uint32_t cand = joined ? s_pend[wv][t][lane] : ok ? tile_valid16(mask, t0 + rt, N, lane) : 0u;
+                const uint32_t rb = (uint32_t)((t0 + rt) * 32) + 4u * (uint32_t)(lane >> 5);
+                uint32_t left = 0;
 #pragma unroll
-            for (int qt = 0; qt < QT; ++qt) pend[rt][qt] = 0u;
-        if (__builtin_expect(tpass != 0u, 0)) {
-#pragma unroll
-            for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-                for (int qt = 0; qt < QT; ++qt) {
-                    if (tpass & (1u << (rt * QT + qt))) {
-                        const uint32_t valid = qok[qt] ? tile_valid16(mask, t0 + rt, N, lane) : 0u;
-                        pend[rt][qt] = insert_pass(rt, qt, thh[qt], valid);
-                        any_left |= pend[rt][qt];
+                for (int v = 0; v < 16; ++v) {
+                    const float sv = HL ? fmaf((float)h[v], uH, (float)l[v] * uL) : (float)h[v] * uH;
+                    const bool p = ((cand >> v) & 1u) && sv > th;
+                    if (__any(p)) {
+                        if (p) {
+                            const float sc = METRIC == 0 ? sv : 2.0f * sv;
+                            const int pos = atomicAdd(&s_cnt[ql], 1);
+                            if (pos < CAP) {
+                                s_sc[ql * CAP + pos] = sc;
+                                s_ix[ql * CAP + pos] = rb + (uint32_t)((v & 3) + 8 * (v >> 2));
+                            } else {
+                                left |= 1u << v;
+                            }
+                        }
                     }
                 }
-        }
-        // compaction rounds (as scan2): lockstep = a workgroup barrier per step; FLAGSYNC = a wave
-        // with leftovers raises s_need and the others join at their step end
-        for (bool joined = false;; joined = true) {
+                if (__any(left != 0u)) {
+                    s_pend[wv][t][lane] = left;
+                    pmask |= 1u << t;
+                }
+            }
+            S8_STAMP(if (!joined) st_y += (S8_NOW() - st_c) << 20;)
+            // compaction rounds (as scan2): lockstep = a workgroup barrier per step; FLAGSYNC = a
+            // wave with leftovers raises s_need and the others join at their step end
             if constexpr (!FLAGSYNC) {
-                if (!__syncthreads_or(any_left != 0)) break;
+                if (!__syncthreads_or(pmask != 0u)) break;
             } else {
-                const bool mine = __any(any_left != 0);
+                const bool mine = pmask != 0u;
                 if (mine && lane == 0) lds_flag_st(&s_need, 1);
                 if (!mine && (joined || !__builtin_amdgcn_readfirstlane(lds_flag_ld(&s_need)))) break;
                 __syncthreads();  // B1
             }
+            S8_STAMP(++st_y;)
             for (int q = wv; q < QB; q += NW)
                 if (s_cnt[q] >= CAP)
                     compact_query<KW, CAP>(s_sc + q * CAP, s_ix + q * CAP, s_cnt + q, s_thr + q,
                                            KW == KP && qb * QB + q < B ? gthr + qb * QB + q : nullptr);
             if (FLAGSYNC && threadIdx.x == 0) lds_flag_st(&s_need, 0);
             __syncthreads();  // B2
-            any_left = 0;
-#pragma unroll
-            for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-                for (int qt = 0; qt < QT; ++qt) {
-                    if (!__any(pend[rt][qt] != 0)) continue;
-                    const int ql = qt * 32 + (lane & 31);
-                    const float thr = fmaxf(s_thr[ql], key_to_float(gk[qt]));
-                    pend[rt][qt] = insert_pass(rt, qt, METRIC == 0 ? thr : 0.5f * thr, pend[rt][qt]);
-                    any_left |= pend[rt][qt];
-                }
+            todo = pmask;
+            pmask = 0;
         }
         S8_STAMP(st_e += S8_NOW() - st_c;)
     }
@@ -470,9 +476,9 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
     {
         const int w = blockIdx.x * NW + wv;
         if (lane == 0 && w < (1 << 16)) {
-            const unsigned long long v[6] = {S8_NOW() - st_t0, st_w, st_k, st_e, st_n, st_t0};
+            const unsigned long long v[9] = {S8_NOW() - st_t0, st_w, st_k, st_e, st_n, st_t0, st_x, st_y, st_z};
 #pragma unroll
-            for (int i = 0; i < 6; ++i) g_scan8_stamps[w][i] = v[i];
+            for (int i = 0; i < 9; ++i) g_scan8_stamps[w][i] = v[i];
         }
     }
 #endif
