@@ -70,11 +70,12 @@ __device__ __forceinline__ uint32_t tile_valid16(const uint32_t* mask, int64_t t
 #else
 #define S2_MAXIMUM(a, b) __builtin_elementwise_maximum(a, b)
 #endif
-__device__ __forceinline__ float tile_max16(const f32x16& a) {
-    float m = S2_MAXIMUM(S2_MAXIMUM(a[0], a[1]), a[2]);
-#pragma unroll
-    for (int v = 3; v < 15; v += 2) m = S2_MAXIMUM(S2_MAXIMUM(m, a[v]), a[v + 1]);
-    return S2_MAXIMUM(m, a[15]);
+__device__ __forceinline__ float tile_max16(const f32x16& a) {  // a depth-3 tree of 3-input maxima
+#define S2_MAX3(x, y, z) S2_MAXIMUM(S2_MAXIMUM(x, y), z)
+    const float m0 = S2_MAX3(a[0], a[1], a[2]), m1 = S2_MAX3(a[3], a[4], a[5]), m2 = S2_MAX3(a[6], a[7], a[8]);
+    const float m3 = S2_MAX3(a[9], a[10], a[11]), m4 = S2_MAX3(a[12], a[13], a[14]);
+    return S2_MAXIMUM(S2_MAX3(m0, m1, m2), S2_MAX3(m3, m4, a[15]));
+#undef S2_MAX3
 }
 
 // split-layout block of (row tile t, 16-dim group g) with GG groups: [t/4][GG][2 planes][4][1 KiB]
@@ -170,6 +171,7 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
     __shared__ uint32_t s_pub[NW][QB];
     __shared__ uint32_t s_sh[QB];
     __shared__ int s_need, s_done;
+    __shared__ uint32_t s_pend[NW][RT * QT][64];  // per wave and tile: each lane's entries left for a compaction round
     extern __shared__ __attribute__((aligned(16))) float s_q[];  // QLDS: [G][plane][QT][256]
 
     const int lane = threadIdx.x & 63;
@@ -449,26 +451,64 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
             thrh[qt] = METRIC == 0 ? thr : 0.5f * thr;
             qok[qt] = qb * QB + ql < B;
         }
-        // Insertion, score by score: v_cmp + a wave-uniform branch per accumulator register;
-        // only the lanes whose score passes append (one returning LDS atomic each), so a tile
-        // with a few passing scores (C4, k = 100: most tiles early on) costs ~4 instructions per
-        // register plus its appends.  Scores that find the buffer full stay pending (`pend`) for
-        // the compaction rounds below.  The lane's best appended score goes to s_best (publish).
-        auto insert_pass = [&](int rt, int qt, float th, uint32_t cand) -> uint32_t {
-            const int ql = qt * 32 + (lane & 31);
-            uint32_t left = 0;
-            float mx = -INFINITY;
+        // The hot path: every tile's maximum against its threshold (wave-uniform bit rt QT + qt)
+        uint32_t todo = 0;
 #pragma unroll
-            for (int v = 0; v < 16; ++v) {
-                const bool p = ((cand >> v) & 1u) && acc[rt][qt][v] > th;
-                if (__any(p)) {
-                    if (p) {
-                        // the empty volatile asm keeps the score scaling and the row id inside
-                        // this rare branch: hoisted, they cost 2 VALU per accumulator register
-                        // and step (the row ids of all 128 registers parked in AGPRs)
-                        float a_ = acc[rt][qt][v];
-                        uint32_t rb = (uint32_t)((t0 + rt) * 32) + 4u * (uint32_t)(lane >> 5);
-                        asm volatile("" : "+v"(a_), "+v"(rb));
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt)
+                todo |= __any(qok[qt] && tile_max16(acc[rt][qt]) > thrh[qt]) ? 1u << (rt * QT + qt) : 0u;
+        // Insertion (as vdb_scan8_kernel.h): one passing tile at a time through ONE copy of the
+        // code (its registers picked by a wave-uniform switch); each lane's pass bits from 16
+        // independent compares, then one round per hit of the lane with the most hits -- with
+        // one wave per SIMD a compare-ballot-branch chain per register cost ~140 cycles, ~2.9 K per
+        // tile.  Only the lanes whose score passes append (one returning LDS atomic each);
+        // entries that find the buffer full wait in s_pend for a compaction round.  The lane's
+        // best appended score goes to s_best (publish).
+        uint32_t pmask = 0;  // wave-uniform: tiles with entries left in s_pend
+        for (bool joined = false;; joined = true) {
+            while (todo != 0u) {
+                const int t = __builtin_amdgcn_readfirstlane(__builtin_ctz(todo));
+                todo &= todo - 1u;
+                f32x16 h;
+                switch (t) {
+#define S2_TILE_CASE(T_)                                               \
+    case T_:                                                           \
+        if constexpr ((T_) < RT * QT) h = acc[(T_) / QT][(T_) % QT];   \
+        break;
+                    S2_TILE_CASE(0) S2_TILE_CASE(1) S2_TILE_CASE(2) S2_TILE_CASE(3)
+                    S2_TILE_CASE(4) S2_TILE_CASE(5) S2_TILE_CASE(6) S2_TILE_CASE(7)
+#undef S2_TILE_CASE
+                    default: __builtin_unreachable();
+                }
+                static_assert(RT * QT <= 8, "tile switch covers 8 tiles");
+                const int rt = t / QT, qt = t - rt * QT;
+                const int ql = qt * 32 + (lane & 31);
+                uint32_t gkq = gk[0];
+                bool ok = qok[0];
+#pragma unroll
+                for (int q2 = 1; q2 < QT; ++q2)
+                    if (qt == q2) {
+                        gkq = gk[q2];
+                        ok = qok[q2];
+                    }
+                const float thr = fmaxf(s_thr[ql], key_to_float(max(gkq, s_sh[ql])));
+                const float th = METRIC == 0 ? thr : 0.5f * thr;
+                const uint32_t cand = joined ? s_pend[wv][t][lane] : ok ? tile_valid16(mask, t0 + rt, N, lane) : 0u;
+                const uint32_t rb = (uint32_t)((t0 + rt) * 32) + 4u * (uint32_t)(lane >> 5);
+                uint32_t pm = 0;
+#pragma unroll
+                for (int v = 0; v < 16; ++v) pm |= (h[v] > th ? 1u : 0u) << v;
+                pm &= cand;
+                uint32_t left = 0;
+                float mx = -INFINITY;
+                while (__any(pm != 0u)) {
+                    if (pm != 0u) {
+                        const int v = __builtin_ctz(pm);
+                        pm &= pm - 1u;
+                        float a_ = h[0];
+#pragma unroll
+                        for (int u = 1; u < 16; ++u) a_ = v == u ? h[u] : a_;
                         const float sc = METRIC == 0 ? a_ : 2.0f * a_;
                         const int pos = atomicAdd(&s_cnt[ql], 1);
                         if (pos < CAP) {
@@ -480,30 +520,18 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
                         mx = fmaxf(mx, sc);
                     }
                 }
-            }
-            if (mx != -INFINITY) atomicMax(&s_best[wv][ql], order_key(mx));
-            return left;
-        };
-        uint32_t pend[RT][QT];
-        uint32_t any_left = 0;
-#pragma unroll
-        for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-            for (int qt = 0; qt < QT; ++qt) {
-                pend[rt][qt] = 0u;
-                if (__any(qok[qt] && tile_max16(acc[rt][qt]) > thrh[qt])) {
-                    const uint32_t valid = qok[qt] ? tile_valid16(mask, t0 + rt, N, lane) : 0u;
-                    pend[rt][qt] = insert_pass(rt, qt, thrh[qt], valid);
-                    any_left |= pend[rt][qt];
+                if (mx != -INFINITY) atomicMax(&s_best[wv][ql], order_key(mx));
+                if (__any(left != 0u)) {
+                    s_pend[wv][t][lane] = left;
+                    pmask |= 1u << t;
                 }
             }
-        // compaction rounds (vdb_scan.hip): lockstep = one workgroup barrier per step;
-        // FLAGSYNC = a wave with leftovers raises s_need and the others join at their step end
-        for (bool joined = false;; joined = true) {
+            // compaction rounds (vdb_scan.hip): lockstep = one workgroup barrier per step;
+            // FLAGSYNC = a wave with leftovers raises s_need and the others join at their step end
             if constexpr (!FLAGSYNC) {
-                if (!__syncthreads_or(any_left != 0)) break;
+                if (!__syncthreads_or(pmask != 0u)) break;
             } else {
-                const bool mine = __any(any_left != 0);
+                const bool mine = pmask != 0u;
                 if (mine && lane == 0) lds_flag_st(&s_need, 1);
                 if (!mine && (joined || !__builtin_amdgcn_readfirstlane(lds_flag_ld(&s_need)))) break;
                 __syncthreads();  // B1
@@ -514,17 +542,8 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
                                            KW == KP && qb * QB + q < B ? gthr + qb * QB + q : nullptr);
             if (FLAGSYNC && threadIdx.x == 0) lds_flag_st(&s_need, 0);
             __syncthreads();  // B2
-            any_left = 0;
-#pragma unroll
-            for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-                for (int qt = 0; qt < QT; ++qt) {
-                    if (!__any(pend[rt][qt] != 0)) continue;
-                    const int ql = qt * 32 + (lane & 31);
-                    const float thr = fmaxf(s_thr[ql], key_to_float(max(gk[qt], s_sh[ql])));
-                    pend[rt][qt] = insert_pass(rt, qt, METRIC == 0 ? thr : 0.5f * thr, pend[rt][qt]);
-                    any_left |= pend[rt][qt];
-                }
+            todo = pmask;
+            pmask = 0;
         }
         // ---- publish (as vdb_scan.hip): per-wave bests into KP slots per query; the slot
         // minimum is a lower bound of the global KP-th best.  Only at steps 1, 2, 4, 8, ... and

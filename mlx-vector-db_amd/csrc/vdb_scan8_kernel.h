@@ -87,11 +87,10 @@ __device__ __forceinline__ void group_mfma8(const f32x4 (&x)[RT][Planes8<PREC>::
         }
 }
 
-__device__ __forceinline__ int imax16(const i32x16& a) {
-    int m = max(max(a[0], a[1]), a[2]);
-#pragma unroll
-    for (int v = 3; v < 15; v += 2) m = max(max(m, a[v]), a[v + 1]);
-    return max(m, a[15]);
+__device__ __forceinline__ int imax16(const i32x16& a) {  // a depth-3 tree of v_max3_i32
+    const int m0 = max(max(a[0], a[1]), a[2]), m1 = max(max(a[3], a[4]), a[5]), m2 = max(max(a[6], a[7]), a[8]);
+    const int m3 = max(max(a[9], a[10]), a[11]), m4 = max(max(a[12], a[13]), a[14]);
+    return max(max(max(m0, m1), m2), max(max(m3, m4), a[15]));
 }
 
 // The streams the K-loop consumes -- corpus tiles, global query tiles, L2 start values -- are
@@ -398,21 +397,32 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
                 const float th = METRIC == 0 ? thr : 0.5f * thr;
                 const uint32_t cand = joined ? s_pend[wv][t][lane] : ok ? tile_valid16(mask, t0 + rt, N, lane) : 0u;
                 const uint32_t rb = (uint32_t)((t0 + rt) * 32) + 4u * (uint32_t)(lane >> 5);
-                uint32_t left = 0;
+                // each lane's pass bits from 16 independent tests (no branch per register: with one
+                // wave per SIMD a test-ballot-branch chain per register cost ~140 cycles, 2.9 K per
+                // tile), then one round per hit of the lane with the most hits (usually one)
+                float sv[16];
+                uint32_t pm = 0;
 #pragma unroll
                 for (int v = 0; v < 16; ++v) {
-                    const float sv = HL ? fmaf((float)h[v], uH, (float)l[v] * uL) : (float)h[v] * uH;
-                    const bool p = ((cand >> v) & 1u) && sv > th;
-                    if (__any(p)) {
-                        if (p) {
-                            const float sc = METRIC == 0 ? sv : 2.0f * sv;
-                            const int pos = atomicAdd(&s_cnt[ql], 1);
-                            if (pos < CAP) {
-                                s_sc[ql * CAP + pos] = sc;
-                                s_ix[ql * CAP + pos] = rb + (uint32_t)((v & 3) + 8 * (v >> 2));
-                            } else {
-                                left |= 1u << v;
-                            }
+                    sv[v] = HL ? fmaf((float)h[v], uH, (float)l[v] * uL) : (float)h[v] * uH;
+                    pm |= (sv[v] > th ? 1u : 0u) << v;
+                }
+                pm &= cand;
+                uint32_t left = 0;
+                while (__any(pm != 0u)) {
+                    if (pm != 0u) {
+                        const int v = __builtin_ctz(pm);
+                        pm &= pm - 1u;
+                        float a_ = sv[0];
+#pragma unroll
+                        for (int u = 1; u < 16; ++u) a_ = v == u ? sv[u] : a_;
+                        const float sc = METRIC == 0 ? a_ : 2.0f * a_;
+                        const int pos = atomicAdd(&s_cnt[ql], 1);
+                        if (pos < CAP) {
+                            s_sc[ql * CAP + pos] = sc;
+                            s_ix[ql * CAP + pos] = rb + (uint32_t)((v & 3) + 8 * (v >> 2));
+                        } else {
+                            left |= 1u << v;
                         }
                     }
                 }
