@@ -1127,18 +1127,23 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     // its uncertified queries cost the exact path
     const bool auto_b16 = k <= kAutoBf16MaxK;
     // AUTO keeps both copies with auto_i8: the one-plane pass is I8 unless an I8 hold is on
-    // (then BF16); the x3 pass (k > 16, holds, re-passes, retries) is BF16X3 -- faster than I8X3,
-    // whose two accumulator sets per tile take half BF16X3's row tiles per wave
+    // (then BF16); the k > 16 pass is I8X3 unless an I8 hold is on (then BF16X3) -- with the
+    // insertion by pass-bit masks I8X3 runs C4 / C3 / C2 at 2.89 / 1.42 / 0.28 ms against BF16X3's
+    // 3.41 / 2.17 / 0.47 (profiles/r03_i8/c4prec, x3prec); holds, re-passes and retries stay
+    // BF16X3 (per-element relative precision: no dependence on the rows' range)
+    const bool x3_i8 = auto_prec && !opt.force_b3 && !auto_b16 && ix->auto_i8;
     const bool auto_x3 = auto_prec && (opt.force_b3 || !auto_b16 || (approx && auto_take_hold(ix)));
-    const bool auto_8 = auto_prec && !auto_x3 && ix->auto_i8 && !(approx && auto_take_hold8(ix));
+    const bool hold8 = auto_prec && ix->auto_i8 && approx && (x3_i8 || !auto_x3) && auto_take_hold8(ix);
+    const bool auto_8 = auto_prec && !auto_x3 && ix->auto_i8 && !hold8;
+    const bool auto_8x3 = x3_i8 && !hold8;
     const int prec_req = !ix->Xs ? PREC_FP32
                          : ix->precision == VDB_PREC_BF16X3 ? PREC_BF16X3
                          : ix->precision == VDB_PREC_BF16 ? PREC_BF16
                          : ix->precision == VDB_PREC_I8X3 ? PREC_I8X3
                          : ix->precision == VDB_PREC_I8 ? PREC_I8
-                         : auto_prec ? (auto_x3 ? PREC_BF16X3 : auto_8 ? PREC_I8 : PREC_BF16)
+                         : auto_prec ? (auto_x3 ? (auto_8x3 ? PREC_I8X3 : PREC_BF16X3) : auto_8 ? PREC_I8 : PREC_BF16)
                                      : PREC_FP32;
-    if (auto_prec && approx && !auto_x3) ix->last_i8 = auto_8;
+    if (auto_prec && approx && (!auto_x3 || x3_i8)) ix->last_i8 = auto_8 || auto_8x3;
     if (approx) ix->n_by_prec[prec_req]++;
     // the "one plane" precisions (a wide certificate: KP = 128 for small k) and their re-pass
     const bool one_plane = prec_req == PREC_BF16 || prec_req == PREC_I8;
@@ -1449,7 +1454,8 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
                     }
                 }
                 rc = run_exact(ix, w, Qd, qn64, flags + 1, B, k, md, out_s, out_i, out_k, index_offset, row_ids, st,
-                               flags, flags + B + 1, done, auto_prec && one_plane ? ix->h_totals : nullptr);
+                               flags, flags + B + 1, done,
+                               auto_prec && (one_plane || prec == PREC_I8X3) ? ix->h_totals : nullptr);
                 return rc;
             }
             HIP_TRY(hipMemcpyAsync(w->host_flag, flags, sizeof(int), hipMemcpyDeviceToHost, st));
@@ -1476,6 +1482,9 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
                     return kRetryBf16x3;
                 }
             }
+            // auto's I8X3 pass: a failure the size of the one-plane passes' retries holds BF16X3
+            // for the next searches (this batch's uncertified queries take the exact path below)
+            if (auto_prec && prec == PREC_I8X3 && n_flag > std::max(1, B / 8) && !ix->no_fallback) auto_fail8(ix);
             if (timed) {
                 const int frc = flush_timing(ix, w);
                 if (frc) return frc;

@@ -205,7 +205,8 @@ def test_bf16_directional_residual_bound(vdb, metric, precision):
 
 def _auto_index(vdb, D, a8):
     """An auto-precision index with (a8 = 1, the default) or without the int8 copy: its
-    one-plane pass is I8 (BF16 during an I8 hold) or BF16; the x3 pass is BF16X3 either way.
+    one-plane pass is I8 (BF16 during an I8 hold) or BF16; the x3 pass of holds, re-passes and
+    retries is BF16X3 either way (k > 16 runs I8X3 with the int8 copy: the test below).
     Returns it and the stat names of its one-plane / x3 passes."""
     ix = vdb.NativeIndex(D, "cosine")
     ix.set_param("auto_int8", a8)
@@ -310,6 +311,47 @@ def test_auto_hold8_holds_bf16_until_the_rows_change(vdb):
     assert ix.stat("auto_hold8") == 0
     ix.search(Q, k)
     assert ix.stat("searches_i8") == 2
+
+
+def test_auto_k_above_16_runs_i8x3_and_holds_bf16x3_after_a_failure(vdb):
+    """With the int8 copy, auto's k > 16 pass is I8X3 (exact results through the certificate);
+    rows the 16-bit planes cannot separate -- two tight clusters far apart, so the one
+    quantisation step is set by the clusters' distance -- leave most queries uncertified: the
+    batch falls back to the exact path and the index holds BF16X3 for the next 16 searches."""
+    rng = np.random.default_rng(47)
+    D, N, B, k = 128, 6000, 16, 40
+    V = rng.random((N, D), dtype=np.float32)
+    Q = rng.random((B, D), dtype=np.float32)
+    ix, _ = _auto_index(vdb, D, 1)
+    ix.add(V)
+    es, ei, ek = ref_cpu.exact_search(Q, V, k, "cosine")
+    s, i, kk = ix.search(Q, k, with_keys=True)
+    np.testing.assert_array_equal(i, ei)
+    np.testing.assert_array_equal(kk, ek)
+    assert ix.stat("searches_i8x3") == 1 and ix.stat("searches_bf16x3") == 0
+    assert ix.stat("fallback_queries") == 0 and ix.stat("auto_hold8") == 0
+    ix.close()
+
+    b1, b2 = rng.random(D, dtype=np.float32), rng.random(D, dtype=np.float32)
+    side = rng.random(N) < 0.5
+    V = (np.where(side[:, None], b1, b2) + 1e-5 * rng.standard_normal((N, D))).astype(np.float32)
+    Q = (V[rng.integers(0, N, B)] + 1e-6 * rng.standard_normal((B, D))).astype(np.float32)
+    ix, _ = _auto_index(vdb, D, 1)
+    ix.add(V)
+    es, ei, ek = ref_cpu.exact_search(Q, V, k, "cosine")
+    s, i, kk = ix.search(Q, k, with_keys=True)
+    np.testing.assert_array_equal(i, ei)
+    np.testing.assert_array_equal(kk, ek)
+    assert ix.stat("searches_i8x3") == 1 and ix.stat("fallback_queries") > B // 8
+    assert ix.stat("auto_hold8") == 16
+    s, i, kk = ix.search(Q, k, with_keys=True)  # the hold: BF16X3
+    np.testing.assert_array_equal(kk, ek)
+    assert ix.stat("searches_i8x3") == 1 and ix.stat("searches_bf16x3") == 1 and ix.stat("auto_hold8") == 15
+    ix.add(V[:1])  # new rows end the hold
+    assert ix.stat("auto_hold8") == 0
+    ix.search(Q, k)
+    assert ix.stat("searches_i8x3") == 2
+    ix.close()
 
 
 @pytest.mark.parametrize("a8", [1, 0])
