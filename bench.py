@@ -682,7 +682,7 @@ def bench_brute(cfg, args, world, rank, local, dev, primary=True):
             "vs_baseline": None,
             "dtype": {"fp32": "f32", "bf16x3": "f32 (bf16x3 split MFMA candidates, fp64 exact rerank)",
                       "bf16": "f32 (bf16 corpus x split query MFMA candidates, fp64 exact rerank)",
-                      "i8": "f32 (int8 centred corpus x 16-bit query integer-MFMA candidates, fp64 exact rerank)",
+                      "i8": "f32 (int8 centred corpus x int8 query integer-MFMA candidates, fp64 exact rerank)",
                       "i8x3": "f32 (16-bit fixed-point corpus x query integer-MFMA candidates, fp64 exact rerank)"}[prec],
             "data": "synthetic uniform [0,1) fp32 (numpy PCG64, corpus seed 0 per 65536-row chunk, queries seed 1)",
             "config": {"workload": f"{cfg}: {desc}", "n_rows": N, "dim": D, "global_batch": Bg,
