@@ -419,6 +419,8 @@ def main():
     ap.add_argument("--pilot-fused", type=int, default=None, help="split pass: 1 the scan derives the pilot bound, "
                     "0 a separate bound kernel (tuning)")
     ap.add_argument("--pilot-rank", type=int, default=None, help="rank of the pilot bound (tuning; default: Poisson rule)")
+    ap.add_argument("--scan-pace", type=int, default=None, help="int8 pass: 1 pace the query blocks of a row range, "
+                    "0 off (default; tuning)")
     ap.add_argument("--rows", type=int, default=None, help="override the corpus rows (exploration only)")
     ap.add_argument("--timing", type=int, default=1,
                     help="1: the library's HIP events around the scan in the timed region (roofline); 0: none "
@@ -516,6 +518,8 @@ def bench_brute(cfg, args, world, rank, local, dev, primary=True):
         ix.set_param("pilot_fused", args.pilot_fused)
     if args.pilot_rank is not None:
         ix.set_param("pilot_rank", args.pilot_rank)
+    if args.scan_pace is not None:
+        ix.set_param("scan_pace", args.scan_pace)
     if args.no_fallback:
         ix.set_param("no_fallback", 1)
     ix.reserve(n_local)
@@ -614,7 +618,7 @@ def bench_brute(cfg, args, world, rank, local, dev, primary=True):
         #     per launch -- every corpus row read once at the element size of the candidate copy it
         #     scans (i8: the hi plane, 1 B; bf16 / i8x3: 2 B; bf16x3 / fp32: 4 B), the L2 row start
         #     values, the queries; its own MFMA count (fp32: 2BND on the FP32 peak; bf16 2x and
-        #     bf16x3 3x the products on the bf16 peak; i8 2x and i8x3 3x on the int8 peak) -- bound
+        #     bf16x3 3x the products on the bf16 peak; i8 1x (xh qh) and i8x3 3x on the int8 peak) -- bound
         #     by whichever floor is longer;
         # (2) "survey_8d": SURVEY.md §8(d)'s algorithmic work for the config (fp32 arithmetic:
         #     2BND flops, 4 B per element; C3 names the bf16 corpus, 2 B) on the roofline §8(d) calls
@@ -623,9 +627,9 @@ def bench_brute(cfg, args, world, rank, local, dev, primary=True):
         #     fp64 rerank + certificate.
         Dp = (D + 63) // 64 * 64
         elem = {"i8": 1, "i8x3": 2, "bf16": 2}.get(prec, 4)
-        q_elem = 2 if prec in ("i8", "i8x3") else 4  # query tiles (int8: two 1-byte planes)
+        q_elem = {"i8": 1, "i8x3": 2}.get(prec, 4)  # query tiles (i8: the hi plane; i8x3: both 1-byte planes)
         hbm_bytes = n_local * Dp * elem + (n_local * 4 if metric == "euclidean" else 0) + Bg * Dp * q_elem
-        n_mfma = {"fp32": 1, "bf16x3": 3, "bf16": 2, "i8": 2, "i8x3": 3}[prec]
+        n_mfma = {"fp32": 1, "bf16x3": 3, "bf16": 2, "i8": 1, "i8x3": 3}[prec]
         mfma_flops = n_mfma * 2.0 * Bg * n_local * D
         mfma_peak = {"fp32": FP32_MFMA_PEAK_TFLOPS, "bf16x3": BF16_MFMA_PEAK_TFLOPS, "bf16": BF16_MFMA_PEAK_TFLOPS,
                      "i8": I8_MFMA_PEAK_TOPS, "i8x3": I8_MFMA_PEAK_TOPS}[prec]

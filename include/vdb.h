@@ -89,19 +89,20 @@ enum { VDB_MEM_HOST = 0, VDB_MEM_DEVICE = 1 };
  *                    along d) and each query's own rounding (vdb_scan8_kernel.h).
  *   VDB_PREC_I8X3    both planes (2 bytes per element): xh.qh + (xh.ql + xl.qh)/256, an
  *                    error bound of bf16x3's order at half its bytes and MFMA cycles.
- *   VDB_PREC_AUTO    (default) the x3 precision for k > 16 (the one-plane ones would need 256
- *                    candidates per query there, a slower pass); otherwise the one-plane one,
- *                    per batch: I8 / I8X3 on the int8 copy (knob "auto_int8" = 1, the default;
- *                    start value from VDB_AUTO_I8), BF16 / BF16X3 on the split copy (0).
- *                    A host-memory search re-passes its
- *                    uncertified queries (at most 1/8 of the batch, at most 64) in the x3 one
- *                    as one gathered sub-search and stays one-plane; more than that reruns the
- *                    batch in x3 and starts a HOLD: the next 16 searches run x3,
- *                    doubling per failed BF16 probe up to 2048 (reset by 64 certified BF16
- *                    searches, or when the rows change).  A device-memory search sees its
- *                    fallback counts a search or more late (no host sync): its flagged
- *                    queries take the device-gated exact path and the next search starts
- *                    the hold.  Stats "repass_queries", "auto_hold". */
+ *   VDB_PREC_AUTO    (default) per batch, on the int8 copy (knob "auto_int8" = 1, the
+ *                    default; start value from VDB_AUTO_I8): I8 for k <= 16, I8X3 for k > 16
+ *                    (a one-plane pass would need 256 candidates per query there); on the split
+ *                    copy (auto_int8 = 0): BF16 / BF16X3.  A host-memory search re-passes its
+ *                    uncertified one-plane queries (at most 1/8 of the batch, at most 64) in
+ *                    BF16X3 as one gathered sub-search and keeps its precision; more than that
+ *                    reruns the batch in BF16X3 and starts a HOLD on the next precision down
+ *                    the list I8 -> BF16 -> BF16X3 (an I8X3 failure: its batch takes the exact
+ *                    path, the hold runs BF16X3) for the next 16 searches, doubling per failed
+ *                    probe up to 2048 (reset by 64 certified searches, or when the rows change).
+ *                    A device-memory search sees its fallback counts a search or more late (no
+ *                    host sync): its flagged queries take the device-gated exact path and the
+ *                    next search starts the hold.  Stats "repass_queries", "auto_hold",
+ *                    "auto_hold8". */
 enum { VDB_PREC_FP32 = 0, VDB_PREC_BF16X3 = 1, VDB_PREC_BF16 = 2, VDB_PREC_AUTO = 3, VDB_PREC_I8 = 4, VDB_PREC_I8X3 = 5 };
 
 typedef struct vdb_index vdb_index;
@@ -130,6 +131,7 @@ int32_t vdb_index_reserve(vdb_index* idx, int64_t rows);
  * "scan_publish" (split pass slot publishing: -1 auto = off (round 3 measurement), 0 off,
  * 1 on), "scan_q4" (split pass 128-query shape for D <= 128, KP = 128, B >= 256: -1 auto = on,
  * 0 off, 1 on where it applies), "scan_qlds" (-1 auto: query block in LDS when it fits, 0 never),
+ * "scan_pace" (int8 pass, 0 default / 1: pace the query blocks that share a row range),
  * "scan3" (large-batch shape, vdb_scan3_kernel.h: 0 default off, 1 on, -1 auto), "scan_qring" (split pass, lockstep step ends: 1 = the
  * query operand through a per-workgroup LDS ring; start value from the environment
  * variable VDB_SCAN_QRING, default 0), "gate_div" (1..64: the device-gated exact

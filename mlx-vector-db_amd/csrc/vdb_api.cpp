@@ -178,6 +178,11 @@ struct vdb_index {
     int64_t finish_split = 1;  // workgroups per query in the finish kernel (tuning)
     int64_t scan3 = 0;         // large-batch candidate pass: -1 auto (B >= 128), 0 off, 1 always (vdb_scan3_kernel.h)
     int64_t scan_qlds = -1;    // split pass: query block in LDS when it fits (-1 auto), 0 never
+    // int8 pass: pace the query blocks of a row range (vdb_scan8_kernel.h), opt-in: it held C4's
+    // 8 blocks within 5 steps (from 26) and ran the scan at 4.99 ms against 2.90 without
+    // (the range at its slowest block's speed, the prefetch drained per sleep; profiles/r03_i8/pace)
+    bool scan_pace = false;
+    std::atomic<uint32_t> pace_seq{0};  // launch tag of the pacing counters
     int64_t scan_q4 = -1;      // split pass 128-query shape (D <= 128, KP = 128, B >= 256): -1 auto, 0 off, 1 on
     // stats
     std::atomic<int64_t> n_searches{0}, n_queries{0}, n_fallback{0}, n_overflow{0}, n_repass{0}, n_scan3{0}, n_q4{0};
@@ -678,6 +683,9 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
     } else if (n == "finish_split") {
         if (value < 1 || value > 8) return set_error(VDB_ERR_INVALID, "finish_split must be in [1, 8]");
         ix->finish_split = value;
+    } else if (n == "scan_pace") {
+        if (value < 0 || value > 1) return set_error(VDB_ERR_INVALID, "scan_pace must be 0 or 1");
+        ix->scan_pace = value != 0;
     } else if (n == "scan_qlds") {
         if (value < -1 || value > 0) return set_error(VDB_ERR_INVALID, "scan_qlds must be -1 or 0");
         ix->scan_qlds = value;
@@ -1244,6 +1252,7 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     bytes += (size_t)Bp * 4 + 256;                          // shared thresholds
     bytes += (size_t)Bp * (KP_MAX + PILOT_SLOTS) * 4 + 256;  // shared threshold slots + pilot slots
     bytes += (size_t)Bp * 12 + 1024;                          // int8 pass: qmax, lsl, qerr [Bp]; qscal
+    bytes += ((size_t)(n_wg + 7) / 8 * 8 * n_qblocks + 64) * 4; // int8 pass: pacing counters
     const bool priv = !exact_all && !split_pass && !i8_pass && scan_priv(prec, variant, KP);
     // global per-query candidate lists: at most 512 entries per workgroup and query
     // (the largest LDS buffer of any variant; 4 x 64 for the wave-private one)
@@ -1312,6 +1321,7 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     float* q8lsl = c.take<float>(Bp);
     float* q8err = c.take<float>(Bp);
     float* q8scal = c.take<float>(64);
+    uint32_t* pace = c.take<uint32_t>((size_t)(n_wg + 7) / 8 * 8 * n_qblocks + 64);
 
     const float* Qd = queries;
     const uint32_t* md = row_mask;
@@ -1385,7 +1395,8 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
             if (q4 && !use_s3) ix->n_q4++;
             if (i8_pass)
                 HIP_TRY(launch_scan8(prec, ix->metric, KP, Xscan, ix->rinit32, md, Qt, q8lsl, q8scal, Gs, N, B,
-                                     n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, lockstep,
+                                     n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr,
+                                     ix->scan_pace ? pace : nullptr, ix->pace_seq.fetch_add(1) + 1, lockstep,
                                      (int)ix->scan_qlds, st));
             else if (use_s3)
                 HIP_TRY(launch_scan3(prec, ix->metric, Xscan, ix->rinit32, md, Qt, Gs, N, B, n_qb3, steps3, n_wg3, spw3,

@@ -56,7 +56,8 @@ int scan8_qb(int KP);  // queries per block of the int8 pass
 hipError_t launch_scan8(int prec, int metric, int KP, const float* Xq, const float* rinit, const uint32_t* mask,
                         const float* Qq, const float* lsl, const float* qscal, int G8, int64_t N, int B,
                         int n_qblocks, int64_t n_steps, int n_wg, int spw, float* gl_s, uint32_t* gl_i,
-                        uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr, int lockstep, int qlds, hipStream_t st);
+                        uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr, uint32_t* pace, uint32_t pace_tag,
+                        int lockstep, int qlds, hipStream_t st);
 
 // Ingest: row-major fp32 [n][D] (device) -> the index's row-major fp32 copy X [cap][Dp]
 // (zero padded to Dp = 8 G; read by the exact paths, export and the graph) rows [row0, row0+n),

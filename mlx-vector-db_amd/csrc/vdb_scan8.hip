@@ -328,7 +328,8 @@ int scan8_qb(int KP) { (void)KP; return 64; }  // every KP (KP = 256: KW = 64, S
 hipError_t launch_scan8(int prec, int metric, int KP, const float* Xq, const float* rinit, const uint32_t* mask,
                         const float* Qq, const float* lsl, const float* qscal, int G8, int64_t N, int B,
                         int n_qblocks, int64_t n_steps, int n_wg, int spw, float* gl_s, uint32_t* gl_i,
-                        uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr, int lockstep, int qlds, hipStream_t st) {
+                        uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr, uint32_t* pace, uint32_t pace_tag,
+                        int lockstep, int qlds, hipStream_t st) {
     // the query block in LDS: auto when it fits (qlds < 0), never with 0 -- except for rows of
     // fewer 32-dim groups than the global-operand variants keep in flight (PX = 4)
     const bool ql = (qlds != 0 && scan8_qlds(G8, KP)) || G8 < 4;
@@ -339,7 +340,7 @@ hipError_t launch_scan8(int prec, int metric, int KP, const float* Xq, const flo
                                    : nullptr;
     if (!unit || metric < 0 || metric > 1) return hipErrorInvalidValue;
     return unit(KP, Xq, rinit, mask, Qq, lsl, qscal, G8, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt,
-                gl_cap, gthr, nt, ql, fs, st);
+                gl_cap, gthr, pace, pace_tag, nt, ql, fs, st);
 }
 
 }  // namespace vdb

@@ -126,6 +126,39 @@ __device__ __forceinline__ void s8_tie(f32x4 (&r)[A][C]) {  // after an s8_wait:
         for (int c = 0; c < C; ++c) asm volatile("" : "+v"(r[a][c]));
 }
 
+// Pacing of the query blocks that share a row range (n_qb > 1): their workgroups start together
+// on one XCD and read the same rows, so L2 serves all but the first -- while they stay within a
+// few steps of each other.  Their insert work differs, and over C4's 1221 steps they drifted 26
+// steps apart on average (48 at most; stamps, profiles/r03_i8/st4c), and the corpus came from HBM
+// 3.3x (8.55 GB per launch against 2.6).  Each workgroup publishes its step count (tagged with
+// the launch, so an earlier launch's counts read as "no information"); a wave more than
+// S8_PACE_W steps ahead of its range's slowest sibling sleeps, at most S8_PACE_SPIN times per
+// step -- a pacing hint only: nothing waits on a sibling that is not running.  Opt-in (index
+// knob "scan_pace"): it held C4's blocks within 5 steps and made the scan slower, 4.99 ms
+// against 2.90 -- the range runs at its slowest block's speed and each sleep drains the
+// prefetch; the L2 misses were not what bounded C4 (profiles/r03_i8/pace).
+#ifndef S8_PACE_W
+#define S8_PACE_W 6
+#endif
+#ifndef S8_PACE_SPIN
+#define S8_PACE_SPIN 64
+#endif
+__device__ __forceinline__ uint32_t s8_ld_u32(const uint32_t* base, uint32_t voff) {  // L2-coherent (sc1)
+    uint32_t r;
+    asm volatile("global_load_dword %0, %1, %2 sc1" : "=v"(r) : "v"(voff), "s"(base));
+    return r;
+}
+__device__ __forceinline__ void s8_st_u32(uint32_t* base, uint32_t voff, uint32_t v) {
+    asm volatile("global_store_dword %0, %1, %2 sc1" : : "v"(voff), "v"(v), "s"(base) : "memory");
+}
+// the slowest sibling's published step count, or 0xFFFFF where none is known (lanes < n_qb)
+__device__ __forceinline__ uint32_t s8_pace_min(uint32_t v, uint32_t tag, int lane, int n_qb) {
+    uint32_t m = (lane < n_qb && (v >> 20) == tag) ? (v & 0xFFFFFu) : 0xFFFFFu;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) m = min(m, (uint32_t)__shfl_xor((int)m, off, 64));
+    return m;
+}
+
 // The smallest H that can still pass threshold th (half units) given |L uL| <= slack, minus a
 // margin for the fp32 evaluation: H <= the result means the tile's scores are all <= th.
 __device__ __forceinline__ int h_floor(float th, float slack, float invU) {
@@ -144,7 +177,8 @@ __global__ void __launch_bounds__(64 * S8_NW, 1)
 scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, const uint32_t* __restrict__ mask,
              const float* __restrict__ Qq, const float* __restrict__ lsl, const float* __restrict__ qscal, int G_arg,
              int64_t N, int B, int64_t n_steps, int steps_per_wg, int n_qb, float* __restrict__ gl_s,
-             uint32_t* __restrict__ gl_i, uint32_t* __restrict__ gl_cnt, int64_t gl_cap, uint32_t* __restrict__ gthr) {
+             uint32_t* __restrict__ gl_i, uint32_t* __restrict__ gl_cnt, int64_t gl_cap, uint32_t* __restrict__ gthr,
+             uint32_t* __restrict__ pace, uint32_t pace_tag) {
     constexpr int RT = RT_, NW = S8_NW;
     constexpr int QB = 32 * QT;
     constexpr int XPL = Planes8<PREC>::XPL, QPL = Planes8<PREC>::QPL;
@@ -167,9 +201,14 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
     const int lane = threadIdx.x & 63;
     const int lane4 = lane * 4;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    S8_STAMP(const unsigned long long st_t0 = S8_NOW(); unsigned long long st_w = 0, st_k = 0, st_e = 0, st_n = 0, st_x = 0, st_y = 0, st_z = 0;)
+    S8_STAMP(const unsigned long long st_t0 = S8_NOW(), st_r0 = __builtin_amdgcn_s_memrealtime(); unsigned long long st_w = 0, st_k = 0, st_e = 0, st_n = 0, st_x = 0, st_y = 0, st_z = 0;)
     int wg, qb;
     xcd_map(n_qb, wg, qb);
+    const uint32_t ptag = pace_tag & 0xFFFu;
+    const uint32_t pbase = (uint32_t)(wg * n_qb) * 4u;  // this range's counters, one per query block
+    const uint32_t poff = pbase + (uint32_t)(lane < n_qb ? lane : 0) * 4u;
+    if (pace && threadIdx.x == 0) s8_st_u32(pace, pbase + (uint32_t)qb * 4u, ptag << 20);
+    uint32_t pv = 0u;  // the siblings' counts, loaded in a step's tail, read in its epilogue
     if (threadIdx.x == 0) {
         s_need = 0;
         s_done = 0;
@@ -322,6 +361,9 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
             for (int p = 0; p < PX; ++p)
                 group(p, gb + p, xs + (size_t)(gb + p + PX) * XGSTEP, Qbase + (size_t)(gb + p + PQ) * GSTEP);
         }
+        // the siblings' counts: issued only where the epilogue waits for them (an asm load never
+        // waited for could land in a register the compiler has reused)
+        if (pace && s + 1 < s_end) pv = s8_ld_u32(pace, poff);
         if (s + 1 < s_end) load_epi(s + 1, rin);
 #pragma unroll
         for (int p = 0; p < PX; ++p)
@@ -452,6 +494,19 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
             todo = pmask;
             pmask = 0;
         }
+        if (pace && s + 1 < s_end) {
+            const uint32_t done = (uint32_t)(s - s_begin + 1);
+            if (wv == 0 && lane == 0) s8_st_u32(pace, pbase + (uint32_t)qb * 4u, (ptag << 20) | min(done, 0xFFFFFu));
+            // younger than the counts: the L2 start values (RT x 4 loads) and the tail's refills
+            asm volatile("s_waitcnt vmcnt(%1)" : "+v"(pv) : "n"(PX * LPS + (METRIC == 1 ? RT * 4 : 0)));
+            uint32_t slow = s8_pace_min(pv, ptag, lane, n_qb);
+            for (int it = 0; it < S8_PACE_SPIN && done > slow + S8_PACE_W; ++it) {
+                __builtin_amdgcn_s_sleep(8);
+                uint32_t v = s8_ld_u32(pace, poff);
+                asm volatile("s_waitcnt vmcnt(0)" : "+v"(v));  // (the stream's loads too: this wave waits anyway)
+                slow = s8_pace_min(v, ptag, lane, n_qb);
+            }
+        }
         S8_STAMP(st_e += S8_NOW() - st_c;)
     }
 
@@ -486,9 +541,10 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
     {
         const int w = blockIdx.x * NW + wv;
         if (lane == 0 && w < (1 << 16)) {
-            const unsigned long long v[9] = {S8_NOW() - st_t0, st_w, st_k, st_e, st_n, st_t0, st_x, st_y, st_z};
+            const unsigned long long v[10] = {S8_NOW() - st_t0, st_w, st_k, st_e, st_n, st_r0, st_x, st_y, st_z,
+                                              __builtin_amdgcn_s_memrealtime()};
 #pragma unroll
-            for (int i = 0; i < 9; ++i) g_scan8_stamps[w][i] = v[i];
+            for (int i = 0; i < 10; ++i) g_scan8_stamps[w][i] = v[i];
         }
     }
 #endif
@@ -500,7 +556,7 @@ template <int P, int M, int QT, int PX, int KP, int CAP, bool NT, bool QL, bool 
 static hipError_t scan8_launch_g(const float* Xq, const float* rinit, const uint32_t* mask, const float* Qq,
                                  const float* lsl, const float* qscal, int G, int64_t N, int B, int n_qblocks,
                                  int64_t n_steps, int n_wg, int spw, float* gl_s, uint32_t* gl_i, uint32_t* gl_cnt,
-                                 int64_t gl_cap, uint32_t* gthr, hipStream_t st) {
+                                 int64_t gl_cap, uint32_t* gthr, uint32_t* pace, uint32_t pace_tag, hipStream_t st) {
     auto k = scan8_kernel<P, M, QT, PX, KP, CAP, NT, QL, FS, GC, RT_, KW>;
     const size_t lds = QL ? (size_t)G * 2 * QT * 1024 : 0;
     if (QL) {
@@ -514,7 +570,8 @@ static hipError_t scan8_launch_g(const float* Xq, const float* rinit, const uint
     }
     const int n_wg8 = (n_wg + 7) / 8 * 8;
     hipLaunchKernelGGL(k, dim3(n_wg8 * n_qblocks), dim3(64 * S8_NW), lds, st, Xq, rinit, mask, Qq, lsl, qscal, G, N, B,
-                       n_steps, spw, n_qblocks, gl_s, gl_i, gl_cnt, gl_cap, gthr);
+                       n_steps, spw, n_qblocks, gl_s, gl_i, gl_cnt, gl_cap, gthr, n_qblocks > 1 ? pace : nullptr,
+                       pace_tag);
     return hipGetLastError();
 }
 
@@ -522,16 +579,16 @@ template <int P, int M, int QT, int PX, int KP, int CAP, bool NT, bool QL, bool 
 static hipError_t scan8_launch(const float* Xq, const float* rinit, const uint32_t* mask, const float* Qq,
                                const float* lsl, const float* qscal, int G, int64_t N, int B, int n_qblocks,
                                int64_t n_steps, int n_wg, int spw, float* gl_s, uint32_t* gl_i, uint32_t* gl_cnt,
-                               int64_t gl_cap, uint32_t* gthr, hipStream_t st) {
+                               int64_t gl_cap, uint32_t* gthr, uint32_t* pace, uint32_t pace_tag, hipStream_t st) {
     if constexpr (QL) {
         if (G == 4)  // D = 128: the group loop unrolls, and the whole next step is in flight
             return scan8_launch_g<P, M, QT, 4, KP, CAP, NT, QL, FS, 4, scan8_rt(P, M), KW>(Xq, rinit, mask, Qq, lsl, qscal, G, N, B,
                                                                         n_qblocks, n_steps, n_wg, spw, gl_s, gl_i,
-                                                                        gl_cnt, gl_cap, gthr, st);
+                                                                        gl_cnt, gl_cap, gthr, pace, pace_tag, st);
     }
     return scan8_launch_g<P, M, QT, PX, KP, CAP, NT, QL, FS, 0, scan8_rt(P, M), KW>(Xq, rinit, mask, Qq, lsl, qscal, G, N, B, n_qblocks,
                                                                 n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr,
-                                                                st);
+                                                                pace, pace_tag, st);
 }
 
 // The query block goes to LDS when it is small (short rows: 64 queries x 128 dims x 2 planes =
@@ -542,9 +599,10 @@ inline bool scan8_qlds(int G8, int KP) { return (size_t)G8 * 2 * 2 * 1024 <= 32 
 #define S8_UNIT_PARAMS                                                                                             \
     int KP, const float *Xq, const float *rinit, const uint32_t *mask, const float *Qq, const float *lsl,          \
         const float *qscal, int G, int64_t N, int B, int n_qblocks, int64_t n_steps, int n_wg, int spw,           \
-        float *gl_s, uint32_t *gl_i, uint32_t *gl_cnt, int64_t gl_cap, uint32_t *gthr, bool nt, bool ql, bool fs, \
-        hipStream_t st
-#define S8_ARGS Xq, rinit, mask, Qq, lsl, qscal, G, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, st
+        float *gl_s, uint32_t *gl_i, uint32_t *gl_cnt, int64_t gl_cap, uint32_t *gthr, uint32_t *pace,            \
+        uint32_t pace_tag, bool nt, bool ql, bool fs, hipStream_t st
+#define S8_ARGS \
+    Xq, rinit, mask, Qq, lsl, qscal, G, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, pace, pace_tag, st
 #define S8_ONE(P, M, KPV, QTV, PXV, CAPV, NTV, QLV, FSV, KWV) \
     if (KP == KPV && nt == NTV && ql == QLV && fs == FSV)       \
         return scan8_launch<P, M, QTV, PXV, KPV, CAPV, NTV, QLV, FSV, KWV>(S8_ARGS);

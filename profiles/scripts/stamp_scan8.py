@@ -1,7 +1,7 @@
-"""Per-wave phase breakdown of scan8_kernel, I8 cosine (diagnostic stamp build lib/libvdb_amd_st8.so,
-make variant VTAG=st8 VDEFS=-DVDB_STAMP8).
+"""Per-wave phase breakdown of scan8_kernel (diagnostic stamp build lib/libvdb_amd_st8.so,
+make variant VTAG=st8 VDEFS=-DVDB_STAMP8): I8 cosine (unit i1c) or I8X3 L2 (unit i3l).
 
-Usage: python profiles/scripts/stamp_scan8.py [config]
+Usage: python profiles/scripts/stamp_scan8.py [config] [i8|i8x3]
 """
 import ctypes, os, sys
 import numpy as np
@@ -13,8 +13,10 @@ from service import _vdb
 import bench
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c6"
+prec = sys.argv[2] if len(sys.argv) > 2 else "i8"
 N, D, B, k, metric, _ = bench.CONFIGS[cfg]
-ix = _vdb.NativeIndex(D, metric, precision="i8")
+unit = {("i8", "cosine"): "i1c", ("i8x3", "euclidean"): "i3l"}[(prec, metric)]
+ix = _vdb.NativeIndex(D, metric, precision=prec)
 ix.reserve(N)
 for s in range(0, N, 1 << 19):
     ix.add(bench.corpus_rows(N, D, s, min(s + (1 << 19), N)))
@@ -24,12 +26,17 @@ for _ in range(4):
 lib = _vdb.load_library()
 n = 1 << 16
 buf = (ctypes.c_ulonglong * (n * 10))()
-lib.vdb_debug_scan8_stamps_i1c(buf, n)
-a = np.array(buf, dtype=np.uint64).reshape(n, 10).astype(np.float64)
-a = a[a[:, 0] > 0]
-t0 = a[:, 5] - a[:, 5].min()
-end = t0 + a[:, 0]
-print(f"{cfg} i8: waves {len(a)}, steps/wave mean {a[:, 4].mean():.2f}; ticks (s_memtime) per wave, mean:")
+getattr(lib, f"vdb_debug_scan8_stamps_{unit}")(buf, n)
+raw = np.array(buf, dtype=np.uint64).reshape(n, 10)
+out = os.environ.get("STAMP_OUT")
+if out:
+    np.save(out, raw)
+a = raw.astype(np.float64)
+live = a[:, 0] > 0
+a = a[live]
+t0 = a[:, 5] - a[:, 5].min()  # s_memrealtime (100 MHz, one clock for the chip)
+end = a[:, 9] - a[:, 5].min()
+print(f"{cfg} {prec}: waves {len(a)}, steps/wave mean {a[:, 4].mean():.2f}; ticks (s_memtime) per wave, mean:")
 for i, name in ((0, "total"), (1, "stream waits"), (2, "k-loop incl. waits"), (3, "epilogue")):
     print(f"  {name:20s} {a[:, i].mean():12.0f}  per step {a[:, i].mean() / max(a[:, 4].mean(), 1):10.0f}")
 sn = max(a[:, 4].mean(), 1)
@@ -38,4 +45,22 @@ print(f"  steps with a passing tile {(x & 0xFFFFF).astype(float).mean() / sn:.3f
       f"{(x >> 20).astype(float).mean() / sn:.3f}; compaction rounds per wave {(y & 0xFFFFF).astype(float).mean():.1f}")
 print(f"  tile tests per step {a[:, 8].mean() / sn:10.0f}; tests + insertions (before the compaction check) per step "
       f"{(y >> 20).astype(float).mean() / sn:10.0f}")
-print(f"  start spread {t0.max():.0f} ticks, end spread {end.max() - end.min():.0f}, span {end.max():.0f}")
+print(f"  start spread {t0.max() / 100:.1f} us, end spread {(end.max() - end.min()) / 100:.1f} us, span {end.max() / 100:.1f} us")
+
+# drift between the query blocks of a row range (xcd_map: block L -> j = L / 8, qb = j % n_qb,
+# range = 8 (j / n_qb) + L % 8): end times of a range's workgroups, in steps of this wave
+n_qb = (B + 63) // 64
+if n_qb > 1:
+    w = np.nonzero(live)[0]
+    L = w // 4
+    j = L // 8
+    rng_id = 8 * (j // n_qb) + L % 8
+    endt = a[:, 9]
+    step_rt = ((a[:, 9] - a[:, 5]) / np.maximum(a[:, 4], 1)).mean()  # real-time ticks per step
+    spans = []
+    for r in np.unique(rng_id):
+        e = endt[rng_id == r]
+        spans.append((e.max() - e.min()) / step_rt)
+    spans = np.array(spans)
+    print(f"  query blocks per range {n_qb}: end-time spread within a range, in steps: "
+          f"mean {spans.mean():.1f}, max {spans.max():.1f} (of {a[:, 4].mean():.0f} steps)")
