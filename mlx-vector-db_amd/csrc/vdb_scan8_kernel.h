@@ -586,6 +586,15 @@ static hipError_t scan8_launch(const float* Xq, const float* rinit, const uint32
                                                                         n_qblocks, n_steps, n_wg, spw, gl_s, gl_i,
                                                                         gl_cnt, gl_cap, gthr, pace, pace_tag, st);
     }
+    // the step loop takes the groups PX at a time: Dp / 32 groups is only even (D = 192: 6), so
+    // where PX does not divide them the 2-deep variant runs (4 deep, the tail's refills would read
+    // the next row tile's groups into this one's scores)
+    if constexpr (PX != 2) {
+        if (G % PX != 0)
+            return scan8_launch_g<P, M, QT, 2, KP, CAP, NT, QL, FS, 0, scan8_rt(P, M), KW>(
+                Xq, rinit, mask, Qq, lsl, qscal, G, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap,
+                gthr, pace, pace_tag, st);
+    }
     return scan8_launch_g<P, M, QT, PX, KP, CAP, NT, QL, FS, 0, scan8_rt(P, M), KW>(Xq, rinit, mask, Qq, lsl, qscal, G, N, B, n_qblocks,
                                                                 n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr,
                                                                 pace, pace_tag, st);

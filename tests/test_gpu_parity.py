@@ -203,6 +203,21 @@ def test_bf16_directional_residual_bound(vdb, metric, precision):
     # i8 (8-bit query: a wider bound) leaves a few of these 1536-dim queries to auto's re-pass
 
 
+@pytest.mark.parametrize("qlds", [-1, 0])
+@pytest.mark.parametrize("D", [192, 320])
+@pytest.mark.parametrize("metric", ["cosine", "euclidean"])
+@pytest.mark.parametrize("precision", ["i8", "i8x3"])
+def test_i8_group_counts_not_a_multiple_of_the_prefetch(vdb, precision, metric, D, qlds):
+    """Dp / 32 groups is only even (D = 192: 6, D = 320: 10): the int8 passes that keep 4 groups
+    in flight cannot step through them, and the launcher falls back to 2 (4 deep, the step's tail
+    would read the next row tile's groups into the scores).  With no_fallback the candidate pass
+    alone must certify and order every query, with the query block in LDS (-1) and from L2 (0)."""
+    rng = np.random.default_rng(D + 5)
+    V = rng.random((6000, D), dtype=np.float32)
+    Q = rng.random((24, D), dtype=np.float32)
+    _check(vdb, V, Q, 10, metric, precision=precision, params={"no_fallback": 1, "scan_qlds": qlds})
+
+
 def _auto_index(vdb, D, a8):
     """An auto-precision index with (a8 = 1, the default) or without the int8 copy: its
     one-plane pass is I8 (BF16 during an I8 hold) or BF16; the x3 pass of holds, re-passes and
