@@ -510,6 +510,20 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
         S8_STAMP(st_e += S8_NOW() - st_c;)
     }
 
+    // The last step's tail refilled the slots (and, global operand, the query tiles) with loads
+    // nothing reads.  To the compiler those registers are free once the loop ends -- but the loads
+    // are still landing: wait for them with the slots tied live until here, so no other value
+    // shares their registers meanwhile (seen: a cold first search of an L2 index returned wrong,
+    // certified results when the one-plane LDS layout moved the flush's registers onto them).
+    if (s_begin < s_end) {
+#pragma unroll
+        for (int p = 0; p < PX; ++p) s8_wait<0>(xr[p]);
+        if constexpr (!QLDS) {
+#pragma unroll
+            for (int p = 0; p < PQ; ++p) s8_tie(qr[p]);
+        }
+    }
+
     // FLAGSYNC: keep answering compaction rounds until every wave is past its last step
     if (FLAGSYNC && lane == 0) atomicAdd(&s_done, 1);
     for (; FLAGSYNC;) {

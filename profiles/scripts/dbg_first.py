@@ -3,8 +3,9 @@ query block in LDS or not; host memory, shard [0, 15000) of test_two_ranks_one_g
 import os, sys, subprocess
 ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), "..", ".."))
 if len(sys.argv) == 1:
-    cases = [("euclidean", "i8", -1)] * 3 + [("euclidean", "i8", -1, "scan_sync", 2)] * 3 + [("cosine", "i8", -1)] * 2
-    libs = {"cur": None, "pl2": os.path.join(ROOT, "mlx-vector-db_amd", "lib", "libvdb_amd_pl2.so")}
+    cases = [("euclidean", "i8", -1)] * 4 + [("cosine", "i8", -1)]
+    L = os.path.join(ROOT, "mlx-vector-db_amd", "lib")
+    libs = {"fixed": None, "onep+fixed": os.path.join(L, "libvdb_amd_onep.so")}
     for tag, lib in libs.items():
         env = dict(os.environ)
         if lib:
