@@ -419,6 +419,7 @@ def main():
     ap.add_argument("--pilot-fused", type=int, default=None, help="split pass: 1 the scan derives the pilot bound, "
                     "0 a separate bound kernel (tuning)")
     ap.add_argument("--pilot-rank", type=int, default=None, help="rank of the pilot bound (tuning; default: Poisson rule)")
+    ap.add_argument("--k", type=int, default=None, help="tuning: the config at another k (not the config's line)")
     ap.add_argument("--scan-pace", type=int, default=None, help="int8 pass: 1 pace the query blocks of a row range, "
                     "0 off (default; tuning)")
     ap.add_argument("--rows", type=int, default=None, help="override the corpus rows (exploration only)")
@@ -482,6 +483,9 @@ def bench_brute(cfg, args, world, rank, local, dev, primary=True):
     elsewhere).  primary=False: the compact secondary line (no CPU baseline / serving)."""
     rec = None
     N, D, B, k, metric, desc = CONFIGS[cfg]
+    if args.k is not None:  # tuning: the config's rows and batch at another k (not a bench line)
+        k = int(args.k)
+        desc = f"{desc} [k = {k}]"
     N = (args.rows if primary else None) or N
     scaling = args.scaling or DEFAULT_SCALING.get(cfg, "weak")
     lo, hi = shard_bounds(N, world, rank)
