@@ -185,7 +185,7 @@ struct vdb_index {
     std::atomic<uint32_t> pace_seq{0};  // launch tag of the pacing counters
     int64_t scan_q4 = -1;      // split pass 128-query shape (D <= 128, KP = 128, B >= 256): -1 auto, 0 off, 1 on
     // stats
-    std::atomic<int64_t> n_searches{0}, n_queries{0}, n_fallback{0}, n_overflow{0}, n_repass{0}, n_scan3{0}, n_q4{0};
+    std::atomic<int64_t> n_searches{0}, n_queries{0}, n_fallback{0}, n_overflow{0}, n_incons{0}, n_repass{0}, n_scan3{0}, n_q4{0};
     std::atomic<int64_t> n_by_prec[N_PREC] = {{0}, {0}, {0}, {0}, {0}};  // candidate passes per PREC_* (VDB_PREC_AUTO's choices)
     std::atomic<int64_t> scan_ns{0}, pipe_ns{0}, n_timed{0};
     unsigned long long* d_totals = nullptr;  // device: flagged / overflowed / flagged-in-bf16 queries of device-gated searches
@@ -711,6 +711,19 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
         ix->scan_publish = value;
     } else if (n == "pilot_fused") {
         ix->pilot_fused = value != 0;
+    } else if (n == "debug_stale_rinit") {
+        // TEST ONLY: plants a stale L2 start value, -|x|^2/2 := 0 for row `value` (the operand a
+        // scan read before its load landed in VERDICT r3), so the consistency guard of the
+        // finish can be seen to flag the query instead of certifying it
+        if (value < 0) return set_error(VDB_ERR_INVALID, "debug_stale_rinit: row must be >= 0");
+        HIP_TRY(hipSetDevice(ix->device));
+        std::unique_lock<std::shared_mutex> g(ix->mu);
+        if (value >= ix->count || !ix->rinit32) return set_error(VDB_ERR_INVALID, "debug_stale_rinit: no row %lld", (long long)value);
+        const int wr = wait_idle(ix);
+        if (wr) return wr;
+        const float zero = 0.0f;
+        HIP_TRY(hipMemcpyAsync(ix->rinit32 + value, &zero, sizeof(float), hipMemcpyHostToDevice, ix->stream));
+        HIP_TRY(hipStreamSynchronize(ix->stream));
     } else if (n == "pilot_rank") {
         if (value < 0 || value > 256) return set_error(VDB_ERR_INVALID, "pilot_rank must be in [0, 256]");
         ix->pilot_rank_override = value;
@@ -745,6 +758,7 @@ int32_t vdb_index_get_stat(const vdb_index* cix, const char* name, int64_t* valu
     else if (n == "auto_hold") *value = ix->auto_hold.load();
     else if (n == "auto_hold8") *value = ix->auto_hold8.load();
     else if (n == "overflow_queries") *value = ix->n_overflow.load() + (int64_t)dt[1];
+    else if (n == "inconsistent_queries") *value = ix->n_incons.load();  // host-memory searches
     else if (n == "capacity") *value = ix->cap_rows;
     else if (n == "scan_ns") *value = ix->scan_ns.load();
     else if (n == "pipeline_ns") *value = ix->pipe_ns.load();
@@ -828,6 +842,15 @@ int32_t vdb_index_add(vdb_index* ix, const float* vectors, int64_t n, int32_t me
     hipStream_t st = ix->stream;
     int rc = ensure_capacity(ix, ix->count + n);
     if (rc) return rc;
+    // While the direction / centring row / int8 step still come from fewer than kDirRows rows,
+    // this add may derive them again and rebuild the int8 copy of rows [0, count) in place
+    // (below): device-memory searches still running on caller streams read those buffers
+    // together with host-captured scalars (sx, i8st) -- wait for them first.  Past
+    // that phase an add only writes rows >= count, which no queued search reads.
+    if (ix->count > 0 && ix->dir_rows < kDirRows) {
+        const int wr = wait_idle(ix);
+        if (wr) return wr;
+    }
     HIP_TRY(hipMemsetAsync(ix->d_nonfinite, 0, sizeof(int), st));
     if (mem == VDB_MEM_DEVICE) {
         // the rows may still be being written on the caller's stream (NULL = the null stream):
@@ -1445,6 +1468,7 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
             fa.out_s = out_s; fa.out_i = out_i; fa.out_k = out_k; fa.index_offset = index_offset;
             fa.row_ids = row_ids;
             fa.flag_count = flags; fa.flag_list = flags + 1; fa.gthr = gthr; fa.overflow_count = flags + B + 1;
+            fa.incons_count = flags + B + 2;
             fa.split = fin_split; fa.sx_ek = fx_ek; fa.sx_ck = fx_ck; fa.sx_cr = fx_cr; fa.sx_n = fx_n; fa.done = done;
             HIP_TRY(launch_finish(ix->metric, KP, fa, B, st));
             if (timed) HIP_TRY(hipEventRecord(tev[2], st));
@@ -1470,10 +1494,11 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
                 return rc;
             }
             HIP_TRY(hipMemcpyAsync(w->host_flag, flags, sizeof(int), hipMemcpyDeviceToHost, st));
-            HIP_TRY(hipMemcpyAsync(w->host_flag + 1, flags + B + 1, sizeof(int), hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipMemcpyAsync(w->host_flag + 1, flags + B + 1, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
             HIP_TRY(hipStreamSynchronize(st));
             n_flag = w->host_flag[0];
             ix->n_overflow += w->host_flag[1];
+            ix->n_incons += w->host_flag[2];
             if (auto_prec && one_plane && n_flag > 0 && !ix->no_fallback) {
                 if (n_flag <= std::max(1, B / 8) && n_flag <= kRepassMax) {
                     // a few uncertified queries: re-pass just those in bf16x3 (the index stays bf16)

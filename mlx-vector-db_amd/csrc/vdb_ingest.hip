@@ -251,6 +251,7 @@ __global__ void __launch_bounds__(256) prep_queries_kernel(const float* __restri
     if (b == 0 && lane == 0 && flag_count) {
         flag_count[0] = 0;      // certificate failures (list follows)
         flag_count[B + 1] = 0;  // of which: candidate-list overflows
+        flag_count[B + 2] = 0;  // of which: the finish's approx-vs-exact consistency guard
     }
     if (b >= Bp) return;
     if (lane == 0 && gthr) gthr[b] = 0u;

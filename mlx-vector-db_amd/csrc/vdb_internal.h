@@ -196,6 +196,7 @@ struct FinishArgs {
     float* out_s; int64_t* out_i; double* out_k; int64_t index_offset;
     int* flag_count; int* flag_list; const uint32_t* gthr;
     int* overflow_count;  // lists longer than the finish kernel holds (they take the exact path)
+    int* incons_count = nullptr;  // optional: queries flagged by the approx-vs-exact consistency guard
     const int64_t* row_ids = nullptr;  // global id per row (multi-device shard), else row + index_offset
     // split > 1: split workgroups per query share the exact rerank (rows by row % split); their
     // shares go to sx_* [B][split][KP] (+ counts sx_n [B][split]) and the last one (done[b],

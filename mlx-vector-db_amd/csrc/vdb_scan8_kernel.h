@@ -290,6 +290,13 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
         }
         if constexpr (QLDS) q_lds(0, qr[0]);
     }
+    // L2 start values: waited for before the loop and again at the end of every step (below),
+    // never carried in flight across the loop header.  The compiler may copy a loop-carried value
+    // at the header (phi copies: seen in the I8 / I8X3 L2 QLDS kernels, tools/vmcnt_check.py), and
+    // a copy of a register an asm load is still filling reads stale data (a cold first
+    // search returned wrong, certified L2 results).  Free in time: the first group waits for the
+    // slots issued after these loads anyway.
+    if constexpr (METRIC == 1) s8_wait<PX * LPS>(rin);
 
     for (int64_t s = s_begin; s < s_end; ++s) {
         S8_STAMP(const unsigned long long st_a = S8_NOW(); ++st_n;)
@@ -303,7 +310,6 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
 #pragma unroll
             for (int v = 0; v < 16; ++v) init[v] = 0;
             if constexpr (METRIC == 1) {
-                if (rt == 0) s8_wait<PX * LPS>(rin);  // issued before the PX slots now in flight
 #pragma unroll
                 for (int a = 0; a < 4; ++a)
 #pragma unroll
@@ -507,22 +513,25 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
                 slow = s8_pace_min(v, ptag, lane, n_qb);
             }
         }
+        // the next step's start values (issued before the tail's PX * LPS refills; younger
+        // epilogue accesses only make this wait stricter) land before the back-edge
+        if constexpr (METRIC == 1) s8_wait<PX * LPS>(rin);
         S8_STAMP(st_e += S8_NOW() - st_c;)
     }
 
     // The last step's tail refilled the slots (and, global operand, the query tiles) with loads
     // nothing reads.  To the compiler those registers are free once the loop ends -- but the loads
     // are still landing: wait for them with the slots tied live until here, so no other value
-    // shares their registers meanwhile (seen: a cold first search of an L2 index returned wrong,
-    // certified results when the one-plane LDS layout moved the flush's registers onto them).
-    if (s_begin < s_end) {
+    // shares their registers meanwhile.  Unconditional, so that every path to the code below --
+    // including the ones the compiler cannot prove infeasible (prologue loads issued, loop not
+    // entered) -- passes a vmcnt(0) (tools/vmcnt_check.py checks this on the built objects).
 #pragma unroll
-        for (int p = 0; p < PX; ++p) s8_wait<0>(xr[p]);
-        if constexpr (!QLDS) {
+    for (int p = 0; p < PX; ++p) s8_wait<0>(xr[p]);
+    if constexpr (!QLDS) {
 #pragma unroll
-            for (int p = 0; p < PQ; ++p) s8_tie(qr[p]);
-        }
+        for (int p = 0; p < PQ; ++p) s8_tie(qr[p]);
     }
+    if constexpr (METRIC == 1) s8_tie(rin);
 
     // FLAGSYNC: keep answering compaction rounds until every wave is past its last step
     if (FLAGSYNC && lane == 0) atomicAdd(&s_done, 1);

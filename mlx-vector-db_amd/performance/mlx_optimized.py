@@ -222,8 +222,10 @@ def _device_index(db):
     ix.add_device(x.data_ptr(), x.shape[0], _stream(x))  # device to device, after the caller's stream
     with _dev_lock:
         _dev_cache[key] = (weakref.ref(db), ix)
+        # an evicted index is only dropped, never closed here: another thread may have taken it
+        # from the cache a moment ago and be searching it; the last reference frees it
         while len(_dev_cache) > _DEV_CACHE_SIZE:
-            _dev_cache.popitem(last=False)[1][1].close()
+            _dev_cache.popitem(last=False)
     return ix
 
 

@@ -59,6 +59,7 @@ class MLXVectorStoreConfig:
     # concurrent single-vector queries (the REST executor's 4 threads, api/routes/vectors.py:43)
     # join one batched device search instead of one corpus scan each (_QueryCoalescer)
     coalesce: bool = True
+    coalesce_inflight: int = 2  # coalesced batches running at once (each on its own stream)
 
 
 def _as_matrix(vectors: Any) -> np.ndarray:
@@ -129,40 +130,54 @@ class _Write(_Read):
 
 
 class _QueryCoalescer:
-    """Continuous batching of concurrent single-vector queries.
+    """Continuous batching of concurrent single-vector queries, pipelined.
 
     The reference serves /vectors/query one vector per request from a 4-thread executor
     (api/routes/vectors.py:43, :226-234): each call is a full scan of the corpus
     (service/optimized_vector_store.py:149-192).  A scan costs about the same for 1 query as
-    for 64 (the corpus read dominates), so while one batch runs on the device the
-    queries that arrive meanwhile wait and then run together as the next batch: no artificial
-    delay when a query arrives alone, up to ``max_batch`` queries per scan under load.  Each
-    caller gets its own row; k differs per caller, the batch runs max(k) (the exact order
-    makes every caller's top-k the prefix of the batch's).  Callers hold the store's read
-    lock while they wait, so every query of a batch sees the same rows."""
+    for 64 (the corpus read dominates), so the queries that arrive while batches
+    run wait and then run together as the next batch: no artificial delay when a query arrives
+    alone, up to ``max_batch`` queries per scan under load.  Up to ``max_inflight`` batches
+    run at once (each on its own workspace stream of the index, so one batch's host work and
+    tail kernels overlap another's scan; with one batch in flight the device idled during the
+    host side and 4 direct callers beat the coalescer).  A batch holds requests of
+    one k class (k <= 16 / <= 200 / larger: the candidate pass a batch runs depends on its
+    largest k, so one caller's large k does not move its co-batched callers to a slower pass);
+    each caller gets its own row and k (the exact order makes every caller's top-k the prefix
+    of the batch's).  Callers hold the store's read lock while they wait, so every query of a
+    batch sees the same rows."""
 
-    def __init__(self, run, max_batch: int = 64):
+    def __init__(self, run, max_batch: int = 64, max_inflight: int = 2):
         self._run = run            # run(Q [B, D], k) -> [(indices, scores, metadata)] * B
         self._max = max_batch
+        self._inflight = max(1, int(max_inflight))
         self._cv = threading.Condition(threading.Lock())
         self._pending: List[list] = []
-        self._running = False
+        self._running = 0
         self.batches = 0
         self.queries = 0
+
+    @staticmethod
+    def _kclass(k: int) -> int:
+        return 0 if k <= 16 else 1 if k <= 200 else 2
 
     def query(self, q: np.ndarray, k: int):
         req = [q, int(k), None, None]  # query, k, result, error
         self._cv.acquire()
         try:
             self._pending.append(req)
-            # wait for a result; whenever no batch is running, lead the next one (FIFO, so this
-            # caller's own query is in one of the batches it leads)
+            # wait for a result; whenever fewer than max_inflight batches run, lead the next one:
+            # the oldest pending request's k class, FIFO (a leader may serve others before its own)
             while req[2] is None and req[3] is None:
-                if self._running:
+                if self._running >= self._inflight or not self._pending:
                     self._cv.wait()
                     continue
-                self._running = True
-                batch, self._pending = self._pending[:self._max], self._pending[self._max:]
+                kc = self._kclass(self._pending[0][1])
+                batch, rest = [], []
+                for r in self._pending:
+                    (batch if len(batch) < self._max and self._kclass(r[1]) == kc else rest).append(r)
+                self._pending = rest
+                self._running += 1
                 self._cv.release()
                 try:
                     kmax = max(r[1] for r in batch)
@@ -174,7 +189,7 @@ class _QueryCoalescer:
                         r[3] = e
                 finally:
                     self._cv.acquire()
-                    self._running = False
+                    self._running -= 1
                     self.batches += 1
                     self.queries += len(batch)
                     self._cv.notify_all()
@@ -203,7 +218,8 @@ class MLXVectorStore:
         self._vector_count = 0
         self._hnsw_index = None
         self._files = StoreFiles(self.store_path)
-        self._coalescer = _QueryCoalescer(lambda Q, k: self._brute_force_search(Q, k, None))
+        self._coalescer = _QueryCoalescer(lambda Q, k: self._brute_force_search(Q, k, None),
+                                          max_inflight=self.config.coalesce_inflight)
         if self.config.enable_hnsw:  # service/optimized_vector_store.py:72-78
             from performance.hnsw_index import ProductionHNSWIndex
             self._hnsw_index = ProductionHNSWIndex(self.config.dimension, self.store_path, self.config.metric,
@@ -322,7 +338,9 @@ class MLXVectorStore:
                     return list(fi), list(fd), list(fm)
                 except Exception as e:
                     logger.warning("HNSW-Suche fehlgeschlagen, falle auf Brute-Force zurück: %s", e)
-            if self.config.coalesce and not filter_metadata and self._compiled_similarity_fn and int(k) > 0:
+            # k above the device limit is not coalesced: its error is the caller's alone
+            if (self.config.coalesce and not filter_metadata and self._compiled_similarity_fn
+                    and 0 < int(k) <= 1024):
                 if q.shape[0] != self._dim:
                     raise ValueError(f"Dimension mismatch: query has {q.shape[0]} dims, store holds {self._dim}")
                 return self._coalescer.query(q, k)
