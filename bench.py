@@ -420,6 +420,7 @@ def main():
                     "0 a separate bound kernel (tuning)")
     ap.add_argument("--pilot-rank", type=int, default=None, help="rank of the pilot bound (tuning; default: Poisson rule)")
     ap.add_argument("--k", type=int, default=None, help="tuning: the config at another k (not the config's line)")
+    ap.add_argument("--finish-split", type=int, default=None, help="workgroups per query in the finish (tuning)")
     ap.add_argument("--scan-pace", type=int, default=None, help="int8 pass: 1 pace the query blocks of a row range, "
                     "0 off (default; tuning)")
     ap.add_argument("--rows", type=int, default=None, help="override the corpus rows (exploration only)")
@@ -524,6 +525,8 @@ def bench_brute(cfg, args, world, rank, local, dev, primary=True):
         ix.set_param("pilot_rank", args.pilot_rank)
     if args.scan_pace is not None:
         ix.set_param("scan_pace", args.scan_pace)
+    if args.finish_split is not None:
+        ix.set_param("finish_split", args.finish_split)
     if args.no_fallback:
         ix.set_param("no_fallback", 1)
     ix.reserve(n_local)

@@ -687,7 +687,7 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
         if (value < 0 || value > 1) return set_error(VDB_ERR_INVALID, "scan_pace must be 0 or 1");
         ix->scan_pace = value != 0;
     } else if (n == "scan_qlds") {
-        if (value < -1 || value > 0) return set_error(VDB_ERR_INVALID, "scan_qlds must be -1 or 0");
+        if (value < -1 || value > 2) return set_error(VDB_ERR_INVALID, "scan_qlds must be -1 (auto), 0, 1 or 2");
         ix->scan_qlds = value;
     } else if (n == "scan_q4") {
         if (value < -1 || value > 1) return set_error(VDB_ERR_INVALID, "scan_q4 must be -1, 0 or 1");

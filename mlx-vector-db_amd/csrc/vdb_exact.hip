@@ -2,6 +2,7 @@
 // (pipeline overview: vdb_scan.hip).  Built with -ffp-contract=off.
 #include "vdb_common.h"
 #include "vdb_internal.h"
+#include <type_traits>
 #include "vdb_merge_block.h"
 
 namespace vdb {
@@ -110,8 +111,67 @@ __device__ __forceinline__ void exact_keys_regs(const float (&qv)[MP][4], double
     }
 }
 
+// As exact_keys_regs for longer rows: every piece of the NB rows in flight at once, the query's
+// pieces read from memory (L1-resident) as each is consumed instead of held in registers.
+template <int METRIC, int NB, int MP>
+__device__ __forceinline__ void exact_keys_rows(const float* __restrict__ q, int D, double qn,
+                                                const float* __restrict__ X, int G, int np, const uint32_t* rows,
+                                                const double* xn, int nb, double* out) {
+    const int lane = threadIdx.x & 63;
+    const int Dp = G * GROUP_DIMS;
+    f32x4 xv[MP][NB];
+#pragma unroll
+    for (int m = 0; m < MP; ++m) {
+        const int p = m * 64 + lane;
+#pragma unroll
+        for (int u = 0; u < NB; ++u)
+            xv[m][u] = (m < np && u < nb && 4 * p < Dp) ? *(const f32x4*)(X + row_piece_offset(rows[u], p, G))
+                                                       : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    double acc[NB];
+#pragma unroll
+    for (int u = 0; u < NB; ++u) acc[u] = 0.0;
+#pragma unroll
+    for (int m = 0; m < MP; ++m) {
+        if (m < np) {
+            float qv[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int d = 4 * (m * 64 + lane) + j;
+                qv[j] = d < D ? q[d] : 0.0f;
+            }
+#pragma unroll
+            for (int u = 0; u < NB; ++u)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const double qd = (double)qv[j];
+                    const double xd = (double)xv[m][u][j];
+                    if (METRIC == 0) {
+                        acc[u] = acc[u] + qd * xd;
+                    } else {
+                        const double df = xd - qd;
+                        acc[u] = acc[u] + df * df;
+                    }
+                }
+        }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1)
+#pragma unroll
+        for (int u = 0; u < NB; ++u) acc[u] = acc[u] + __shfl_xor(acc[u], off, 64);
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+        if (u < nb) out[u] = METRIC == 0 ? acc[u] / (fmax(qn, 1e-8) * fmax(xn[u], 1e-8)) : -acc[u];
+    }
+}
+
 constexpr int FIN_MP = 4;   // fast path: D <= 1024
 constexpr int FIN_NB4 = 3;  // rows per wave per batch on the fast path (4 spills at 128 VGPRs)
+// D <= 2048 (C3: 1536): 1 row per wave per batch, all 8 of its pieces in flight (8 KiB
+// of row pieces in flight per wave; the loop form below keeps one 1 KiB piece per row in flight
+// and ran C3's exact keys at 150 us for 256 candidates x 256 queries, profiles/r04 fin stamps)
+constexpr int FIN_MP8 = 8;
+constexpr int FIN_NB8 = 1;
 
 template <int METRIC, int KP>
 __global__ void __launch_bounds__(64 * RERANK_WAVES) rerank_kernel(RerankArgs a) {
@@ -541,7 +601,8 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
         s_epsb = METRIC == 0 ? a.eps_rel + s_bq + qe
                              : a.eps_rel * (2.0 * qn * a.xmax + a.xmax * a.xmax) + 2.0 * s_bq + qe;
         s_bad = 0;
-        const bool defer = S == 1 && have_k && !ok;  // decided after the exact keys
+        // decided after the exact keys (split > 1: by the workgroup that gathers the shares)
+        const bool defer = have_k && !ok;
         s_fl0 = !ok && !defer;  // flagged here (the same decision in every workgroup of the query)
         if (!ok && !defer && sp == 0) {
             const int pos = atomicAdd(a.flag_count, 1);
@@ -585,6 +646,9 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
         __syncthreads();
         m = s_m;
     }
+#ifdef VDB_STAMP
+    if (threadIdx.x == 0) g_fin_stamps[b][6] = (unsigned long long)m;  // the rerank set
+#endif
     // split > 1: the candidates with row % S == sp are this workgroup's (the selected set is
     // the same in every workgroup of the query, its LDS order is not)
     uint32_t* xr = s_cr;
@@ -614,29 +678,52 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
     const float* q = a.Q + (int64_t)b * a.D;
     // exact keys: wave wv takes candidates wv NB, ... in batches of NB
     const int np = (a.D + 255) / 256;
-    if (np <= FIN_MP) {
-        float qv[FIN_MP][4];
+    // the register path: the query's pieces held, NB rows' pieces loaded at once per batch
+    auto keys_regs = [&](auto mp_c, auto nb_c) {
+        constexpr int MP = decltype(mp_c)::value, NB = decltype(nb_c)::value;
+        float qv[MP][4];
 #pragma unroll
-        for (int mm = 0; mm < FIN_MP; ++mm)
+        for (int mm = 0; mm < MP; ++mm)
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int d = 4 * (mm * 64 + lane) + j;
                 qv[mm][j] = (mm < np && d < a.D) ? q[d] : 0.0f;
             }
-        for (int j0 = wv * FIN_NB4; j0 < mx; j0 += FIN_WAVES * FIN_NB4) {
-            uint32_t rows[FIN_NB4];
-            double xn[FIN_NB4];
-            const int nb = min(FIN_NB4, mx - j0);
+        for (int j0 = wv * NB; j0 < mx; j0 += FIN_WAVES * NB) {
+            uint32_t rows[NB];
+            double xn[NB];
+            const int nb = min(NB, mx - j0);
 #pragma unroll
-            for (int u = 0; u < FIN_NB4; ++u) {
+            for (int u = 0; u < NB; ++u) {
                 rows[u] = u < nb ? xr[j0 + u] : 0u;
                 xn[u] = (METRIC == 0 && u < nb) ? a.nrm64[rows[u]] : 1.0;
             }
-            double keys[FIN_NB4];
-            exact_keys_regs<METRIC, FIN_NB4, FIN_MP>(qv, qn, a.X, a.G, np, rows, xn, nb, keys);
+            double keys[NB];
+            exact_keys_regs<METRIC, NB, MP>(qv, qn, a.X, a.G, np, rows, xn, nb, keys);
             if (lane == 0) {
 #pragma unroll
-                for (int u = 0; u < FIN_NB4; ++u)
+                for (int u = 0; u < NB; ++u)
+                    if (u < nb) xek[j0 + u] = keys[u];
+            }
+        }
+    };
+    if (np <= FIN_MP) {
+        keys_regs(std::integral_constant<int, FIN_MP>{}, std::integral_constant<int, FIN_NB4>{});
+    } else if (np <= FIN_MP8) {
+        for (int j0 = wv * FIN_NB8; j0 < mx; j0 += FIN_WAVES * FIN_NB8) {
+            uint32_t rows[FIN_NB8];
+            double xn[FIN_NB8];
+            const int nb = min(FIN_NB8, mx - j0);
+#pragma unroll
+            for (int u = 0; u < FIN_NB8; ++u) {
+                rows[u] = u < nb ? xr[j0 + u] : 0u;
+                xn[u] = (METRIC == 0 && u < nb) ? a.nrm64[rows[u]] : 1.0;
+            }
+            double keys[FIN_NB8];
+            exact_keys_rows<METRIC, FIN_NB8, FIN_MP8>(q, a.D, qn, a.X, a.G, np, rows, xn, nb, keys);
+            if (lane == 0) {
+#pragma unroll
+                for (int u = 0; u < FIN_NB8; ++u)
                     if (u < nb) xek[j0 + u] = keys[u];
             }
         }
@@ -742,9 +829,9 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
     if (tid == 0 && !s_fl0) {
         const double ekk = s_ekk - s_shift;  // the exact k-th best in approximate units (+ fp64 rounding)
         const double tol = 4e-16 * (fabs(s_ekk) + fabs(s_shift));
-        // neither certificate (S == 1), or a reranked row outside its bound: the exact path
-        // rewrites the query
-        if ((S == 1 && !s_ok1 && !(ekk - tol > s_bar)) || s_bad) {
+        // neither certificate, or a reranked row outside its bound: the exact path rewrites
+        // the query
+        if ((!s_ok1 && !(ekk - tol > s_bar)) || s_bad) {
             const int pos = atomicAdd(a.flag_count, 1);
             a.flag_list[pos] = b;
             if (s_bad && a.incons_count) atomicAdd(a.incons_count, 1);

@@ -3,6 +3,13 @@
 // arithmetic, and the dispatch to the instantiation units.
 #include "vdb_scan8_kernel.h"
 
+// scan_qlds auto (-1): the query block in LDS for short rows (rule 1) and, past 768 dims,
+// whenever it fits (rule 2).  Measured (profiles/r04_qlds, same box): C3 (D = 1536) scan 0.625
+// -> 0.572 ms with rule 2; C2 (D = 768) 0.153 -> 0.161 ms (slower: kept on rule 1); C6 equal.
+#ifndef VDB_S8_QLDS_BIG_G8
+#define VDB_S8_QLDS_BIG_G8 24
+#endif
+
 namespace vdb {
 
 // =============================================================================
@@ -330,9 +337,11 @@ hipError_t launch_scan8(int prec, int metric, int KP, const float* Xq, const flo
                         int n_qblocks, int64_t n_steps, int n_wg, int spw, float* gl_s, uint32_t* gl_i,
                         uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr, uint32_t* pace, uint32_t pace_tag,
                         int lockstep, int qlds, hipStream_t st) {
-    // the query block in LDS: auto when it fits (qlds < 0), never with 0 -- except for rows of
-    // fewer 32-dim groups than the global-operand variants keep in flight (PX = 4)
-    const bool ql = (qlds != 0 && scan8_qlds(G8, KP)) || G8 < 4;
+    // the query block in LDS (scan8_qlds): qlds 1 = the round-3 rule (short rows), 2 = whenever
+    // it fits, -1 = auto (rule 2 past VDB_S8_QLDS_BIG_G8 groups), 0 = never -- except for rows of fewer 32-dim groups
+    // than the global-operand variants keep in flight (PX = 4)
+    const int mode = qlds < 0 ? (G8 > VDB_S8_QLDS_BIG_G8 ? 2 : 1) : qlds;
+    const bool ql = (mode != 0 && scan8_qlds(G8, KP, prec, mode == 1)) || G8 < 4;
     const bool fs = !lockstep;
     const bool nt = !ql && n_qblocks == 1;
     auto* unit = prec == PREC_I8X3 ? (metric == 0 ? launch_scan8_i3c : launch_scan8_i3l)

@@ -3,5 +3,5 @@
 #include "vdb_scan8_kernel.h"
 
 namespace vdb {
-S8_UNIT(launch_scan8_i1l, PREC_I8, 1, 4, 2)
+S8_UNIT(launch_scan8_i1l, PREC_I8, 1, 4, 4)
 }  // namespace vdb

@@ -185,6 +185,7 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
     constexpr bool HL = Planes8<PREC>::L;
     const int G = GC > 0 ? GC : G_arg;
     constexpr int PQ = QLDS ? 1 : PX;
+    constexpr int LQP = QPL;  // planes of the query block in LDS (I8 reads qh alone)
     constexpr size_t GSTEP = 8 * BLOCK_FLOATS;  // query: consecutive groups of one super tile
     constexpr size_t PLANE = 4 * BLOCK_FLOATS;  // query: lo plane after hi
     constexpr size_t XGSTEP = corpus_gstep();
@@ -196,7 +197,7 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
     __shared__ float s_thr[QB];
     __shared__ int s_need, s_done;
     __shared__ uint32_t s_pend[S8_NW][8][64];  // per wave and tile: each lane's entries left for a compaction round
-    extern __shared__ __attribute__((aligned(16))) float s_q[];  // QLDS: [G][plane][QT][256]
+    extern __shared__ __attribute__((aligned(16))) float s_q[];  // QLDS: [G][LQP planes][QT][256]
 
     const int lane = threadIdx.x & 63;
     const int lane4 = lane * 4;
@@ -226,8 +227,8 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
     }
     const float* Qbase = Qq + s2_blk((uint64_t)(qb * QT), 0, G + QG_EXTRA);
     if constexpr (QLDS) {
-        for (int e = threadIdx.x; e < G * 2 * QT * 64; e += 64 * NW) {
-            const int l = e & 63, qt = (e >> 6) % QT, pl = (e / (64 * QT)) & 1, g = e / (128 * QT);
+        for (int e = threadIdx.x; e < G * LQP * QT * 64; e += 64 * NW) {
+            const int l = e & 63, qt = (e >> 6) % QT, pl = (e / (64 * QT)) % LQP, g = e / (64 * QT * LQP);
             *(f32x4*)(s_q + (size_t)e * 4) = *(const f32x4*)(Qbase + g * GSTEP + pl * PLANE + qt * BLOCK_FLOATS + 4 * l);
         }
     }
@@ -243,7 +244,7 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
 #pragma unroll
         for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
-            for (int pl = 0; pl < QPL; ++pl) q[qt][pl] = *(const f32x4*)(s_q + ((size_t)(g * 2 + pl) * QT + qt) * 256 + lane4);
+            for (int pl = 0; pl < QPL; ++pl) q[qt][pl] = *(const f32x4*)(s_q + ((size_t)(g * LQP + pl) * QT + qt) * 256 + lane4);
     };
     // The shared bound is read once: with KW < KP (the I8 shape) nothing raises it during the
     // scan but the pilot (before it); with KW == KP other workgroups' compactions do, and a
@@ -581,7 +582,7 @@ static hipError_t scan8_launch_g(const float* Xq, const float* rinit, const uint
                                  int64_t n_steps, int n_wg, int spw, float* gl_s, uint32_t* gl_i, uint32_t* gl_cnt,
                                  int64_t gl_cap, uint32_t* gthr, uint32_t* pace, uint32_t pace_tag, hipStream_t st) {
     auto k = scan8_kernel<P, M, QT, PX, KP, CAP, NT, QL, FS, GC, RT_, KW>;
-    const size_t lds = QL ? (size_t)G * 2 * QT * 1024 : 0;
+    const size_t lds = QL ? (size_t)G * Planes8<P>::QPL * QT * 1024 : 0;
     if (QL) {
         static std::atomic<size_t> lds_set{0};
         size_t cur = lds_set.load();
@@ -623,9 +624,18 @@ static hipError_t scan8_launch(const float* Xq, const float* rinit, const uint32
                                                                 pace, pace_tag, st);
 }
 
-// The query block goes to LDS when it is small (short rows: 64 queries x 128 dims x 2 planes =
-// 16 KiB).
-inline bool scan8_qlds(int G8, int KP) { return (size_t)G8 * 2 * 2 * 1024 <= 32 * 1024; }
+// The query block in LDS takes the query operand off each wave's vector-memory path (from L2,
+// 64 queries x 32 dims per plane and group beside the corpus tiles).  It fits when the block
+// (64 queries x D bytes per plane; I8 reads qh alone) plus the static LDS (64 queries x CAP x
+// 8 B of lists, s_pend 8 KiB, counters) is within the CU's 160 KiB: C3 (D = 1536, I8, KP = 256
+// with CAP 96): 96 + 56.5 KiB.  `small` keeps the round-3 rule (block <= 32 KiB: short rows).
+inline int scan8_cap(int KP, bool ql) { return KP == 128 ? 192 : KP == 256 ? (ql ? 96 : 128) : 128; }  // as S8_KP
+inline bool scan8_qlds(int G8, int KP, int prec, bool small) {
+    const size_t q = (size_t)G8 * (prec == PREC_I8X3 ? 2 : 1) * 2 * 1024;
+    if (small) return q <= 32 * 1024;
+    const size_t lists = (size_t)64 * scan8_cap(KP, true) * 8 + 8192 + 1024;
+    return lists + q <= 160 * 1024;
+}
 
 
 #define S8_UNIT_PARAMS                                                                                             \
@@ -638,13 +648,14 @@ inline bool scan8_qlds(int G8, int KP) { return (size_t)G8 * 2 * 2 * 1024 <= 32 
 #define S8_ONE(P, M, KPV, QTV, PXV, CAPV, NTV, QLV, FSV, KWV) \
     if (KP == KPV && nt == NTV && ql == QLV && fs == FSV)       \
         return scan8_launch<P, M, QTV, PXV, KPV, CAPV, NTV, QLV, FSV, KWV>(S8_ARGS);
-// KP = 256 keeps 64-query blocks: a workgroup keeps its best KW = 64 per query (LDS 64 KiB; the
-// drop bound -> gthr, vdb_scan2_kernel.h), so a 64-query batch reads the corpus once
+// KP = 256 keeps 64-query blocks: a workgroup keeps its best KW = 64 per query (LDS 64 KiB, 48
+// with the query block in LDS beside it; the drop bound -> gthr, vdb_scan2_kernel.h), so a
+// 64-query batch reads the corpus once
 #define S8_KP(P, M, PXV, NTV, QLV, FSV)               \
     S8_ONE(P, M, 32, 2, PXV, 128, NTV, QLV, FSV, 32)   \
     S8_ONE(P, M, 64, 2, PXV, 128, NTV, QLV, FSV, 64)   \
     S8_ONE(P, M, 128, 2, PXV, 192, NTV, QLV, FSV, 128) \
-    S8_ONE(P, M, 256, 2, PXV, 128, NTV, QLV, FSV, 64)
+    S8_ONE(P, M, 256, 2, PXV, (QLV ? 96 : 128), NTV, QLV, FSV, 64)
 #define S8_MODES(P, M, PXV, PXL)                                               \
     S8_KP(P, M, PXV, false, false, false) S8_KP(P, M, PXV, true, false, false) \
     S8_KP(P, M, PXL, false, true, false) S8_KP(P, M, PXL, false, true, true)   \

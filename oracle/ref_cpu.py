@@ -340,3 +340,149 @@ def graph_search(vectors: np.ndarray, nbr: np.ndarray, entries: np.ndarray, quer
     if metric != "cosine":
         dists = np.maximum(dists, 0.0)
     return labels, dists, scored
+
+
+# ---------------------------------------------------------------------------------
+# Graph build (performance/hnsw_index.py:44-77 -> hnswlib init_index(M=16,
+# ef_construction=200) + add_items).  hnswlib is absent (the reference
+# does not pin a version: requirements list `hnswlib` unversioned), so this restates
+# its published neighbour selection, getNeighborsByHeuristic2 (hnswalg.h: walk the
+# candidates nearest first, keep c unless an already kept r is closer to c than the
+# node is, dist(c, r) < dist(c, node), stop at M kept; keepPrunedConnections tops the
+# list up with the nearest pruned), in the form the device build runs it
+# (vdb_graph.hip graph_prune_kernel, vdb_api.cpp vdb_graph_build): one level of
+# out-degree R = 2M, pass 1 selects <= M out-edges from each row's exact kNN, pass 2
+# re-selects <= R from out- plus in-edges (hnswlib's level-0 lists after the later
+# insertions' links), entry rows evenly spread.
+#
+# Distances come from fp32 dot products of the stored rows, combined in fp32 as the
+# kernel does (cosine 1 - (g * s_c) * s_r with s = fp32 1 / max(|x|, 1e-8); L2
+# fma(-2, g, |x_c|^2 + |x_r|^2) with fp32 |x|^2).  The dot products are taken in
+# fp64 and rounded to fp32: bit-identical to the kernel's MFMA sums whenever they are
+# exact (integer-valued rows, the test's pin); otherwise within fp32 rounding, and
+# comparisons that close are reported as ambiguous.
+# ---------------------------------------------------------------------------------
+def _row_scales(X: np.ndarray, metric: str) -> np.ndarray:
+    """pack_rows_kernel's fp32 row scale: cosine 1 / max(|x|, 1e-8), L2 |x|^2 (canonical fp64 sums)."""
+    ss = canonical_sumsq64(X)
+    if metric == "cosine":
+        return (1.0 / np.maximum(np.sqrt(ss), EPS)).astype(np.float32)
+    return ss.astype(np.float32)
+
+
+def _fp32_dist_matrix(gram: np.ndarray, sc: np.ndarray, metric: str) -> np.ndarray:
+    """D[c, r] = the kernel's fp32 distance between Gram rows c and r with c's scale applied
+    first: cosine 1 - (g * s_c) * s_r, L2 fmaf(-2, g, s_c + s_r) (one rounding)."""
+    g = gram.astype(np.float32)
+    sc = sc.astype(np.float32)
+    if metric == "cosine":
+        return (np.float32(1.0) - (g * sc[:, None]) * sc[None, :]).astype(np.float32)
+    s = (sc[:, None] + sc[None, :]).astype(np.float32)
+    return (-2.0 * g.astype(np.float64) + s.astype(np.float64)).astype(np.float32)
+
+
+def select_neighbors(X: np.ndarray, scales: np.ndarray, node: int, cands, limit: int, metric: str = "cosine",
+                     fill: bool = False, sort: bool = False, tol: float = 0.0):
+    """hnswlib's getNeighborsByHeuristic2 for one node over <= 63 candidate rows (-1 padded
+    at the tail), as graph_prune_kernel: visiting order = candidate order (the kNN lists
+    arrive nearest first) or, with sort, by (fp32 distance to the node, position).
+    Returns (rows int32 [limit] -1 padded, fp32 distances [limit] inf padded, ambiguous):
+    ambiguous = some decision compared two distances within `tol` (fp32 rounding)."""
+    cands = [int(c) for c in cands][:63]
+    nvalid = 0
+    while nvalid < len(cands) and cands[nvalid] >= 0:
+        nvalid += 1
+    valid_pos = [i for i, c in enumerate(cands) if c >= 0] if sort else list(range(nvalid))
+    rows = np.asarray([node] + [cands[i] for i in valid_pos], np.int64)
+    Xr = np.asarray(X, np.float32)[rows].astype(np.float64)
+    Dm = _fp32_dist_matrix(Xr @ Xr.T, scales[rows], metric).astype(np.float64)
+    d0 = Dm[:, 0]  # my_d0 of lane c: (g[0, c] * s_c) * s_node
+    amb = False
+    order = list(range(1, len(rows)))
+    if sort:
+        order.sort(key=lambda i: (d0[i], valid_pos[i - 1]))
+        if tol > 0:
+            ds = d0[order]
+            amb |= bool(np.any((np.abs(np.diff(ds)) <= tol) & (np.diff(ds) != 0)))
+    kept = []
+    for c in order:
+        if len(kept) >= limit:
+            break
+        if kept:
+            dcr = Dm[c, kept]
+            if tol > 0 and np.any(np.abs(dcr - d0[c]) <= tol):
+                amb = True
+            if np.any(dcr < d0[c]):
+                continue
+        kept.append(c)
+    if fill:
+        for c in order:
+            if len(kept) >= limit:
+                break
+            if c not in kept:
+                kept.append(c)
+    rank = {c: j for j, c in enumerate(order)}
+    kept.sort(key=lambda c: rank[c])  # nearest first = visiting order
+    out = np.full(limit, -1, np.int32)
+    dist = np.full(limit, np.inf, np.float32)
+    for j, c in enumerate(kept):
+        out[j] = rows[c]
+        dist[j] = d0[c]
+    return out, dist, amb
+
+
+def graph_build(X: np.ndarray, metric: str = "cosine", degree: int = 32, knn: int = 32, n_entries: int = 256,
+                fill: bool = False, tol: float = 0.0):
+    """vdb_graph_build restated: (neighbours int32 [N, degree], entries int32 [E], ambiguous
+    bool [N] = the node's list may differ from the kernel's by fp32 rounding)."""
+    X = np.asarray(X, np.float32)
+    N = X.shape[0]
+    R, F = degree, degree // 2
+    scales = _row_scales(X, metric)
+    nbr = np.full((N, R), -1, np.int32)
+    amb = np.zeros(N, bool)
+    if N > 1:
+        kk = min(knn + 1, max(N, 1))
+        _, kid, _ = exact_search(X, X, kk, metric)
+        CW = min(knn, 63)
+        fwd = np.full((N, F), -1, np.int32)
+        fdist = np.full((N, F), np.inf, np.float32)
+        amb1 = np.zeros(N, bool)
+        cand1 = []
+        for i in range(N):
+            c = [int(v) for v in kid[i] if v >= 0 and v != i][:CW]
+            cand1.append(c)
+            fwd[i], fdist[i], amb1[i] = select_neighbors(X, scales, i, c + [-1] * (CW - len(c)), F, metric,
+                                                         tol=tol)
+        # pools: out-edges and in-edges, nearest first by (fp32 distance, row), <= 63 distinct
+        rev = [[] for _ in range(N)]
+        for u in range(N):
+            for j in range(F):
+                w = int(fwd[u, j])
+                if w >= 0:
+                    rev[w].append((float(fdist[u, j]), u))
+        # a node's pool is uncertain where an ambiguous pass-1 list could have added or dropped it
+        touched = np.zeros(N, bool)
+        for u in np.nonzero(amb1)[0]:
+            touched[u] = True
+            for v in cand1[u]:
+                touched[v] = True
+        for v in range(N):
+            pool = [(float(fdist[v, j]), int(fwd[v, j])) for j in range(F) if fwd[v, j] >= 0] + rev[v]
+            pool.sort()
+            row = []
+            for _, u in pool:
+                if len(row) >= 63:
+                    break
+                if u not in row:
+                    row.append(u)
+            if tol > 0:
+                ds = sorted(d for d, _ in pool)
+                if any(abs(a - b) <= tol and a != b for a, b in zip(ds, ds[1:])):
+                    touched[v] = True
+            out, _, a2 = select_neighbors(X, scales, v, row + [-1] * (63 - len(row)), R, metric, fill=fill, tol=tol)
+            nbr[v] = out
+            amb[v] = a2 or touched[v]
+    E = min(n_entries, max(N, 1))
+    ent = np.asarray([i * N // E for i in range(E)], np.int32)
+    return nbr, ent, amb

@@ -26,7 +26,8 @@ lib = _vdb.load_library()
 fb = (ctypes.c_ulonglong * (B * 8))()
 lib.vdb_debug_finish_stamps(fb, B)
 f = np.array(fb, dtype=np.uint64).reshape(B, 8).astype(np.float64)
-print(f"{cfg} {prec}: list length mean {f[:, 7].mean():.0f} p50 {np.median(f[:, 7]):.0f} max {f[:, 7].max():.0f}")
-for i, name in enumerate(["load", "select", "exact keys", "ranks+write", "certificate"]):
+print(f"{cfg} {prec}: list length mean {f[:, 7].mean():.0f} p50 {np.median(f[:, 7]):.0f} max {f[:, 7].max():.0f}; "
+      f"rerank set mean {f[:, 6].mean():.1f} max {f[:, 6].max():.0f}")
+for i, name in enumerate(["load", "select", "exact keys", "ranks+write"]):
     d = f[:, i + 1] - f[:, i]
     print(f"  {name:12s} mean {d.mean():9.0f}  max {d.max():9.0f}  (s_memtime ticks)")

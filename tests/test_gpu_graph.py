@@ -25,6 +25,31 @@ def _recall(labels, exact_idx):
     return hits / float(exact_idx[exact_idx >= 0].size)
 
 
+@pytest.mark.parametrize("fill", [0, 1])
+@pytest.mark.parametrize("metric", ["cosine", "euclidean"])
+def test_graph_build_matches_restated_heuristic(vdb, metric, fill):
+    """Row a14 pinned: the device build (exact kNN + graph_prune's two selection passes)
+    against oracle.graph_build, which restates hnswlib's getNeighborsByHeuristic2 over the
+    same exact kNN candidates (/root/reference/performance/hnsw_index.py:44-77 builds with
+    hnswlib M = 16).  Integer-valued rows make every fp32 dot product the kernel's MFMAs sum
+    exact, so the restatement reproduces every distance bit for bit and the neighbour lists
+    must be IDENTICAL (order included), not merely close; ties follow the kernel's rule (a
+    candidate is pruned only by a strictly closer kept row; equal pool distances by row)."""
+    rng = np.random.default_rng(57)
+    N, D = 5000, 64
+    V = rng.integers(0, 4, (N, D)).astype(np.float32)
+    ix = vdb.NativeIndex(D, metric)
+    ix.set_param("graph_fill", fill)
+    ix.add(V)
+    g = vdb.NativeGraph.build(ix, degree=32, knn=32, n_entries=64)
+    nbr, ent = g.to_arrays()
+    want, went, amb = ref_cpu.graph_build(V, metric, degree=32, knn=32, n_entries=64, fill=bool(fill))
+    assert not amb.any()
+    np.testing.assert_array_equal(ent, went)
+    diff = np.nonzero((nbr != want).any(axis=1))[0]
+    assert diff.size == 0, f"{diff.size} of {N} lists differ, first {diff[:5]}: {nbr[diff[0]]} vs {want[diff[0]]}"
+
+
 @pytest.mark.parametrize("metric", ["cosine", "euclidean"])
 def test_graph_recall_and_distances(vdb, metric):
     rng = np.random.default_rng(31)

@@ -203,7 +203,7 @@ def test_bf16_directional_residual_bound(vdb, metric, precision):
     # i8 (8-bit query: a wider bound) leaves a few of these 1536-dim queries to auto's re-pass
 
 
-@pytest.mark.parametrize("qlds", [-1, 0])
+@pytest.mark.parametrize("qlds", [-1, 0, 2])
 @pytest.mark.parametrize("D", [192, 320])
 @pytest.mark.parametrize("metric", ["cosine", "euclidean"])
 @pytest.mark.parametrize("precision", ["i8", "i8x3"])
@@ -216,6 +216,23 @@ def test_i8_group_counts_not_a_multiple_of_the_prefetch(vdb, precision, metric, 
     V = rng.random((6000, D), dtype=np.float32)
     Q = rng.random((24, D), dtype=np.float32)
     _check(vdb, V, Q, 10, metric, precision=precision, params={"no_fallback": 1, "scan_qlds": qlds})
+
+
+@pytest.mark.parametrize("qlds", [1, 2])
+@pytest.mark.parametrize("D,B,k", [(768, 64, 10), (1536, 150, 10), (768, 100, 40), (384, 64, 100), (1000, 70, 3)])
+@pytest.mark.parametrize("metric", ["cosine", "euclidean"])
+@pytest.mark.parametrize("precision", ["i8", "i8x3"])
+def test_i8_query_block_in_lds_whenever_it_fits(vdb, precision, metric, D, B, k, qlds):
+    """scan_qlds 2: the query block sits in LDS whenever it fits beside the lists (I8 keeps
+    the qh plane alone: 64 x 1536 B = 96 KiB beside 56.5 KiB of lists at KP = 256), against
+    the round-3 rule (1: short rows only).  Exact either way; the fallback counts are printed."""
+    rng = np.random.default_rng(D + B + k)
+    V = rng.random((9000, D), dtype=np.float32)
+    V[4000:4003] = V[7]
+    Q = rng.random((B, D), dtype=np.float32)
+    Q[1] = V[7]
+    ix, _, _ = _check(vdb, V, Q, k, metric, precision=precision, params={"scan_qlds": qlds})
+    print(f"{precision} {metric} D {D} B {B} k {k} qlds {qlds}: fallbacks {ix.stat('fallback_queries')}")
 
 
 def _auto_index(vdb, D, a8):

@@ -171,3 +171,46 @@ def test_merge_of_shards_equals_global():
     es, ei, ek = ref_cpu.exact_search(Q, V, k, "cosine")
     np.testing.assert_array_equal(mi, ei)
     np.testing.assert_array_equal(mk, ek)
+
+
+def test_select_neighbors_known_answers():
+    """hnswlib's heuristic (oracle.select_neighbors, restating getNeighborsByHeuristic2 as
+    graph_prune_kernel runs it) on hand-built cases: candidates along one ray from the node
+    keep only the nearest (each farther one is closer to a kept one than to the node);
+    orthogonal candidates are all kept; keepPrunedConnections (fill) tops up nearest first."""
+    D = 8
+    X = np.zeros((8, D), np.float32)
+    X[0] = 0.0
+    X[0, 0] = 1.0            # node at e0
+    for i, t in enumerate((2.0, 3.0, 4.0)):   # rows 1..3 on the ray e0 * t
+        X[1 + i, 0] = t
+    X[4, 1] = 1.0; X[5, 2] = 1.0; X[6, 3] = 1.0  # unit axes, orthogonal to each other
+    X[7, 0] = 1.0; X[7, 4] = 0.5
+    sc = ref_cpu._row_scales(X, "euclidean")
+    out, dist, amb = ref_cpu.select_neighbors(X, sc, 0, [1, 2, 3, -1], 4, "euclidean")
+    assert out.tolist() == [1, -1, -1, -1] and not amb
+    assert dist[0] == 1.0
+    out, _, _ = ref_cpu.select_neighbors(X, sc, 0, [1, 2, 3, -1], 3, "euclidean", fill=True)
+    assert out.tolist() == [1, 2, 3]
+    # node at the origin direction e0 (cosine): axes e1, e2, e3 all at distance 1, pairwise 1
+    # (not < 1): all kept in candidate order
+    scc = ref_cpu._row_scales(X, "cosine")
+    out, _, _ = ref_cpu.select_neighbors(X, scc, 0, [4, 5, 6], 3, "cosine")
+    assert out.tolist() == [4, 5, 6]
+    # sort: candidates given far-first come back nearest first
+    out, dist, _ = ref_cpu.select_neighbors(X, sc, 0, [3, 7, 4], 3, "euclidean", sort=True)
+    assert out[0] == 7 and dist[0] == np.float32(0.25)
+
+
+def test_graph_build_restatement_small():
+    """The restated build: every list holds distinct rows other than the node, at most
+    `degree` of them, each node with at least one out-edge, entries evenly spread."""
+    rng = np.random.default_rng(3)
+    X = rng.integers(0, 4, (300, 16)).astype(np.float32)
+    for metric in ("cosine", "euclidean"):
+        nbr, ent, amb = ref_cpu.graph_build(X, metric, degree=16, knn=16, n_entries=8)
+        assert nbr.shape == (300, 16) and not amb.any()
+        for v in range(300):
+            row = nbr[v][nbr[v] >= 0]
+            assert row.size >= 1 and v not in row and len(set(row.tolist())) == row.size
+        assert ent.tolist() == [i * 300 // 8 for i in range(8)]
