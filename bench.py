@@ -52,7 +52,7 @@ CONFIGS = {
     # second half of BASELINE.json's metric ("cosine top-10 batch=64: ... 10M x 128D @8 GPU")
     "c1": (10_000, 384, 1, 10, "cosine", "10K x 384 cosine top-10, single query"),
     "c2": (1_000_000, 768, 64, 10, "cosine", "1M x 768 fp32 cosine top-10, batch 64"),
-    "c3": (1_000_000, 1536, 256, 10, "cosine", "1M x 1536 cosine top-10, batch 256 (bf16 candidate pass)"),
+    "c3": (1_000_000, 1536, 256, 10, "cosine", "1M x 1536 cosine top-10, batch 256 (auto: int8 candidate pass)"),
     "c4": (10_000_000, 128, 512, 100, "euclidean", "10M x 128 L2 top-100, batch 512, row-sharded"),
     # graph path (performance/hnsw_index.py): batch 1, hnswlib M=16 -> out-degree 2M, efSearch 128
     "c5": (5_000_000, 384, 1, 10, "cosine", "5M x 384 graph index (HNSW M=16) cosine top-10, efSearch=128, batch 1"),
@@ -421,6 +421,8 @@ def main():
     ap.add_argument("--pilot-rank", type=int, default=None, help="rank of the pilot bound (tuning; default: Poisson rule)")
     ap.add_argument("--k", type=int, default=None, help="tuning: the config at another k (not the config's line)")
     ap.add_argument("--finish-split", type=int, default=None, help="workgroups per query in the finish (tuning)")
+    ap.add_argument("--device-repass", type=int, default=None,
+                    help="device re-pass of uncertified queries: -1 auto (armed after a fallback), 0 off, 1 always")
     ap.add_argument("--scan-pace", type=int, default=None, help="int8 pass: 1 pace the query blocks of a row range, "
                     "0 off (default; tuning)")
     ap.add_argument("--rows", type=int, default=None, help="override the corpus rows (exploration only)")
@@ -527,6 +529,8 @@ def bench_brute(cfg, args, world, rank, local, dev, primary=True):
         ix.set_param("scan_pace", args.scan_pace)
     if args.finish_split is not None:
         ix.set_param("finish_split", args.finish_split)
+    if args.device_repass is not None:
+        ix.set_param("device_repass", args.device_repass)
     if args.no_fallback:
         ix.set_param("no_fallback", 1)
     ix.reserve(n_local)

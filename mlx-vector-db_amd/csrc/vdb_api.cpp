@@ -182,6 +182,11 @@ struct vdb_index {
     // 8 blocks within 5 steps (from 26) and ran the scan at 4.99 ms against 2.90 without
     // (the range at its slowest block's speed, the prefetch drained per sleep; profiles/r03_i8/pace)
     bool scan_pace = false;
+    // device-memory searches: uncertified queries of an I8 / BF16 / I8X3 pass re-passed in BF16X3
+    // on the device (gated kernels, no host wait) instead of the fp64 exact scan.  -1 auto: armed
+    // for kRepassArm searches once a device fallback has been seen; 0 off; 1 always
+    int64_t device_repass = -1;
+    std::atomic<int> repass_arm{0};
     std::atomic<uint32_t> pace_seq{0};  // launch tag of the pacing counters
     int64_t scan_q4 = -1;      // split pass 128-query shape (D <= 128, KP = 128, B >= 256): -1 auto, 0 off, 1 on
     // stats
@@ -284,8 +289,13 @@ int ensure_capacity(vdb_index* ix, int64_t rows) {
     CAP_TRY(hipMalloc(&X, x_bytes));
     CAP_TRY(hipMalloc(&Xs, x_bytes));
     CAP_TRY(hipMemsetAsync(Xs, 0, x_bytes, ix->stream));
-    CAP_TRY(hipMalloc(&Xq, x_bytes / 2));
-    CAP_TRY(hipMemsetAsync(Xq, 0, x_bytes / 2, ix->stream));
+    // the int8 copy only where a setting reads it (FP32 / BF16X3 / BF16 / AUTO without
+    // auto_int8 never do; set_param allocates it when a setting starts to, ensure_xq)
+    const bool with_xq = ix->Xq || needs_i8(ix->precision, ix->auto_i8);
+    if (with_xq) {
+        CAP_TRY(hipMalloc(&Xq, x_bytes / 2));
+        CAP_TRY(hipMemsetAsync(Xq, 0, x_bytes / 2, ix->stream));
+    }
     CAP_TRY(hipMalloc(&n64, cap * sizeof(double)));
     CAP_TRY(hipMalloc(&i32, cap * sizeof(float)));
     CAP_TRY(hipMalloc(&s32, cap * sizeof(float)));
@@ -301,8 +311,9 @@ int ensure_capacity(vdb_index* ix, int64_t rows) {
                                ix->stream));
         CAP_TRY(hipMemcpyAsync(Xs, ix->Xs, (size_t)used_tiles * tile_floats * sizeof(float), hipMemcpyDeviceToDevice,
                                ix->stream));
-        CAP_TRY(hipMemcpyAsync(Xq, ix->Xq, (size_t)used_tiles * tile_floats * sizeof(float) / 2,
-                               hipMemcpyDeviceToDevice, ix->stream));
+        if (Xq && ix->Xq)
+            CAP_TRY(hipMemcpyAsync(Xq, ix->Xq, (size_t)used_tiles * tile_floats * sizeof(float) / 2,
+                                   hipMemcpyDeviceToDevice, ix->stream));
         CAP_TRY(hipMemcpyAsync(n64, ix->nrm64, ix->count * sizeof(double), hipMemcpyDeviceToDevice, ix->stream));
         CAP_TRY(hipMemcpyAsync(i32, ix->inv32, ix->count * sizeof(float), hipMemcpyDeviceToDevice, ix->stream));
         CAP_TRY(hipMemcpyAsync(s32, ix->sq32, ix->count * sizeof(float), hipMemcpyDeviceToDevice, ix->stream));
@@ -327,6 +338,23 @@ int ensure_capacity(vdb_index* ix, int64_t rows) {
     ix->sq32 = s32;
     ix->rinit32 = r32;
     ix->cap_rows = cap;
+    return VDB_OK;
+}
+
+// The int8 copy for a setting that starts to read it (lazily: ensure_capacity keeps it only
+// while a setting does).  Zeroed; the caller rebuilds rows [0, count) (build_candidate_rows).
+int ensure_xq(vdb_index* ix) {
+    if (ix->Xq || ix->cap_rows == 0) return VDB_OK;
+    const size_t bytes = (size_t)(ix->cap_rows / 32) * ix->G * BLOCK_FLOATS * sizeof(float) / 2;
+    float* Xq = nullptr;
+    hipError_t e = hipMalloc(&Xq, bytes);
+    if (e == hipSuccess) e = hipMemsetAsync(Xq, 0, bytes, ix->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ix->stream);
+    if (e != hipSuccess) {
+        if (Xq) (void)hipFree(Xq);
+        return set_error(e == hipErrorOutOfMemory ? VDB_ERR_OOM : VDB_ERR_HIP, "int8 copy: %s", hipGetErrorString(e));
+    }
+    ix->Xq = Xq;
     return VDB_OK;
 }
 
@@ -373,6 +401,18 @@ void release_ws(vdb_index* ix, Workspace* w, hipStream_t st) {
 // Remember the last work a search without a workspace queued on `st` (wait_idle).
 int note_use(vdb_index* ix, hipStream_t st) {
     std::lock_guard<std::mutex> g(ix->ws_mu);
+    // a server that makes a stream per request would grow this map without bound:
+    // past 64 entries, the ones whose last recorded work has completed are dropped
+    if (ix->uses.size() >= 64 && !ix->uses.count(st)) {
+        for (auto it = ix->uses.begin(); it != ix->uses.end();) {
+            if (hipEventQuery(it->second) == hipSuccess) {
+                (void)hipEventDestroy(it->second);
+                it = ix->uses.erase(it);
+            } else {
+                ++it;
+            }
+        }
+    }
     hipEvent_t& e = ix->uses[st];
     if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIP_TRY(hipEventRecord(e, st));
@@ -637,6 +677,10 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
         // rebuild a copy the new setting reads that the old one did not keep up to date
         const bool xs = xs_kind(value) != kXsNone && xs_kind(value) != xs_kind(ix->precision);
         const bool xq = needs_i8(value, ix->auto_i8) && !needs_i8(ix->precision, ix->auto_i8);
+        if (xq) {
+            const int xr = ensure_xq(ix);
+            if (xr) return xr;
+        }
         ix->precision = value;
         if ((xs || xq) && ix->Xs && ix->count > 0) {
             HIP_TRY(build_candidate_rows(ix, 0, ix->count, ix->stream, xs, xq));
@@ -650,6 +694,10 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
         const int wr = wait_idle(ix);
         if (wr) return wr;
         const bool xq = needs_i8(ix->precision, v) && !needs_i8(ix->precision, ix->auto_i8);
+        if (xq) {
+            const int xr = ensure_xq(ix);
+            if (xr) return xr;
+        }
         ix->auto_i8 = v;
         if (xq && ix->Xs && ix->count > 0) {
             HIP_TRY(build_candidate_rows(ix, 0, ix->count, ix->stream, false, true));
@@ -711,6 +759,9 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
         ix->scan_publish = value;
     } else if (n == "pilot_fused") {
         ix->pilot_fused = value != 0;
+    } else if (n == "device_repass") {
+        if (value < -1 || value > 1) return set_error(VDB_ERR_INVALID, "device_repass must be -1, 0 or 1");
+        ix->device_repass = value;
     } else if (n == "debug_stale_rinit") {
         // TEST ONLY: plants a stale L2 start value, -|x|^2/2 := 0 for row `value` (the operand a
         // scan read before its load landed in VERDICT r3), so the consistency guard of the
@@ -737,8 +788,8 @@ int32_t vdb_index_get_stat(const vdb_index* cix, const char* name, int64_t* valu
     if (!cix || !name || !value) return set_error(VDB_ERR_INVALID, "NULL argument");
     vdb_index* ix = const_cast<vdb_index*>(cix);  // pending device-side counts are folded in
     std::string n(name);
-    unsigned long long dt[2] = {0, 0};
-    if ((n == "fallback_queries" || n == "overflow_queries") && ix->d_totals) {
+    unsigned long long dt[4] = {0, 0, 0, 0};
+    if ((n == "fallback_queries" || n == "overflow_queries" || n == "repass_queries") && ix->d_totals) {
         HIP_TRY(hipSetDevice(ix->device));
         const int wr = wait_idle(ix);  // device-memory searches queued on caller streams
         if (wr) return wr;
@@ -752,7 +803,7 @@ int32_t vdb_index_get_stat(const vdb_index* cix, const char* name, int64_t* valu
     if (n == "searches") *value = ix->n_searches.load();
     else if (n == "queries") *value = ix->n_queries.load();
     else if (n == "fallback_queries") *value = ix->n_fallback.load() + (int64_t)dt[0];
-    else if (n == "repass_queries") *value = ix->n_repass.load();
+    else if (n == "repass_queries") *value = ix->n_repass.load() + (int64_t)dt[3];  // + device re-passes
     else if (n == "searches_scan3") *value = ix->n_scan3.load();
     else if (n == "searches_q4") *value = ix->n_q4.load();
     else if (n == "auto_hold") *value = ix->auto_hold.load();
@@ -772,7 +823,7 @@ int32_t vdb_index_get_stat(const vdb_index* cix, const char* name, int64_t* valu
     else if (n == "searches_i8x3") *value = ix->n_by_prec[PREC_I8X3].load();
     else if (n == "auto_int8") *value = ix->auto_i8 ? 1 : 0;
     else if (n == "device_bytes")
-        *value = (int64_t)(ix->cap_rows / 32) * ix->G * BLOCK_FLOATS * 10 + ix->cap_rows * 20;  // X, Xs, Xq
+        *value = (int64_t)(ix->cap_rows / 32) * ix->G * BLOCK_FLOATS * (ix->Xq ? 10 : 8) + ix->cap_rows * 20;  // X, Xs (+ Xq)
     else return set_error(VDB_ERR_INVALID, "unknown stat '%s'", name);
     return VDB_OK;
 }
@@ -1019,6 +1070,11 @@ constexpr int32_t kRetryBf16x3 = 1 << 20;
 // A host-memory bf16 search re-passes its uncertified queries in bf16x3 (gathered into one
 // device-memory sub-search) when they are at most 1/8 of the batch and at most this many.
 constexpr int kRepassMax = 64;
+// Device-memory searches (device_repass): up to this many uncertified queries of a batch are
+// gathered into a gated BF16X3 sub-search on the device (more go to the exact path); auto arms
+// the re-pass for kRepassArm searches after a device fallback was seen.
+constexpr int kRepassDev = 16;
+constexpr int kRepassArm = 256;
 // VDB_PREC_AUTO uses the bf16 pass up to this k (its KP = next_pow2(k + 112) stays 128)
 constexpr int kAutoBf16MaxK = 16;
 
@@ -1069,6 +1125,9 @@ static int repass_flagged(vdb_index* ix, const float* Qd, const int* flag_list, 
 struct SearchOpts {
     bool force_b3 = false;  // VDB_PREC_AUTO: this search runs bf16x3 (retry / re-pass)
     bool repass = false;    // an internal sub-search of a re-pass (no search / query counts)
+    // device re-pass: the sub-search's query count lives on the device (B is its capacity);
+    // its candidate pass and finish are gated on it, and it runs without a pilot
+    const int* gate = nullptr;
 };
 
 static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int32_t k, const uint32_t* row_mask,
@@ -1149,6 +1208,7 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
         if (seen > prev) {
             if (ix->last_i8) auto_fail8(ix);
             else auto_fail(ix);
+            ix->repass_arm = kRepassArm;  // device_repass auto: re-pass on the device for a while
         }
     }
     const bool approx = N > 0 && !(ix->force_exact || k > kMaxApproxK);
@@ -1202,15 +1262,19 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     // each row range is re-read from L2 by half as many workgroups (C4: 8 -> 4 blocks)
     const bool q4 = split_pass && !exact_all && KP == 128 && B >= 256 && Gs <= 8 &&
                     (ix->scan_q4 == 1 || (ix->scan_q4 < 0));
+    // The int8 pass's 128-query shape (vdb_scan8_kernel.h S8_ONE4): the same rule for short rows
+    // (D <= 128), KP = 128, batches of >= 256 (C4: I8X3, 8 -> 4 query blocks per row range)
+    const bool q4_8 = i8_pass && !exact_all && !opt.gate && KP == 128 && B >= 256 && scan8_q4_ok(Gs, prec) &&
+                      (ix->scan_q4 == 1 || (ix->scan_q4 < 0));
     // query rows per candidate-pass block: the int8 pass keeps 64 at KP = 256 (KW = 64 kept per
     // workgroup, vdb_scan8_kernel.h), the split pass 32 there
-    const int QB = q4 ? 128 : i8_pass ? scan8_qb(KP) : KP == 256 ? 32 : 64;
+    const int QB = q4 ? 128 : i8_pass ? scan8_qb(KP, q4_8) : KP == 256 ? 32 : 64;
     const int QB_pilot = i8_pass ? 64 : KP == 256 ? 32 : 64;  // the pilot's own query blocks (instantiations)
     const int Bp = (int)round_up(B, 128);  // whole query super tiles (tiled layout)
     const int n_qblocks = (B + QB - 1) / QB;
     int variant = split_pass || i8_pass ? 0 : (int)ix->scan_variant;
     if (!split_pass && !i8_pass && !scan_variant_ok(prec, variant, Gs)) variant = 0;  // e.g. PX=8 needs Dp % 128 == 0
-    const int64_t step_rows = i8_pass ? scan8_rows_per_step(prec, ix->metric)
+    const int64_t step_rows = i8_pass ? scan8_rows_per_step(prec, ix->metric, q4_8)
                               : split_pass ? scan2_rows_per_step(q4) : scan_rows_per_step(prec, variant);
     const int64_t n_steps = std::max<int64_t>(1, round_up(N, step_rows) / step_rows);
     // one 4-wave workgroup per CU (1 wave per SIMD, all of its 512 registers):
@@ -1275,6 +1339,8 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     bytes += (size_t)Bp * 4 + 256;                          // shared thresholds
     bytes += (size_t)Bp * (KP_MAX + PILOT_SLOTS) * 4 + 256;  // shared threshold slots + pilot slots
     bytes += (size_t)Bp * 12 + 1024;                          // int8 pass: qmax, lsl, qerr [Bp]; qscal
+    const int R_rep = std::min(B, kRepassDev);                // device re-pass: gathered queries + results
+    bytes += mem == VDB_MEM_DEVICE ? (size_t)R_rep * (D * 4 + (size_t)k * 20) + 1024 : 0;
     bytes += ((size_t)(n_wg + 7) / 8 * 8 * n_qblocks + 64) * 4; // int8 pass: pacing counters
     const bool priv = !exact_all && !split_pass && !i8_pass && scan_priv(prec, variant, KP);
     // global per-query candidate lists: at most 512 entries per workgroup and query
@@ -1289,7 +1355,9 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     // 200 K -> 250 K QPS; C2 / C3, 1 M rows: larger samples only add pilot time,
     // profiles/r03_i8/pilot).
     const int64_t pilot_def = std::min<int64_t>(4096, std::max<int64_t>(512 * std::max(1, k / 12), N / (32 * 160)));
-    const int n_pilot = (int)std::min<int64_t>(ix->pilot_tiles >= 0 ? ix->pilot_tiles : pilot_def, round_up(N, 32) / 32);
+    const int n_pilot = opt.gate ? 0  // a gated re-pass sub-search: no pilot (few queries; its launches stay light)
+                                 : (int)std::min<int64_t>(ix->pilot_tiles >= 0 ? ix->pilot_tiles : pilot_def,
+                                                          round_up(N, 32) / 32);
     // Rank of the pilot's bound among its sampled scores.  The KP-th best sample is a
     // guaranteed lower bound of the global KP-th best but sits at global rank ~KP N / S (C2:
     // ~2000), so the candidate pass inserts every score above that until its own buffers
@@ -1345,6 +1413,10 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     float* q8err = c.take<float>(Bp);
     float* q8scal = c.take<float>(64);
     uint32_t* pace = c.take<uint32_t>((size_t)(n_wg + 7) / 8 * 8 * n_qblocks + 64);
+    float* rep_q = mem == VDB_MEM_DEVICE ? c.take<float>((size_t)R_rep * D) : nullptr;
+    float* rep_s = mem == VDB_MEM_DEVICE ? c.take<float>((size_t)R_rep * k) : nullptr;
+    int64_t* rep_i = mem == VDB_MEM_DEVICE ? c.take<int64_t>((size_t)R_rep * k) : nullptr;
+    double* rep_k = mem == VDB_MEM_DEVICE ? c.take<double>((size_t)R_rep * k) : nullptr;
 
     const float* Qd = queries;
     const uint32_t* md = row_mask;
@@ -1413,14 +1485,16 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
             }
             // scan_ns times the scan kernel alone (the roofline's kernel); pipeline_ns
             // everything from the pilot to the rerank
+            if (opt.gate && (use_s3 || q4 || !(split_pass || i8_pass)))  // only these passes are gated
+                return set_error(VDB_ERR_INVALID, "device re-pass: the sub-search has no gated candidate pass");
             if (timed) HIP_TRY(hipEventRecord(tev[0], st));
             if (use_s3) ix->n_scan3++;
-            if (q4 && !use_s3) ix->n_q4++;
+            if ((q4 && !use_s3) || q4_8) ix->n_q4++;
             if (i8_pass)
                 HIP_TRY(launch_scan8(prec, ix->metric, KP, Xscan, ix->rinit32, md, Qt, q8lsl, q8scal, Gs, N, B,
                                      n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr,
                                      ix->scan_pace ? pace : nullptr, ix->pace_seq.fetch_add(1) + 1, lockstep,
-                                     (int)ix->scan_qlds, st));
+                                     (int)ix->scan_qlds, st, opt.gate, q4_8));
             else if (use_s3)
                 HIP_TRY(launch_scan3(prec, ix->metric, Xscan, ix->rinit32, md, Qt, Gs, N, B, n_qb3, steps3, n_wg3, spw3,
                                      gl_s, gl_i, gl_cnt, gl_cap, gthr, st));
@@ -1428,7 +1502,7 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
                 HIP_TRY(launch_scan2(prec, ix->metric, KP, Xscan, ix->rinit32, md, Qt, Gs, N, B, n_qblocks, n_steps,
                                      n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, pslots,
                                      n_pilot > 0 && ix->pilot_fused && !q4 ? pilot_rank : 0, lockstep, publish,
-                                     (int)ix->scan_qring, st, q4, (int)ix->scan_qlds));
+                                     (int)ix->scan_qring, st, q4, (int)ix->scan_qlds, opt.gate));
             else if (priv)
                 HIP_TRY(launch_scan_topk_priv(prec, ix->metric, KP, Xscan, rowscale, md, Qt, Gs, N, B, n_qblocks,
                                               n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, st));
@@ -1469,6 +1543,7 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
             fa.row_ids = row_ids;
             fa.flag_count = flags; fa.flag_list = flags + 1; fa.gthr = gthr; fa.overflow_count = flags + B + 1;
             fa.incons_count = flags + B + 2;
+            fa.gate = opt.gate;
             fa.split = fin_split; fa.sx_ek = fx_ek; fa.sx_ck = fx_ck; fa.sx_cr = fx_cr; fa.sx_n = fx_n; fa.done = done;
             HIP_TRY(launch_finish(ix->metric, KP, fa, B, st));
             if (timed) HIP_TRY(hipEventRecord(tev[2], st));
@@ -1483,14 +1558,45 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
                         HIP_TRY(hipHostMalloc(&ix->h_totals, 2 * sizeof(unsigned long long), hipHostMallocDefault));
                         ix->h_totals[0] = ix->h_totals[1] = 0;
                         unsigned long long* d = nullptr;
-                        HIP_TRY(hipMalloc(&d, 3 * sizeof(unsigned long long)));  // flagged, overflowed, flagged bf16
-                        HIP_TRY(hipMemset(d, 0, 3 * sizeof(unsigned long long)));
+                        // flagged, overflowed, flagged in a one-plane pass, re-passed on the device
+                        HIP_TRY(hipMalloc(&d, 4 * sizeof(unsigned long long)));
+                        HIP_TRY(hipMemset(d, 0, 4 * sizeof(unsigned long long)));
                         ix->d_totals = d;
                     }
                 }
+                unsigned long long* htot = auto_prec && (one_plane || prec == PREC_I8X3) ? ix->h_totals : nullptr;
+                // The device re-pass: up to kRepassDev uncertified queries gathered on the
+                // device into a BF16X3 sub-search on this stream, gated on their count (its candidate
+                // pass and finish exit at once when nothing was flagged), its rows scattered back;
+                // the rest, if any, take the gated exact path.  Like the host re-pass (repass_flagged)
+                // for auto's one-plane / I8X3 passes, with the split copy kept beside the int8 one.
+                const bool can_rep = !opt.repass && auto_prec && (one_plane || prec == PREC_I8X3) && ix->Xs &&
+                                     xs_kind(VDB_PREC_BF16X3) == xs_kind(ix->precision) && rep_q;
+                bool rep = can_rep && ix->device_repass == 1;
+                if (can_rep && ix->device_repass < 0) {
+                    int a = ix->repass_arm.load();
+                    while (a > 0 && !ix->repass_arm.compare_exchange_weak(a, a - 1)) {}
+                    rep = a > 0;
+                }
+                if (rep) {
+                    int* counts = flags + B + 3;  // [0] gathered (the sub-search's gate), [1] left over
+                    HIP_TRY(launch_repass_gather(Qd, D, flags, R_rep, rep_q, counts, ix->d_totals + 3, st));
+                    SearchOpts o;
+                    o.force_b3 = true;
+                    o.repass = true;
+                    o.gate = counts;
+                    rc = search_locked(ix, rep_q, R_rep, k, md, VDB_MEM_DEVICE, rep_s, rep_i, rep_k, index_offset, st,
+                                       row_ids, o);
+                    if (rc) return rc;
+                    HIP_TRY(launch_scatter_results(flags + 1, R_rep, k, rep_s, rep_i, rep_k, out_s, out_i, out_k, st,
+                                                   counts));
+                    if (B > R_rep)
+                        rc = run_exact(ix, w, Qd, qn64, flags + 1 + R_rep, B - R_rep, k, md, out_s, out_i, out_k,
+                                       index_offset, row_ids, st, counts + 1, flags + B + 1, done + R_rep, htot);
+                    return rc;
+                }
                 rc = run_exact(ix, w, Qd, qn64, flags + 1, B, k, md, out_s, out_i, out_k, index_offset, row_ids, st,
-                               flags, flags + B + 1, done,
-                               auto_prec && (one_plane || prec == PREC_I8X3) ? ix->h_totals : nullptr);
+                               flags, flags + B + 1, done, htot);
                 return rc;
             }
             HIP_TRY(hipMemcpyAsync(w->host_flag, flags, sizeof(int), hipMemcpyDeviceToHost, st));

@@ -336,6 +336,7 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
     const int wv = tid >> 6;
     const int b = blockIdx.x;
     const int S = a.split, sp = blockIdx.y;  // split > 1: S workgroups per query share the rerank
+    if (a.gate && b >= *a.gate) return;  // device re-pass: a slot past the gathered count
     FIN_STAMP(0);
     const int64_t c = min((int64_t)a.gl_cnt[b], a.gl_cap);
 #ifdef VDB_STAMP

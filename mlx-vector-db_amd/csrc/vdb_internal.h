@@ -51,13 +51,14 @@ hipError_t launch_prep8(const float* Q, const double* qn64, const float* qmax, i
 hipError_t launch_pilot8(int prec, int metric, const float* Xq, const float* rinit, const uint32_t* mask,
                          const float* Qq, const float* qscal, int G8, int64_t N, int B, int n_qblocks, int QB,
                          int n_sample, uint32_t* pslots, hipStream_t st);
-int scan8_rows_per_step(int prec, int metric);
-int scan8_qb(int KP);  // queries per block of the int8 pass
+int scan8_rows_per_step(int prec, int metric, bool q4 = false);
+int scan8_qb(int KP, bool q4 = false);  // queries per block of the int8 pass
+bool scan8_q4_ok(int G8, int prec);     // the 128-query shape fits (short rows)
 hipError_t launch_scan8(int prec, int metric, int KP, const float* Xq, const float* rinit, const uint32_t* mask,
                         const float* Qq, const float* lsl, const float* qscal, int G8, int64_t N, int B,
                         int n_qblocks, int64_t n_steps, int n_wg, int spw, float* gl_s, uint32_t* gl_i,
                         uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr, uint32_t* pace, uint32_t pace_tag,
-                        int lockstep, int qlds, hipStream_t st);
+                        int lockstep, int qlds, hipStream_t st, const int* gate = nullptr, bool q4 = false);
 
 // Ingest: row-major fp32 [n][D] (device) -> the index's row-major fp32 copy X [cap][Dp]
 // (zero padded to Dp = 8 G; read by the exact paths, export and the graph) rows [row0, row0+n),
@@ -149,7 +150,7 @@ hipError_t launch_scan2(int prec, int metric, int KP, const float* Xs, const flo
                         const float* Qs, int G, int64_t N, int B, int n_qblocks, int64_t n_steps, int n_wg, int spw,
                         float* gl_s, uint32_t* gl_i, uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr,
                         uint32_t* gslots, const uint32_t* pslots, int prank, int lockstep, int publish, int qring,
-                        hipStream_t st, bool q4 = false, int qlds = -1);
+                        hipStream_t st, bool q4 = false, int qlds = -1, const int* gate = nullptr);
 // The large-batch split pass (vdb_scan3_kernel.h): 256 queries per workgroup (n_qb blocks), row
 // groups shared by the waves through LDS, KW = 32 kept per query and workgroup (drop bound ->
 // gthr).  Steps of scan3_rows_per_step() rows; same inputs / outputs as launch_scan2.
@@ -197,6 +198,7 @@ struct FinishArgs {
     int* flag_count; int* flag_list; const uint32_t* gthr;
     int* overflow_count;  // lists longer than the finish kernel holds (they take the exact path)
     int* incons_count = nullptr;  // optional: queries flagged by the approx-vs-exact consistency guard
+    const int* gate = nullptr;  // optional (device re-pass): only queries b < *gate are finished
     const int64_t* row_ids = nullptr;  // global id per row (multi-device shard), else row + index_offset
     // split > 1: split workgroups per query share the exact rerank (rows by row % split); their
     // shares go to sx_* [B][split][KP] (+ counts sx_n [B][split]) and the last one (done[b],
@@ -247,9 +249,14 @@ hipError_t launch_finalize_i64(int metric, const double* sk, const int64_t* si, 
                                int k, float* out_s, int64_t* out_i, double* out_k, hipStream_t st);
 // out[r] = Q[list[r]] (rows of D floats), r < n
 hipError_t launch_gather_rows(const float* Q, int D, const int* list, int n, float* out, hipStream_t st);
+// The device-memory re-pass (vdb_api.cpp): the first min(c, R) of the c = flags[0] flagged queries
+// flags[1..c] gathered into out [R][D]; counts[0] = min(c, R) (the sub-search's gate), counts[1] =
+// max(c - R, 0) (left to the exact path); totals (optional) += counts[0].
+hipError_t launch_repass_gather(const float* Q, int D, const int* flags, int R, float* out, int* counts,
+                                unsigned long long* totals, hipStream_t st);
 // o*[list[r]][e] = s*[r][e] for r < n, e < k (ok may be NULL)
 hipError_t launch_scatter_results(const int* list, int n, int k, const float* ss, const int64_t* si, const double* sk,
-                                  float* os, int64_t* oi, double* ok, hipStream_t st);
+                                  float* os, int64_t* oi, double* ok, hipStream_t st, const int* n_dev = nullptr);
 // n "no result" entries: score 0, row -1, key -inf (as write_result's invalid entries)
 hipError_t launch_empty_results(int64_t n, float* out_s, int64_t* out_i, double* out_k, hipStream_t st);
 

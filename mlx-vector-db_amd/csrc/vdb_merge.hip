@@ -99,11 +99,38 @@ hipError_t launch_gather_rows(const float* Q, int D, const int* list, int n, flo
     return hipGetLastError();
 }
 
+__global__ void __launch_bounds__(256) repass_gather_kernel(const float* __restrict__ Q, int D,
+                                                            const int* __restrict__ flags, int R,
+                                                            float* __restrict__ out, int* __restrict__ counts,
+                                                            unsigned long long* __restrict__ totals) {
+    const int c = flags[0];
+    const int n = c < R ? c : R;
+    const int r = blockIdx.y;
+    if (r == 0 && blockIdx.x == 0 && threadIdx.x == 0) {
+        counts[0] = n;
+        counts[1] = c > R ? c - R : 0;
+        if (totals && n > 0) atomicAdd(totals, (unsigned long long)n);
+    }
+    if (r >= n) return;
+    const int b = flags[1 + r];
+    for (int d = blockIdx.x * 256 + threadIdx.x; d < D; d += gridDim.x * 256) out[(size_t)r * D + d] = Q[(size_t)b * D + d];
+}
+
+hipError_t launch_repass_gather(const float* Q, int D, const int* flags, int R, float* out, int* counts,
+                                unsigned long long* totals, hipStream_t st) {
+    if (R <= 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(repass_gather_kernel, dim3((unsigned)std::min(8, (D + 255) / 256), (unsigned)R), dim3(256), 0,
+                       st, Q, D, flags, R, out, counts, totals);
+    return hipGetLastError();
+}
+
 __global__ void __launch_bounds__(256) scatter_results_kernel(const int* __restrict__ list, int n, int k,
                                                               const float* __restrict__ ss, const int64_t* __restrict__ si,
                                                               const double* __restrict__ sk, float* __restrict__ os,
-                                                              int64_t* __restrict__ oi, double* __restrict__ ok) {
+                                                              int64_t* __restrict__ oi, double* __restrict__ ok,
+                                                              const int* __restrict__ n_dev) {
     const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (n_dev && *n_dev < n) n = *n_dev;  // device re-pass: the gathered count
     if (t >= (int64_t)n * k) return;
     const int r = (int)(t / k), e = (int)(t % k);
     const size_t o = (size_t)list[r] * k + e;
@@ -113,11 +140,11 @@ __global__ void __launch_bounds__(256) scatter_results_kernel(const int* __restr
 }
 
 hipError_t launch_scatter_results(const int* list, int n, int k, const float* ss, const int64_t* si, const double* sk,
-                                  float* os, int64_t* oi, double* ok, hipStream_t st) {
+                                  float* os, int64_t* oi, double* ok, hipStream_t st, const int* n_dev) {
     const int64_t m = (int64_t)n * k;
     if (m <= 0) return hipSuccess;
     hipLaunchKernelGGL(scatter_results_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, list, n, k, ss, si,
-                       sk, os, oi, ok);
+                       sk, os, oi, ok, n_dev);
     return hipGetLastError();
 }
 

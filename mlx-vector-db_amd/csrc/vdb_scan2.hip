@@ -142,7 +142,7 @@ hipError_t launch_scan2(int prec, int metric, int KP, const float* Xs, const flo
                         const float* Qs, int G, int64_t N, int B, int n_qblocks, int64_t n_steps, int n_wg, int spw,
                         float* gl_s, uint32_t* gl_i, uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr,
                         uint32_t* gslots, const uint32_t* pslots, int prank, int lockstep, int publish, int qring,
-                        hipStream_t st, bool q4, int qlds) {
+                        hipStream_t st, bool q4, int qlds, const int* gate) {
     // the query block in LDS: auto (qlds < 0) when it fits, 0 = from global memory (then, with one
     // query block, the corpus stream takes the non-temporal policy)
     const bool ql = q4 || (qlds != 0 && scan2_qlds(G, KP, q4));
@@ -155,7 +155,7 @@ hipError_t launch_scan2(int prec, int metric, int KP, const float* Xs, const flo
                                      : nullptr;
     if (!unit || metric < 0 || metric > 1) return hipErrorInvalidValue;
     return unit(KP, Xs, rinit, mask, Qs, G, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr,
-                gslots, pslots, prank, nt, ql, fs, qch, q4, publish, st);
+                gslots, pslots, prank, nt, ql, fs, qch, q4, publish, gate, st);
 }
 
 }  // namespace vdb

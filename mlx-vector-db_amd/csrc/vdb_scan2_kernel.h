@@ -146,7 +146,9 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
              const float* __restrict__ Qs, int G_arg, int64_t N, int B, int64_t n_steps, int steps_per_wg, int n_qb,
              float* __restrict__ gl_s, uint32_t* __restrict__ gl_i, uint32_t* __restrict__ gl_cnt, int64_t gl_cap,
              uint32_t* __restrict__ gthr, uint32_t* __restrict__ gslots, const uint32_t* __restrict__ pslots,
-             int prank, int publish) {
+             int prank, int publish, const int* __restrict__ gate) {
+    // a gated launch (the device-memory re-pass, vdb_api.cpp): nothing to do when its count is 0
+    if (gate && *gate == 0) return;
     constexpr int RT = RT_, NW = S2_NW;
     constexpr int QB = 32 * QT;
     constexpr int XPL = Planes<PREC>::XPL, QPL = 2;
@@ -664,7 +666,7 @@ template <int P, int M, int QT, int PX, int KP, int CAP, bool NT, bool QL, bool 
 static hipError_t scan2_launch_g(const float* Xs, const float* rinit, const uint32_t* mask, const float* Qs, int G,
                                  int64_t N, int B, int n_qblocks, int64_t n_steps, int n_wg, int spw, float* gl_s,
                                  uint32_t* gl_i, uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr, uint32_t* gslots,
-                                 const uint32_t* pslots, int prank, int publish, hipStream_t st) {
+                                 const uint32_t* pslots, int prank, int publish, const int* gate, hipStream_t st) {
     auto k = scan2_kernel<P, M, QT, PX, KP, CAP, NT, QL, FS, GC, QC, RT_, KW>;
     const size_t lds = QL ? (size_t)G * 2 * QT * 1024 : QC ? (size_t)2 * S2_QCG * 2 * QT * 1024 : 0;
     if (QL || QC) {
@@ -681,7 +683,7 @@ static hipError_t scan2_launch_g(const float* Xs, const float* rinit, const uint
     }
     const int n_wg8 = (n_wg + 7) / 8 * 8;
     hipLaunchKernelGGL(k, dim3(n_wg8 * n_qblocks), dim3(64 * S2_NW), lds, st, Xs, rinit, mask, Qs, G, N, B, n_steps, spw,
-                       n_qblocks, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, pslots, prank, publish);
+                       n_qblocks, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, pslots, prank, publish, gate);
     return hipGetLastError();
 }
 
@@ -691,16 +693,16 @@ template <int P, int M, int QT, int PX, int KP, int CAP, bool NT, bool QL, bool 
 static hipError_t scan2_launch(const float* Xs, const float* rinit, const uint32_t* mask, const float* Qs, int G,
                                int64_t N, int B, int n_qblocks, int64_t n_steps, int n_wg, int spw, float* gl_s,
                                uint32_t* gl_i, uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr, uint32_t* gslots,
-                               const uint32_t* pslots, int prank, int publish, hipStream_t st) {
+                               const uint32_t* pslots, int prank, int publish, const int* gate, hipStream_t st) {
     if constexpr (QL) {
         if (G == 8)
             return scan2_launch_g<P, M, QT, PX, KP, CAP, NT, QL, FS, 8, false, RT_, KW>(
                 Xs, rinit, mask, Qs, G, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots,
-                pslots, prank, publish, st);
+                pslots, prank, publish, gate, st);
     }
     return scan2_launch_g<P, M, QT, PX, KP, CAP, NT, QL, FS, 0, false, RT_, KW>(
         Xs, rinit, mask, Qs, G, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, pslots,
-        prank, publish, st);
+        prank, publish, gate, st);
 }
 
 // The argument list of one (precision, metric) unit's launcher (launch_scan2 dispatches).
@@ -708,9 +710,9 @@ static hipError_t scan2_launch(const float* Xs, const float* rinit, const uint32
     int KP, const float *Xs, const float *rinit, const uint32_t *mask, const float *Qs, int G, int64_t N, int B,    \
         int n_qblocks, int64_t n_steps, int n_wg, int spw, float *gl_s, uint32_t *gl_i, uint32_t *gl_cnt,          \
         int64_t gl_cap, uint32_t *gthr, uint32_t *gslots, const uint32_t *pslots, int prank, bool nt, bool ql,     \
-        bool fs, bool qch, bool q4, int publish, hipStream_t st
+        bool fs, bool qch, bool q4, int publish, const int *gate, hipStream_t st
 #define S2_ARGS Xs, rinit, mask, Qs, G, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, \
-                pslots, prank, publish, st
+                pslots, prank, publish, gate, st
 #define S2_ONE(P, M, KPV, QTV, PXV, CAPV, NTV, QLV, FSV)                 \
     if (KP == KPV && nt == NTV && ql == QLV && fs == FSV && !qch && !q4) \
         return scan2_launch<P, M, QTV, PXV, KPV, CAPV, NTV, QLV, FSV>(S2_ARGS);

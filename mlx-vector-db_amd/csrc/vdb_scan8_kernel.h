@@ -178,7 +178,9 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
              const float* __restrict__ Qq, const float* __restrict__ lsl, const float* __restrict__ qscal, int G_arg,
              int64_t N, int B, int64_t n_steps, int steps_per_wg, int n_qb, float* __restrict__ gl_s,
              uint32_t* __restrict__ gl_i, uint32_t* __restrict__ gl_cnt, int64_t gl_cap, uint32_t* __restrict__ gthr,
-             uint32_t* __restrict__ pace, uint32_t pace_tag) {
+             uint32_t* __restrict__ pace, uint32_t pace_tag, const int* __restrict__ gate) {
+    // a gated launch (the device-memory re-pass, vdb_api.cpp): nothing to do when its count is 0
+    if (gate && *gate == 0) return;
     constexpr int RT = RT_, NW = S8_NW;
     constexpr int QB = 32 * QT;
     constexpr int XPL = Planes8<PREC>::XPL, QPL = Planes8<PREC>::QPL;
@@ -290,14 +292,15 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
             }
         }
         if constexpr (QLDS) q_lds(0, qr[0]);
+        // L2 start values: waited for here, inside the block that loads them, and again at the
+        // end of every step (below) -- never carried in flight across a join or the loop header.
+        // The compiler may copy a value at a join (phi copies: seen at the loop header of the I8 /
+        // I8X3 L2 QLDS kernels and after this block in the 128-query shape, tools/vmcnt_check.py),
+        // and a copy of a register an asm load is still filling reads stale data (a
+        // cold first search returned wrong, certified L2 results).  Free in time: the first group
+        // waits for the slots issued after these loads anyway.
+        if constexpr (METRIC == 1) s8_wait<PX * LPS>(rin);
     }
-    // L2 start values: waited for before the loop and again at the end of every step (below),
-    // never carried in flight across the loop header.  The compiler may copy a loop-carried value
-    // at the header (phi copies: seen in the I8 / I8X3 L2 QLDS kernels, tools/vmcnt_check.py), and
-    // a copy of a register an asm load is still filling reads stale data (a cold first
-    // search returned wrong, certified L2 results).  Free in time: the first group waits for the
-    // slots issued after these loads anyway.
-    if constexpr (METRIC == 1) s8_wait<PX * LPS>(rin);
 
     for (int64_t s = s_begin; s < s_end; ++s) {
         S8_STAMP(const unsigned long long st_a = S8_NOW(); ++st_n;)
@@ -580,7 +583,8 @@ template <int P, int M, int QT, int PX, int KP, int CAP, bool NT, bool QL, bool 
 static hipError_t scan8_launch_g(const float* Xq, const float* rinit, const uint32_t* mask, const float* Qq,
                                  const float* lsl, const float* qscal, int G, int64_t N, int B, int n_qblocks,
                                  int64_t n_steps, int n_wg, int spw, float* gl_s, uint32_t* gl_i, uint32_t* gl_cnt,
-                                 int64_t gl_cap, uint32_t* gthr, uint32_t* pace, uint32_t pace_tag, hipStream_t st) {
+                                 int64_t gl_cap, uint32_t* gthr, uint32_t* pace, uint32_t pace_tag, const int* gate,
+                                 hipStream_t st) {
     auto k = scan8_kernel<P, M, QT, PX, KP, CAP, NT, QL, FS, GC, RT_, KW>;
     const size_t lds = QL ? (size_t)G * Planes8<P>::QPL * QT * 1024 : 0;
     if (QL) {
@@ -595,33 +599,35 @@ static hipError_t scan8_launch_g(const float* Xq, const float* rinit, const uint
     const int n_wg8 = (n_wg + 7) / 8 * 8;
     hipLaunchKernelGGL(k, dim3(n_wg8 * n_qblocks), dim3(64 * S8_NW), lds, st, Xq, rinit, mask, Qq, lsl, qscal, G, N, B,
                        n_steps, spw, n_qblocks, gl_s, gl_i, gl_cnt, gl_cap, gthr, n_qblocks > 1 ? pace : nullptr,
-                       pace_tag);
+                       pace_tag, gate);
     return hipGetLastError();
 }
 
-template <int P, int M, int QT, int PX, int KP, int CAP, bool NT, bool QL, bool FS, int KW = KP>
+template <int P, int M, int QT, int PX, int KP, int CAP, bool NT, bool QL, bool FS, int KW = KP,
+          int RT_ = scan8_rt(P, M)>
 static hipError_t scan8_launch(const float* Xq, const float* rinit, const uint32_t* mask, const float* Qq,
                                const float* lsl, const float* qscal, int G, int64_t N, int B, int n_qblocks,
                                int64_t n_steps, int n_wg, int spw, float* gl_s, uint32_t* gl_i, uint32_t* gl_cnt,
-                               int64_t gl_cap, uint32_t* gthr, uint32_t* pace, uint32_t pace_tag, hipStream_t st) {
+                               int64_t gl_cap, uint32_t* gthr, uint32_t* pace, uint32_t pace_tag, const int* gate,
+                               hipStream_t st) {
     if constexpr (QL) {
         if (G == 4)  // D = 128: the group loop unrolls, and the whole next step is in flight
-            return scan8_launch_g<P, M, QT, 4, KP, CAP, NT, QL, FS, 4, scan8_rt(P, M), KW>(Xq, rinit, mask, Qq, lsl, qscal, G, N, B,
+            return scan8_launch_g<P, M, QT, 4, KP, CAP, NT, QL, FS, 4, RT_, KW>(Xq, rinit, mask, Qq, lsl, qscal, G, N, B,
                                                                         n_qblocks, n_steps, n_wg, spw, gl_s, gl_i,
-                                                                        gl_cnt, gl_cap, gthr, pace, pace_tag, st);
+                                                                        gl_cnt, gl_cap, gthr, pace, pace_tag, gate, st);
     }
     // the step loop takes the groups PX at a time: Dp / 32 groups is only even (D = 192: 6), so
     // where PX does not divide them the 2-deep variant runs (4 deep, the tail's refills would read
     // the next row tile's groups into this one's scores)
     if constexpr (PX != 2) {
         if (G % PX != 0)
-            return scan8_launch_g<P, M, QT, 2, KP, CAP, NT, QL, FS, 0, scan8_rt(P, M), KW>(
+            return scan8_launch_g<P, M, QT, 2, KP, CAP, NT, QL, FS, 0, RT_, KW>(
                 Xq, rinit, mask, Qq, lsl, qscal, G, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap,
-                gthr, pace, pace_tag, st);
+                gthr, pace, pace_tag, gate, st);
     }
-    return scan8_launch_g<P, M, QT, PX, KP, CAP, NT, QL, FS, 0, scan8_rt(P, M), KW>(Xq, rinit, mask, Qq, lsl, qscal, G, N, B, n_qblocks,
+    return scan8_launch_g<P, M, QT, PX, KP, CAP, NT, QL, FS, 0, RT_, KW>(Xq, rinit, mask, Qq, lsl, qscal, G, N, B, n_qblocks,
                                                                 n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr,
-                                                                pace, pace_tag, st);
+                                                                pace, pace_tag, gate, st);
 }
 
 // The query block in LDS takes the query operand off each wave's vector-memory path (from L2,
@@ -629,6 +635,9 @@ static hipError_t scan8_launch(const float* Xq, const float* rinit, const uint32
 // (64 queries x D bytes per plane; I8 reads qh alone) plus the static LDS (64 queries x CAP x
 // 8 B of lists, s_pend 8 KiB, counters) is within the CU's 160 KiB: C3 (D = 1536, I8, KP = 256
 // with CAP 96): 96 + 56.5 KiB.  `small` keeps the round-3 rule (block <= 32 KiB: short rows).
+// rows per step of the 128-query shape (one row tile per wave)
+constexpr int scan8_rows_q4() { return 1 * S8_NW * 32; }
+inline bool scan8_q4_fits(int G8, int prec) { return (size_t)G8 * (prec == PREC_I8X3 ? 2 : 1) * 4 * 1024 <= 32 * 1024; }
 inline int scan8_cap(int KP, bool ql) { return KP == 128 ? 192 : KP == 256 ? (ql ? 96 : 128) : 128; }  // as S8_KP
 inline bool scan8_qlds(int G8, int KP, int prec, bool small) {
     const size_t q = (size_t)G8 * (prec == PREC_I8X3 ? 2 : 1) * 2 * 1024;
@@ -642,12 +651,20 @@ inline bool scan8_qlds(int G8, int KP, int prec, bool small) {
     int KP, const float *Xq, const float *rinit, const uint32_t *mask, const float *Qq, const float *lsl,          \
         const float *qscal, int G, int64_t N, int B, int n_qblocks, int64_t n_steps, int n_wg, int spw,           \
         float *gl_s, uint32_t *gl_i, uint32_t *gl_cnt, int64_t gl_cap, uint32_t *gthr, uint32_t *pace,            \
-        uint32_t pace_tag, bool nt, bool ql, bool fs, hipStream_t st
+        uint32_t pace_tag, bool nt, bool ql, bool fs, bool q4, const int *gate, hipStream_t st
 #define S8_ARGS \
-    Xq, rinit, mask, Qq, lsl, qscal, G, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, pace, pace_tag, st
-#define S8_ONE(P, M, KPV, QTV, PXV, CAPV, NTV, QLV, FSV, KWV) \
-    if (KP == KPV && nt == NTV && ql == QLV && fs == FSV)       \
+    Xq, rinit, mask, Qq, lsl, qscal, G, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, pace, pace_tag, gate, st
+#define S8_ONE(P, M, KPV, QTV, PXV, CAPV, NTV, QLV, FSV, KWV)   \
+    if (KP == KPV && nt == NTV && ql == QLV && fs == FSV && !q4) \
         return scan8_launch<P, M, QTV, PXV, KPV, CAPV, NTV, QLV, FSV, KWV>(S8_ARGS);
+// The 128-query shape (scan8_q4, short rows, KP = 128): the query block (128 x D x planes) in
+// LDS, ONE row tile per wave and step (the I8X3 H and L sets of 4 query tiles: 128 registers),
+// a workgroup keeps KW = 48 of KP = 128 per query (CAP 64: 64 KiB of lists).  Twice the MFMAs
+// per corpus byte of the 64-query shape, and half the query blocks re-reading each row range
+// (C4, 10M x 128, B = 512: 8 -> 4 blocks).
+#define S8_ONE4(P, M, FSV)                    \
+    if (KP == 128 && ql && fs == FSV && q4)   \
+        return scan8_launch<P, M, 4, 4, 128, 64, false, true, FSV, 48, 1>(S8_ARGS);
 // KP = 256 keeps 64-query blocks: a workgroup keeps its best KW = 64 per query (LDS 64 KiB, 48
 // with the query block in LDS beside it; the drop bound -> gthr, vdb_scan2_kernel.h), so a
 // 64-query batch reads the corpus once
@@ -659,7 +676,8 @@ inline bool scan8_qlds(int G8, int KP, int prec, bool small) {
 #define S8_MODES(P, M, PXV, PXL)                                               \
     S8_KP(P, M, PXV, false, false, false) S8_KP(P, M, PXV, true, false, false) \
     S8_KP(P, M, PXL, false, true, false) S8_KP(P, M, PXL, false, true, true)   \
-    S8_KP(P, M, PXV, false, false, true) S8_KP(P, M, PXV, true, false, true)
+    S8_KP(P, M, PXV, false, false, true) S8_KP(P, M, PXV, true, false, true)   \
+    S8_ONE4(P, M, false) S8_ONE4(P, M, true)
 #define S8_UNIT(NAME, P, M, PXV, PXL)  \
     hipError_t NAME(S8_UNIT_PARAMS) {  \
         S8_MODES(P, M, PXV, PXL)       \

@@ -742,6 +742,55 @@ def test_scan2_q4_shape(vdb, metric):
     ix.close()
 
 
+@pytest.mark.parametrize("metric", ["cosine", "euclidean"])
+def test_scan8_q4_shape(vdb, metric):
+    """The int8 pass's 128-query shape (D <= 128, KP = 128, B >= 256; auto, or knob scan_q4 = 1):
+    the query block of 128 in LDS, one row tile per wave, 48 kept per query and workgroup with the
+    drop bound raising gthr at the end.  Bit-exact vs the oracle for I8X3 (k = 100) and I8 at
+    KP = 128 (margin 100), compile-time (D = 128) and runtime (D = 64, 96) group counts, ragged
+    batches, a mask, against the 64-query shape (scan_q4 = 0), and clustered rows that put more
+    than 48 of a query's top 100 into one workgroup."""
+    rng = np.random.default_rng(71)
+    for D, N in ((128, 120_000), (64, 50_003), (96, 40_000)):
+        V = rng.random((N, D), dtype=np.float32)
+        Q = rng.random((520, D), dtype=np.float32)
+        Q[3], Q[519] = V[N - 1], V[777]
+        for prec, k, margin in (("i8x3", 100, None), ("i8", 10, 100)):
+            for q4 in (1, 0):
+                ix = vdb.NativeIndex(D, metric, precision=prec)
+                ix.set_param("scan_q4", q4)
+                if margin is not None:
+                    ix.set_param("margin", margin)
+                ix.add(V)
+                for B in (520, 256):
+                    s, i, kk = ix.search(Q[:B], k, with_keys=True)
+                    es, ei, ek = ref_cpu.exact_search(Q[:B], V, k, metric)
+                    np.testing.assert_array_equal(i, ei, err_msg=f"{prec} D {D} B {B} q4 {q4}")
+                    np.testing.assert_array_equal(kk, ek)
+                mask = rng.random(N) < 0.4
+                bits = np.zeros(((N + 31) // 32) * 32, bool)
+                bits[:N] = mask
+                words = np.packbits(bits, bitorder="little").view("<u4").astype(np.uint32)
+                s, i, kk = ix.search(Q[:300], k, row_mask=words, with_keys=True)
+                es, ei, ek = ref_cpu.exact_search(Q[:300], V, k, metric, row_mask=mask)
+                np.testing.assert_array_equal(i, ei)
+                np.testing.assert_array_equal(kk, ek)
+                assert ix.stat("searches_q4") == (3 if q4 else 0)
+                print(f"{metric} {prec} D {D} q4 {q4}: fallbacks {ix.stat('fallback_queries')}")
+                ix.close()
+    V = rng.random((60_000, 128), dtype=np.float32)
+    V[30_000:30_070] = (V[9] + 1e-3 * rng.random((70, 128))).astype(np.float32)
+    Q = np.concatenate([V[9:10], rng.random((299, 128), dtype=np.float32)])
+    ix = vdb.NativeIndex(128, metric, precision="i8x3")
+    ix.add(V)
+    s, i, kk = ix.search(Q, 100, with_keys=True)
+    es, ei, ek = ref_cpu.exact_search(Q, V, 100, metric)
+    np.testing.assert_array_equal(i, ei)
+    np.testing.assert_array_equal(kk, ek)
+    assert ix.stat("searches_q4") == 1
+    ix.close()
+
+
 @pytest.mark.parametrize("precision", ["i8", "i8x3"])
 @pytest.mark.parametrize("metric", ["cosine", "euclidean"])
 def test_i8_quantisation_edges(vdb, metric, precision):
@@ -805,3 +854,82 @@ def test_i8_store_filled_one_add_at_a_time(vdb, metric):
     np.testing.assert_array_equal(kk, ek)
     assert ix.stat("searches_i8") == 1
     assert ix.stat("fallback_queries") <= 2, ix.stat("fallback_queries")
+
+
+@pytest.mark.parametrize("metric", ["cosine", "euclidean"])
+def test_device_repass_of_uncertified_queries(vdb, metric):
+    """in a device-memory search (the bench's and a GPU-resident server's path)
+    the few queries auto's int8 pass leaves uncertified are gathered ON THE DEVICE into a gated
+    BF16X3 sub-search on the same stream (device_repass 1) -- no exact scan, no host wait.  A
+    batch of 64 with one near-duplicate query (300 rows within ~1e-3 of it) searched three times
+    back to back: every result exact, no fallback, one re-passed query per batch."""
+    import torch
+    rng = np.random.default_rng(47)
+    N, D, B, k = 40000, 128, 64, 10
+    V = rng.random((N, D), dtype=np.float32)
+    V[1000:1300] = V[11] + 1e-3 * rng.standard_normal((300, D)).astype(np.float32)
+    Q = rng.random((B, D), dtype=np.float32)
+    Q[5] = V[11]
+    ix = vdb.NativeIndex(D, metric)  # auto: the I8 pass for k <= 16
+    ix.set_param("device_repass", 1)
+    ix.add(V)
+    _, ei, ek = ref_cpu.exact_search(Q, V, k, metric)
+    qd = torch.from_numpy(Q).cuda()
+    st = torch.cuda.Stream()
+    st.wait_stream(torch.cuda.current_stream())
+    outs = []
+    for _ in range(3):
+        sd = torch.empty((B, k), dtype=torch.float32, device="cuda")
+        idd = torch.empty((B, k), dtype=torch.int64, device="cuda")
+        kd = torch.empty((B, k), dtype=torch.float64, device="cuda")
+        ix.search_device(qd.data_ptr(), B, k, sd.data_ptr(), idd.data_ptr(), kd.data_ptr(), stream=st.cuda_stream)
+        outs.append((idd, kd))
+    torch.cuda.synchronize()
+    for idd, kd in outs:
+        np.testing.assert_array_equal(idd.cpu().numpy(), ei)
+        np.testing.assert_array_equal(kd.cpu().numpy(), ek)
+    assert ix.stat("searches_i8") == 3
+    assert ix.stat("fallback_queries") == 0, ix.stat("fallback_queries")
+    assert ix.stat("repass_queries") == 3, ix.stat("repass_queries")
+    # a batch with no uncertified query: the gated sub-search does nothing
+    Q2 = rng.random((B, D), dtype=np.float32)
+    _, ei2, ek2 = ref_cpu.exact_search(Q2, V, k, metric)
+    q2 = torch.from_numpy(Q2).cuda()
+    sd = torch.empty((B, k), dtype=torch.float32, device="cuda")
+    idd = torch.empty((B, k), dtype=torch.int64, device="cuda")
+    kd = torch.empty((B, k), dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
+    ix.search_device(q2.data_ptr(), B, k, sd.data_ptr(), idd.data_ptr(), kd.data_ptr(), stream=0)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(idd.cpu().numpy(), ei2)
+    np.testing.assert_array_equal(kd.cpu().numpy(), ek2)
+    assert ix.stat("repass_queries") == 3 and ix.stat("fallback_queries") == 0
+
+
+def test_device_repass_more_flagged_than_gathered(vdb):
+    """More uncertified queries than the device re-pass gathers (16): the first 16 are
+    re-passed, the rest take the gated exact path; all exact."""
+    import torch
+    rng = np.random.default_rng(53)
+    N, D, B, k = 30000, 96, 40, 10
+    V = rng.random((N, D), dtype=np.float32)
+    Q = rng.random((B, D), dtype=np.float32)
+    for j in range(20):  # 20 queries, each with 300 near-duplicate rows
+        V[1000 + 300 * j:1300 + 300 * j] = V[j] + 1e-3 * rng.standard_normal((300, D)).astype(np.float32)
+        Q[2 * j] = V[j]
+    ix = vdb.NativeIndex(D, "cosine")
+    ix.set_param("device_repass", 1)
+    ix.add(V)
+    _, ei, ek = ref_cpu.exact_search(Q, V, k, "cosine")
+    qd = torch.from_numpy(Q).cuda()
+    sd = torch.empty((B, k), dtype=torch.float32, device="cuda")
+    idd = torch.empty((B, k), dtype=torch.int64, device="cuda")
+    kd = torch.empty((B, k), dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
+    ix.search_device(qd.data_ptr(), B, k, sd.data_ptr(), idd.data_ptr(), kd.data_ptr(), stream=0)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(idd.cpu().numpy(), ei)
+    np.testing.assert_array_equal(kd.cpu().numpy(), ek)
+    rp, fb = ix.stat("repass_queries"), ix.stat("fallback_queries")
+    print(f"re-passed {rp}, exact path {fb}")
+    assert rp == 16 and fb >= 1
