@@ -421,6 +421,7 @@ def main():
     ap.add_argument("--pilot-rank", type=int, default=None, help="rank of the pilot bound (tuning; default: Poisson rule)")
     ap.add_argument("--k", type=int, default=None, help="tuning: the config at another k (not the config's line)")
     ap.add_argument("--finish-split", type=int, default=None, help="workgroups per query in the finish (tuning)")
+    ap.add_argument("--i8-refine", type=int, default=None, help="0: the finish's I8 refinement off (tuning)")
     ap.add_argument("--device-repass", type=int, default=None,
                     help="device re-pass of uncertified queries: -1 auto (armed after a fallback), 0 off, 1 always")
     ap.add_argument("--scan-pace", type=int, default=None, help="int8 pass: 1 pace the query blocks of a row range, "
@@ -531,6 +532,8 @@ def bench_brute(cfg, args, world, rank, local, dev, primary=True):
         ix.set_param("finish_split", args.finish_split)
     if args.device_repass is not None:
         ix.set_param("device_repass", args.device_repass)
+    if args.i8_refine is not None:
+        ix.set_param("i8_refine", args.i8_refine)
     if args.no_fallback:
         ix.set_param("no_fallback", 1)
     ix.reserve(n_local)

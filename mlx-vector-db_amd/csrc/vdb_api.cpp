@@ -106,6 +106,9 @@ struct vdb_index {
     float* Xs = nullptr;  // the candidate pass's copy, same bytes: split-bf16 tiles (PREC_BF16X3 / BF16 /
                           // AUTO) or fp32 tiles (PREC_FP32), rebuilt from X when the precision class changes
     float* Xq = nullptr;  // the int8 copy (PREC_I8 / I8X3, AUTO with auto_i8): half the bytes of X
+    // its xh plane row-major [cap][Dp] (with Xq): the finish refines I8 candidates' scores with
+    // the query's rounding residual, reading each candidate's row whole (vdb_exact.hip)
+    int8_t* Xh = nullptr;
     double* nrm64 = nullptr;
     float* inv32 = nullptr;
     float* sq32 = nullptr;
@@ -182,6 +185,7 @@ struct vdb_index {
     // 8 blocks within 5 steps (from 26) and ran the scan at 4.99 ms against 2.90 without
     // (the range at its slowest block's speed, the prefetch drained per sleep; profiles/r03_i8/pace)
     bool scan_pace = false;
+    bool no_refine = false;  // A/B knob "i8_refine" = 0: the finish's I8 refinement off
     // device-memory searches: uncertified queries of an I8 / BF16 / I8X3 pass re-passed in BF16X3
     // on the device (gated kernels, no host wait) instead of the fp64 exact scan.  -1 auto: armed
     // for kRepassArm searches once a device fallback has been seen; 0 off; 1 always
@@ -242,7 +246,7 @@ hipError_t build_candidate_rows(const vdb_index* ix, int64_t row0, int64_t n, hi
     if (xs && xs_kind(ix->precision) == kXsFp32) e = launch_tile_rows(ix->X, ix->G, row0, n, ix->Xs, st);
     if (xs && xs_kind(ix->precision) == kXsSplit) e = launch_split_rows(ix->X, ix->G, row0, n, inv, ix->Xs, st);
     if (e == hipSuccess && xq && needs_i8(ix->precision, ix->auto_i8))
-        e = launch_quant_rows(ix->X, inv, ix->d_mu, ix->d_dir, ix->sx, row0, n, ix->G, ix->Xq, ix->d_i8, st);
+        e = launch_quant_rows(ix->X, inv, ix->d_mu, ix->d_dir, ix->sx, row0, n, ix->G, ix->Xq, ix->d_i8, st, ix->Xh);
     return e;
 }
 
@@ -269,6 +273,7 @@ int ensure_capacity(vdb_index* ix, int64_t rows) {
     float* X = nullptr;
     float* Xs = nullptr;
     float* Xq = nullptr;
+    int8_t* Xh = nullptr;
     double* n64 = nullptr;
     float *i32 = nullptr, *s32 = nullptr, *r32 = nullptr;
     // All new buffers are allocated and filled before the index switches to them; on
@@ -276,7 +281,7 @@ int ensure_capacity(vdb_index* ix, int64_t rows) {
     // and the index keeps its current buffers, so a later retry sees the same HBM.
     auto fail = [&](hipError_t e, const char* what) {
         (void)hipStreamSynchronize(ix->stream);
-        for (void* p : {(void*)X, (void*)Xs, (void*)Xq, (void*)n64, (void*)i32, (void*)s32, (void*)r32})
+        for (void* p : {(void*)X, (void*)Xs, (void*)Xq, (void*)Xh, (void*)n64, (void*)i32, (void*)s32, (void*)r32})
             if (p) (void)hipFree(p);
         return set_error(e == hipErrorOutOfMemory ? VDB_ERR_OOM : VDB_ERR_HIP,
                          "growing the index to %lld rows: %s failed: %s", (long long)cap, what, hipGetErrorString(e));
@@ -295,6 +300,8 @@ int ensure_capacity(vdb_index* ix, int64_t rows) {
     if (with_xq) {
         CAP_TRY(hipMalloc(&Xq, x_bytes / 2));
         CAP_TRY(hipMemsetAsync(Xq, 0, x_bytes / 2, ix->stream));
+        CAP_TRY(hipMalloc(&Xh, x_bytes / 4));
+        CAP_TRY(hipMemsetAsync(Xh, 0, x_bytes / 4, ix->stream));
     }
     CAP_TRY(hipMalloc(&n64, cap * sizeof(double)));
     CAP_TRY(hipMalloc(&i32, cap * sizeof(float)));
@@ -314,6 +321,8 @@ int ensure_capacity(vdb_index* ix, int64_t rows) {
         if (Xq && ix->Xq)
             CAP_TRY(hipMemcpyAsync(Xq, ix->Xq, (size_t)used_tiles * tile_floats * sizeof(float) / 2,
                                    hipMemcpyDeviceToDevice, ix->stream));
+        if (Xh && ix->Xh)
+            CAP_TRY(hipMemcpyAsync(Xh, ix->Xh, (size_t)ix->count * ix->Dp, hipMemcpyDeviceToDevice, ix->stream));
         CAP_TRY(hipMemcpyAsync(n64, ix->nrm64, ix->count * sizeof(double), hipMemcpyDeviceToDevice, ix->stream));
         CAP_TRY(hipMemcpyAsync(i32, ix->inv32, ix->count * sizeof(float), hipMemcpyDeviceToDevice, ix->stream));
         CAP_TRY(hipMemcpyAsync(s32, ix->sq32, ix->count * sizeof(float), hipMemcpyDeviceToDevice, ix->stream));
@@ -325,6 +334,7 @@ int ensure_capacity(vdb_index* ix, int64_t rows) {
         (void)hipFree(ix->X);
         if (ix->Xs) (void)hipFree(ix->Xs);
         if (ix->Xq) (void)hipFree(ix->Xq);
+        if (ix->Xh) (void)hipFree(ix->Xh);
         (void)hipFree(ix->nrm64);
         (void)hipFree(ix->inv32);
         (void)hipFree(ix->sq32);
@@ -333,6 +343,7 @@ int ensure_capacity(vdb_index* ix, int64_t rows) {
     ix->X = X;
     ix->Xs = Xs;
     ix->Xq = Xq;
+    ix->Xh = Xh;
     ix->nrm64 = n64;
     ix->inv32 = i32;
     ix->sq32 = s32;
@@ -347,14 +358,19 @@ int ensure_xq(vdb_index* ix) {
     if (ix->Xq || ix->cap_rows == 0) return VDB_OK;
     const size_t bytes = (size_t)(ix->cap_rows / 32) * ix->G * BLOCK_FLOATS * sizeof(float) / 2;
     float* Xq = nullptr;
+    int8_t* Xh = nullptr;
     hipError_t e = hipMalloc(&Xq, bytes);
+    if (e == hipSuccess) e = hipMalloc(&Xh, bytes / 2);
     if (e == hipSuccess) e = hipMemsetAsync(Xq, 0, bytes, ix->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(Xh, 0, bytes / 2, ix->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(ix->stream);
     if (e != hipSuccess) {
         if (Xq) (void)hipFree(Xq);
+        if (Xh) (void)hipFree(Xh);
         return set_error(e == hipErrorOutOfMemory ? VDB_ERR_OOM : VDB_ERR_HIP, "int8 copy: %s", hipGetErrorString(e));
     }
     ix->Xq = Xq;
+    ix->Xh = Xh;
     return VDB_OK;
 }
 
@@ -634,6 +650,7 @@ int32_t vdb_index_destroy(vdb_index* ix) {
     if (ix->X) (void)hipFree(ix->X);
     if (ix->Xs) (void)hipFree(ix->Xs);
     if (ix->Xq) (void)hipFree(ix->Xq);
+    if (ix->Xh) (void)hipFree(ix->Xh);
     if (ix->nrm64) (void)hipFree(ix->nrm64);
     if (ix->inv32) (void)hipFree(ix->inv32);
     if (ix->sq32) (void)hipFree(ix->sq32);
@@ -759,6 +776,9 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
         ix->scan_publish = value;
     } else if (n == "pilot_fused") {
         ix->pilot_fused = value != 0;
+    } else if (n == "i8_refine") {
+        if (value < 0 || value > 1) return set_error(VDB_ERR_INVALID, "i8_refine must be 0 or 1");
+        ix->no_refine = value == 0;
     } else if (n == "device_repass") {
         if (value < -1 || value > 1) return set_error(VDB_ERR_INVALID, "device_repass must be -1, 0 or 1");
         ix->device_repass = value;
@@ -823,7 +843,7 @@ int32_t vdb_index_get_stat(const vdb_index* cix, const char* name, int64_t* valu
     else if (n == "searches_i8x3") *value = ix->n_by_prec[PREC_I8X3].load();
     else if (n == "auto_int8") *value = ix->auto_i8 ? 1 : 0;
     else if (n == "device_bytes")
-        *value = (int64_t)(ix->cap_rows / 32) * ix->G * BLOCK_FLOATS * (ix->Xq ? 10 : 8) + ix->cap_rows * 20;  // X, Xs (+ Xq)
+        *value = (int64_t)(ix->cap_rows / 32) * ix->G * BLOCK_FLOATS * (ix->Xq ? 11 : 8) + ix->cap_rows * 20;  // X, Xs (+ Xq, Xh)
     else return set_error(VDB_ERR_INVALID, "unknown stat '%s'", name);
     return VDB_OK;
 }
@@ -1339,6 +1359,8 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     bytes += (size_t)Bp * 4 + 256;                          // shared thresholds
     bytes += (size_t)Bp * (KP_MAX + PILOT_SLOTS) * 4 + 256;  // shared threshold slots + pilot slots
     bytes += (size_t)Bp * 12 + 1024;                          // int8 pass: qmax, lsl, qerr [Bp]; qscal
+    const bool i8_refine = prec == PREC_I8 && ix->Xh && !ix->no_refine;  // the finish's I8 refinement
+    bytes += i8_refine ? (size_t)Bp * (ix->Dp + 1) * 4 + 512 : 0;  // query residuals [Bp][Dp] + qerr2 [Bp]
     const int R_rep = std::min(B, kRepassDev);                // device re-pass: gathered queries + results
     bytes += mem == VDB_MEM_DEVICE ? (size_t)R_rep * (D * 4 + (size_t)k * 20) + 1024 : 0;
     bytes += ((size_t)(n_wg + 7) / 8 * 8 * n_qblocks + 64) * 4; // int8 pass: pacing counters
@@ -1412,6 +1434,8 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     float* q8lsl = c.take<float>(Bp);
     float* q8err = c.take<float>(Bp);
     float* q8scal = c.take<float>(64);
+    float* q8res = i8_refine ? c.take<float>((size_t)Bp * ix->Dp) : nullptr;
+    float* q8err2 = i8_refine ? c.take<float>(Bp) : nullptr;
     uint32_t* pace = c.take<uint32_t>((size_t)(n_wg + 7) / 8 * 8 * n_qblocks + 64);
     float* rep_q = mem == VDB_MEM_DEVICE ? c.take<float>((size_t)R_rep * D) : nullptr;
     float* rep_s = mem == VDB_MEM_DEVICE ? c.take<float>((size_t)R_rep * k) : nullptr;
@@ -1449,7 +1473,8 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
             c8.zmax_h = ix->i8st[4];
             c8.xl_max = ix->i8st[5];
             c8.rmax_half = 0.5 * ix->xmax * ix->xmax;
-            HIP_TRY(launch_prep8(Qd, qn64, q8max, B, Bp, D, Gs, ix->metric, prec, c8, Qt, q8lsl, q8err, q8scal, st));
+            HIP_TRY(launch_prep8(Qd, qn64, q8max, B, Bp, D, Gs, ix->metric, prec, c8, Qt, q8lsl, q8err, q8scal, st,
+                                 q8res, q8err2));
         }
         int n_flag = 0;
         if (!exact_all) {
@@ -1538,6 +1563,14 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
                 fa.dres = 1.01 * ix->i8st[prec == PREC_I8 ? 1 : 3];
                 fa.qerr = q8err;
                 fa.mu = ix->d_mu;
+                if (i8_refine) {
+                    fa.xh_rm = ix->Xh;
+                    fa.qres = q8res;
+                    fa.qerr2 = q8err2;
+                    fa.qscal = q8scal;
+                    fa.sx = ix->sx;
+                    fa.Dp = ix->Dp;
+                }
             }
             fa.out_s = out_s; fa.out_i = out_i; fa.out_k = out_k; fa.index_offset = index_offset;
             fa.row_ids = row_ids;

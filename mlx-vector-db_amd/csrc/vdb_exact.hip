@@ -165,8 +165,12 @@ __device__ __forceinline__ void exact_keys_rows(const float* __restrict__ q, int
     }
 }
 
+// waves of the finish's one workgroup per query (1024 threads: 128 VGPRs each)
+#ifndef VDB_FIN_WAVES
+#define VDB_FIN_WAVES 16
+#endif
 constexpr int FIN_MP = 4;   // fast path: D <= 1024
-constexpr int FIN_NB4 = 3;  // rows per wave per batch on the fast path (4 spills at 128 VGPRs)
+constexpr int FIN_NB4 = VDB_FIN_WAVES > 8 ? 3 : 6;  // rows per wave per batch on the fast path (4 spills at 128 VGPRs)
 // D <= 2048 (C3: 1536): 1 row per wave per batch, all 8 of its pieces in flight (8 KiB
 // of row pieces in flight per wave; the loop form below keeps one 1 KiB piece per row in flight
 // and ran C3's exact keys at 150 us for 256 candidates x 256 queries, profiles/r04 fin stamps)
@@ -266,7 +270,7 @@ hipError_t launch_rerank(int metric, int KP, const RerankArgs& a, int B, hipStre
 // several threads per candidate.  A list longer than FIN_CAP goes to the exact scan.
 constexpr int FIN_CAP = 16384;  // 128 KiB of (key, row) in LDS
 constexpr int FIN_NB = 2;        // candidates per wave per batch
-constexpr int FIN_WAVES = 16;
+constexpr int FIN_WAVES = VDB_FIN_WAVES;
 
 #ifdef VDB_STAMP
 // Diagnostic build only: per-query phase timestamps of finish_kernel + list length.
@@ -625,6 +629,104 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
         s_cut = (ok || defer) && have_k ? ak - 2.001 * eps : -INFINITY;
     }
     __syncthreads();
+    // ---- the I8 refinement: a' = a + f s_x xh.r per candidate (xh the row's 8-bit plane, r the
+    // query's rounding residual), then the rerank cut on a' with eps' = eps without the query's
+    // rounding term (prep8 qerr2) plus the refinement's own fp32 rounding per row.  The pass's
+    // wide 8-bit-query bound left every one of KP = 256 candidates within 2 eps of a_k at C2 /
+    // C3 (finish stamps, profiles/r04): each then cost a whole fp32 row of exact key.
+    __shared__ float s_ca[KP];
+    __shared__ uint32_t s_cbmax;
+    __shared__ float s_ak2;
+    const bool refine = a.xh_rm != nullptr && s_cut > -INFINITY;
+    if (refine) {
+        if (tid == 0) s_cbmax = 0u;
+        __syncthreads();
+        constexpr int NBR = 4;  // candidates per wave per batch (their row loads in flight together)
+        const float* rq = a.qres + (size_t)b * a.Dp;
+        const float fsx = (METRIC == 0 ? 1.0f : 2.0f) * a.sx;
+        const float qmx = 127.0f * a.qscal[0] / a.sx;  // s_q * 127 = max |q'|
+        for (int j0 = wv * NBR; j0 < m; j0 += FIN_WAVES * NBR) {
+            float sum[NBR], sab[NBR], sxh[NBR];
+#pragma unroll
+            for (int u = 0; u < NBR; ++u) sum[u] = sab[u] = sxh[u] = 0.0f;
+            for (int off = 16 * lane; off < a.Dp; off += 1024) {
+                f32x4 xv[NBR];
+#pragma unroll
+                for (int u = 0; u < NBR; ++u)
+                    xv[u] = j0 + u < m ? *(const f32x4*)(a.xh_rm + (size_t)s_cr[j0 + u] * a.Dp + off)
+                                       : f32x4{0.f, 0.f, 0.f, 0.f};
+                f32x4 rv[4];
+#pragma unroll
+                for (int w4 = 0; w4 < 4; ++w4) rv[w4] = *(const f32x4*)(rq + off + 4 * w4);
+#pragma unroll
+                for (int u = 0; u < NBR; ++u)
+#pragma unroll
+                    for (int w4 = 0; w4 < 4; ++w4) {
+                        const uint32_t word = __float_as_uint(xv[u][w4]);
+#pragma unroll
+                        for (int bt = 0; bt < 4; ++bt) {
+                            const float xh = (float)(int8_t)((word >> (8 * bt)) & 255u);
+                            const float pr = xh * rv[w4][bt];
+                            sum[u] += pr;
+                            sab[u] += fabsf(pr);
+                            sxh[u] += fabsf(xh);
+                        }
+                    }
+            }
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1)
+#pragma unroll
+                for (int u = 0; u < NBR; ++u) {
+                    sum[u] += __shfl_xor(sum[u], off, 64);
+                    sab[u] += __shfl_xor(sab[u], off, 64);
+                    sxh[u] += __shfl_xor(sxh[u], off, 64);
+                }
+            if (lane == 0) {
+#pragma unroll
+                for (int u = 0; u < NBR; ++u) {
+                    const int j = j0 + u;
+                    if (j < m) {
+                        const float ap = key_to_float(s_ck[j]) + fsx * sum[u];
+                        s_ca[j] = ap;
+                        // fp32: the D products and sums (|xh r| summed), q' - s_q qh (<= 2 ulp of
+                        // |q'| per element), f s_x times it, and the roundings of a' itself
+                        const float bd = fsx * (((float)a.Dp + 4.0f) * 5.97e-8f * sab[u] + 1.2e-7f * qmx * sxh[u]) +
+                                         2.4e-7f * fabsf(ap);
+                        atomicMax(&s_cbmax, __float_as_uint(bd * 1.01f));
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        // a'_k by rank counting over (a' desc, row asc), TPC threads per candidate
+        for (int jt = tid; jt < KP * TPC; jt += 64 * FIN_WAVES) {
+            const int j = jt / TPC, sub = jt % TPC;
+            int ar = 0;
+            float cj = 0.0f;
+            uint32_t r = 0u;
+            if (j < m) {
+                cj = s_ca[j];
+                r = s_cr[j];
+                for (int i = sub; i < m; i += TPC) {
+                    const float ci = s_ca[i];
+                    ar += (ci > cj || (ci == cj && s_cr[i] < r)) ? 1 : 0;
+                }
+            }
+#pragma unroll
+            for (int off = 1; off < TPC; off <<= 1) ar += __shfl_xor(ar, off, 64);
+            if (sub == 0 && j < m && ar == a.k - 1) s_ak2 = cj;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            const double ak2 = (double)s_ak2;
+            const double qe2 = a.qerr2 ? (double)a.qerr2[b] : 0.0;
+            const double e2 = (METRIC == 0 ? a.eps_rel + s_bq + qe2
+                                           : a.eps_rel * (2.0 * qn * a.xmax + a.xmax * a.xmax) + 2.0 * s_bq + qe2) +
+                              (double)__uint_as_float(s_cbmax);
+            s_cut = fmax(ak2 - 2.001 * e2, -3.0e38);  // never below the unrefined cut's domain
+        }
+        __syncthreads();
+    }
     if (s_cut > -INFINITY) {
         const double cut = s_cut;
         if (wv == 0) {
@@ -633,7 +735,7 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
                 const int e = e0 + lane;
                 const bool in = e < m;
                 const uint32_t kk = in ? s_ck[e] : 0u, rr = in ? s_cr[e] : 0u;
-                const bool keep = in && (double)key_to_float(kk) >= cut;
+                const bool keep = in && (refine ? (double)s_ca[e] : (double)key_to_float(kk)) >= cut;
                 const unsigned long long bm = __ballot(keep);
                 if (keep) {
                     const int pos = base + __popcll(bm & ((1ull << lane) - 1ull));

@@ -43,11 +43,11 @@ hipError_t launch_zmax(const float* X, const float* inv32, const float* mu, int6
 // order); stats[0..6) running maxima (fp64 bits): |z - s_x xh|, |dir.(z - s_x xh)|, |z - z~|,
 // |dir.(z - z~)|, |s_x xh|, |s_x xl / 256|
 hipError_t launch_quant_rows(const float* X, const float* inv32, const float* mu, const float* dir, float sx,
-                             int64_t row0, int64_t n, int G, float* Xq, unsigned long long* stats, hipStream_t st);
+                             int64_t row0, int64_t n, int G, float* Xq, unsigned long long* stats, hipStream_t st, int8_t* xh_rm = nullptr);
 // queries -> int8 tiles Qq (G8 + QG_EXTRA groups), per query lsl / qerr, per batch qscal[3]
 hipError_t launch_prep8(const float* Q, const double* qn64, const float* qmax, int B, int Bp, int D, int G8,
                         int metric, int prec, const Int8Consts& c, float* Qq, float* lsl, float* qerr, float* qscal,
-                        hipStream_t st);
+                        hipStream_t st, float* qres = nullptr, float* qerr2 = nullptr);
 hipError_t launch_pilot8(int prec, int metric, const float* Xq, const float* rinit, const uint32_t* mask,
                          const float* Qq, const float* qscal, int G8, int64_t N, int B, int n_qblocks, int QB,
                          int n_sample, uint32_t* pslots, hipStream_t st);
@@ -199,6 +199,15 @@ struct FinishArgs {
     int* overflow_count;  // lists longer than the finish kernel holds (they take the exact path)
     int* incons_count = nullptr;  // optional: queries flagged by the approx-vs-exact consistency guard
     const int* gate = nullptr;  // optional (device re-pass): only queries b < *gate are finished
+    // optional, the I8 pass: refine each candidate's approximate score with the query's rounding
+    // residual (a' = a + f s_x xh.r, f = 1 cosine / 2 L2) before the rerank cut, so only the
+    // corpus term is left of eps (qerr2 = the query's share without its rounding term)
+    const int8_t* xh_rm = nullptr;  // the xh plane row-major [rows][Dp]
+    const float* qres = nullptr;    // r = q' - s_q qh per query [Bp][Dp]
+    const float* qerr2 = nullptr;
+    const float* qscal = nullptr;   // [0] = s_x s_q
+    float sx = 0.0f;
+    int Dp = 0;
     const int64_t* row_ids = nullptr;  // global id per row (multi-device shard), else row + index_offset
     // split > 1: split workgroups per query share the exact rerank (rows by row % split); their
     // shares go to sx_* [B][split][KP] (+ counts sx_n [B][split]) and the last one (done[b],

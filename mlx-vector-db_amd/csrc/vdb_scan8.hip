@@ -70,7 +70,8 @@ __device__ __forceinline__ void split_i8(float t, int& hi, int& lo) {
 __global__ void __launch_bounds__(256) quant_rows_kernel(const float* __restrict__ X, const float* __restrict__ inv32,
                                                          const float* __restrict__ mu, const float* __restrict__ dir,
                                                          float sx, int64_t row0, int64_t n, int G,
-                                                         float* __restrict__ Xq, unsigned long long* __restrict__ stats) {
+                                                         float* __restrict__ Xq, unsigned long long* __restrict__ stats,
+                                                         int8_t* __restrict__ xh_rm) {
     const int lane = threadIdx.x & 63;
     const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (i >= n) return;
@@ -109,6 +110,8 @@ __global__ void __launch_bounds__(256) quant_rows_kernel(const float* __restrict
         float* dst = Xq + corpus_block(t, c >> 1, 0, G8) + (size_t)((r & 31) + 32 * (c & 1)) * 4;
         *(f32x4*)dst = pack_i8x16(hv);
         *(f32x4*)(dst + corpus_plane(G8)) = pack_i8x16(lv);
+        // the xh plane row-major too: the finish's refinement reads candidates' rows whole
+        if (xh_rm) *(f32x4*)(xh_rm + r * (size_t)(8 * G) + 16 * c) = pack_i8x16(hv);
     }
     s_r8 = wave_sum_butterfly(s_r8);
     s_d8 = wave_sum_butterfly(s_d8);
@@ -130,10 +133,11 @@ __global__ void __launch_bounds__(256) quant_rows_kernel(const float* __restrict
 }
 
 hipError_t launch_quant_rows(const float* X, const float* inv32, const float* mu, const float* dir, float sx,
-                             int64_t row0, int64_t n, int G, float* Xq, unsigned long long* stats, hipStream_t st) {
+                             int64_t row0, int64_t n, int G, float* Xq, unsigned long long* stats, hipStream_t st,
+                             int8_t* xh_rm) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(quant_rows_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, X, inv32, mu, dir, sx, row0,
-                       n, G, Xq, stats);
+                       n, G, Xq, stats, xh_rm);
     return hipGetLastError();
 }
 
@@ -147,7 +151,8 @@ __global__ void __launch_bounds__(256) prep8_kernel(const float* __restrict__ Q,
                                                     const float* __restrict__ qmax, int B, int Bp, int D, int G8,
                                                     int metric, int prec, Int8Consts c, float* __restrict__ Qq,
                                                     float* __restrict__ lsl, float* __restrict__ qerr,
-                                                    float* __restrict__ qscal) {
+                                                    float* __restrict__ qscal, float* __restrict__ qres,
+                                                    float* __restrict__ qerr2) {
     const int lane = threadIdx.x & 63;
     const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (b >= Bp) return;
@@ -193,6 +198,20 @@ __global__ void __launch_bounds__(256) prep8_kernel(const float* __restrict__ Q,
         float* dst = Qq + s2_blk((uint64_t)(b >> 5), g, GQ) + (size_t)((b & 31) + 32 * h) * 4;
         *(f32x4*)dst = pack_i8x16(hv);
         *(f32x4*)(dst + 4 * BLOCK_FLOATS) = pack_i8x16(lv);
+        if (qres && g < G8) {  // I8: the query's rounding residual r = q' - s_q qh, row-major [Bp][8 G8 * 4]
+            float* rd = qres + (size_t)b * (size_t)(32 * G8) + d0;
+#pragma unroll
+            for (int j4 = 0; j4 < 4; ++j4) {
+                f32x4 v;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int d = d0 + 4 * j4 + j;
+                    const float qv = (real && d < D) ? q[d] * scale : 0.0f;
+                    v[j] = qv - sq * (float)hv[4 * j4 + j];
+                }
+                *(f32x4*)(rd + 4 * j4) = v;
+            }
+        }
     }
     s_rq = wave_sum_butterfly(s_rq);
     s_r8 = wave_sum_butterfly(s_r8);
@@ -210,14 +229,17 @@ __global__ void __launch_bounds__(256) prep8_kernel(const float* __restrict__ Q,
         e = 1.01 * (metric == 0 ? e : 2.0 * e);
         lsl[b] = real ? (float)(1.01 * sl) * (1.0f + 1e-5f) + 1e-30f : 0.0f;
         qerr[b] = real ? (float)e * (1.0f + 1e-5f) : 0.0f;
+        // with the query rounding corrected per candidate (the finish's refinement, I8): only
+        // the L2 start value's rounding is left of the query's share
+        if (qerr2) qerr2[b] = real ? (float)(1.01 * (metric == 1 ? 2.0 * (double)uH : 0.0)) * (1.0f + 1e-5f) : 0.0f;
     }
 }
 
 hipError_t launch_prep8(const float* Q, const double* qn64, const float* qmax, int B, int Bp, int D, int G8,
                         int metric, int prec, const Int8Consts& c, float* Qq, float* lsl, float* qerr, float* qscal,
-                        hipStream_t st) {
+                        hipStream_t st, float* qres, float* qerr2) {
     hipLaunchKernelGGL(prep8_kernel, dim3((Bp + 3) / 4), dim3(256), 0, st, Q, qn64, qmax, B, Bp, D, G8, metric, prec, c,
-                       Qq, lsl, qerr, qscal);
+                       Qq, lsl, qerr, qscal, qres, qerr2);
     return hipGetLastError();
 }
 
