@@ -4,10 +4,10 @@ One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI).
 Rank g of G holds corpus rows [g*ceil(N/G), min((g+1)*ceil(N/G), N)) in its own
 device index; queries are replicated; each rank searches its shard for the
 per-shard top-k with GLOBAL row ids (index_offset) and the fp64 exact ranking
-keys, the lists are all-gathered ([G, B, k] keys f64 + ids i64, one collective
-each), and every rank merges them on device by (key desc, row asc)
-(vdb_merge_topk).  Because shard offsets preserve row order and the keys are the
-exact fp64 values, the merged result is bit-identical to a single-GPU search.
+keys, the lists are all-gathered (keys f64 + ids i64 packed as one [2, B, k] int64
+buffer: one collective), and every rank merges them on device by (key desc, row
+asc) (vdb_merge_topk).  Because shard offsets preserve row order and the keys are
+the exact fp64 values, the merged result is bit-identical to a single-GPU search.
 
 The reference is single-device (no distributed code); this is the
 MI355X-native scale-out of `optimized_batch_similarity_search`
@@ -65,14 +65,18 @@ class ShardedSearcher:
                                out_k.data_ptr() if out_k is not None else 0, stream)
 
     def _buffers(self, B: int, k: int, device):
-        # per stream: searches queued on several streams (bench.py --streams) each need their own
+        # per stream: searches queued on several streams (bench.py --streams) each need their own.
+        # The local keys (f64) and ids (i64) share one [2, B, k] int64 buffer, so ONE all-gather
+        # moves both ([G, 2, B, k]): the exchange is latency-bound on xGMI (C4: 819 KB per rank,
+        # c6 at 8 GPUs: 10 KB), so one collective instead of two halves its cost per batch.
         stream = torch.cuda.current_stream(device).cuda_stream if device.type == "cuda" else 0
         key = (B, k, str(device), stream)
         if key not in self._bufs:
             f = dict(device=device)
+            pack = torch.empty((2, B, k), dtype=torch.int64, **f)
             self._bufs[key] = (
-                torch.empty((B, k), dtype=torch.float32, **f), torch.empty((B, k), dtype=torch.int64, **f),
-                torch.empty((B, k), dtype=torch.float64, **f),
+                torch.empty((B, k), dtype=torch.float32, **f), pack,
+                torch.empty((self.world, 2, B, k), dtype=torch.int64, **f),
                 torch.empty((self.world, B, k), dtype=torch.float64, **f),
                 torch.empty((self.world, B, k), dtype=torch.int64, **f))
         return self._bufs[key]
@@ -81,7 +85,8 @@ class ShardedSearcher:
                out_keys: Optional[torch.Tensor] = None) -> None:
         """q [B, D] (replicated on every rank) -> global top-k in out_* (every rank)."""
         B = q.shape[0]
-        ls, li, lk, g_keys, g_idx = self._buffers(B, k, q.device)
+        ls, pack, gathered, g_keys, g_idx = self._buffers(B, k, q.device)
+        lk, li = pack[0].view(torch.float64), pack[1]  # contiguous [B, k] planes of the pack
         self.local_search(q, k, ls, li, lk, self.row_offset)
         if self.world == 1:
             out_scores.copy_(ls)
@@ -89,16 +94,15 @@ class ShardedSearcher:
             if out_keys is not None:
                 out_keys.copy_(lk)
             return
-        # [G*B, k] views: gloo wants the output split along dim 0 in input-shaped chunks
+        # [G*2B, k] view: the output split along dim 0 in input-shaped chunks
         if q.is_cuda and dist.get_backend(self.group) == "gloo":
             # gloo moves host memory only (tests run several ranks on one GPU this way; RCCL
             # takes the device buffers directly)
-            hk, hi = g_keys.cpu(), g_idx.cpu()
-            dist.all_gather_into_tensor(hk.view(self.world * B, k), lk.cpu(), group=self.group)
-            dist.all_gather_into_tensor(hi.view(self.world * B, k), li.cpu(), group=self.group)
-            g_keys.copy_(hk)
-            g_idx.copy_(hi)
+            hg = gathered.cpu()
+            dist.all_gather_into_tensor(hg.view(self.world * 2 * B, k), pack.cpu().view(2 * B, k), group=self.group)
+            gathered.copy_(hg)
         else:
-            dist.all_gather_into_tensor(g_keys.view(self.world * B, k), lk, group=self.group)
-            dist.all_gather_into_tensor(g_idx.view(self.world * B, k), li, group=self.group)
+            dist.all_gather_into_tensor(gathered.view(self.world * 2 * B, k), pack.view(2 * B, k), group=self.group)
+        g_keys.copy_(gathered[:, 0].view(torch.float64))
+        g_idx.copy_(gathered[:, 1])
         self.merge(g_keys, g_idx, k, out_scores, out_idx, out_keys)
