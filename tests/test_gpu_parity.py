@@ -282,9 +282,13 @@ def test_auto_precision_switches_on_fallbacks(vdb, mem, a8):
             assert ix.stat("fallback_queries") * 64 > B  # the x3 pass cannot separate these rows either
             if a8:
                 # the I8 failure holds BF16 (host: the batch is rerun in BF16X3 at once); the
-                # second search runs BF16, fails too and (host) reruns in BF16X3
+                # second search runs BF16, fails too and (host) reruns in BF16X3; (device) the
+                # first failure seen also arms the device re-pass, so the second search re-passes
+                # 16 of its uncertified queries in a BF16X3 sub-search (the rest: the exact path)
                 assert ix.stat("searches_bf16") == 1
-                assert ix.stat(x3) == (2 if mem == "host" else 0)
+                assert ix.stat(x3) == (2 if mem == "host" else 1)
+                if mem == "device":
+                    assert ix.stat("repass_queries") == 16, ix.stat("repass_queries")
             else:
                 # host memory: the uncertified one-plane pass is rerun at once in x3, then the second
                 # search runs x3; device memory: the first search falls back, the second runs x3
@@ -856,18 +860,30 @@ def test_i8_store_filled_one_add_at_a_time(vdb, metric):
     assert ix.stat("fallback_queries") <= 2, ix.stat("fallback_queries")
 
 
+def _graded_neighbours(rng, x, n, lo=1e-3, hi=4e-3):
+    """n rows around x whose cosine to x falls evenly in [1 - hi, 1 - lo] (L2: squared distance
+    2 c |x|^2): closer together than the int8 pass can separate (its eps ~4e-3), far enough
+    apart for BF16X3 (eps ~1e-4)."""
+    c = np.linspace(lo, hi, n)
+    u = rng.standard_normal((n, x.size))
+    xd = x.astype(np.float64)
+    u -= np.outer(u @ xd / (xd @ xd), xd)
+    u *= np.linalg.norm(xd) / np.linalg.norm(u, axis=1, keepdims=True)
+    return (xd + np.sqrt(2.0 * c)[:, None] * u).astype(np.float32)
+
+
 @pytest.mark.parametrize("metric", ["cosine", "euclidean"])
 def test_device_repass_of_uncertified_queries(vdb, metric):
     """in a device-memory search (the bench's and a GPU-resident server's path)
     the few queries auto's int8 pass leaves uncertified are gathered ON THE DEVICE into a gated
     BF16X3 sub-search on the same stream (device_repass 1) -- no exact scan, no host wait.  A
-    batch of 64 with one near-duplicate query (300 rows within ~1e-3 of it) searched three times
+    batch of 64 with one query that has 300 close rows (cosine 1 - [1e-3, 4e-3]) searched three times
     back to back: every result exact, no fallback, one re-passed query per batch."""
     import torch
     rng = np.random.default_rng(47)
     N, D, B, k = 40000, 128, 64, 10
     V = rng.random((N, D), dtype=np.float32)
-    V[1000:1300] = V[11] + 1e-3 * rng.standard_normal((300, D)).astype(np.float32)
+    V[1000:1300] = _graded_neighbours(rng, V[11], 300)
     Q = rng.random((B, D), dtype=np.float32)
     Q[5] = V[11]
     ix = vdb.NativeIndex(D, metric)  # auto: the I8 pass for k <= 16
@@ -914,8 +930,8 @@ def test_device_repass_more_flagged_than_gathered(vdb):
     N, D, B, k = 30000, 96, 40, 10
     V = rng.random((N, D), dtype=np.float32)
     Q = rng.random((B, D), dtype=np.float32)
-    for j in range(20):  # 20 queries, each with 300 near-duplicate rows
-        V[1000 + 300 * j:1300 + 300 * j] = V[j] + 1e-3 * rng.standard_normal((300, D)).astype(np.float32)
+    for j in range(20):  # 20 queries, each with 300 graded close rows
+        V[1000 + 300 * j:1300 + 300 * j] = _graded_neighbours(rng, V[j], 300)
         Q[2 * j] = V[j]
     ix = vdb.NativeIndex(D, "cosine")
     ix.set_param("device_repass", 1)
