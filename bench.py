@@ -422,6 +422,8 @@ def main():
     ap.add_argument("--k", type=int, default=None, help="tuning: the config at another k (not the config's line)")
     ap.add_argument("--finish-split", type=int, default=None, help="workgroups per query in the finish (tuning)")
     ap.add_argument("--i8-refine", type=int, default=None, help="0: the finish's I8 refinement off (tuning)")
+    ap.add_argument("--plant-close", type=int, default=None,
+                    help="one GPU: P queries per batch with 300 rows the int8 pass cannot separate (re-pass test)")
     ap.add_argument("--device-repass", type=int, default=None,
                     help="device re-pass of uncertified queries: -1 auto (armed after a fallback), 0 off, 1 always")
     ap.add_argument("--scan-pace", type=int, default=None, help="int8 pass: 1 pace the query blocks of a row range, "
@@ -538,14 +540,30 @@ def bench_brute(cfg, args, world, rank, local, dev, primary=True):
         ix.set_param("no_fallback", 1)
     ix.reserve(n_local)
     host_parts = []
+    # --plant-close P (one GPU): P query targets, each with 300 rows closer to it than the int8
+    # pass can separate (cosine 1 - [1e-3, 4e-3]): those queries come back uncertified from the
+    # candidate pass -- the device re-pass's case, measured against the plain line
+    plant = int(args.plant_close or 0) if world == 1 else 0
+    targets = [7 + 4001 * j for j in range(plant)]
     for s in range(lo, hi, 8 * CHUNK_ROWS):
         part = corpus_rows(N, D, s, min(s + 8 * CHUNK_ROWS, hi))
+        if plant and s == lo:
+            prng = np.random.default_rng(99)
+            for j, t in enumerate(targets):
+                x = part[t].astype(np.float64)
+                c = np.linspace(1e-3, 4e-3, 300)
+                u = prng.standard_normal((300, D))
+                u -= np.outer(u @ x / (x @ x), x)
+                u *= np.linalg.norm(x) / np.linalg.norm(u, axis=1, keepdims=True)
+                part[t + 1:t + 301] = (x + np.sqrt(2.0 * c)[:, None] * u).astype(np.float32)
         ix.add(part)
         if keep_host:
             host_parts.append(part)
     assert ix.count() == n_local
     Bg = B * world if (world > 1 and scaling == "weak") else B  # global batch
     Q = np.random.default_rng(1).random((Bg, D), dtype=np.float32)  # large_scale_benchmark.py:61
+    for j, t in enumerate(targets):
+        Q[(j * Bg) // max(plant, 1)] = host_parts[0][t] if keep_host else corpus_rows(N, D, t, t + 1)[0]
     q_dev = torch.from_numpy(Q).to(dev)
     n_str = max(1, args.streams)
     outs = [(torch.empty((Bg, k), dtype=torch.float32, device=dev), torch.empty((Bg, k), dtype=torch.int64, device=dev))

@@ -1148,6 +1148,7 @@ struct SearchOpts {
     // device re-pass: the sub-search's query count lives on the device (B is its capacity);
     // its candidate pass and finish are gated on it, and it runs without a pilot
     const int* gate = nullptr;
+    bool force_i8x3 = false;  // the re-pass in I8X3 (the int8 copy's two planes: half BF16X3's bytes)
 };
 
 static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int32_t k, const uint32_t* row_mask,
@@ -1247,7 +1248,9 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     const bool hold8 = auto_prec && ix->auto_i8 && approx && (x3_i8 || !auto_x3) && auto_take_hold8(ix);
     const bool auto_8 = auto_prec && !auto_x3 && ix->auto_i8 && !hold8;
     const bool auto_8x3 = x3_i8 && !hold8;
+    const bool force_8x3 = auto_prec && opt.force_i8x3 && ix->auto_i8 && ix->Xq;
     const int prec_req = !ix->Xs ? PREC_FP32
+                         : force_8x3 ? PREC_I8X3
                          : ix->precision == VDB_PREC_BF16X3 ? PREC_BF16X3
                          : ix->precision == VDB_PREC_BF16 ? PREC_BF16
                          : ix->precision == VDB_PREC_I8X3 ? PREC_I8X3
@@ -1255,7 +1258,8 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
                          : auto_prec ? (auto_x3 ? (auto_8x3 ? PREC_I8X3 : PREC_BF16X3) : auto_8 ? PREC_I8 : PREC_BF16)
                                      : PREC_FP32;
     if (auto_prec && approx && (!auto_x3 || x3_i8)) ix->last_i8 = auto_8 || auto_8x3;
-    if (approx) ix->n_by_prec[prec_req]++;
+    // (a device re-pass's gated sub-search is counted by the device: repass_queries)
+    if (approx && !opt.gate) ix->n_by_prec[prec_req]++;
     // the "one plane" precisions (a wide certificate: KP = 128 for small k) and their re-pass
     const bool one_plane = prec_req == PREC_BF16 || prec_req == PREC_I8;
 
@@ -1268,6 +1272,11 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     // I8 (the 8-bit query's wider bound): KP = 256.  1M x 768 uniform, B = 64: KP = 128 left one
     // query per batch uncertified; 256 none (profiles/r03_i8/c2_i8_kp*)
     if (prec_req == PREC_I8) margin_def = std::max(16, 256 - k);
+    // a re-pass sub-search (host or device) takes KP = 128: its few queries are the ones whose
+    // rows sit closer together than the one-plane pass could separate, so they need the wider
+    // gap between the k-th and the KP-th candidate (C2 with 300 rows in a 3e-3 cosine band:
+    // BF16X3 at KP = 32 left every such query to the exact scan)
+    if (opt.repass) margin_def = std::max(margin_def, 128 - k);
     const int margin = ix->margin >= 0 ? (int)ix->margin : margin_def;
     int KP = std::max(32, next_pow2(k + margin));
     const bool exact_all = ix->force_exact || k > kMaxApproxK || KP > 256;
@@ -1284,8 +1293,9 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
                     (ix->scan_q4 == 1 || (ix->scan_q4 < 0));
     // The int8 pass's 128-query shape (vdb_scan8_kernel.h S8_ONE4): the same rule for short rows
     // (D <= 128), KP = 128, batches of >= 256 (C4: I8X3, 8 -> 4 query blocks per row range)
+    // Opt-in (scan_q4 = 1): C4 ran 2.91 -> 3.08 ms with it (profiles/r04_q48, same box).
     const bool q4_8 = i8_pass && !exact_all && !opt.gate && KP == 128 && B >= 256 && scan8_q4_ok(Gs, prec) &&
-                      (ix->scan_q4 == 1 || (ix->scan_q4 < 0));
+                      ix->scan_q4 == 1;
     // query rows per candidate-pass block: the int8 pass keeps 64 at KP = 256 (KW = 64 kept per
     // workgroup, vdb_scan8_kernel.h), the split pass 32 there
     const int QB = q4 ? 128 : i8_pass ? scan8_qb(KP, q4_8) : KP == 256 ? 32 : 64;
@@ -1478,7 +1488,7 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
         }
         int n_flag = 0;
         if (!exact_all) {
-            const bool timed = ix->timing != 0;
+            const bool timed = ix->timing != 0 && !opt.gate;  // a gated sub-search may not run at all
             hipEvent_t* tev = nullptr;
             if (timed) {
                 if (w->t_pending == Workspace::kTRing) {  // ring full: read the oldest set
@@ -1604,7 +1614,8 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
                 // the rest, if any, take the gated exact path.  Like the host re-pass (repass_flagged)
                 // for auto's one-plane / I8X3 passes, with the split copy kept beside the int8 one.
                 const bool can_rep = !opt.repass && auto_prec && (one_plane || prec == PREC_I8X3) && ix->Xs &&
-                                     xs_kind(VDB_PREC_BF16X3) == xs_kind(ix->precision) && rep_q;
+                                     xs_kind(VDB_PREC_BF16X3) == xs_kind(ix->precision) && rep_q &&
+                                     k <= kMaxApproxK;
                 bool rep = can_rep && ix->device_repass == 1;
                 if (can_rep && ix->device_repass < 0) {
                     int a = ix->repass_arm.load();
@@ -1616,6 +1627,7 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
                     HIP_TRY(launch_repass_gather(Qd, D, flags, R_rep, rep_q, counts, ix->d_totals + 3, st));
                     SearchOpts o;
                     o.force_b3 = true;
+                    o.force_i8x3 = true;  // (I8X3 where the int8 copy is kept, else BF16X3)
                     o.repass = true;
                     o.gate = counts;
                     rc = search_locked(ix, rep_q, R_rep, k, md, VDB_MEM_DEVICE, rep_s, rep_i, rep_k, index_offset, st,

@@ -166,8 +166,11 @@ __device__ __forceinline__ void exact_keys_rows(const float* __restrict__ q, int
 }
 
 // waves of the finish's one workgroup per query (1024 threads: 128 VGPRs each)
+// 8 (512 threads, up to 256 VGPRs: no spills) measured faster than 16 (1024 threads, 128 VGPRs)
+// under the bench's 3 streams: C2 0.188 -> 0.175 ms per batch (profiles/r04_fw8) -- its waves fit
+// beside a scan wave on a SIMD (a 128-VGPR x 4-wave-per-SIMD workgroup cannot), C3 equal
 #ifndef VDB_FIN_WAVES
-#define VDB_FIN_WAVES 16
+#define VDB_FIN_WAVES 8
 #endif
 constexpr int FIN_MP = 4;   // fast path: D <= 1024
 constexpr int FIN_NB4 = VDB_FIN_WAVES > 8 ? 3 : 6;  // rows per wave per batch on the fast path (4 spills at 128 VGPRs)
@@ -641,14 +644,35 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
     if (refine) {
         if (tid == 0) s_cbmax = 0u;
         __syncthreads();
-        constexpr int NBR = 4;  // candidates per wave per batch (their row loads in flight together)
+        constexpr int NBR = FIN_WAVES > 8 ? 4 : 8;  // candidates per wave per batch (row loads in flight together)
         const float* rq = a.qres + (size_t)b * a.Dp;
         const float fsx = (METRIC == 0 ? 1.0f : 2.0f) * a.sx;
         const float qmx = 127.0f * a.qscal[0] / a.sx;  // s_q * 127 = max |q'|
-        for (int j0 = wv * NBR; j0 < m; j0 += FIN_WAVES * NBR) {
-            float sum[NBR], sab[NBR], sxh[NBR];
+        // the rows are stored as u = xh + 128: xh.r = u.r - 128 sum(r); sum(r) and sum|r| once
+        float rsum = 0.0f, rabs = 0.0f;
+        for (int off = 16 * lane; off < a.Dp; off += 1024)
 #pragma unroll
-            for (int u = 0; u < NBR; ++u) sum[u] = sab[u] = sxh[u] = 0.0f;
+            for (int w4 = 0; w4 < 4; ++w4) {
+                const f32x4 rv = *(const f32x4*)(rq + off + 4 * w4);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    rsum += rv[e];
+                    rabs += fabsf(rv[e]);
+                }
+            }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            rsum += __shfl_xor(rsum, off, 64);
+            rabs += __shfl_xor(rabs, off, 64);
+        }
+        // fp32 bound of the correction, per query: the D biased products and their sum (|u r|
+        // <= 256 |r|), the subtraction of 128 sum(r), r = q' - s_q qh itself (<= 2 ulp of |q'|
+        // per element), times f s_x; plus (per row) the roundings of a'
+        const float bq2 = fsx * (((float)a.Dp + 8.0f) * 5.97e-8f * 256.0f * rabs + 1.2e-7f * qmx * 127.0f * (float)a.D);
+        for (int j0 = wv * NBR; j0 < m; j0 += FIN_WAVES * NBR) {
+            float sum[NBR];
+#pragma unroll
+            for (int u = 0; u < NBR; ++u) sum[u] = 0.0f;
             for (int off = 16 * lane; off < a.Dp; off += 1024) {
                 f32x4 xv[NBR];
 #pragma unroll
@@ -664,37 +688,26 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
                     for (int w4 = 0; w4 < 4; ++w4) {
                         const uint32_t word = __float_as_uint(xv[u][w4]);
 #pragma unroll
-                        for (int bt = 0; bt < 4; ++bt) {
-                            const float xh = (float)(int8_t)((word >> (8 * bt)) & 255u);
-                            const float pr = xh * rv[w4][bt];
-                            sum[u] += pr;
-                            sab[u] += fabsf(pr);
-                            sxh[u] += fabsf(xh);
-                        }
+                        for (int bt = 0; bt < 4; ++bt)
+                            sum[u] = fmaf((float)((word >> (8 * bt)) & 255u), rv[w4][bt], sum[u]);
                     }
             }
 #pragma unroll
             for (int off = 32; off >= 1; off >>= 1)
 #pragma unroll
-                for (int u = 0; u < NBR; ++u) {
-                    sum[u] += __shfl_xor(sum[u], off, 64);
-                    sab[u] += __shfl_xor(sab[u], off, 64);
-                    sxh[u] += __shfl_xor(sxh[u], off, 64);
-                }
+                for (int u = 0; u < NBR; ++u) sum[u] += __shfl_xor(sum[u], off, 64);
             if (lane == 0) {
+                float bmax = 0.0f;
 #pragma unroll
                 for (int u = 0; u < NBR; ++u) {
                     const int j = j0 + u;
                     if (j < m) {
-                        const float ap = key_to_float(s_ck[j]) + fsx * sum[u];
+                        const float ap = key_to_float(s_ck[j]) + fsx * (sum[u] - 128.0f * rsum);
                         s_ca[j] = ap;
-                        // fp32: the D products and sums (|xh r| summed), q' - s_q qh (<= 2 ulp of
-                        // |q'| per element), f s_x times it, and the roundings of a' itself
-                        const float bd = fsx * (((float)a.Dp + 4.0f) * 5.97e-8f * sab[u] + 1.2e-7f * qmx * sxh[u]) +
-                                         2.4e-7f * fabsf(ap);
-                        atomicMax(&s_cbmax, __float_as_uint(bd * 1.01f));
+                        bmax = fmaxf(bmax, 2.4e-7f * fabsf(ap));
                     }
                 }
+                atomicMax(&s_cbmax, __float_as_uint((bq2 + bmax) * 1.01f));
             }
         }
         __syncthreads();

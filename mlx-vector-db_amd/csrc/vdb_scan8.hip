@@ -110,8 +110,13 @@ __global__ void __launch_bounds__(256) quant_rows_kernel(const float* __restrict
         float* dst = Xq + corpus_block(t, c >> 1, 0, G8) + (size_t)((r & 31) + 32 * (c & 1)) * 4;
         *(f32x4*)dst = pack_i8x16(hv);
         *(f32x4*)(dst + corpus_plane(G8)) = pack_i8x16(lv);
-        // the xh plane row-major too: the finish's refinement reads candidates' rows whole
-        if (xh_rm) *(f32x4*)(xh_rm + r * (size_t)(8 * G) + 16 * c) = pack_i8x16(hv);
+        // the xh plane row-major too (as xh + 128): the finish's refinement reads candidates' rows whole
+        if (xh_rm) {  // biased to unsigned (xh + 128): one v_cvt_f32_ubyte per element in the finish
+            int uv[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) uv[j] = hv[j] + 128;
+            *(f32x4*)(xh_rm + r * (size_t)(8 * G) + 16 * c) = pack_i8x16(uv);
+        }
     }
     s_r8 = wave_sum_butterfly(s_r8);
     s_d8 = wave_sum_butterfly(s_d8);

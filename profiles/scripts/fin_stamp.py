@@ -16,6 +16,8 @@ cfg = sys.argv[1] if len(sys.argv) > 1 else "c2"
 prec = sys.argv[2] if len(sys.argv) > 2 else "bf16x3"
 N, D, B, k, metric, _ = bench.CONFIGS[cfg]
 ix = _vdb.NativeIndex(D, metric, precision=prec)
+if os.environ.get("VDB_FIN_REFINE") is not None:
+    ix.set_param("i8_refine", int(os.environ["VDB_FIN_REFINE"]))
 ix.reserve(N)
 for s in range(0, N, 1 << 19):
     ix.add(bench.corpus_rows(N, D, s, min(s + (1 << 19), N)))

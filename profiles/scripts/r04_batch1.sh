@@ -12,4 +12,5 @@ bash profiles/scripts/r04_ab.sh r04_two "c6 c2" "base two" || exit 1
 bash profiles/scripts/r04_knob.sh r04_refine "c2 c6 c3" --i8-refine "0 1" || exit 1
 bash profiles/scripts/r04_ab.sh r04_fw8 "c2 c3" "base fw8" || exit 1
 bash profiles/scripts/r04_knob.sh r04_rep "c2" --device-repass "0 1" || exit 1
-bash profiles/scripts/r04_knob.sh r04_q48 "c4" --scan-q4 "0 -1"
+bash profiles/scripts/r04_knob.sh r04_q48 "c4" --scan-q4 "0 -1" || exit 1
+bash profiles/scripts/r04_knob.sh r04_plant "c2" --device-repass "0 1" "--plant-close 1"

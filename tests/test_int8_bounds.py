@@ -155,11 +155,12 @@ def test_i8_refinement_bound_holds(metric):
         exact = np.empty_like(approx)
         for b in range(Q.shape[0]):
             exact[ei[b], b] = ek[b]
-        # eps' = eps without the query's rounding share (its CS term), plus the fp32 rounding term
-        sab = np.abs(xh).astype(np.float64) @ np.abs(r).T.astype(np.float64)
-        sxh = np.abs(xh).sum(1)[:, None]
+        # eps' = eps without the query's rounding share (its CS term), plus the refinement's fp32
+        # rounding as the kernel bounds it (per query, rows stored as xh + 128; + 2.4e-7 |a'| per row)
         qmx = 127.0 * float(sq)
-        rnd = fs * float(sx) * ((D + 4) * 5.97e-8 * sab + 1.2e-7 * qmx * sxh) + 2.4e-7 * np.abs(refined)
+        Dp = (D + 63) // 64 * 64
+        rabs = np.abs(r).sum(1)[None, :]
+        rnd = fs * float(sx) * ((Dp + 8) * 5.97e-8 * 256.0 * rabs + 1.2e-7 * qmx * 127.0 * D) + 2.4e-7 * np.abs(refined)
         uH = float(sx) * float(sq)
         qerr2 = 1.01 * (2.0 * uH if metric == "euclidean" else 0.0)
         # the corpus share of eps: eps minus the model's qerr (recomputed: |z~|max |q' - q~|)
