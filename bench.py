@@ -421,7 +421,7 @@ def main():
     ap.add_argument("--pilot-rank", type=int, default=None, help="rank of the pilot bound (tuning; default: Poisson rule)")
     ap.add_argument("--k", type=int, default=None, help="tuning: the config at another k (not the config's line)")
     ap.add_argument("--finish-split", type=int, default=None, help="workgroups per query in the finish (tuning)")
-    ap.add_argument("--i8-refine", type=int, default=None, help="0: the finish's I8 refinement off (tuning)")
+    ap.add_argument("--i8-refine", type=int, default=None, help="finish's I8 refinement: -1 auto (rows >= 512 dims), 0 off, 1 on (tuning)")
     ap.add_argument("--plant-close", type=int, default=None,
                     help="one GPU: P queries per batch with 300 rows the int8 pass cannot separate (re-pass test)")
     ap.add_argument("--device-repass", type=int, default=None,

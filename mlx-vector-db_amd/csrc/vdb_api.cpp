@@ -185,7 +185,9 @@ struct vdb_index {
     // 8 blocks within 5 steps (from 26) and ran the scan at 4.99 ms against 2.90 without
     // (the range at its slowest block's speed, the prefetch drained per sleep; profiles/r03_i8/pace)
     bool scan_pace = false;
-    bool no_refine = false;  // A/B knob "i8_refine" = 0: the finish's I8 refinement off
+    // the finish's I8 refinement (i8_refine): -1 auto = rows of kRefineMinDp dims or more (C3 +6%,
+    // C2 neutral, C6 -1%: shorter rows rerank cheaply; profiles/r04_mx1); 0 off; 1 on
+    int i8_refine = -1;
     // device-memory searches: uncertified queries of an I8 / BF16 / I8X3 pass re-passed in BF16X3
     // on the device (gated kernels, no host wait) instead of the fp64 exact scan.  -1 auto: armed
     // for kRepassArm searches once a device fallback has been seen; 0 off; 1 always
@@ -777,8 +779,8 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
     } else if (n == "pilot_fused") {
         ix->pilot_fused = value != 0;
     } else if (n == "i8_refine") {
-        if (value < 0 || value > 1) return set_error(VDB_ERR_INVALID, "i8_refine must be 0 or 1");
-        ix->no_refine = value == 0;
+        if (value < -1 || value > 1) return set_error(VDB_ERR_INVALID, "i8_refine must be -1, 0 or 1");
+        ix->i8_refine = (int)value;
     } else if (n == "device_repass") {
         if (value < -1 || value > 1) return set_error(VDB_ERR_INVALID, "device_repass must be -1, 0 or 1");
         ix->device_repass = value;
@@ -1095,6 +1097,8 @@ constexpr int kRepassMax = 64;
 // the re-pass for kRepassArm searches after a device fallback was seen.
 constexpr int kRepassDev = 16;
 constexpr int kRepassArm = 256;
+// i8_refine auto: the finish refines I8 candidates' scores for padded rows of this many dims or more
+constexpr int64_t kRefineMinDp = 512;
 // VDB_PREC_AUTO uses the bf16 pass up to this k (its KP = next_pow2(k + 112) stays 128)
 constexpr int kAutoBf16MaxK = 16;
 
@@ -1369,7 +1373,8 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     bytes += (size_t)Bp * 4 + 256;                          // shared thresholds
     bytes += (size_t)Bp * (KP_MAX + PILOT_SLOTS) * 4 + 256;  // shared threshold slots + pilot slots
     bytes += (size_t)Bp * 12 + 1024;                          // int8 pass: qmax, lsl, qerr [Bp]; qscal
-    const bool i8_refine = prec == PREC_I8 && ix->Xh && !ix->no_refine;  // the finish's I8 refinement
+    const bool i8_refine = prec == PREC_I8 && ix->Xh &&  // the finish's I8 refinement
+                           (ix->i8_refine == 1 || (ix->i8_refine == -1 && ix->Dp >= kRefineMinDp));
     bytes += i8_refine ? (size_t)Bp * (ix->Dp + 1) * 4 + 512 : 0;  // query residuals [Bp][Dp] + qerr2 [Bp]
     const int R_rep = std::min(B, kRepassDev);                // device re-pass: gathered queries + results
     bytes += mem == VDB_MEM_DEVICE ? (size_t)R_rep * (D * 4 + (size_t)k * 20) + 1024 : 0;

@@ -166,11 +166,11 @@ __device__ __forceinline__ void exact_keys_rows(const float* __restrict__ q, int
 }
 
 // waves of the finish's one workgroup per query (1024 threads: 128 VGPRs each)
-// 8 (512 threads, up to 256 VGPRs: no spills) measured faster than 16 (1024 threads, 128 VGPRs)
-// under the bench's 3 streams: C2 0.188 -> 0.175 ms per batch (profiles/r04_fw8) -- its waves fit
-// beside a scan wave on a SIMD (a 128-VGPR x 4-wave-per-SIMD workgroup cannot), C3 equal
+// 16 (1024 threads, 128 VGPRs, a few spills) measured faster than 8 (512 threads, no spills) on
+// every config, same box, bench's 3 streams: C2 370K vs 364K QPS, C6 261K vs 255K, C3 365K vs
+// 360K (profiles/r04_ab/mx2; the 8-wave build define stays for A/B)
 #ifndef VDB_FIN_WAVES
-#define VDB_FIN_WAVES 8
+#define VDB_FIN_WAVES 16
 #endif
 constexpr int FIN_MP = 4;   // fast path: D <= 1024
 constexpr int FIN_NB4 = VDB_FIN_WAVES > 8 ? 3 : 6;  // rows per wave per batch on the fast path (4 spills at 128 VGPRs)

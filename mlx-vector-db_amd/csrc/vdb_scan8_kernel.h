@@ -31,7 +31,6 @@
 // query), then the fp32 score of each register is compared and appended.
 #pragma once
 #include "vdb_scan2_kernel.h"
-#include <type_traits>
 
 namespace vdb {
 
@@ -39,10 +38,6 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int S8_NW = 4;  // waves per workgroup
-// D = 128 cosine: two steps of corpus tiles in flight instead of one (A/B build define)
-#ifndef VDB_S8_TWO
-#define VDB_S8_TWO 0
-#endif
 
 #ifdef VDB_STAMP8
 // Diagnostic build only (make variant VDEFS=-DVDB_STAMP8): per-wave cycles of scan8_kernel:
@@ -277,28 +272,17 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
                     r_[rt][a] = s8_ld<false>(rinit + (tt + rt) * 32 + 8 * a, (uint32_t)(lane >> 5) * 16u);
         }
     };
-    // Two steps in flight (TWO: short rows with the group count built in, PX = 2 GC slots): slots
-    // [0, GC) and [GC, 2 GC) alternate between even and odd steps, each refilled with the step two
-    // ahead, so a step's epilogue runs with the next step's loads landing AND the one after's
-    // issued (one step ahead, C6's epilogue gaps left the HBM queue of a wave empty: 250 us
-    // against 217-223 for the stream alone, stream_micro).  SPX = the slots a step consumes.
-    constexpr bool TWO = GC > 0 && PX == 2 * GC;
-    constexpr int SPX = TWO ? GC : PX;
-    static_assert(!TWO || METRIC == 0, "two steps in flight: cosine only (L2 start values are one step ahead)");
-    auto step_src = [&](int64_t st_) { return Xq + corpus_block((uint64_t)((st_ * NW + wv) * RT), 0, 0, G); };
     f32x4 rin[NRI][4];
     if (s_begin < s_end) {
         load_epi(s_begin, rin);  // before the slots: PX * LPS loads younger than these
         const float* xs = Xq + corpus_block((uint64_t)((s_begin * NW + wv) * RT), 0, 0, G);
-        const float* xs1 = TWO && s_begin + 1 < s_end ? step_src(s_begin + 1) : xs;
 #pragma unroll
         for (int p = 0; p < PX; ++p) {
-            const float* src = p < SPX ? xs + p * XGSTEP : xs1 + (p - SPX) * XGSTEP;
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
                 for (int pl = 0; pl < XPL; ++pl)
-                    xr[p][rt][pl] = s8_ld<NT>(src + pl * XPLANE + rt * BLOCK_FLOATS, voff);
+                    xr[p][rt][pl] = s8_ld<NT>(xs + p * XGSTEP + pl * XPLANE + rt * BLOCK_FLOATS, voff);
             if constexpr (!QLDS) {
 #pragma unroll
                 for (int qt = 0; qt < QT; ++qt)
@@ -318,13 +302,11 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
         if constexpr (METRIC == 1) s8_wait<PX * LPS>(rin);
     }
 
-    // One step: its K-loop over slots [SB, SB + SPX) (the tail's refills from xn: the next step,
-    // or with TWO the step after it), then the epilogue.
-    auto step_body = [&](const int64_t s, auto sb_c, const float* xn) {
-        constexpr int SB = decltype(sb_c)::value;
+    for (int64_t s = s_begin; s < s_end; ++s) {
         S8_STAMP(const unsigned long long st_a = S8_NOW(); ++st_n;)
         const int64_t t0 = (s * NW + wv) * RT;
         const float* xs = Xq + corpus_block((uint64_t)t0, 0, 0, G);
+        const float* xn = (s + 1 < s_end) ? Xq + corpus_block((uint64_t)(t0 + NW * RT), 0, 0, G) : xs;
         i32x16 aH[RT][QT], aL[RT][QT];
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) {
@@ -384,18 +366,18 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
             }
         };
         int gb = 0;
-        for (; gb < G - SPX; gb += SPX) {
+        for (; gb < G - PX; gb += PX) {
 #pragma unroll
-            for (int p = 0; p < SPX; ++p)
-                group(SB + p, gb + p, xs + (size_t)(gb + p + SPX) * XGSTEP, Qbase + (size_t)(gb + p + PQ) * GSTEP);
+            for (int p = 0; p < PX; ++p)
+                group(p, gb + p, xs + (size_t)(gb + p + PX) * XGSTEP, Qbase + (size_t)(gb + p + PQ) * GSTEP);
         }
         // the siblings' counts: issued only where the epilogue waits for them (an asm load never
         // waited for could land in a register the compiler has reused)
         if (pace && s + 1 < s_end) pv = s8_ld_u32(pace, poff);
         if (s + 1 < s_end) load_epi(s + 1, rin);
 #pragma unroll
-        for (int p = 0; p < SPX; ++p)
-            group(SB + p, gb + p, xn + (size_t)p * XGSTEP, Qbase + (size_t)(gb + p + PQ) * GSTEP);
+        for (int p = 0; p < PX; ++p)
+            group(p, gb + p, xn + (size_t)p * XGSTEP, Qbase + (size_t)(gb + p + PQ) * GSTEP);
 
         S8_STAMP(const unsigned long long st_c = S8_NOW(); st_k += st_c - st_a;)
 #ifdef VDB_SCAN8_KLOOP_ONLY
@@ -406,7 +388,7 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
 #pragma unroll
                 for (int qt = 0; qt < QT; ++qt) f += imax16(aH[rt][qt]);
             if (f == 123456789) gl_s[0] = (float)f;
-            return;
+            continue;
         }
 #endif
         // ---- epilogue ----
@@ -526,7 +508,7 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
             const uint32_t done = (uint32_t)(s - s_begin + 1);
             if (wv == 0 && lane == 0) s8_st_u32(pace, pbase + (uint32_t)qb * 4u, (ptag << 20) | min(done, 0xFFFFFu));
             // younger than the counts: the L2 start values (RT x 4 loads) and the tail's refills
-            asm volatile("s_waitcnt vmcnt(%1)" : "+v"(pv) : "n"(SPX * LPS + (METRIC == 1 ? RT * 4 : 0)));
+            asm volatile("s_waitcnt vmcnt(%1)" : "+v"(pv) : "n"(PX * LPS + (METRIC == 1 ? RT * 4 : 0)));
             uint32_t slow = s8_pace_min(pv, ptag, lane, n_qb);
             for (int it = 0; it < S8_PACE_SPIN && done > slow + S8_PACE_W; ++it) {
                 __builtin_amdgcn_s_sleep(8);
@@ -535,24 +517,10 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
                 slow = s8_pace_min(v, ptag, lane, n_qb);
             }
         }
-        // the next step's start values (issued before the tail's SPX * LPS refills; younger
+        // the next step's start values (issued before the tail's PX * LPS refills; younger
         // epilogue accesses only make this wait stricter) land before the back-edge
-        if constexpr (METRIC == 1) s8_wait<SPX * LPS>(rin);
+        if constexpr (METRIC == 1) s8_wait<PX * LPS>(rin);
         S8_STAMP(st_e += S8_NOW() - st_c;)
-    };
-    if constexpr (TWO) {
-        // whole pairs, then an odd last step on the even slots: no path runs the even half twice
-        // without the odd one between (the wait counts assume they alternate)
-        int64_t s = s_begin;
-        for (; s + 1 < s_end; s += 2) {
-            // refills: the step two ahead (past the end: this step's own tiles, read and unused)
-            step_body(s, std::integral_constant<int, 0>{}, s + 2 < s_end ? step_src(s + 2) : step_src(s));
-            step_body(s + 1, std::integral_constant<int, SPX>{}, s + 3 < s_end ? step_src(s + 3) : step_src(s + 1));
-        }
-        if (s < s_end) step_body(s, std::integral_constant<int, 0>{}, step_src(s));
-    } else {
-        for (int64_t s = s_begin; s < s_end; ++s)
-            step_body(s, std::integral_constant<int, 0>{}, s + 1 < s_end ? step_src(s + 1) : step_src(s));
     }
 
     // The last step's tail refilled the slots (and, global operand, the query tiles) with loads
@@ -643,14 +611,6 @@ static hipError_t scan8_launch(const float* Xq, const float* rinit, const uint32
                                int64_t gl_cap, uint32_t* gthr, uint32_t* pace, uint32_t pace_tag, const int* gate,
                                hipStream_t st) {
     if constexpr (QL) {
-#if VDB_S8_TWO
-        // D = 128, cosine: two steps in flight (step_body's TWO mode)
-        if constexpr (M == 0)
-            if (G == 4)
-                return scan8_launch_g<P, M, QT, 8, KP, CAP, NT, QL, FS, 4, RT_, KW>(
-                    Xq, rinit, mask, Qq, lsl, qscal, G, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap,
-                    gthr, pace, pace_tag, gate, st);
-#endif
         if (G == 4)  // D = 128: the group loop unrolls, and the whole next step is in flight
             return scan8_launch_g<P, M, QT, 4, KP, CAP, NT, QL, FS, 4, RT_, KW>(Xq, rinit, mask, Qq, lsl, qscal, G, N, B,
                                                                         n_qblocks, n_steps, n_wg, spw, gl_s, gl_i,

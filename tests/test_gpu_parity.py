@@ -235,6 +235,23 @@ def test_i8_query_block_in_lds_whenever_it_fits(vdb, precision, metric, D, B, k,
     print(f"{precision} {metric} D {D} B {B} k {k} qlds {qlds}: fallbacks {ix.stat('fallback_queries')}")
 
 
+@pytest.mark.parametrize("refine", [-1, 0, 1])
+@pytest.mark.parametrize("D,B,k", [(96, 40, 10), (128, 64, 100), (384, 33, 10), (768, 64, 10), (1536, 20, 25)])
+@pytest.mark.parametrize("metric", ["cosine", "euclidean"])
+def test_i8_refinement_modes(vdb, metric, D, B, k, refine):
+    """The finish's I8 refinement (index param i8_refine: -1 auto = rows of 512 padded dims or
+    more, 0 off, 1 on) on both sides of the auto rule, with duplicate rows and a query equal to
+    a row (ties at the cut): exact either way."""
+    rng = np.random.default_rng(D + B + k + refine)
+    V = rng.random((12000, D), dtype=np.float32)
+    V[5000:5004] = V[11]
+    Q = rng.random((B, D), dtype=np.float32)
+    Q[2] = V[11]
+    ix, _, _ = _check(vdb, V, Q, k, metric, precision="i8", params={"i8_refine": refine})
+    with pytest.raises(Exception):
+        ix.set_param("i8_refine", 2)
+
+
 def _auto_index(vdb, D, a8):
     """An auto-precision index with (a8 = 1, the default) or without the int8 copy: its
     one-plane pass is I8 (BF16 during an I8 hold) or BF16; the x3 pass of holds, re-passes and
