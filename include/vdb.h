@@ -126,7 +126,8 @@ int32_t vdb_index_reserve(vdb_index* idx, int64_t rows);
 /* Tuning / test knobs: "precision" (VDB_PREC_*), "margin" (extra candidates
  * per query), "force_exact" (0/1), "n_wg" (candidate-pass workgroups),
  * "scan_variant" / "scan_variant_bf16x3" (0..2, kernel tiling variants),
- * "scan_sync" (candidate-pass step end: 0 auto by dimension, 1 per-step barrier,
+ * "scan_sync" (candidate-pass step end: 0 auto = flag-gated for the int8 pass and for
+ * rows of <= 128 dims, a per-step barrier otherwise; 1 per-step barrier,
  * 2 flag-gated compaction rounds; results identical, speed differs),
  * "scan_publish" (split pass slot publishing: -1 auto = off (round 3 measurement), 0 off,
  * 1 on), "scan_q4" (split pass 128-query shape for D <= 128, KP = 128, B >= 256: -1 auto = on,

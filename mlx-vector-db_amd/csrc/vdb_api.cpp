@@ -1320,7 +1320,11 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     // Step end of the scan (vdb_scan.hip): short steps (Dp <= 128: C4's 10M x 128 runs 8 split
     // groups per step, the epilogue ~half of it) gain from dropping the per-step workgroup barrier
     // (C4 scan 7.58 -> 6.22 ms); long steps lose (C2 0.57 -> 0.65 ms, C3 2.62 -> 2.90 ms), measured.
-    const int lockstep = ix->scan_sync == 0 ? (ix->Dp > 128) : ix->scan_sync == 1;
+    // The int8 pass drops it at every length: a per-step barrier lines up the 4 waves' epilogues,
+    // so the CU's stream idles through all of them at once; flag-gated, one wave's epilogue runs
+    // under the others' loads (C2 366 -> 384 K QPS, C3 365 -> 401 K with its scan 0.576 -> 0.487 ms,
+    // profiles/r04_ab/sync, same box).
+    const int lockstep = ix->scan_sync == 0 ? (!i8_pass && ix->Dp > 128) : ix->scan_sync == 1;
     // Slot publishing (shared bound from the workgroups' own bests, vdb_scan2.hip): round 2 found it
     // paying off over many steps (C4: 610 per workgroup) and not over few (C2: 8, profiles/r02_ab/).
     // Measured again in round 3 (profiles/r03_ab/publish): off is as fast or faster everywhere --

@@ -388,6 +388,8 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
 #pragma unroll
                 for (int qt = 0; qt < QT; ++qt) f += imax16(aH[rt][qt]);
             if (f == 123456789) gl_s[0] = (float)f;
+            if (pace && s + 1 < s_end) asm volatile("s_waitcnt vmcnt(%1)" : "+v"(pv) : "n"(PX * LPS + (METRIC == 1 ? RT * 4 : 0)));
+            if constexpr (METRIC == 1) s8_wait<PX * LPS>(rin);
             continue;
         }
 #endif

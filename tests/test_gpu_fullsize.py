@@ -162,7 +162,7 @@ def test_c4_10m_x_128_l2_b512_top100(vdb, sync):
     for b, r in plant.items():
         Q[b] = V[r]
     ix = vdb.NativeIndex(D, "euclidean")
-    ix.set_param("scan_sync", sync)  # 0 = auto (flag-gated at Dp = 128), 1 = lockstep
+    ix.set_param("scan_sync", sync)  # 0 = auto (flag-gated: int8 pass, Dp = 128), 1 = lockstep
     ix.reserve(N)
     for s0 in range(0, N, 1 << 21):
         ix.add(V[s0:s0 + (1 << 21)])

@@ -129,10 +129,11 @@ def test_scan_query_ring(vdb, precision, metric, D, B, k):
         ix.set_param("scan_qring", 2)
 
 
+@pytest.mark.parametrize("precision", ["bf16x3", "i8", "i8x3"])
 @pytest.mark.parametrize("sync", [1, 2])
 @pytest.mark.parametrize("metric", ["cosine", "euclidean"])
-@pytest.mark.parametrize("D,B,k", [(128, 150, 100), (384, 70, 10)])
-def test_scan_step_sync_modes(vdb, sync, metric, D, B, k):
+@pytest.mark.parametrize("D,B,k", [(128, 150, 100), (384, 70, 10), (1536, 40, 10)])
+def test_scan_step_sync_modes(vdb, sync, metric, D, B, k, precision):
     """Both step ends of the scan (lockstep barrier / flag-gated compaction rounds,
     vdb_scan.hip) on data that keeps every workgroup's buffers overflowing: rows
     approach the queries' direction as the row index grows, so each step beats the
@@ -142,7 +143,7 @@ def test_scan_step_sync_modes(vdb, sync, metric, D, B, k):
     Q = rng.random((B, D), dtype=np.float32)
     t = (np.arange(N, dtype=np.float32) / N)[:, None]
     V = (Q[rng.integers(0, B, N)] * t + rng.random((N, D), dtype=np.float32) * (1.0 - t)).astype(np.float32)
-    ix, _, _ = _check(vdb, V, Q, k, metric, params={"scan_sync": sync})
+    ix, _, _ = _check(vdb, V, Q, k, metric, precision=precision, params={"scan_sync": sync})
     with pytest.raises(Exception):
         ix.set_param("scan_sync", 3)
 
