@@ -37,7 +37,12 @@ namespace vdb {
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int S8_NW = 4;  // waves per workgroup
+// waves per workgroup (one workgroup per CU: 4 = one wave per SIMD with all its registers;
+// 8 = two, 256 registers each, one wave's epilogue under the other's K-loop -- A/B build define)
+#ifndef VDB_S8_NW
+#define VDB_S8_NW 4
+#endif
+constexpr int S8_NW = VDB_S8_NW;
 
 #ifdef VDB_STAMP8
 // Diagnostic build only (make variant VDEFS=-DVDB_STAMP8): per-wave cycles of scan8_kernel:
@@ -639,12 +644,12 @@ static hipError_t scan8_launch(const float* Xq, const float* rinit, const uint32
 // with CAP 96): 96 + 56.5 KiB.  `small` keeps the round-3 rule (block <= 32 KiB: short rows).
 // rows per step of the 128-query shape (one row tile per wave)
 constexpr int scan8_rows_q4() { return 1 * S8_NW * 32; }
-inline bool scan8_q4_fits(int G8, int prec) { return (size_t)G8 * (prec == PREC_I8X3 ? 2 : 1) * 4 * 1024 <= 32 * 1024; }
+inline bool scan8_q4_fits(int G8, int prec) { return S8_NW == 4 && (size_t)G8 * (prec == PREC_I8X3 ? 2 : 1) * 4 * 1024 <= 32 * 1024; }
 inline int scan8_cap(int KP, bool ql) { return KP == 128 ? 192 : KP == 256 ? (ql ? 96 : 128) : 128; }  // as S8_KP
 inline bool scan8_qlds(int G8, int KP, int prec, bool small) {
     const size_t q = (size_t)G8 * (prec == PREC_I8X3 ? 2 : 1) * 2 * 1024;
     if (small) return q <= 32 * 1024;
-    const size_t lists = (size_t)64 * scan8_cap(KP, true) * 8 + 8192 + 1024;
+    const size_t lists = (size_t)64 * scan8_cap(KP, true) * 8 + S8_NW * 2048 + 1024;
     return lists + q <= 160 * 1024;
 }
 
@@ -664,9 +669,13 @@ inline bool scan8_qlds(int G8, int KP, int prec, bool small) {
 // a workgroup keeps KW = 48 of KP = 128 per query (CAP 64: 64 KiB of lists).  Twice the MFMAs
 // per corpus byte of the 64-query shape, and half the query blocks re-reading each row range
 // (C4, 10M x 128, B = 512: 8 -> 4 blocks).
+#if VDB_S8_NW == 4
 #define S8_ONE4(P, M, FSV)                    \
     if (KP == 128 && ql && fs == FSV && q4)   \
         return scan8_launch<P, M, 4, 4, 128, 64, false, true, FSV, 48, 1>(S8_ARGS);
+#else  // (4 waves only: scan8_q4_fits says no)
+#define S8_ONE4(P, M, FSV)
+#endif
 // KP = 256 keeps 64-query blocks: a workgroup keeps its best KW = 64 per query (LDS 64 KiB, 48
 // with the query block in LDS beside it; the drop bound -> gthr, vdb_scan2_kernel.h), so a
 // 64-query batch reads the corpus once
