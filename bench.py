@@ -429,6 +429,8 @@ def main():
     ap.add_argument("--scan-pace", type=int, default=None, help="int8 pass: 1 pace the query blocks of a row range, "
                     "0 off (default; tuning)")
     ap.add_argument("--rows", type=int, default=None, help="override the corpus rows (exploration only)")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="override the batch (exploration only: e.g. one rank's shape of a weak-scaled run)")
     ap.add_argument("--timing", type=int, default=1,
                     help="1: the library's HIP events around the scan in the timed region (roofline); 0: none "
                          "(A/B of their cost; the roofline then comes from an untimed second loop)")
@@ -493,6 +495,7 @@ def bench_brute(cfg, args, world, rank, local, dev, primary=True):
         k = int(args.k)
         desc = f"{desc} [k = {k}]"
     N = (args.rows if primary else None) or N
+    B = (args.batch if primary else None) or B
     scaling = args.scaling or DEFAULT_SCALING.get(cfg, "weak")
     lo, hi = shard_bounds(N, world, rank)
     n_local = hi - lo

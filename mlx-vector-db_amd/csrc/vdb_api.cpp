@@ -193,6 +193,11 @@ struct vdb_index {
     // for kRepassArm searches once a device fallback has been seen; 0 off; 1 always
     int64_t device_repass = -1;
     std::atomic<int> repass_arm{0};
+    // auto's I8 pass on indexes of <= kI8NarrowRows rows: KP = 128 instead of 256 (a weak-scaled
+    // rank's shard: the k-th to KP-th gap widens as rows thin out) until any search of this index
+    // flags a query, then 256 for good (i8_wide).  Knob "i8_narrow": -1 auto, 0 off.
+    int64_t i8_narrow = -1;
+    std::atomic<bool> i8_wide{false};
     std::atomic<uint32_t> pace_seq{0};  // launch tag of the pacing counters
     int64_t scan_q4 = -1;      // split pass 128-query shape (D <= 128, KP = 128, B >= 256): -1 auto, 0 off, 1 on
     // stats
@@ -781,6 +786,9 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
     } else if (n == "i8_refine") {
         if (value < -1 || value > 1) return set_error(VDB_ERR_INVALID, "i8_refine must be -1, 0 or 1");
         ix->i8_refine = (int)value;
+    } else if (n == "i8_narrow") {
+        if (value < -1 || value > 0) return set_error(VDB_ERR_INVALID, "i8_narrow must be -1 or 0");
+        ix->i8_narrow = value;
     } else if (n == "device_repass") {
         if (value < -1 || value > 1) return set_error(VDB_ERR_INVALID, "device_repass must be -1, 0 or 1");
         ix->device_repass = value;
@@ -844,6 +852,7 @@ int32_t vdb_index_get_stat(const vdb_index* cix, const char* name, int64_t* valu
     else if (n == "searches_i8") *value = ix->n_by_prec[PREC_I8].load();
     else if (n == "searches_i8x3") *value = ix->n_by_prec[PREC_I8X3].load();
     else if (n == "auto_int8") *value = ix->auto_i8 ? 1 : 0;
+    else if (n == "i8_wide") *value = ix->i8_wide ? 1 : 0;
     else if (n == "device_bytes")
         *value = (int64_t)(ix->cap_rows / 32) * ix->G * BLOCK_FLOATS * (ix->Xq ? 11 : 8) + ix->cap_rows * 20;  // X, Xs (+ Xq, Xh)
     else return set_error(VDB_ERR_INVALID, "unknown stat '%s'", name);
@@ -1097,6 +1106,8 @@ constexpr int kRepassMax = 64;
 // the re-pass for kRepassArm searches after a device fallback was seen.
 constexpr int kRepassDev = 16;
 constexpr int kRepassArm = 256;
+// auto's I8 pass: KP = 128 up to this many rows (i8_narrow)
+constexpr int64_t kI8NarrowRows = 512 * 1024;
 // i8_refine auto: the finish refines I8 candidates' scores for padded rows of this many dims or more
 constexpr int64_t kRefineMinDp = 512;
 // VDB_PREC_AUTO uses the bf16 pass up to this k (its KP = next_pow2(k + 112) stays 128)
@@ -1231,8 +1242,12 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
         const unsigned long long seen = ix->h_totals[0];
         const unsigned long long prev = ix->auto_seen.exchange(seen);
         if (seen > prev) {
-            if (ix->last_i8) auto_fail8(ix);
-            else auto_fail(ix);
+            if (ix->last_i8) {
+                auto_fail8(ix);
+                ix->i8_wide = true;
+            } else {
+                auto_fail(ix);
+            }
             ix->repass_arm = kRepassArm;  // device_repass auto: re-pass on the device for a while
         }
     }
@@ -1275,7 +1290,12 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     if (one_plane) margin_def = std::max(16, std::min(std::max(112, k / 2), 256 - k));
     // I8 (the 8-bit query's wider bound): KP = 256.  1M x 768 uniform, B = 64: KP = 128 left one
     // query per batch uncertified; 256 none (profiles/r03_i8/c2_i8_kp*)
-    if (prec_req == PREC_I8) margin_def = std::max(16, 256 - k);
+    // -- except auto on small indexes (i8_narrow): at <= 512 K rows KP = 128 (one rank of an 8-way
+    // weak-scaled C2, 125 K rows x 512 queries: step 0.248 -> 0.207 ms, 0 fallbacks; 250 K: 0.181 ->
+    // 0.157; KP = 64 failed thousands of queries, profiles/r04_ab/rank*), widened for good at the
+    // first flagged query
+    const bool i8_narrow = auto_prec && ix->i8_narrow != 0 && !ix->i8_wide && N <= kI8NarrowRows;
+    if (prec_req == PREC_I8) margin_def = std::max(16, (i8_narrow ? 128 : 256) - k);
     // a re-pass sub-search (host or device) takes KP = 128: its few queries are the ones whose
     // rows sit closer together than the one-plane pass could separate, so they need the wider
     // gap between the k-th and the KP-th candidate (C2 with 300 rows in a 3e-3 cosine band:
@@ -1657,6 +1677,7 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
             HIP_TRY(hipMemcpyAsync(w->host_flag + 1, flags + B + 1, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
             HIP_TRY(hipStreamSynchronize(st));
             n_flag = w->host_flag[0];
+            if (prec == PREC_I8 && n_flag > 0) ix->i8_wide = true;
             ix->n_overflow += w->host_flag[1];
             ix->n_incons += w->host_flag[2];
             if (auto_prec && one_plane && n_flag > 0 && !ix->no_fallback) {

@@ -968,3 +968,49 @@ def test_device_repass_more_flagged_than_gathered(vdb):
     rp, fb = ix.stat("repass_queries"), ix.stat("fallback_queries")
     print(f"re-passed {rp}, exact path {fb}")
     assert rp == 16 and fb >= 1
+
+
+@pytest.mark.parametrize("mem", ["host", "device"])
+def test_i8_narrow_kp_on_small_indexes(vdb, mem):
+    """auto's I8 pass keeps KP = 128 instead of 256 on indexes of <= 512 K rows (one rank's shard
+    of a weak-scaled run) until a search flags a query; from then on 256 (stat i8_wide).  Exact
+    either way: a uniform batch (no flag, stays narrow), then a batch with one query among 300
+    close rows (flagged: re-passed or sent to the exact path), then uniform again (wide)."""
+    import torch
+    rng = np.random.default_rng(71)
+    N, D, B, k = 60000, 256, 64, 10
+    V = rng.random((N, D), dtype=np.float32)
+    V[3000:3300] = _graded_neighbours(rng, V[17], 300)
+    Q1 = rng.random((B, D), dtype=np.float32)
+    Q2 = rng.random((B, D), dtype=np.float32)
+    Q2[9] = V[17]
+    ix = vdb.NativeIndex(D, "cosine")
+    ix.add(V)
+
+    def run(Q):
+        _, ei, ek = ref_cpu.exact_search(Q, V, k, "cosine")
+        if mem == "host":
+            _, i, kk = ix.search(Q, k, with_keys=True)
+        else:
+            qd = torch.from_numpy(Q).cuda()
+            sd = torch.empty((B, k), dtype=torch.float32, device="cuda")
+            idd = torch.empty((B, k), dtype=torch.int64, device="cuda")
+            kd = torch.empty((B, k), dtype=torch.float64, device="cuda")
+            torch.cuda.synchronize()
+            ix.search_device(qd.data_ptr(), B, k, sd.data_ptr(), idd.data_ptr(), kd.data_ptr(), stream=0)
+            torch.cuda.synchronize()
+            i, kk = idd.cpu().numpy(), kd.cpu().numpy()
+        np.testing.assert_array_equal(i, ei)
+        np.testing.assert_array_equal(kk, ek)
+
+    run(Q1)
+    assert ix.stat("i8_wide") == 0
+    run(Q2)
+    run(Q1)  # (device memory: the flag of the batch before is seen by this search)
+    run(Q1)
+    assert ix.stat("i8_wide") == 1
+    assert ix.stat("searches_i8") >= 2  # (device memory: the seen fallback also starts an I8 hold)
+    ix2 = vdb.NativeIndex(D, "cosine")
+    ix2.set_param("i8_narrow", 0)
+    with pytest.raises(Exception):
+        ix2.set_param("i8_narrow", 1)
