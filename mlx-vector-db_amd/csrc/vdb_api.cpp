@@ -1108,6 +1108,7 @@ constexpr int kRepassDev = 16;
 constexpr int kRepassArm = 256;
 // auto's I8 pass: KP = 128 up to this many rows (i8_narrow)
 constexpr int64_t kI8NarrowRows = 512 * 1024;
+constexpr int64_t kI8NarrowRowsShort = 4 * 1024 * 1024;  // rows of <= 128 dims
 // i8_refine auto: the finish refines I8 candidates' scores for padded rows of this many dims or more
 constexpr int64_t kRefineMinDp = 512;
 // VDB_PREC_AUTO uses the bf16 pass up to this k (its KP = next_pow2(k + 112) stays 128)
@@ -1294,7 +1295,12 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     // weak-scaled C2, 125 K rows x 512 queries: step 0.248 -> 0.207 ms, 0 fallbacks; 250 K: 0.181 ->
     // 0.157; KP = 64 failed thousands of queries, profiles/r04_ab/rank*), widened for good at the
     // first flagged query
-    const bool i8_narrow = auto_prec && ix->i8_narrow != 0 && !ix->i8_wide && N <= kI8NarrowRows;
+    // Rows of <= 128 dims (C6's 10M x 128): 0 fallbacks at KP = 128 even at 10 M rows, faster up to
+    // the 4-way shard (8-way 1.25 M x 512: 1.38 -> 1.56 M QPS; 4-way 2.5 M x 256: +4%) and slower
+    // at 10 M (262 -> 248 K: the KP = 128 scan's 106 KiB of LDS leaves no room beside it for the
+    // next batch's pilot, profiles/r04_ab/rank6m, c6m), hence 4 M
+    const bool i8_narrow = auto_prec && ix->i8_narrow != 0 && !ix->i8_wide &&
+                           (N <= kI8NarrowRows || (ix->Dp <= 128 && N <= kI8NarrowRowsShort));
     if (prec_req == PREC_I8) margin_def = std::max(16, (i8_narrow ? 128 : 256) - k);
     // a re-pass sub-search (host or device) takes KP = 128: its few queries are the ones whose
     // rows sit closer together than the one-plane pass could separate, so they need the wider

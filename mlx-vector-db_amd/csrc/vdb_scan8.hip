@@ -263,7 +263,8 @@ pilot8_scores_kernel(const float* __restrict__ Xq, const float* __restrict__ rin
     constexpr int QB = 32 * QT;
     constexpr int XPL = Planes8<PREC>::XPL;
     constexpr size_t GSTEP = 8 * BLOCK_FLOATS, PLANE = 4 * BLOCK_FLOATS;
-    __shared__ int s_part[PILOT8_WAVES][2][QT][16][64];
+    constexpr bool HL = Planes8<PREC>::L;
+    __shared__ int s_part[PILOT8_WAVES][HL ? 2 : 1][QT][16][64];  // (I8: 32 KiB, room beside a scan)
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
     const int W = pilot8_w(G);
@@ -297,7 +298,7 @@ pilot8_scores_kernel(const float* __restrict__ Xq, const float* __restrict__ rin
 #pragma unroll
             for (int v = 0; v < 16; ++v) {
                 s_part[wv][0][qt][v][lane] = aH[0][qt][v];
-                s_part[wv][1][qt][v][lane] = aL[0][qt][v];
+                if constexpr (HL) s_part[wv][HL ? 1 : 0][qt][v][lane] = aL[0][qt][v];
             }
     }
     __syncthreads();
@@ -308,7 +309,7 @@ pilot8_scores_kernel(const float* __restrict__ Xq, const float* __restrict__ rin
 #pragma unroll
             for (int v = 0; v < 16; ++v) {
                 aH[0][qt][v] += s_part[wv + w][0][qt][v][lane];
-                aL[0][qt][v] += s_part[wv + w][1][qt][v][lane];
+                if constexpr (HL) aL[0][qt][v] += s_part[wv + w][HL ? 1 : 0][qt][v][lane];
             }
     const float uH = qscal[0], uL = qscal[1];
     const uint32_t valid = tile_valid16(mask, (int64_t)t, N, lane);
