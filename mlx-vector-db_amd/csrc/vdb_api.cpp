@@ -1391,6 +1391,7 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     bytes += (size_t)(mask_words + 64) * 4 + 256;           // mask (host mode)
     bytes += (size_t)Bp * (ix->Dp + 16 * QG_EXTRA) * 4 + 256;  // Qt (tiled fp32 or split, duplicated groups)
     bytes += (size_t)Bp * 8 + 256;                          // qn64
+    bytes += (size_t)Bp * 24 + 256;                         // qconst: the finish's per-query constants
     bytes += (size_t)Bp * KP * 8 + 512;                     // merged approx lists
     bytes += (size_t)B * k * 20 + 768;                      // outputs (host mode)
     bytes += (size_t)(B + 64) * 4 + 256;                    // flags
@@ -1460,6 +1461,10 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     uint32_t* maskd = c.take<uint32_t>(mask_words + 64);
     float* Qt = c.take<float>((size_t)Bp * (ix->Dp + 16 * QG_EXTRA));
     double* qn64 = c.take<double>(Bp);
+    double* qconst = c.take<double>((size_t)Bp * 3);
+    // the finish's centring row and residual direction (the same conditions as its arguments below)
+    const float* q_mu = i8_pass ? ix->d_mu : nullptr;
+    const float* q_dir = (prec == PREC_BF16 || i8_pass) && ix->dir_set && !ix->no_dir_bound ? ix->d_dir : nullptr;
     float* os = c.take<float>((size_t)B * k);
     int64_t* oi = c.take<int64_t>((size_t)B * k);
     double* ok = c.take<double>((size_t)B * k);
@@ -1511,7 +1516,7 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     } else {
         HIP_TRY(launch_prep_queries(Qd, B, Bp, D, ix->G, ix->metric, prec == PREC_FP32 ? Qt : nullptr,
                                     split_pass ? Qt : nullptr, qn64, flags, gthr, gslots, gl_cnt, done, st,
-                                    i8_pass ? q8max : nullptr));
+                                    i8_pass ? q8max : nullptr, q_mu, q_dir, qconst));
         if (i8_pass && !exact_all) {
             Int8Consts c8;
             c8.sx = ix->sx;
@@ -1622,6 +1627,7 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
             fa.flag_count = flags; fa.flag_list = flags + 1; fa.gthr = gthr; fa.overflow_count = flags + B + 1;
             fa.incons_count = flags + B + 2;
             fa.gate = opt.gate;
+            fa.qconst = fa.mu == q_mu && fa.dir == q_dir ? qconst : nullptr;  // (prep_queries' constants)
             fa.split = fin_split; fa.sx_ek = fx_ek; fa.sx_ck = fx_ck; fa.sx_cr = fx_cr; fa.sx_n = fx_n; fa.done = done;
             HIP_TRY(launch_finish(ix->metric, KP, fa, B, st));
             if (timed) HIP_TRY(hipEventRecord(tev[2], st));

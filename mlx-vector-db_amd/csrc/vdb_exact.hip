@@ -535,7 +535,9 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
         // and the rerank cut only compare approximate scores with each other; the exact-key
         // test compares an exact key with them.
         double mq = 0.0;
-        if (a.mu) {
+        if (a.mu && a.qconst) {
+            mq = a.qconst[3 * (size_t)b];
+        } else if (a.mu) {
             const float* qq = a.Q + (int64_t)b * a.D;
             const double qs = METRIC == 0 ? 1.0 / fmax(qn, 1e-8) : 1.0;
             for (int d = lane; d < a.D; d += 64) mq += (double)qq[d] * qs * (double)a.mu[d];
@@ -548,17 +550,21 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
         if (a.xres > 0.0) {
             bq = METRIC == 0 ? a.xres : qn * a.xres;
             if (a.dir) {
-                const float* qq = a.Q + (int64_t)b * a.D;
-                const double qs = METRIC == 0 ? 1.0 / fmax(qn, 1e-8) : 1.0;
-                double c = 0.0;
-                for (int d = lane; d < a.D; d += 64) c += (double)qq[d] * qs * (double)a.dir[d];
-                c = wave_sum_butterfly(c);
-                double w2 = 0.0;
-                for (int d = lane; d < a.D; d += 64) {
-                    const double w = (double)qq[d] * qs - c * (double)a.dir[d];
-                    w2 += w * w;
+                double c = 0.0, w2 = 0.0;
+                if (a.qconst) {
+                    c = a.qconst[3 * (size_t)b + 1];
+                    w2 = a.qconst[3 * (size_t)b + 2];
+                } else {
+                    const float* qq = a.Q + (int64_t)b * a.D;
+                    const double qs = METRIC == 0 ? 1.0 / fmax(qn, 1e-8) : 1.0;
+                    for (int d = lane; d < a.D; d += 64) c += (double)qq[d] * qs * (double)a.dir[d];
+                    c = wave_sum_butterfly(c);
+                    for (int d = lane; d < a.D; d += 64) {
+                        const double w = (double)qq[d] * qs - c * (double)a.dir[d];
+                        w2 += w * w;
+                    }
+                    w2 = wave_sum_butterfly(w2);
                 }
-                w2 = wave_sum_butterfly(w2);
                 // (1 + 1e-6) and + 1e-6 R: the fp64 evaluation and the fp32-normalised query
                 const double bd = (sqrt(w2) * a.xres + fabs(c) * a.dres) * (1.0 + 1e-6) + 1e-6 * a.xres;
                 bq = fmin(bq, bd);
@@ -637,6 +643,9 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
     // rounding term (prep8 qerr2) plus the refinement's own fp32 rounding per row.  The pass's
     // wide 8-bit-query bound left every one of KP = 256 candidates within 2 eps of a_k at C2 /
     // C3 (finish stamps, profiles/r04): each then cost a whole fp32 row of exact key.
+#ifdef VDB_STAMP
+    if (threadIdx.x == 0) g_fin_stamps[blockIdx.x][6] = __builtin_amdgcn_s_memtime();
+#endif
     __shared__ float s_ca[KP];
     __shared__ uint32_t s_cbmax;
     __shared__ float s_ak2;
@@ -763,7 +772,9 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
         m = s_m;
     }
 #ifdef VDB_STAMP
-    if (threadIdx.x == 0) g_fin_stamps[b][6] = (unsigned long long)m;  // the rerank set
+    // [6] (time after the certificate) -> ticks of the refinement and the cut; the rerank set
+    // size in the high bits
+    if (threadIdx.x == 0) g_fin_stamps[b][6] = (__builtin_amdgcn_s_memtime() - g_fin_stamps[b][6]) | ((unsigned long long)m << 40);
 #endif
     // split > 1: the candidates with row % S == sp are this workgroup's (the selected set is
     // the same in every workgroup of the query, its LDS order is not)
@@ -791,6 +802,7 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
         xek = s_oek;
         mx = s_mown;
     }
+    FIN_STAMP(3);
     const float* q = a.Q + (int64_t)b * a.D;
     // exact keys: wave wv takes candidates wv NB, ... in batches of NB
     const int np = (a.D + 255) / 256;
@@ -895,7 +907,7 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
         m = off;
         __syncthreads();
     }
-    FIN_STAMP(3);
+    FIN_STAMP(4);
     // exact ranks by counting (output order), TPC threads per candidate as above
     for (int jt = tid; jt < KP * TPC; jt += 64 * FIN_WAVES) {
         const int j = jt / TPC, sub = jt % TPC;
@@ -953,7 +965,6 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
             if (s_bad && a.incons_count) atomicAdd(a.incons_count, 1);
         }
     }
-    FIN_STAMP(4);
     FIN_STAMP(5);
 }
 

@@ -245,7 +245,10 @@ __global__ void __launch_bounds__(256) prep_queries_kernel(const float* __restri
                                                            double* __restrict__ qn64, int* __restrict__ flag_count,
                                                            uint32_t* __restrict__ gthr,
                                                            uint32_t* __restrict__ gslots, uint32_t* __restrict__ gl_cnt,
-                                                           int* __restrict__ done, float* __restrict__ qmax) {
+                                                           int* __restrict__ done, float* __restrict__ qmax,
+                                                           const float* __restrict__ mu,
+                                                           const float* __restrict__ dir,
+                                                           double* __restrict__ qconst) {
     const int lane = threadIdx.x & 63;
     const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (b == 0 && lane == 0 && flag_count) {
@@ -278,6 +281,40 @@ __global__ void __launch_bounds__(256) prep_queries_kernel(const float* __restri
     if (lane == 0) qn64[b] = nq;
     // cosine: the candidate pass works on q/max(|q|,1e-8) rounded to fp32.
     const float scale = metric == 0 ? (float)(1.0 / fmax(nq, 1e-8)) : 1.0f;
+    if (qconst) {
+        // the finish's per-query constants (vdb_exact.hip finish_kernel): mu.q' (the int8 pass's
+        // shift) and, for the directional corpus bound, c = dir.q' and |q' - c dir|^2 =
+        // |q'|^2 - 2 c^2 + c^2 |dir|^2 (fp64; one pass of float4 loads, all in flight together)
+        const double qs = metric == 0 ? 1.0 / fmax(nq, 1e-8) : 1.0;
+        double mq = 0.0, c = 0.0, q2 = 0.0, d2 = 0.0;
+        for (int m = 0; m < np; ++m) {
+            const int d0 = 4 * (m * 64 + lane);
+            f32x4 qv = {0.f, 0.f, 0.f, 0.f}, mv = {0.f, 0.f, 0.f, 0.f}, dv = {0.f, 0.f, 0.f, 0.f};
+            if (d0 < Dp) {  // mu / dir are [Dp], zero padded; the query row is [D]
+#pragma unroll
+                for (int j = 0; j < 4; ++j) qv[j] = (real && d0 + j < D) ? q[d0 + j] : 0.0f;
+                if (mu) mv = *(const f32x4*)(mu + d0);
+                if (dir) dv = *(const f32x4*)(dir + d0);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const double x = (double)qv[j] * qs;
+                mq += x * (double)mv[j];
+                c += x * (double)dv[j];
+                q2 += x * x;
+                d2 += (double)dv[j] * (double)dv[j];
+            }
+        }
+        mq = wave_sum_butterfly(mq);
+        c = wave_sum_butterfly(c);
+        q2 = wave_sum_butterfly(q2);
+        d2 = wave_sum_butterfly(d2);
+        if (lane == 0) {
+            qconst[3 * (size_t)b] = mu ? mq : 0.0;
+            qconst[3 * (size_t)b + 1] = dir ? c : 0.0;
+            qconst[3 * (size_t)b + 2] = dir ? fmax(q2 - 2.0 * c * c + c * c * d2, 0.0) : 0.0;
+        }
+    }
     if (qmax && real) {  // the int8 pass's batch scale (vdb_scan8.hip prep8)
         float m = 0.0f;
         for (int d = lane; d < D; d += 64) m = fmaxf(m, fabsf(q[d] * scale));
@@ -322,9 +359,10 @@ __global__ void __launch_bounds__(256) prep_queries_kernel(const float* __restri
 
 hipError_t launch_prep_queries(const float* Q, int B, int Bp, int D, int G, int metric, float* Qt, float* Qs,
                                double* qn64, int* flag_count, uint32_t* gthr, uint32_t* gslots, uint32_t* gl_cnt,
-                               int* done, hipStream_t st, float* qmax) {
+                               int* done, hipStream_t st, float* qmax, const float* mu, const float* dir,
+                               double* qconst) {
     hipLaunchKernelGGL(prep_queries_kernel, dim3((Bp + 3) / 4), dim3(256), 0, st, Q, B, Bp, D, G, metric, Qt, Qs,
-                       qn64, flag_count, gthr, gslots, gl_cnt, done, qmax);
+                       qn64, flag_count, gthr, gslots, gl_cnt, done, qmax, mu, dir, qconst);
     return hipGetLastError();
 }
 }  // namespace vdb

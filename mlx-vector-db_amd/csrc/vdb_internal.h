@@ -104,7 +104,8 @@ constexpr int PILOT_SLOTS = 256;  // pilot bound slots per query (pslots [Bp][PI
 hipError_t launch_prep_queries(const float* Q, int B, int Bp, int D, int G, int metric,
                                float* Qt, float* Qs, double* qn64, int* flag_count, uint32_t* gthr,
                                uint32_t* gslots, uint32_t* gl_cnt, int* done, hipStream_t st,
-                               float* qmax = nullptr);
+                               float* qmax = nullptr, const float* mu = nullptr, const float* dir = nullptr,
+                               double* qconst = nullptr);
 
 // Candidate pass: MFMA fp32 scores fused with a per-workgroup top-KP.
 // Output lists cand_[s|i][B][n_wg][KP], each sorted best first.
@@ -194,6 +195,10 @@ struct FinishArgs {
     const float* qerr = nullptr;
     // the int8 pass's centring row (its scores leave out mu.q; the exact-key certificate adds it)
     const float* mu = nullptr;
+    // optional, per query [Bp][3] from prep_queries: mu.q', dir.q', |q' - (dir.q') dir|^2 (fp64;
+    // q' the pass's query, cosine unit) -- computed there for the whole batch at once instead of
+    // by two waves of each finish workgroup (three dependent fp64 passes over the query, ~14 us)
+    const double* qconst = nullptr;
     float* out_s; int64_t* out_i; double* out_k; int64_t index_offset;
     int* flag_count; int* flag_list; const uint32_t* gthr;
     int* overflow_count;  // lists longer than the finish kernel holds (they take the exact path)

@@ -15,6 +15,8 @@ import bench
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c2"
 prec = sys.argv[2] if len(sys.argv) > 2 else "bf16x3"
 N, D, B, k, metric, _ = bench.CONFIGS[cfg]
+N = int(os.environ.get("FIN_ROWS", N))  # e.g. one rank's shard of a weak-scaled run
+B = int(os.environ.get("FIN_B", B))
 ix = _vdb.NativeIndex(D, metric, precision=prec)
 if os.environ.get("VDB_FIN_REFINE") is not None:
     ix.set_param("i8_refine", int(os.environ["VDB_FIN_REFINE"]))
@@ -28,8 +30,11 @@ lib = _vdb.load_library()
 fb = (ctypes.c_ulonglong * (B * 8))()
 lib.vdb_debug_finish_stamps(fb, B)
 f = np.array(fb, dtype=np.uint64).reshape(B, 8).astype(np.float64)
-print(f"{cfg} {prec}: list length mean {f[:, 7].mean():.0f} p50 {np.median(f[:, 7]):.0f} max {f[:, 7].max():.0f}; "
-      f"rerank set mean {f[:, 6].mean():.1f} max {f[:, 6].max():.0f}")
-for i, name in enumerate(["load", "select", "exact keys", "ranks+write"]):
+rs = f[:, 6].astype(np.uint64) >> np.uint64(40)
+rt = (f[:, 6].astype(np.uint64) & np.uint64((1 << 40) - 1)).astype(np.float64)
+print(f"{cfg} {prec} N {N} B {B}: list length mean {f[:, 7].mean():.0f} p50 {np.median(f[:, 7]):.0f} max {f[:, 7].max():.0f}; "
+      f"rerank set mean {rs.astype(float).mean():.1f} max {rs.max()}")
+for i, name in enumerate(["load", "select", "cert+refine+cut", "exact keys", "ranks+write"]):
     d = f[:, i + 1] - f[:, i]
-    print(f"  {name:12s} mean {d.mean():9.0f}  max {d.max():9.0f}  (s_memtime ticks)")
+    print(f"  {name:16s} mean {d.mean():9.0f}  max {d.max():9.0f}  (s_memtime ticks)")
+print(f"    (of which refinement + cut: mean {rt.mean():.0f})")
