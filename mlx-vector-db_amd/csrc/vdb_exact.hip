@@ -330,7 +330,7 @@ template <int METRIC, int KP>
 __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
     __shared__ uint32_t s_key[FIN_CAP];
     __shared__ uint32_t s_row[FIN_CAP];
-    __shared__ uint32_t s_ck[KP];
+    __shared__ __attribute__((aligned(16))) uint32_t s_ck[KP];
     __shared__ uint32_t s_cr[KP];
     __shared__ double s_ek[KP];
     __shared__ uint32_t s_ock[KP];  // split > 1: this workgroup's share of the candidates
@@ -505,23 +505,38 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
     // (DESIGN.md §3.2); with |approx - exact| <= eps per row the certificate is
     // acut + eps < a_k - eps.
     constexpr int TPC = KP >= 64 * FIN_WAVES ? 1 : (64 * FIN_WAVES) / KP > 64 ? 64 : (64 * FIN_WAVES) / KP;
+    // Only the VALUES of the k-th and KP-th are needed: the candidate whose key v has fewer than
+    // k keys above it and at least k at or above it holds it (ties give the same value), so each
+    // of TPC threads counts a contiguous chunk with 16-byte LDS reads (the rank by (key, row) of
+    // every candidate was ~20 K cycles at KP = 256: an unpipelined LDS round trip per entry)
+    const int chunk = ((m + TPC - 1) / TPC + 3) & ~3;
     for (int jt = tid; jt < KP * TPC; jt += 64 * FIN_WAVES) {
         const int j = jt / TPC, sub = jt % TPC;
-        int ar = 0;
-        uint32_t ck = 0u, r = 0u;
+        int g = 0, ge = 0;
+        uint32_t ck = 0u;
         if (j < m) {
             ck = s_ck[j];
-            r = s_cr[j];
-            for (int i = sub; i < m; i += TPC) {
-                const uint32_t ci = s_ck[i], ri = s_cr[i];
-                ar += (ci > ck || (ci == ck && ri < r)) ? 1 : 0;
+            const int i0 = sub * chunk, i1 = min(m, i0 + chunk);
+            int i = i0;
+            for (; i + 4 <= i1; i += 4) {
+                const uint4 v = *(const uint4*)(s_ck + i);
+                g += (v.x > ck) + (v.y > ck) + (v.z > ck) + (v.w > ck);
+                ge += (v.x >= ck) + (v.y >= ck) + (v.z >= ck) + (v.w >= ck);
+            }
+            for (; i < i1; ++i) {
+                const uint32_t v = s_ck[i];
+                g += v > ck;
+                ge += v >= ck;
             }
         }
 #pragma unroll
-        for (int off = 1; off < TPC; off <<= 1) ar += __shfl_xor(ar, off, 64);
+        for (int off = 1; off < TPC; off <<= 1) {
+            g += __shfl_xor(g, off, 64);
+            ge += __shfl_xor(ge, off, 64);
+        }
         if (sub == 0 && j < m) {
-            if (ar == a.k - 1) s_ak = ck;
-            if (ar == KP - 1) s_akp = ck;
+            if (g < a.k && ge >= a.k) s_ak = ck;
+            if (g < KP && ge >= KP) s_akp = ck;
         }
     }
     // bf16 corpus rounding: |q.(y - bf16(y))| <= bq, Cauchy-Schwarz |q| R or, along the index's
@@ -646,7 +661,7 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
 #ifdef VDB_STAMP
     if (threadIdx.x == 0) g_fin_stamps[blockIdx.x][6] = __builtin_amdgcn_s_memtime();
 #endif
-    __shared__ float s_ca[KP];
+    __shared__ __attribute__((aligned(16))) float s_ca[KP];
     __shared__ uint32_t s_cbmax;
     __shared__ float s_ak2;
     const bool refine = a.xh_rm != nullptr && s_cut > -INFINITY;
@@ -721,22 +736,31 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
         }
         __syncthreads();
         // a'_k by rank counting over (a' desc, row asc), TPC threads per candidate
-        for (int jt = tid; jt < KP * TPC; jt += 64 * FIN_WAVES) {
+        for (int jt = tid; jt < KP * TPC; jt += 64 * FIN_WAVES) {  // (the value alone, as above)
             const int j = jt / TPC, sub = jt % TPC;
-            int ar = 0;
+            int g = 0, ge = 0;
             float cj = 0.0f;
-            uint32_t r = 0u;
             if (j < m) {
                 cj = s_ca[j];
-                r = s_cr[j];
-                for (int i = sub; i < m; i += TPC) {
-                    const float ci = s_ca[i];
-                    ar += (ci > cj || (ci == cj && s_cr[i] < r)) ? 1 : 0;
+                const int i0 = sub * chunk, i1 = min(m, i0 + chunk);
+                int i = i0;
+                for (; i + 4 <= i1; i += 4) {
+                    const f32x4 v = *(const f32x4*)(s_ca + i);
+                    g += (v[0] > cj) + (v[1] > cj) + (v[2] > cj) + (v[3] > cj);
+                    ge += (v[0] >= cj) + (v[1] >= cj) + (v[2] >= cj) + (v[3] >= cj);
+                }
+                for (; i < i1; ++i) {
+                    const float v = s_ca[i];
+                    g += v > cj;
+                    ge += v >= cj;
                 }
             }
 #pragma unroll
-            for (int off = 1; off < TPC; off <<= 1) ar += __shfl_xor(ar, off, 64);
-            if (sub == 0 && j < m && ar == a.k - 1) s_ak2 = cj;
+            for (int off = 1; off < TPC; off <<= 1) {
+                g += __shfl_xor(g, off, 64);
+                ge += __shfl_xor(ge, off, 64);
+            }
+            if (sub == 0 && j < m && g < a.k && ge >= a.k) s_ak2 = cj;
         }
         __syncthreads();
         if (tid == 0) {
