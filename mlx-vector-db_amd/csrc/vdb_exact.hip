@@ -331,8 +331,8 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
     __shared__ uint32_t s_key[FIN_CAP];
     __shared__ uint32_t s_row[FIN_CAP];
     __shared__ __attribute__((aligned(16))) uint32_t s_ck[KP];
-    __shared__ uint32_t s_cr[KP];
-    __shared__ double s_ek[KP];
+    __shared__ __attribute__((aligned(16))) uint32_t s_cr[KP];
+    __shared__ __attribute__((aligned(16))) double s_ek[KP];
     __shared__ uint32_t s_ock[KP];  // split > 1: this workgroup's share of the candidates
     __shared__ uint32_t s_ocr[KP];
     __shared__ double s_oek[KP];
@@ -932,7 +932,10 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
         __syncthreads();
     }
     FIN_STAMP(4);
-    // exact ranks by counting (output order), TPC threads per candidate as above
+    // exact ranks by counting (output order), TPC threads per candidate as above, each over a
+    // contiguous chunk in 16-byte LDS reads; a count that reaches k stops (only ranks < k are
+    // written, and rank k - 1's key)
+    const int chunk2 = ((m + TPC - 1) / TPC + 3) & ~3;
     for (int jt = tid; jt < KP * TPC; jt += 64 * FIN_WAVES) {
         const int j = jt / TPC, sub = jt % TPC;
         int er = 0;
@@ -941,10 +944,12 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
         if (j < m) {
             ek = s_ek[j];
             r = s_cr[j];
-            for (int i = sub; i < m; i += TPC) {
-                const double ei = s_ek[i];
-                const uint32_t ri = s_cr[i];
-                er += (ei > ek || (ei == ek && ri < r)) ? 1 : 0;
+            const int i0 = sub * chunk2, i1 = min(m, i0 + chunk2);
+            for (int i = i0; i < i1 && er < a.k; i += 2) {
+                const double2 e2 = *(const double2*)(s_ek + i);
+                const uint2 r2 = *(const uint2*)(s_cr + i);
+                er += (e2.x > ek || (e2.x == ek && r2.x < r)) ? 1 : 0;
+                if (i + 1 < i1) er += (e2.y > ek || (e2.y == ek && r2.y < r)) ? 1 : 0;
             }
         }
 #pragma unroll
