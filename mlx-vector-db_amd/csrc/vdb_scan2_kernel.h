@@ -47,6 +47,10 @@ static __device__ unsigned long long g_scan2_stamps[1 << 16][8];
 #ifndef VDB_S2_NW
 #define VDB_S2_NW 4
 #endif
+// the step's group loop: one loop with the tail selected inside (1) or the tail peeled (0)
+#ifndef VDB_S2_ONELOOP
+#define VDB_S2_ONELOOP 0
+#endif
 constexpr int S2_RT = VDB_S2_RT;  // row tiles (32 rows) per wave per step
 constexpr int S2_NW = VDB_S2_NW;  // waves per workgroup
 constexpr int S2_ROWS = S2_RT * S2_NW * 32;
@@ -414,6 +418,18 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
                 __builtin_amdgcn_sched_barrier(0);
             }
         };
+#if VDB_S2_ONELOOP
+        // one loop, the tail's refill source selected inside (as scan8: a peeled tail gave the
+        // accumulators a rotated register assignment and a shuffle through VGPRs every step)
+        for (int gb = 0; gb < G; gb += PX) {
+            const bool last = gb + PX >= G;
+            if (last && s + 1 < s_end) load_epi(s + 1, gkn, rin);
+#pragma unroll
+            for (int p = 0; p < PX; ++p)
+                group(p, gb + p, last ? xn + (size_t)p * XGSTEP : xs + (size_t)(gb + p + PX) * XGSTEP,
+                      Qbase + (size_t)(gb + p + PQ) * GSTEP);
+        }
+#else
         int gb = 0;
         for (; gb < G - PX; gb += PX) {
 #pragma unroll
@@ -424,6 +440,7 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
 #pragma unroll
         for (int p = 0; p < PX; ++p)
             group(p, gb + p, xn + (size_t)p * XGSTEP, Qbase + (size_t)(gb + p + PQ) * GSTEP);
+#endif
 
 #ifdef VDB_SCAN2_KLOOP_ONLY
         {  // diagnostic build (make variant): the K-loop alone, results are garbage

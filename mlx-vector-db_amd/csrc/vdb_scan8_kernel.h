@@ -43,6 +43,10 @@ typedef int i32x16 __attribute__((ext_vector_type(16)));
 #define VDB_S8_NW 4
 #endif
 constexpr int S8_NW = VDB_S8_NW;
+// the step's group loop: one loop with the tail selected inside (1) or the tail peeled (0)
+#ifndef VDB_S8_ONELOOP
+#define VDB_S8_ONELOOP 0
+#endif
 
 #ifdef VDB_STAMP8
 // Diagnostic build only (make variant VDEFS=-DVDB_STAMP8): per-wave cycles of scan8_kernel:
@@ -370,6 +374,25 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
                 __builtin_amdgcn_sched_barrier(0);
             }
         };
+#if VDB_S8_ONELOOP
+        // One loop over all groups, the last PX of them (whose refills read the next step's first
+        // groups) picked by a scalar select: with the tail peeled into code of its own, the
+        // register allocator gave the accumulators a rotated assignment in the loop and moved all
+        // 128 of them through VGPRs at the loop exit of every step (208 accvgpr moves, C2 I8).
+        for (int gb = 0; gb < G; gb += PX) {
+            const bool last = gb + PX >= G;
+            if (last) {
+                // the siblings' counts: issued only where the epilogue waits for them (an asm
+                // load never waited for could land in a register the compiler has reused)
+                if (pace && s + 1 < s_end) pv = s8_ld_u32(pace, poff);
+                if (s + 1 < s_end) load_epi(s + 1, rin);
+            }
+#pragma unroll
+            for (int p = 0; p < PX; ++p)
+                group(p, gb + p, last ? xn + (size_t)p * XGSTEP : xs + (size_t)(gb + p + PX) * XGSTEP,
+                      Qbase + (size_t)(gb + p + PQ) * GSTEP);
+        }
+#else
         int gb = 0;
         for (; gb < G - PX; gb += PX) {
 #pragma unroll
@@ -383,6 +406,7 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
 #pragma unroll
         for (int p = 0; p < PX; ++p)
             group(p, gb + p, xn + (size_t)p * XGSTEP, Qbase + (size_t)(gb + p + PQ) * GSTEP);
+#endif
 
         S8_STAMP(const unsigned long long st_c = S8_NOW(); st_k += st_c - st_a;)
 #ifdef VDB_SCAN8_KLOOP_ONLY
