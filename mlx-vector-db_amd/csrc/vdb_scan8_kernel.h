@@ -47,6 +47,11 @@ constexpr int S8_NW = VDB_S8_NW;
 #ifndef VDB_S8_ONELOOP
 #define VDB_S8_ONELOOP 0
 #endif
+// the epilogue's insertions: the step's thresholds reused in the first round and one round per
+// wave-uniform register index (1), or thresholds re-read and a per-lane select per hit (0)
+#ifndef VDB_S8_INS2
+#define VDB_S8_INS2 0
+#endif
 
 #ifdef VDB_STAMP8
 // Diagnostic build only (make variant VDEFS=-DVDB_STAMP8): per-wave cycles of scan8_kernel:
@@ -425,11 +430,13 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
         // ---- epilogue ----
         int thi[QT];
         bool qok[QT];
+        float thf[QT];  // the (half-)score thresholds: s_thr changes only in compaction rounds
 #pragma unroll
         for (int qt = 0; qt < QT; ++qt) {
             const int ql = qt * 32 + (lane & 31);
             const float thr = fmaxf(s_thr[ql], key_to_float(gk[qt]));
-            thi[qt] = h_floor(METRIC == 0 ? thr : 0.5f * thr, qsl[qt], invU);
+            thf[qt] = METRIC == 0 ? thr : 0.5f * thr;
+            thi[qt] = h_floor(thf[qt], qsl[qt], invU);
             qok[qt] = qb * QB + ql < B;
         }
         // The hot path: every tile's H maximum against the integer floor of its threshold
@@ -470,14 +477,27 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
                 const int ql = qt * 32 + (lane & 31);
                 uint32_t gkq = gk[0];
                 bool ok = qok[0];
+                float thq = thf[0];
 #pragma unroll
                 for (int q2 = 1; q2 < QT; ++q2)
                     if (qt == q2) {
                         gkq = gk[q2];
                         ok = qok[q2];
+                        thq = thf[q2];
                     }
+#if VDB_S8_INS2
+                // first round: the step's thresholds (no compaction since they were read);
+                // rounds after a compaction read the raised s_thr
+                float th = thq;
+                if (joined) {
+                    const float thr = fmaxf(s_thr[ql], key_to_float(gkq));
+                    th = METRIC == 0 ? thr : 0.5f * thr;
+                }
+#else
+                (void)thq;
                 const float thr = fmaxf(s_thr[ql], key_to_float(gkq));
                 const float th = METRIC == 0 ? thr : 0.5f * thr;
+#endif
                 const uint32_t cand = joined ? s_pend[wv][t][lane] : ok ? tile_valid16(mask, t0 + rt, N, lane) : 0u;
                 const uint32_t rb = (uint32_t)((t0 + rt) * 32) + 4u * (uint32_t)(lane >> 5);
                 // each lane's pass bits from 16 independent tests (no branch per register: with one
@@ -492,6 +512,33 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
                 }
                 pm &= cand;
                 uint32_t left = 0;
+#if VDB_S8_INS2
+                // one round per register index v that some lane hits (usually one): v is
+                // wave-uniform (the first hit of the first lane with hits), so the score's select
+                // runs on scalar conditions, not a 16-way compare-and-select per lane
+                for (;;) {
+                    const unsigned long long bl = __ballot(pm != 0u);
+                    if (bl == 0ull) break;
+                    const int L = (int)__builtin_ctzll(bl);
+                    const uint32_t pmL = (uint32_t)__builtin_amdgcn_readlane((int)pm, L);
+                    const int v = __builtin_amdgcn_readfirstlane(__builtin_ctz(pmL));
+                    const bool mine = (pm >> v) & 1u;
+                    pm &= ~(1u << v);
+                    if (mine) {
+                        float a_ = sv[0];  // v uniform: scalar-masked selects, no per-lane compares
+#pragma unroll
+                        for (int u = 1; u < 16; ++u) a_ = v == u ? sv[u] : a_;
+                        const float sc = METRIC == 0 ? a_ : 2.0f * a_;
+                        const int pos = atomicAdd(&s_cnt[ql], 1);
+                        if (pos < CAP) {
+                            s_sc[ql * CAP + pos] = sc;
+                            s_ix[ql * CAP + pos] = rb + (uint32_t)((v & 3) + 8 * (v >> 2));
+                        } else {
+                            left |= 1u << v;
+                        }
+                    }
+                }
+#else
                 while (__any(pm != 0u)) {
                     if (pm != 0u) {
                         const int v = __builtin_ctz(pm);
@@ -509,6 +556,7 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
                         }
                     }
                 }
+#endif
                 if (__any(left != 0u)) {
                     s_pend[wv][t][lane] = left;
                     pmask |= 1u << t;
