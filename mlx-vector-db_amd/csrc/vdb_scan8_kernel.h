@@ -52,6 +52,10 @@ constexpr int S8_NW = VDB_S8_NW;
 #ifndef VDB_S8_INS2
 #define VDB_S8_INS2 0
 #endif
+// the first round's thresholds alone (the per-lane select kept)
+#ifndef VDB_S8_INSTHR
+#define VDB_S8_INSTHR 0
+#endif
 
 #ifdef VDB_STAMP8
 // Diagnostic build only (make variant VDEFS=-DVDB_STAMP8): per-wave cycles of scan8_kernel:
@@ -485,7 +489,7 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
                         ok = qok[q2];
                         thq = thf[q2];
                     }
-#if VDB_S8_INS2
+#if VDB_S8_INS2 || VDB_S8_INSTHR
                 // first round: the step's thresholds (no compaction since they were read);
                 // rounds after a compaction read the raised s_thr
                 float th = thq;
