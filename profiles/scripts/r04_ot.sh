@@ -1,6 +1,6 @@
 #!/bin/bash
-# Insertions with the step's thresholds and a wave-uniform register index (VDB_S8_INSTHR=1: the step thresholds alone, per-lane select kept; on the base of
-# the one-loop step, lib/libvdb_amd_ot.so): its parity tests first, then the same-box A/B.
+# Insertions with the step's thresholds in the first round (VDB_S8_INSTHR=1, per-lane select kept;
+# lib/libvdb_amd_ot.so): its parity tests first, then the same-box A/B against the base library.
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/${1:-r04_ot}; mkdir -p $O
