@@ -43,6 +43,15 @@ typedef int i32x16 __attribute__((ext_vector_type(16)));
 #define VDB_S8_NW 4
 #endif
 constexpr int S8_NW = VDB_S8_NW;
+// the I8X3 L2 pass's own wave count (C4: 8 waves, two per SIMD, one wave's epilogue under the
+// other's K-loop; A/B build define -- the others keep S8_NW)
+#ifndef VDB_S8_NW_X3L
+#define VDB_S8_NW_X3L 4
+#endif
+// (the 128-query shape, QT = 4, keeps S8_NW: its host-side rows per step are scan8_rows_q4)
+constexpr int scan8_nw(int prec, int metric, int QT = 2) {
+    return prec == PREC_I8X3 && metric == 1 && QT != 4 ? VDB_S8_NW_X3L : S8_NW;
+}
 // the step's group loop: one loop with the tail selected inside (1) or the tail peeled (0)
 #ifndef VDB_S8_ONELOOP
 #define VDB_S8_ONELOOP 0
@@ -75,8 +84,13 @@ static __device__ unsigned long long g_scan8_stamps[1 << 16][10];
 #ifndef VDB_S8_RT3
 #define VDB_S8_RT3 2
 #endif
-constexpr int scan8_rt(int prec, int metric) { return prec == PREC_I8X3 || metric == 1 ? VDB_S8_RT3 : VDB_S8_RT1; }
-constexpr int scan8_rows(int prec, int metric) { return scan8_rt(prec, metric) * S8_NW * 32; }
+// (the 8-wave I8X3 L2 shape: one row tile per wave, the same rows per step with 256 registers)
+constexpr int scan8_rt(int prec, int metric) {
+    return prec == PREC_I8X3 && metric == 1 && VDB_S8_NW_X3L == 8 ? 1
+           : prec == PREC_I8X3 || metric == 1                   ? VDB_S8_RT3
+                                                                : VDB_S8_RT1;
+}
+constexpr int scan8_rows(int prec, int metric) { return scan8_rt(prec, metric) * scan8_nw(prec, metric) * 32; }
 
 template <int PREC>
 struct Planes8 {
@@ -191,7 +205,7 @@ __device__ __forceinline__ int h_floor(float th, float slack, float invU) {
 // Per-batch scalars written by prep8 (device): [0] uH = s_x s_q, [1] uL = uH / 256, [2] 1 / uH.
 template <int PREC, int METRIC, int QT, int PX, int KP, int CAP, bool NT, bool QLDS, bool FLAGSYNC, int GC = 0,
           int RT_ = scan8_rt(PREC, METRIC), int KW = KP>
-__global__ void __launch_bounds__(64 * S8_NW, 1)
+__global__ void __launch_bounds__(64 * scan8_nw(PREC, METRIC, QT), 1)
 scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, const uint32_t* __restrict__ mask,
              const float* __restrict__ Qq, const float* __restrict__ lsl, const float* __restrict__ qscal, int G_arg,
              int64_t N, int B, int64_t n_steps, int steps_per_wg, int n_qb, float* __restrict__ gl_s,
@@ -199,7 +213,7 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
              uint32_t* __restrict__ pace, uint32_t pace_tag, const int* __restrict__ gate) {
     // a gated launch (the device-memory re-pass, vdb_api.cpp): nothing to do when its count is 0
     if (gate && *gate == 0) return;
-    constexpr int RT = RT_, NW = S8_NW;
+    constexpr int RT = RT_, NW = scan8_nw(PREC, METRIC, QT);
     constexpr int QB = 32 * QT;
     constexpr int XPL = Planes8<PREC>::XPL, QPL = Planes8<PREC>::QPL;
     constexpr bool HL = Planes8<PREC>::L;
@@ -216,7 +230,7 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
     __shared__ int s_cnt[QB];
     __shared__ float s_thr[QB];
     __shared__ int s_need, s_done;
-    __shared__ uint32_t s_pend[S8_NW][8][64];  // per wave and tile: each lane's entries left for a compaction round
+    __shared__ uint32_t s_pend[NW][8][64];  // per wave and tile: each lane's entries left for a compaction round
     extern __shared__ __attribute__((aligned(16))) float s_q[];  // QLDS: [G][LQP planes][QT][256]
 
     const int lane = threadIdx.x & 63;
@@ -680,7 +694,7 @@ static hipError_t scan8_launch_g(const float* Xq, const float* rinit, const uint
         }
     }
     const int n_wg8 = (n_wg + 7) / 8 * 8;
-    hipLaunchKernelGGL(k, dim3(n_wg8 * n_qblocks), dim3(64 * S8_NW), lds, st, Xq, rinit, mask, Qq, lsl, qscal, G, N, B,
+    hipLaunchKernelGGL(k, dim3(n_wg8 * n_qblocks), dim3(64 * scan8_nw(P, M, QT)), lds, st, Xq, rinit, mask, Qq, lsl, qscal, G, N, B,
                        n_steps, spw, n_qblocks, gl_s, gl_i, gl_cnt, gl_cap, gthr, n_qblocks > 1 ? pace : nullptr,
                        pace_tag, gate);
     return hipGetLastError();
@@ -725,7 +739,7 @@ inline int scan8_cap(int KP, bool ql) { return KP == 128 ? 192 : KP == 256 ? (ql
 inline bool scan8_qlds(int G8, int KP, int prec, bool small) {
     const size_t q = (size_t)G8 * (prec == PREC_I8X3 ? 2 : 1) * 2 * 1024;
     if (small) return q <= 32 * 1024;
-    const size_t lists = (size_t)64 * scan8_cap(KP, true) * 8 + S8_NW * 2048 + 1024;
+    const size_t lists = (size_t)64 * scan8_cap(KP, true) * 8 + 8 * 2048 + 1024;  // s_pend of up to 8 waves
     return lists + q <= 160 * 1024;
 }
 
