@@ -43,10 +43,11 @@ typedef int i32x16 __attribute__((ext_vector_type(16)));
 #define VDB_S8_NW 4
 #endif
 constexpr int S8_NW = VDB_S8_NW;
-// the I8X3 L2 pass's own wave count (C4: 8 waves, two per SIMD, one wave's epilogue under the
-// other's K-loop; A/B build define -- the others keep S8_NW)
+// the I8X3 L2 pass's own wave count: 8 waves, two per SIMD, one wave's epilogue under the other's
+// K-loop (C4 scan 2.92 -> 2.77 ms, +4% QPS, profiles/r04_ab/x8; build define, 4 = the old shape).
+// The others keep S8_NW = 4 (8 waves there: C2 -15%, C3 -25%, C6 -6%, profiles/r04_ab/nw8).
 #ifndef VDB_S8_NW_X3L
-#define VDB_S8_NW_X3L 4
+#define VDB_S8_NW_X3L 8
 #endif
 // (the 128-query shape, QT = 4, keeps S8_NW: its host-side rows per step are scan8_rows_q4)
 constexpr int scan8_nw(int prec, int metric, int QT = 2) {
