@@ -62,16 +62,13 @@ CONFIGS = {
 # over the GPUs (configs[3] "batch=512 ... sharded across 8"; the metric's "10M x 128D @8 GPU" at
 # batch 64) keep that batch (strong scaling); the single-GPU configs run B per GPU (weak scaling)
 DEFAULT_SCALING = {"c4": "strong", "c6": "strong"}
-# the binding roofline of each config's algorithmic work (fp32 arithmetic on fp32
-# rows): C2 / C4 (and c6, same intensity 2 B D / 4 D = B/2 F/B above the fp32 ridge) FP32-MFMA,
-# C3 HBM with the bf16 corpus it names (2 B per element)
-SURVEY_BOUND = {"c1": "hbm", "c2": "mfma_fp32", "c3": "hbm", "c4": "mfma_fp32", "c6": "mfma_fp32"}
 GRAPH_M, GRAPH_EF = 16, 128
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md, Peak FP32 (matrix)
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md, Peak BF16 MFMA, dense
 I8_MFMA_PEAK_TOPS = 5000.0      # MI355X_MICROARCH.md, I8 MFMA: 2x BF16 per clock (2x the K), dense
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md, HBM3E peak (spec)
 CHUNK_ROWS = 1 << 16
+_HOST_CORPUS = {}  # (N, D, lo, hi) -> host parts of a corpus the next sub-record reuses
 
 
 def corpus_rows(N, D, start, stop, seed=0):
@@ -85,6 +82,31 @@ def corpus_rows(N, D, start, stop, seed=0):
         lo, hi = c * CHUNK_ROWS, min((c + 1) * CHUNK_ROWS, N)
         blk = np.random.Generator(np.random.PCG64(np.random.SeedSequence([seed, c]))).random((hi - lo, D),
                                                                                             dtype=np.float32)
+        a, b = max(lo, start), min(hi, stop)
+        out[a - start:b - start] = blk[a - lo:b - lo]
+    return out
+
+
+CLUSTERS, CLUSTER_SIGMA = 10_000, 0.1
+
+
+def cluster_centres(D, seed=0):
+    return np.random.Generator(np.random.PCG64(np.random.SeedSequence([seed, 1 << 30]))).random((CLUSTERS, D),
+                                                                                                dtype=np.float32)
+
+
+def corpus_rows_clustered(N, D, start, stop, seed=0, centres=None):
+    """Rows [start, stop) of a structured corpus (the graph's case): each row a
+    uniform centre of CLUSTERS plus N(0, CLUSTER_SIGMA^2) per dimension, chunk-seeded like
+    corpus_rows so any shard is reproducible alone."""
+    C = cluster_centres(D, seed) if centres is None else centres
+    out = np.empty((stop - start, D), np.float32)
+    c0, c1 = start // CHUNK_ROWS, (stop - 1) // CHUNK_ROWS
+    for c in range(c0, c1 + 1):
+        lo, hi = c * CHUNK_ROWS, min((c + 1) * CHUNK_ROWS, N)
+        g = np.random.Generator(np.random.PCG64(np.random.SeedSequence([seed, c, 7])))
+        lab = g.integers(0, CLUSTERS, hi - lo)
+        blk = C[lab] + g.standard_normal((hi - lo, D), dtype=np.float32) * np.float32(CLUSTER_SIGMA)
         a, b = max(lo, start), min(hi, stop)
         out[a - start:b - start] = blk[a - lo:b - lo]
     return out
@@ -222,8 +244,11 @@ def main_graph(args, world, rank, local, dev):
     ix.reserve(N)
     keep_host = world == 1 and rank == 0 and not args.no_cpu_baseline
     parts = []
+    clustered = args.data == "clustered"
+    cen = cluster_centres(D) if clustered else None
     for s0 in range(0, N, 8 * CHUNK_ROWS):
-        part = corpus_rows(N, D, s0, min(s0 + 8 * CHUNK_ROWS, N))
+        part = (corpus_rows_clustered(N, D, s0, min(s0 + 8 * CHUNK_ROWS, N), centres=cen) if clustered
+                else corpus_rows(N, D, s0, min(s0 + 8 * CHUNK_ROWS, N)))
         ix.add(part)
         if keep_host:
             parts.append(part)
@@ -232,7 +257,12 @@ def main_graph(args, world, rank, local, dev):
     build_s = time.perf_counter() - t0
     g.set_param("teams", args.teams)
     nq = args.warmup + args.steps
-    Q = np.random.default_rng(1 + rank).random((nq, D), dtype=np.float32)
+    qrng = np.random.default_rng(1 + rank)
+    if clustered:  # queries from the same distribution: a centre plus the rows' noise
+        Q = (cen[qrng.integers(0, CLUSTERS, nq)] + qrng.standard_normal((nq, D), dtype=np.float32) *
+             np.float32(CLUSTER_SIGMA)).astype(np.float32)
+    else:
+        Q = qrng.random((nq, D), dtype=np.float32)
     q_dev = torch.from_numpy(Q).to(dev)
     lab = torch.empty((nq, k), dtype=torch.int64, device=dev)
     dst = torch.empty((nq, k), dtype=torch.float32, device=dev)
@@ -324,8 +354,12 @@ def main_graph(args, world, rank, local, dev):
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic uniform [0,1) fp32 (numpy PCG64, corpus seed 0 per 65536-row chunk, queries seed 1)",
-            "config": {"workload": f"c5: {desc}", "n_rows": N, "dim": D, "global_batch": 1, "k": k,
+            "data": ("synthetic uniform [0,1) fp32 (numpy PCG64, corpus seed 0 per 65536-row chunk, queries seed 1)"
+                     if not clustered else
+                     f"synthetic clustered fp32: {CLUSTERS} uniform [0,1) centres + N(0, {CLUSTER_SIGMA}^2) per "
+                     "dimension (corpus seed 0 per 65536-row chunk; queries the same distribution, seed 1)"),
+            "config": {"workload": f"c5: {desc}" + (" [clustered data]" if clustered else ""), "n_rows": N, "dim": D,
+                       "global_batch": 1, "k": k,
                        "metric": metric, "ef": GRAPH_EF, "degree": R, "build_knn": knn, "entries": N_ENTRIES,
                        "teams": args.teams,
                        "parallelism": f"replicas x{world}" if world > 1 else "single GPU"},
@@ -394,6 +428,8 @@ def main():
                     help="default: c2 (BASELINE.json configs[1]) plus the metric's 8-GPU workload c6 as a sub-record")
     ap.add_argument("--no-metric-workload", action="store_true",
                     help="default run: skip the c6 sub-record (the metric's 10M x 128 workload)")
+    ap.add_argument("--no-other-configs", action="store_true",
+                    help="default run: skip the c3 / c4 sub-records (BASELINE.json configs[2], [3])")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-serving", action="store_true",
                     help="c1/c2 at N=1: skip the store-API serving numbers (batch-1 p50, 4-thread QPS)")
@@ -444,6 +480,9 @@ def main():
     ap.add_argument("--graph-knn", type=int, default=None, help="c5: kNN candidates per row for the build")
     ap.add_argument("--teams", type=int, default=64, help="c5: workgroups per query (vdb_graph_set_param teams)")
     ap.add_argument("--teams-sweep", default="1,16,256", help="c5: extra teams settings reported beside the line")
+    ap.add_argument("--data", default="uniform", choices=["uniform", "clustered"],
+                    help="c5: the corpus (BASELINE's uniform [0,1) rows, or rows around cluster centres: the "
+                         "structured data a graph index is for)")
     ap.add_argument("--pmc-json", default=None,
                     help="HBM traffic of the scan kernel from a separate rocprofv3 --pmc pass "
                          "(default: newest profiles/*/pmc.json for this config, see profiles/scripts/)")
@@ -469,18 +508,27 @@ def main():
 
     cfg = args.config or "c2"
     rec = bench_brute(cfg, args, world, rank, local, dev, primary=True)
-    if args.config is None and not args.no_metric_workload:
-        # the default run also measures the second half of BASELINE.json's metric, "10M x 128D @8
-        # GPU" (c6: cosine top-10, batch 64, row-sharded over the ranks with the batch fixed), on
-        # the same ranks: the driver's N = 1, 2, 4, 8 series then carries both workloads
-        sub = bench_brute("c6", args, world, rank, local, dev, primary=False)
-        if rank == 0:
-            rec["metric_workload_10m_x_128"] = {
-                k_: sub[k_] for k_ in ("value", "unit", "n_gpus", "steps", "ms_per_step", "p50_ms", "scaling", "dtype",
-                                       "config", "fallback_queries_timed")}
-            rec["metric_workload_10m_x_128"]["roofline"] = {
-                k_: sub["roofline"][k_] for k_ in ("bound", "achieved", "peak", "unit", "frac", "avg_launch_ms",
-                                                   "precision", "basis", "survey_8d")}
+    if args.config is None:
+        # The default run also measures, on the same ranks, as compact sub-records (so the driver's
+        # N = 1, 2, 4, 8 series carries them all):
+        #   c6, the second half of BASELINE.json's metric, "10M x 128D @8 GPU" (cosine top-10,
+        #       batch 64, row-sharded with the batch fixed);
+        #   c3 and c4, BASELINE.json's configs[2] and [3] (the reference's own
+        #       harness reports every shape it runs, benchmarks/large_scale_benchmark.py:32-104).
+        subs = [] if args.no_metric_workload else [("metric_workload_10m_x_128", "c6")]
+        if not args.no_other_configs:
+            subs += [("config_c3", "c3"), ("config_c4", "c4")]
+        for key, scfg in subs:
+            sub = bench_brute(scfg, args, world, rank, local, dev, primary=False)
+            if rank == 0:
+                rec[key] = {k_: sub[k_] for k_ in ("value", "unit", "n_gpus", "steps", "ms_per_step", "p50_ms",
+                                                   "scaling", "dtype", "config", "fallback_queries_timed",
+                                                   "fallback_queries_total")}
+                rec[key]["roofline"] = {
+                    k_: sub["roofline"][k_] for k_ in ("bound", "achieved", "peak", "unit", "frac", "traffic",
+                                                       "traffic_source", "avg_launch_ms", "precision", "basis",
+                                                       "fp32_equivalent")}
+        _HOST_CORPUS.clear()
     if rank == 0:
         print(json.dumps(rec), flush=True)
     if world > 1:
@@ -550,8 +598,14 @@ def bench_brute(cfg, args, world, rank, local, dev, primary=True):
     # candidate pass -- the device re-pass's case, measured against the plain line
     plant = int(args.plant_close or 0) if world == 1 else 0
     targets = [7 + 4001 * j for j in range(plant)]
+    # the default run's c6 and c4 sub-records share their corpus (10M x 128, seed 0): generated once
+    ckey = (N, D, lo, hi)
+    cached = _HOST_CORPUS.get(ckey) if not plant else None
+    keep_for_next = not plant and not primary and cfg == "c6"
     for s in range(lo, hi, 8 * CHUNK_ROWS):
-        part = corpus_rows(N, D, s, min(s + 8 * CHUNK_ROWS, hi))
+        part = cached[(s - lo) // (8 * CHUNK_ROWS)] if cached else corpus_rows(N, D, s, min(s + 8 * CHUNK_ROWS, hi))
+        if keep_for_next:
+            _HOST_CORPUS.setdefault(ckey, []).append(part)
         if plant and s == lo:
             prng = np.random.default_rng(99)
             for j, t in enumerate(targets):
@@ -657,11 +711,12 @@ def bench_brute(cfg, args, world, rank, local, dev, primary=True):
         #     values, the queries; its own MFMA count (fp32: 2BND on the FP32 peak; bf16 2x and
         #     bf16x3 3x the products on the bf16 peak; i8 1x (xh qh) and i8x3 3x on the int8 peak) -- bound
         #     by whichever floor is longer;
-        # (2) "survey_8d": SURVEY.md §8(d)'s algorithmic work for the config (fp32 arithmetic:
-        #     2BND flops, 4 B per element; C3 names the bf16 corpus, 2 B) on the roofline §8(d) calls
-        #     binding.  frac > 1 there means the kernel does that fp32-equivalent work in cheaper
-        #     MFMAs (split bf16) than §8(d)'s FP32-MFMA roofline assumes; exactness comes from the
-        #     fp64 rerank + certificate.
+        # (2) "fp32_equivalent": SURVEY.md §8(d)'s algorithmic work for the config (fp32 arithmetic:
+        #     2BND flops, 4 B per element; C3 names the bf16 corpus, 2 B) per launch, reported as a
+        #     RATE only.  The kernel does not read the fp32 rows nor issue fp32 MFMAs (int8 /
+        #     split-bf16 candidates + an exact fp64 rerank), so that work over the
+        #     launch time is not a fraction of any roofline (it exceeded 1); the
+        #     roofline fraction is the implementation's, above.
         Dp = (D + 63) // 64 * 64
         elem = {"i8": 1, "i8x3": 2, "bf16": 2}.get(prec, 4)
         q_elem = {"i8": 1, "i8x3": 2}.get(prec, 4)  # query tiles (i8: the hi plane; i8x3: both 1-byte planes)
@@ -683,19 +738,14 @@ def bench_brute(cfg, args, world, rank, local, dev, primary=True):
         roof["basis"] = (f"implementation: {elem} B per corpus element read once + queries; "
                          f"{n_mfma} MFMA product(s) per fp32 product "
                          f"({ {'fp32': 'fp32', 'i8': 'int8', 'i8x3': 'int8'}.get(prec, 'bf16')} peak)")
-        s_bound = SURVEY_BOUND.get(cfg, "mfma_fp32")
         s_flops = 2.0 * Bg * n_local * D
         s_bytes = n_local * D * (2 if cfg == "c3" else 4) + 4 * n_local + 4 * Bg * D + 12 * Bg * k
-        if s_bound == "hbm":
-            s_ach = s_bytes / (scan_ms * 1e-3) / 1e9
-            survey = {"bound": "hbm", "work": s_bytes, "work_unit": "B", "achieved": s_ach, "peak": HBM_PEAK_GBS,
-                      "unit": "GB/s", "frac": s_ach / HBM_PEAK_GBS}
-        else:
-            s_ach = s_flops / (scan_ms * 1e-3) / 1e12
-            survey = {"bound": "mfma_fp32", "work": s_flops, "work_unit": "FLOP", "achieved": s_ach,
-                      "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": s_ach / FP32_MFMA_PEAK_TFLOPS}
-        survey["note"] = ("SURVEY.md §8(d) work per launch (fp32: 2BND flops, 4 B/element; c3: bf16 corpus); "
-                          "frac > 1 = the fp32-equivalent work done in split-bf16 / int8 MFMAs with an exact fp64 rerank")
+        fp32_eq = {"flops_per_launch": s_flops, "bytes_per_launch": s_bytes,
+                   "tflops_equivalent": s_flops / (scan_ms * 1e-3) / 1e12,
+                   "gbs_equivalent": s_bytes / (scan_ms * 1e-3) / 1e9,
+                   "note": "SURVEY.md §8(d) fp32 work per launch (2BND flops, 4 B/element; c3: 2 B) over the scan's "
+                           "launch time: a throughput, not a roofline fraction (the scan reads the int8 / bf16 "
+                           "copy, not the fp32 rows)"}
         traffic = None
         traffic_src = None
         cands = [args.pmc_json] if (args.pmc_json and primary) else sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc.json")))
@@ -732,7 +782,7 @@ def bench_brute(cfg, args, world, rank, local, dev, primary=True):
                        "rows_per_gpu": n_local},
             "roofline": dict(roof, traffic=traffic,
                              kernel={"fp32": "scan_topk", "i8": "scan8_kernel", "i8x3": "scan8_kernel"}.get(prec, "scan2_kernel"),
-                             survey_8d=survey, precision=prec,
+                             fp32_equivalent=fp32_eq, precision=prec,
                              precision_requested=args.precision, searches_by_precision=by_prec,
                              traffic_source=traffic_src, algorithmic_bytes=hbm_bytes, algorithmic_flops=mfma_flops,
                              avg_launch_ms=scan_ms, hbm_gbs=achieved_gbs, mfma_tflops=achieved_tf,

@@ -104,7 +104,9 @@ struct vdb_index {
     int64_t cap_rows = 0;  // multiple of kRowAlign
     float* X = nullptr;   // row-major fp32 [cap_rows][Dp] (rerank, exact scan, export, graph)
     float* Xs = nullptr;  // the candidate pass's copy, same bytes: split-bf16 tiles (PREC_BF16X3 / BF16 /
-                          // AUTO) or fp32 tiles (PREC_FP32), rebuilt from X when the precision class changes
+                          // AUTO) or fp32 tiles (PREC_FP32), rebuilt from X when the precision class changes.
+                          // AUTO with the int8 copy allocates it lazily, on the first search that runs a
+                          // split pass (a hold, a host re-pass or retry): ensure_xs
     float* Xq = nullptr;  // the int8 copy (PREC_I8 / I8X3, AUTO with auto_i8): half the bytes of X
     // its xh plane row-major [cap][Dp] (with Xq): the finish refines I8 candidates' scores with
     // the query's rounding residual, reading each candidate's row whole (vdb_exact.hip)
@@ -133,6 +135,10 @@ struct vdb_index {
     int64_t dir_rows = 0;  // rows dir / mu / sx were derived from (re-derived as the index doubles, up to kDirRows)
     unsigned long long* d_i8 = nullptr;
     double i8st[6] = {0, 0, 0, 0, 0, 0};
+    // the int8 pass's checksum (vdb_scan8.hip): column sums (mod 2^32) of the int8 copy's xh and
+    // xl planes over rows [0, count), [2][Dp]; kept by build_candidate_rows
+    uint32_t* d_csum = nullptr;
+    int64_t scan_checksum = 1;  // knob: 1 the pass's sums are checked by the finish, 0 off (A/B)
     // VDB_PREC_AUTO's candidate copy: the int8 one (I8 / I8X3) when set, else the split-bf16 one
     bool auto_i8 = true;
     hipStream_t stream = nullptr;
@@ -202,10 +208,12 @@ struct vdb_index {
     int64_t scan_q4 = -1;      // split pass 128-query shape (D <= 128, KP = 128, B >= 256): -1 auto, 0 off, 1 on
     // stats
     std::atomic<int64_t> n_searches{0}, n_queries{0}, n_fallback{0}, n_overflow{0}, n_incons{0}, n_repass{0}, n_scan3{0}, n_q4{0};
+    std::atomic<int64_t> n_xs_builds{0};  // lazy builds of the split copy (ensure_xs)
     std::atomic<int64_t> n_by_prec[N_PREC] = {{0}, {0}, {0}, {0}, {0}};  // candidate passes per PREC_* (VDB_PREC_AUTO's choices)
     std::atomic<int64_t> scan_ns{0}, pipe_ns{0}, n_timed{0};
     unsigned long long* d_totals = nullptr;  // device: flagged / overflowed / flagged-in-bf16 queries of device-gated searches
     std::shared_mutex mu;  // add/clear/reserve exclusive; search shared
+    std::mutex xs_mu;      // the lazy split copy's allocation + build (under the shared lock)
     std::mutex ws_mu;
     std::vector<Workspace*> pool;
     // last work queued on each caller stream by searches without a workspace (graph searches):
@@ -243,6 +251,15 @@ int xs_kind(int64_t precision) {
 bool needs_i8(int64_t precision, bool auto_i8) {
     return precision == VDB_PREC_I8 || precision == VDB_PREC_I8X3 || (precision == VDB_PREC_AUTO && auto_i8);
 }
+// Settings whose candidate pass reads Xs on every search keep it allocated and up to date from the
+// start; AUTO with the int8 copy reads it only for holds, host re-passes and retries, so it is
+// built on first use (ensure_xs): 7 instead of 11 B per element (fp32 rows 4, int8 planes 2, the
+// row-major xh 1) while no search needs it.  I8 / I8X3 never read it.
+bool xs_eager(const vdb_index* ix) {
+    const int kind = xs_kind(ix->precision);
+    return kind == kXsFp32 || (kind == kXsSplit && !(ix->precision == VDB_PREC_AUTO && ix->auto_i8));
+}
+float* xs_ptr(const vdb_index* ix) { return __atomic_load_n(&ix->Xs, __ATOMIC_ACQUIRE); }
 
 // The candidate copies of rows [row0, row0 + n) from the row-major rows (tiles: whole row tiles;
 // the int8 copy row by row, its statistics into d_i8).  xs / xq: which copies to build.
@@ -250,10 +267,15 @@ hipError_t build_candidate_rows(const vdb_index* ix, int64_t row0, int64_t n, hi
                                 bool xq = true) {
     const float* inv = ix->metric == VDB_METRIC_COSINE ? ix->inv32 : nullptr;
     hipError_t e = hipSuccess;
-    if (xs && xs_kind(ix->precision) == kXsFp32) e = launch_tile_rows(ix->X, ix->G, row0, n, ix->Xs, st);
-    if (xs && xs_kind(ix->precision) == kXsSplit) e = launch_split_rows(ix->X, ix->G, row0, n, inv, ix->Xs, st);
-    if (e == hipSuccess && xq && needs_i8(ix->precision, ix->auto_i8))
-        e = launch_quant_rows(ix->X, inv, ix->d_mu, ix->d_dir, ix->sx, row0, n, ix->G, ix->Xq, ix->d_i8, st, ix->Xh);
+    if (xs && ix->Xs && xs_kind(ix->precision) == kXsFp32) e = launch_tile_rows(ix->X, ix->G, row0, n, ix->Xs, st);
+    if (xs && ix->Xs && xs_kind(ix->precision) == kXsSplit) e = launch_split_rows(ix->X, ix->G, row0, n, inv, ix->Xs, st);
+    if (e == hipSuccess && xq && needs_i8(ix->precision, ix->auto_i8)) {
+        // (rows [0, n) rebuild the whole copy: its column sums start again)
+        if (row0 == 0) e = hipMemsetAsync(ix->d_csum, 0, (size_t)2 * ix->Dp * sizeof(uint32_t), st);
+        if (e == hipSuccess)
+            e = launch_quant_rows(ix->X, inv, ix->d_mu, ix->d_dir, ix->sx, row0, n, ix->G, ix->Xq, ix->d_i8, st, ix->Xh);
+        if (e == hipSuccess) e = launch_colsum8(ix->Xq, row0, n, ix->G / 4, ix->d_csum, st);
+    }
     return e;
 }
 
@@ -264,6 +286,11 @@ hipError_t read_i8_stats(vdb_index* ix, hipStream_t st) {
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e == hipSuccess) std::memcpy(ix->i8st, b, sizeof(b));
     return e;
+}
+
+bool debug_knobs_enabled() {
+    const char* e = std::getenv("VDB_DEBUG_KNOBS");
+    return e && std::strcmp(e, "1") == 0;
 }
 
 int ensure_capacity(vdb_index* ix, int64_t rows) {
@@ -299,8 +326,10 @@ int ensure_capacity(vdb_index* ix, int64_t rows) {
         if (_e != hipSuccess) return fail(_e, #expr); \
     } while (0)
     CAP_TRY(hipMalloc(&X, x_bytes));
-    CAP_TRY(hipMalloc(&Xs, x_bytes));
-    CAP_TRY(hipMemsetAsync(Xs, 0, x_bytes, ix->stream));
+    if (ix->Xs || xs_eager(ix)) {  // (AUTO with the int8 copy: lazily, ensure_xs)
+        CAP_TRY(hipMalloc(&Xs, x_bytes));
+        CAP_TRY(hipMemsetAsync(Xs, 0, x_bytes, ix->stream));
+    }
     // the int8 copy only where a setting reads it (FP32 / BF16X3 / BF16 / AUTO without
     // auto_int8 never do; set_param allocates it when a setting starts to, ensure_xq)
     const bool with_xq = ix->Xq || needs_i8(ix->precision, ix->auto_i8);
@@ -323,8 +352,9 @@ int ensure_capacity(vdb_index* ix, int64_t rows) {
         const int64_t used_tiles = round_up(ix->count, 128) / 32;  // whole super tiles (prefix of the layout)
         CAP_TRY(hipMemcpyAsync(X, ix->X, (size_t)ix->count * ix->Dp * sizeof(float), hipMemcpyDeviceToDevice,
                                ix->stream));
-        CAP_TRY(hipMemcpyAsync(Xs, ix->Xs, (size_t)used_tiles * tile_floats * sizeof(float), hipMemcpyDeviceToDevice,
-                               ix->stream));
+        if (Xs && ix->Xs)
+            CAP_TRY(hipMemcpyAsync(Xs, ix->Xs, (size_t)used_tiles * tile_floats * sizeof(float),
+                                   hipMemcpyDeviceToDevice, ix->stream));
         if (Xq && ix->Xq)
             CAP_TRY(hipMemcpyAsync(Xq, ix->Xq, (size_t)used_tiles * tile_floats * sizeof(float) / 2,
                                    hipMemcpyDeviceToDevice, ix->stream));
@@ -378,6 +408,34 @@ int ensure_xq(vdb_index* ix) {
     }
     ix->Xq = Xq;
     ix->Xh = Xh;
+    return VDB_OK;
+}
+
+// The candidate copy Xs for a search that runs a split (or fp32) pass while it is not allocated
+// (AUTO with the int8 copy: xs_eager).  Called under the index's shared lock (no add, growth or
+// clear runs meanwhile); concurrent searches serialise on xs_mu, and the first allocates it, builds
+// rows [0, count) on the index's stream and waits, then publishes the pointer.
+int ensure_xs(vdb_index* ix) {
+    if (xs_ptr(ix) || ix->cap_rows == 0 || xs_kind(ix->precision) == kXsNone) return VDB_OK;
+    std::lock_guard<std::mutex> lg(ix->xs_mu);
+    if (ix->Xs) return VDB_OK;
+    const size_t bytes = (size_t)(ix->cap_rows / 32) * ix->G * BLOCK_FLOATS * sizeof(float);
+    float* Xs = nullptr;
+    hipError_t e = hipMalloc(&Xs, bytes);
+    if (e == hipSuccess) e = hipMemsetAsync(Xs, 0, bytes, ix->stream);
+    if (e == hipSuccess && ix->count > 0) {
+        const float* inv = ix->metric == VDB_METRIC_COSINE ? ix->inv32 : nullptr;
+        e = xs_kind(ix->precision) == kXsFp32 ? launch_tile_rows(ix->X, ix->G, 0, ix->count, Xs, ix->stream)
+                                              : launch_split_rows(ix->X, ix->G, 0, ix->count, inv, Xs, ix->stream);
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(ix->stream);
+    if (e != hipSuccess) {
+        if (Xs) (void)hipFree(Xs);
+        return set_error(e == hipErrorOutOfMemory ? VDB_ERR_OOM : VDB_ERR_HIP, "split candidate copy: %s",
+                         hipGetErrorString(e));
+    }
+    __atomic_store_n(&ix->Xs, Xs, __ATOMIC_RELEASE);
+    ix->n_xs_builds++;
     return VDB_OK;
 }
 
@@ -624,6 +682,8 @@ int32_t vdb_index_create(int32_t dim, int32_t metric, int32_t device, vdb_index*
     if (e == hipSuccess) e = hipMemset(ix->d_xmax, 0, 64);
     if (e == hipSuccess) e = hipMalloc(&ix->d_i8, 64);
     if (e == hipSuccess) e = hipMemset(ix->d_i8, 0, 64);
+    if (e == hipSuccess) e = hipMalloc(&ix->d_csum, (size_t)2 * ix->Dp * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemset(ix->d_csum, 0, (size_t)2 * ix->Dp * sizeof(uint32_t));
     if (e != hipSuccess) {
         delete ix;
         return set_error(VDB_ERR_HIP, "index setup failed: %s", hipGetErrorString(e));
@@ -666,6 +726,7 @@ int32_t vdb_index_destroy(vdb_index* ix) {
     if (ix->d_dir) (void)hipFree(ix->d_dir);
     if (ix->d_mu) (void)hipFree(ix->d_mu);
     if (ix->d_i8) (void)hipFree(ix->d_i8);
+    if (ix->d_csum) (void)hipFree(ix->d_csum);
     if (ix->d_totals) (void)hipFree(ix->d_totals);
     if (ix->h_totals) (void)hipHostFree(ix->h_totals);
     for (auto& kv : ix->uses) (void)hipEventDestroy(kv.second);
@@ -706,8 +767,14 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
             if (xr) return xr;
         }
         ix->precision = value;
-        if ((xs || xq) && ix->Xs && ix->count > 0) {
-            HIP_TRY(build_candidate_rows(ix, 0, ix->count, ix->stream, xs, xq));
+        bool built = false;
+        if (!ix->Xs && xs_eager(ix)) {  // a setting that reads it on every search: allocated + built now
+            const int xr = ensure_xs(ix);
+            if (xr) return xr;
+            built = true;
+        }
+        if (((xs && !built) || xq) && ix->X && ix->count > 0) {
+            HIP_TRY(build_candidate_rows(ix, 0, ix->count, ix->stream, xs && !built, xq));
             HIP_TRY(read_i8_stats(ix, ix->stream));
         }
     } else if (n == "auto_int8") {  // VDB_PREC_AUTO's candidate copy: 1 int8, 0 split-bf16
@@ -723,7 +790,11 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
             if (xr) return xr;
         }
         ix->auto_i8 = v;
-        if (xq && ix->Xs && ix->count > 0) {
+        if (!ix->Xs && xs_eager(ix)) {  // AUTO on the split copy alone: reads it on every search
+            const int xr = ensure_xs(ix);
+            if (xr) return xr;
+        }
+        if (xq && ix->X && ix->count > 0) {
             HIP_TRY(build_candidate_rows(ix, 0, ix->count, ix->stream, false, true));
             HIP_TRY(read_i8_stats(ix, ix->stream));
         }
@@ -792,6 +863,24 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
     } else if (n == "device_repass") {
         if (value < -1 || value > 1) return set_error(VDB_ERR_INVALID, "device_repass must be -1, 0 or 1");
         ix->device_repass = value;
+    } else if (n.rfind("debug_", 0) == 0 && !debug_knobs_enabled()) {
+        // test-only knobs corrupt the index on purpose: only with VDB_DEBUG_KNOBS=1
+        return set_error(VDB_ERR_INVALID, "'%s' is a test-only knob (set VDB_DEBUG_KNOBS=1)", name);
+    } else if (n == "debug_negate_row8") {
+        // TEST ONLY: negates both int8 planes of row `value` (the column sums untouched): a corpus
+        // operand the int8 pass reads wrong, which under-scores a row that matches the query --
+        // the side the finish's approx-vs-exact check cannot see; the pass's checksum flags it
+        HIP_TRY(hipSetDevice(ix->device));
+        std::unique_lock<std::shared_mutex> g(ix->mu);
+        if (value < 0 || value >= ix->count || !ix->Xq)
+            return set_error(VDB_ERR_INVALID, "debug_negate_row8: no int8 row %lld", (long long)value);
+        const int wr = wait_idle(ix);
+        if (wr) return wr;
+        HIP_TRY(launch_negate_row8(ix->Xq, value, ix->G / 4, ix->stream));
+        HIP_TRY(hipStreamSynchronize(ix->stream));
+    } else if (n == "scan_checksum") {
+        if (value < 0 || value > 1) return set_error(VDB_ERR_INVALID, "scan_checksum must be 0 or 1");
+        ix->scan_checksum = value;
     } else if (n == "debug_stale_rinit") {
         // TEST ONLY: plants a stale L2 start value, -|x|^2/2 := 0 for row `value` (the operand a
         // scan read before its load landed in VERDICT r3), so the consistency guard of the
@@ -853,8 +942,11 @@ int32_t vdb_index_get_stat(const vdb_index* cix, const char* name, int64_t* valu
     else if (n == "searches_i8x3") *value = ix->n_by_prec[PREC_I8X3].load();
     else if (n == "auto_int8") *value = ix->auto_i8 ? 1 : 0;
     else if (n == "i8_wide") *value = ix->i8_wide ? 1 : 0;
-    else if (n == "device_bytes")
-        *value = (int64_t)(ix->cap_rows / 32) * ix->G * BLOCK_FLOATS * (ix->Xq ? 11 : 8) + ix->cap_rows * 20;  // X, Xs (+ Xq, Xh)
+    else if (n == "device_bytes") {  // the row buffers actually allocated
+        const int64_t xb = (int64_t)(ix->cap_rows / 32) * ix->G * BLOCK_FLOATS * 4;  // fp32 X: 4 B per element
+        *value = xb + (xs_ptr(ix) ? xb : 0) + (ix->Xq ? xb / 2 : 0) + (ix->Xh ? xb / 4 : 0) + ix->cap_rows * 20;
+    } else if (n == "split_copy") *value = xs_ptr(ix) ? 1 : 0;
+    else if (n == "split_copy_builds") *value = ix->n_xs_builds.load();
     else return set_error(VDB_ERR_INVALID, "unknown stat '%s'", name);
     return VDB_OK;
 }
@@ -1049,6 +1141,7 @@ int32_t vdb_index_clear(vdb_index* ix) {
     }
     HIP_TRY(hipMemsetAsync(ix->d_xmax, 0, 64, ix->stream));
     HIP_TRY(hipMemsetAsync(ix->d_i8, 0, 64, ix->stream));
+    HIP_TRY(hipMemsetAsync(ix->d_csum, 0, (size_t)2 * ix->Dp * sizeof(uint32_t), ix->stream));
     HIP_TRY(hipStreamSynchronize(ix->stream));
     std::memset(ix->i8st, 0, sizeof(ix->i8st));
     ix->count = 0;
@@ -1269,7 +1362,7 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     const bool auto_8 = auto_prec && !auto_x3 && ix->auto_i8 && !hold8;
     const bool auto_8x3 = x3_i8 && !hold8;
     const bool force_8x3 = auto_prec && opt.force_i8x3 && ix->auto_i8 && ix->Xq;
-    const int prec_req = !ix->Xs ? PREC_FP32
+    const int prec_req = !ix->X ? PREC_FP32
                          : force_8x3 ? PREC_I8X3
                          : ix->precision == VDB_PREC_BF16X3 ? PREC_BF16X3
                          : ix->precision == VDB_PREC_BF16 ? PREC_BF16
@@ -1314,12 +1407,16 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     const int prec = prec_req;
     const bool i8_pass = prec_is_i8(prec);  // vdb_scan8.hip
     const int Gs = prec == PREC_FP32 ? ix->G : i8_pass ? ix->G / 4 : ix->G / 2;  // scan groups (8, 32 or 16 dims)
+    if (!i8_pass && !exact_all && N > 0 && !xs_ptr(ix)) {  // a split pass under AUTO + int8: the lazy copy
+        const int xr = ensure_xs(ix);
+        if (xr) return xr;
+    }
     // fp32: vdb_scan.hip (variants); split-bf16 (bf16x3, bf16): vdb_scan2.hip
     const bool split_pass = prec == PREC_BF16X3 || prec == PREC_BF16;
     // The split pass's 128-query shape (vdb_scan2_kernel.h, q4): short rows whose query block
     // fits LDS at 128 queries (D <= 128), KP = 128, batches of >= 256: half the query blocks, so
     // each row range is re-read from L2 by half as many workgroups (C4: 8 -> 4 blocks)
-    const bool q4 = split_pass && !exact_all && KP == 128 && B >= 256 && Gs <= 8 &&
+    const bool q4 = split_pass && !exact_all && !opt.gate && KP == 128 && B >= 256 && Gs <= 8 &&
                     (ix->scan_q4 == 1 || (ix->scan_q4 < 0));
     // The int8 pass's 128-query shape (vdb_scan8_kernel.h S8_ONE4): the same rule for short rows
     // (D <= 128), KP = 128, batches of >= 256 (C4: I8X3, 8 -> 4 query blocks per row range)
@@ -1366,7 +1463,8 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     const int wg3_target = ix->n_wg_override > 0 ? (int)ix->n_wg_override : std::max(1, ix->n_cu / n_qb3);
     const int spw3 = (int)std::max<int64_t>(1, (steps3 + wg3_target - 1) / wg3_target);
     const int n_wg3 = (int)((steps3 + spw3 - 1) / spw3);
-    const bool use_s3 = split_pass && !exact_all &&
+    // (a gated sub-search -- the device re-pass -- runs the gated 64-query shapes: ADVICE r4)
+    const bool use_s3 = split_pass && !exact_all && !opt.gate &&
                         (ix->scan3 == 1 || (ix->scan3 < 0 && B >= 128 && n_wg3 >= std::max(8, 4 * k / 32)));
 
     Workspace* w = acquire_ws(ix, st, own_stream);
@@ -1410,6 +1508,10 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     const int R_rep = std::min(B, kRepassDev);                // device re-pass: gathered queries + results
     bytes += mem == VDB_MEM_DEVICE ? (size_t)R_rep * (D * 4 + (size_t)k * 20) + 1024 : 0;
     bytes += ((size_t)(n_wg + 7) / 8 * 8 * n_qblocks + 64) * 4; // int8 pass: pacing counters
+    // the int8 pass's checksum: partial sums [2][n_wg8][Bp], expected values [Bp][2], L2 start sum
+    const bool chk = i8_pass && !exact_all && ix->scan_checksum && ix->d_csum && N > 0;
+    const int n_wg8 = (n_wg + 7) / 8 * 8;
+    bytes += chk ? ((size_t)2 * n_wg8 * Bp + (size_t)2 * Bp + 64) * 4 + 768 : 0;
     const bool priv = !exact_all && !split_pass && !i8_pass && scan_priv(prec, variant, KP);
     // global per-query candidate lists: at most 512 entries per workgroup and query
     // (the largest LDS buffer of any variant; 4 x 64 for the wave-private one)
@@ -1487,6 +1589,9 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     float* q8res = i8_refine ? c.take<float>((size_t)Bp * ix->Dp) : nullptr;
     float* q8err2 = i8_refine ? c.take<float>(Bp) : nullptr;
     uint32_t* pace = c.take<uint32_t>((size_t)(n_wg + 7) / 8 * 8 * n_qblocks + 64);
+    uint32_t* chkp = chk ? c.take<uint32_t>((size_t)2 * n_wg8 * Bp) : nullptr;
+    uint32_t* chke = chk ? c.take<uint32_t>((size_t)2 * Bp) : nullptr;
+    uint32_t* chkr = chk && ix->metric == 1 ? c.take<uint32_t>(64) : nullptr;
     float* rep_q = mem == VDB_MEM_DEVICE ? c.take<float>((size_t)R_rep * D) : nullptr;
     float* rep_s = mem == VDB_MEM_DEVICE ? c.take<float>((size_t)R_rep * k) : nullptr;
     int64_t* rep_i = mem == VDB_MEM_DEVICE ? c.take<int64_t>((size_t)R_rep * k) : nullptr;
@@ -1524,7 +1629,11 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
             c8.xl_max = ix->i8st[5];
             c8.rmax_half = 0.5 * ix->xmax * ix->xmax;
             HIP_TRY(launch_prep8(Qd, qn64, q8max, B, Bp, D, Gs, ix->metric, prec, c8, Qt, q8lsl, q8err, q8scal, st,
-                                 q8res, q8err2));
+                                 q8res, q8err2, chk ? ix->d_csum : nullptr, chke));
+            if (chkr) {  // L2: the start values' sum at this batch's scale
+                HIP_TRY(hipMemsetAsync(chkr, 0, sizeof(uint32_t), st));
+                HIP_TRY(launch_rinsum8(ix->rinit32, N, q8scal, chkr, st));
+            }
         }
         int n_flag = 0;
         if (!exact_all) {
@@ -1543,7 +1652,7 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
                 HIP_TRY(hipEventRecord(tev[3], st));
             }
             const float* rowscale = ix->metric == 0 ? ix->inv32 : ix->sq32;
-            const float* Xscan = i8_pass ? ix->Xq : ix->Xs;  // the copy this pass reads
+            const float* Xscan = i8_pass ? ix->Xq : xs_ptr(ix);  // the copy this pass reads
             if (n_pilot > 0) {
                 if (i8_pass) {
                     HIP_TRY(launch_pilot8(prec, ix->metric, Xscan, ix->rinit32, md, Qt, q8scal, Gs, N, B,
@@ -1569,7 +1678,7 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
                 HIP_TRY(launch_scan8(prec, ix->metric, KP, Xscan, ix->rinit32, md, Qt, q8lsl, q8scal, Gs, N, B,
                                      n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr,
                                      ix->scan_pace ? pace : nullptr, ix->pace_seq.fetch_add(1) + 1, lockstep,
-                                     (int)ix->scan_qlds, st, opt.gate, q4_8));
+                                     (int)ix->scan_qlds, st, opt.gate, q4_8, chkp, Bp));
             else if (use_s3)
                 HIP_TRY(launch_scan3(prec, ix->metric, Xscan, ix->rinit32, md, Qt, Gs, N, B, n_qb3, steps3, n_wg3, spw3,
                                      gl_s, gl_i, gl_cnt, gl_cap, gthr, st));
@@ -1627,6 +1736,14 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
             fa.flag_count = flags; fa.flag_list = flags + 1; fa.gthr = gthr; fa.overflow_count = flags + B + 1;
             fa.incons_count = flags + B + 2;
             fa.gate = opt.gate;
+            if (chk) {
+                fa.chkp = chkp;
+                fa.chke = chke;
+                fa.chkr = chkr;
+                fa.chk_nw = n_wg8;
+                fa.chk_ld = Bp;
+                fa.chk_l = prec == PREC_I8X3;
+            }
             fa.qconst = fa.mu == q_mu && fa.dir == q_dir ? qconst : nullptr;  // (prep_queries' constants)
             fa.split = fin_split; fa.sx_ek = fx_ek; fa.sx_ck = fx_ck; fa.sx_cr = fx_cr; fa.sx_n = fx_n; fa.done = done;
             HIP_TRY(launch_finish(ix->metric, KP, fa, B, st));
@@ -1654,7 +1771,7 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
                 // pass and finish exit at once when nothing was flagged), its rows scattered back;
                 // the rest, if any, take the gated exact path.  Like the host re-pass (repass_flagged)
                 // for auto's one-plane / I8X3 passes, with the split copy kept beside the int8 one.
-                const bool can_rep = !opt.repass && auto_prec && (one_plane || prec == PREC_I8X3) && ix->Xs &&
+                const bool can_rep = !opt.repass && auto_prec && (one_plane || prec == PREC_I8X3) &&
                                      xs_kind(VDB_PREC_BF16X3) == xs_kind(ix->precision) && rep_q &&
                                      k <= kMaxApproxK;
                 bool rep = can_rep && ix->device_repass == 1;

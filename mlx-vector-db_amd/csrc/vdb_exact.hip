@@ -345,6 +345,28 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
     const int S = a.split, sp = blockIdx.y;  // split > 1: S workgroups per query share the rerank
     if (a.gate && b >= *a.gate) return;  // device re-pass: a slot past the gathered count
     FIN_STAMP(0);
+    // The int8 pass's checksum (vdb_scan8.hip): the workgroups' partial sums of this query's H (and
+    // L) accumulators against the value the stored operands imply.  Read first, decided last.
+    __shared__ int s_ckbad;
+    if (a.chkp && tid < 64) {
+        uint32_t h = 0u, l = 0u;
+        for (int w = tid; w < a.chk_nw; w += 64) {
+            h += a.chkp[(size_t)w * a.chk_ld + b];
+            if (a.chk_l) l += a.chkp[((size_t)a.chk_nw + w) * a.chk_ld + b];
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            h += (uint32_t)__shfl_xor((int)h, off, 64);
+            l += (uint32_t)__shfl_xor((int)l, off, 64);
+        }
+        if (tid == 0) {
+            const uint32_t eh = a.chke[2 * (size_t)b] + (a.chkr ? *a.chkr : 0u);
+            s_ckbad = h != eh || (a.chk_l && l != a.chke[2 * (size_t)b + 1]);
+        }
+    } else if (tid == 0) {
+        s_ckbad = 0;
+    }
+    __syncthreads();
     const int64_t c = min((int64_t)a.gl_cnt[b], a.gl_cap);
 #ifdef VDB_STAMP
     if (threadIdx.x == 0) g_fin_stamps[b][7] = (unsigned long long)c;
@@ -636,6 +658,7 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
         if (!ok && !defer && sp == 0) {
             const int pos = atomicAdd(a.flag_count, 1);
             a.flag_list[pos] = b;
+            if (s_ckbad && a.incons_count) atomicAdd(a.incons_count, 1);
         }
         s_ok1 = defer ? 0 : 1;  // 0: the exact-key test decides the flag
         s_ekk = -INFINITY;
@@ -664,6 +687,7 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
     __shared__ __attribute__((aligned(16))) float s_ca[KP];
     __shared__ uint32_t s_cbmax;
     __shared__ float s_ak2;
+    __shared__ double s_e2;  // the refined bound eps' (the consistency guard checks a' against it too)
     const bool refine = a.xh_rm != nullptr && s_cut > -INFINITY;
     if (refine) {
         if (tid == 0) s_cbmax = 0u;
@@ -770,6 +794,7 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
                                            : a.eps_rel * (2.0 * qn * a.xmax + a.xmax * a.xmax) + 2.0 * s_bq + qe2) +
                               (double)__uint_as_float(s_cbmax);
             s_cut = fmax(ak2 - 2.001 * e2, -3.0e38);  // never below the unrefined cut's domain
+            s_e2 = e2;
         }
         __syncthreads();
     }
@@ -781,12 +806,14 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
                 const int e = e0 + lane;
                 const bool in = e < m;
                 const uint32_t kk = in ? s_ck[e] : 0u, rr = in ? s_cr[e] : 0u;
-                const bool keep = in && (refine ? (double)s_ca[e] : (double)key_to_float(kk)) >= cut;
+                const float ca = in && refine ? s_ca[e] : 0.0f;
+                const bool keep = in && (refine ? (double)ca : (double)key_to_float(kk)) >= cut;
                 const unsigned long long bm = __ballot(keep);
                 if (keep) {
                     const int pos = base + __popcll(bm & ((1ull << lane) - 1ull));
                     s_ck[pos] = kk;
                     s_cr[pos] = rr;
+                    if (refine) s_ca[pos] = ca;  // (carried for the consistency guard)
                 }
                 base += __popcll(bm);
             }
@@ -974,11 +1001,22 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
     {
         const double sh = s_shift, eb = s_epsb;
         bool bad = false;
+        // with the I8 refinement the rerank cut relied on |a' - (exact - shift)| <= eps' (the
+        // refined bound): a stale or misindexed row-major xh plane breaks that one, so it is
+        // checked too.  (split > 1 reorders the candidates: the refined check is
+        // skipped there; the refinement runs with split 1.)
+        const bool chk2 = refine && S == 1;
+        const double e2 = chk2 ? s_e2 : 0.0;
         for (int j = tid; j < m; j += 64 * FIN_WAVES) {
             const double ap = (double)key_to_float(s_ck[j]), ex = s_ek[j] - sh;
-            const double bound = 1.01 * (eb + (METRIC == 1 ? 2.4e-7 * fmax(fabs(ap), fabs(ex)) : 0.0)) +
-                                 4e-16 * (fabs(s_ek[j]) + fabs(sh));
+            const double fr = 4e-16 * (fabs(s_ek[j]) + fabs(sh));
+            const double bound = 1.01 * (eb + (METRIC == 1 ? 2.4e-7 * fmax(fabs(ap), fabs(ex)) : 0.0)) + fr;
             bad |= !(fabs(ap - ex) <= bound);
+            if (chk2) {
+                const double a2 = (double)s_ca[j];
+                const double bound2 = 1.01 * (e2 + (METRIC == 1 ? 2.4e-7 * fmax(fabs(a2), fabs(ex)) : 0.0)) + fr;
+                bad |= !(fabs(a2 - ex) <= bound2);
+            }
         }
         if (__any(bad) && lane == 0) atomicOr(&s_bad, 1);
     }
@@ -988,10 +1026,10 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
         const double tol = 4e-16 * (fabs(s_ekk) + fabs(s_shift));
         // neither certificate, or a reranked row outside its bound: the exact path rewrites
         // the query
-        if ((!s_ok1 && !(ekk - tol > s_bar)) || s_bad) {
+        if ((!s_ok1 && !(ekk - tol > s_bar)) || s_bad || s_ckbad) {
             const int pos = atomicAdd(a.flag_count, 1);
             a.flag_list[pos] = b;
-            if (s_bad && a.incons_count) atomicAdd(a.incons_count, 1);
+            if ((s_bad || s_ckbad) && a.incons_count) atomicAdd(a.incons_count, 1);
         }
     }
     FIN_STAMP(5);

@@ -47,7 +47,14 @@ hipError_t launch_quant_rows(const float* X, const float* inv32, const float* mu
 // queries -> int8 tiles Qq (G8 + QG_EXTRA groups), per query lsl / qerr, per batch qscal[3]
 hipError_t launch_prep8(const float* Q, const double* qn64, const float* qmax, int B, int Bp, int D, int G8,
                         int metric, int prec, const Int8Consts& c, float* Qq, float* lsl, float* qerr, float* qscal,
-                        hipStream_t st, float* qres = nullptr, float* qerr2 = nullptr);
+                        hipStream_t st, float* qres = nullptr, float* qerr2 = nullptr,
+                        const uint32_t* csum = nullptr, uint32_t* chke = nullptr);
+// The int8 pass's checksum (vdb_scan8.hip): column sums of the int8 copy's two planes over rows
+// [row0, row0 + n) added into csum [2][Dp]; the L2 start values' sum for a batch (*out +=); and a
+// test-only corpus fault (one row's planes negated, the column sums left as they were)
+hipError_t launch_colsum8(const float* Xq, int64_t row0, int64_t n, int G8, uint32_t* csum, hipStream_t st);
+hipError_t launch_rinsum8(const float* rinit, int64_t N, const float* qscal, uint32_t* out, hipStream_t st);
+hipError_t launch_negate_row8(float* Xq, int64_t row, int G8, hipStream_t st);
 hipError_t launch_pilot8(int prec, int metric, const float* Xq, const float* rinit, const uint32_t* mask,
                          const float* Qq, const float* qscal, int G8, int64_t N, int B, int n_qblocks, int QB,
                          int n_sample, uint32_t* pslots, hipStream_t st);
@@ -58,7 +65,8 @@ hipError_t launch_scan8(int prec, int metric, int KP, const float* Xq, const flo
                         const float* Qq, const float* lsl, const float* qscal, int G8, int64_t N, int B,
                         int n_qblocks, int64_t n_steps, int n_wg, int spw, float* gl_s, uint32_t* gl_i,
                         uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr, uint32_t* pace, uint32_t pace_tag,
-                        int lockstep, int qlds, hipStream_t st, const int* gate = nullptr, bool q4 = false);
+                        int lockstep, int qlds, hipStream_t st, const int* gate = nullptr, bool q4 = false,
+                        uint32_t* chkp = nullptr, int chk_ld = 0);
 
 // Ingest: row-major fp32 [n][D] (device) -> the index's row-major fp32 copy X [cap][Dp]
 // (zero padded to Dp = 8 G; read by the exact paths, export and the graph) rows [row0, row0+n),
@@ -220,6 +228,14 @@ struct FinishArgs {
     int split = 1;
     double* sx_ek = nullptr; uint32_t* sx_ck = nullptr; uint32_t* sx_cr = nullptr; int* sx_n = nullptr;
     int* done = nullptr;
+    // optional, the int8 pass's checksum (vdb_scan8.hip): per-workgroup partial sums of the H (and
+    // L) accumulators chkp [2][chk_nw][chk_ld], the expected values chke [Bp][2] (prep8) and, for
+    // L2, the start values' sum *chkr; a mismatch flags the query (exact path)
+    const uint32_t* chkp = nullptr;
+    const uint32_t* chke = nullptr;
+    const uint32_t* chkr = nullptr;
+    int chk_nw = 0, chk_ld = 0;
+    bool chk_l = false;
 };
 hipError_t launch_finish(int metric, int KP, const FinishArgs& a, int B, hipStream_t st);
 

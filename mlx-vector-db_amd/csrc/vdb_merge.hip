@@ -111,7 +111,13 @@ __global__ void __launch_bounds__(256) repass_gather_kernel(const float* __restr
         counts[1] = c > R ? c - R : 0;
         if (totals && n > 0) atomicAdd(totals, (unsigned long long)n);
     }
-    if (r >= n) return;
+    // Slots past the gathered count are zeroed: the gated sub-search's query prep runs
+    // over all R slots, and prep8 takes the batch's int8 scale as the maximum over every slot --
+    // stale workspace bytes there (an earlier search's scores or ids) would coarsen it.
+    if (r >= n) {
+        for (int d = blockIdx.x * 256 + threadIdx.x; d < D; d += gridDim.x * 256) out[(size_t)r * D + d] = 0.0f;
+        return;
+    }
     const int b = flags[1 + r];
     for (int d = blockIdx.x * 256 + threadIdx.x; d < D; d += gridDim.x * 256) out[(size_t)r * D + d] = Q[(size_t)b * D + d];
 }

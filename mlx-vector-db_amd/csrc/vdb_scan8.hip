@@ -147,6 +147,101 @@ hipError_t launch_quant_rows(const float* X, const float* inv32, const float* mu
 }
 
 // =============================================================================
+// The pass's checksum (ABFT): the integer MFMA sums are exact, so over all rows
+// r < N of a query block the accumulators the pass produced must add up (mod 2^32) to
+//   sum_r H[r][q] = sum_r rint(rinit[r] / (s_x s_q)) [L2] + sum_d CH[d] qh[q][d]
+//   sum_r L[r][q] = sum_d CH[d] ql[q][d] + CL[d] qh[q][d]                        [I8X3]
+// with CH / CL the column sums of the int8 copy's planes, kept here at ingest.  A wrong operand
+// anywhere in the pass (a stale start value or corpus register, a misindexed tile) moves the sum
+// whichever way it moves the row's score -- the under-scoring half included, which the finish's
+// approx-vs-exact check (rerank set only) cannot see.
+// =============================================================================
+// csum[pl * Dp + d] += sum over rows [row0, row0 + n) of plane pl (xh, xl), d < Dp = 32 G8.
+// One thread per (plane, 16-dim chunk), kColsumRows rows per workgroup.
+constexpr int kColsumRows = 2048;
+__global__ void __launch_bounds__(256) colsum8_kernel(const float* __restrict__ Xq, int64_t row0, int64_t n, int G8,
+                                                      uint32_t* __restrict__ csum) {
+    const int nc = 2 * G8;  // 16-dim chunks per plane
+    const int tid = threadIdx.x + blockIdx.y * 256;
+    if (tid >= 2 * nc) return;
+    const int pl = tid / nc, c = tid - pl * nc;
+    const int64_t r0 = row0 + (int64_t)blockIdx.x * kColsumRows;
+    const int64_t r1 = min(r0 + (int64_t)kColsumRows, row0 + n);
+    int acc[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[j] = 0;
+    for (int64_t r = r0; r < r1; ++r) {
+        const float* src = Xq + corpus_block((uint64_t)r >> 5, c >> 1, 0, G8) + (size_t)((r & 31) + 32 * (c & 1)) * 4 +
+                           (pl ? corpus_plane(G8) : 0);
+        const f32x4 v = *(const f32x4*)src;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const uint32_t u = __float_as_uint(v[w]);
+#pragma unroll
+            for (int bt = 0; bt < 4; ++bt) acc[4 * w + bt] += (int)(int8_t)((u >> (8 * bt)) & 255u);
+        }
+    }
+    if (r0 < r1)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) atomicAdd(csum + (size_t)pl * 32 * G8 + 16 * c + j, (uint32_t)acc[j]);
+}
+
+hipError_t launch_colsum8(const float* Xq, int64_t row0, int64_t n, int G8, uint32_t* csum, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    const int threads = 4 * G8;  // 2 planes x 2 G8 chunks
+    hipLaunchKernelGGL(colsum8_kernel, dim3((unsigned)((n + kColsumRows - 1) / kColsumRows), (unsigned)((threads + 255) / 256)),
+                       dim3(256), 0, st, Xq, row0, n, G8, csum);
+    return hipGetLastError();
+}
+
+// *out += sum over rows r < N of rint(rinit[r] * (1 / (s_x s_q))) (mod 2^32): the L2 pass's
+// accumulator start values, as scan8_kernel computes them (qscal[2] from prep8)
+__global__ void __launch_bounds__(256) rinsum8_kernel(const float* __restrict__ rinit, int64_t N,
+                                                      const float* __restrict__ qscal, uint32_t* __restrict__ out) {
+    const float invU = qscal[2];
+    uint32_t s = 0u;
+    for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < N; r += (int64_t)gridDim.x * 256)
+        s += (uint32_t)__float2int_rn(rinit[r] * invU);
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) s += (uint32_t)__shfl_xor((int)s, off, 64);
+    if ((threadIdx.x & 63) == 0) atomicAdd(out, s);
+}
+
+hipError_t launch_rinsum8(const float* rinit, int64_t N, const float* qscal, uint32_t* out, hipStream_t st) {
+    if (N <= 0) return hipSuccess;
+    const int64_t blocks = std::min<int64_t>(1024, (N + 255) / 256);
+    hipLaunchKernelGGL(rinsum8_kernel, dim3((unsigned)blocks), dim3(256), 0, st, rinit, N, qscal, out);
+    return hipGetLastError();
+}
+
+// TEST ONLY (index knob debug_negate_row8, behind VDB_DEBUG_KNOBS=1): negates both planes of one
+// row of the int8 copy without touching the column sums -- a corpus operand the pass reads
+// wrong, which under-scores a row that matched the query (tests/test_gpu_guards.py)
+__global__ void __launch_bounds__(64) negate_row8_kernel(float* __restrict__ Xq, int64_t r, int G8) {
+    const int nc = 2 * G8;
+    for (int t = threadIdx.x; t < 2 * nc; t += 64) {
+        const int pl = t / nc, c = t - pl * nc;
+        float* p = Xq + corpus_block((uint64_t)r >> 5, c >> 1, 0, G8) + (size_t)((r & 31) + 32 * (c & 1)) * 4 +
+                   (pl ? corpus_plane(G8) : 0);
+        f32x4 v = *(f32x4*)p;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const uint32_t u = __float_as_uint(v[w]);
+            uint32_t o = 0u;
+#pragma unroll
+            for (int bt = 0; bt < 4; ++bt) o |= ((uint32_t)(-(int)(int8_t)((u >> (8 * bt)) & 255u)) & 255u) << (8 * bt);
+            v[w] = __uint_as_float(o);
+        }
+        *(f32x4*)p = v;
+    }
+}
+
+hipError_t launch_negate_row8(float* Xq, int64_t row, int G8, hipStream_t st) {
+    hipLaunchKernelGGL(negate_row8_kernel, dim3(1), dim3(64), 0, st, Xq, row, G8);
+    return hipGetLastError();
+}
+
+// =============================================================================
 // Queries: one scale per batch, s_q = max |q'| / 127 (q' the fp32 query the other passes use:
 // cosine normalised), 16-bit fixed point in two int8 planes, tiles as the split layout
 // (s2_blk, G8 + QG_EXTRA groups, the leading ones repeated).  Per query: lsl = the prefilter's
@@ -157,7 +252,8 @@ __global__ void __launch_bounds__(256) prep8_kernel(const float* __restrict__ Q,
                                                     int metric, int prec, Int8Consts c, float* __restrict__ Qq,
                                                     float* __restrict__ lsl, float* __restrict__ qerr,
                                                     float* __restrict__ qscal, float* __restrict__ qres,
-                                                    float* __restrict__ qerr2) {
+                                                    float* __restrict__ qerr2, const uint32_t* __restrict__ csum,
+                                                    uint32_t* __restrict__ chke) {
     const int lane = threadIdx.x & 63;
     const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (b >= Bp) return;
@@ -182,6 +278,8 @@ __global__ void __launch_bounds__(256) prep8_kernel(const float* __restrict__ Q,
     const float isq = 1.0f / sq;
     const int GQ = G8 + QG_EXTRA;
     double s_rq = 0.0, s_r8 = 0.0, s_ql = 0.0, s_qh = 0.0;
+    uint32_t eh = 0u, el = 0u;  // the checksum's query terms: sum_d CH qh, sum_d CH ql + CL qh (mod 2^32)
+    const int Dp = 32 * G8;
     for (int cc = lane; cc < 2 * GQ; cc += 64) {
         const int g = cc >> 1, h = cc & 1;
         const int d0 = 32 * (g % G8) + 16 * h;
@@ -191,6 +289,11 @@ __global__ void __launch_bounds__(256) prep8_kernel(const float* __restrict__ Q,
             const int d = d0 + j;
             const float qv = (real && d < D) ? q[d] * scale : 0.0f;
             split_i8(qv * isq, hv[j], lv[j]);
+            if (csum && g < G8) {
+                const uint32_t ch = csum[d], cl = csum[Dp + d];
+                eh += (uint32_t)hv[j] * ch;
+                el += (uint32_t)lv[j] * ch + (uint32_t)hv[j] * cl;
+            }
             if (g < G8) {
                 const double qh = (double)sq * hv[j], ql = (double)sq * lv[j] / 256.0;
                 const double r8 = (double)qv - qh, rq = r8 - ql;
@@ -222,6 +325,15 @@ __global__ void __launch_bounds__(256) prep8_kernel(const float* __restrict__ Q,
     s_r8 = wave_sum_butterfly(s_r8);
     s_ql = wave_sum_butterfly(s_ql);
     s_qh = wave_sum_butterfly(s_qh);
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        eh += (uint32_t)__shfl_xor((int)eh, off, 64);
+        el += (uint32_t)__shfl_xor((int)el, off, 64);
+    }
+    if (chke && lane == 0) {
+        chke[2 * b] = eh;
+        chke[2 * b + 1] = el;
+    }
     if (lane == 0) {
         const bool x3 = prec == PREC_I8X3;
         const double za = c.zmax_h + (x3 ? c.xl_max : 0.0);  // bound of |z~|
@@ -242,9 +354,9 @@ __global__ void __launch_bounds__(256) prep8_kernel(const float* __restrict__ Q,
 
 hipError_t launch_prep8(const float* Q, const double* qn64, const float* qmax, int B, int Bp, int D, int G8,
                         int metric, int prec, const Int8Consts& c, float* Qq, float* lsl, float* qerr, float* qscal,
-                        hipStream_t st, float* qres, float* qerr2) {
+                        hipStream_t st, float* qres, float* qerr2, const uint32_t* csum, uint32_t* chke) {
     hipLaunchKernelGGL(prep8_kernel, dim3((Bp + 3) / 4), dim3(256), 0, st, Q, qn64, qmax, B, Bp, D, G8, metric, prec, c,
-                       Qq, lsl, qerr, qscal, qres, qerr2);
+                       Qq, lsl, qerr, qscal, qres, qerr2, csum, chke);
     return hipGetLastError();
 }
 
@@ -365,12 +477,12 @@ hipError_t launch_scan8(int prec, int metric, int KP, const float* Xq, const flo
                         const float* Qq, const float* lsl, const float* qscal, int G8, int64_t N, int B,
                         int n_qblocks, int64_t n_steps, int n_wg, int spw, float* gl_s, uint32_t* gl_i,
                         uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr, uint32_t* pace, uint32_t pace_tag,
-                        int lockstep, int qlds, hipStream_t st, const int* gate, bool q4) {
+                        int lockstep, int qlds, hipStream_t st, const int* gate, bool q4, uint32_t* chkp, int chk_ld) {
     // the query block in LDS (scan8_qlds): qlds 1 = the round-3 rule (short rows), 2 = whenever
     // it fits, -1 = auto (rule 2 past VDB_S8_QLDS_BIG_G8 groups), 0 = never -- except for rows of fewer 32-dim groups
     // than the global-operand variants keep in flight (PX = 4)
     const int mode = qlds < 0 ? (G8 > VDB_S8_QLDS_BIG_G8 ? 2 : 1) : qlds;
-    const bool ql = q4 || (mode != 0 && scan8_qlds(G8, KP, prec, mode == 1)) || G8 < 4;
+    const bool ql = q4 || (mode != 0 && scan8_qlds(G8, KP, prec, metric, mode == 1)) || G8 < 4;
     if (q4 && (KP != 128 || !scan8_q4_ok(G8, prec))) return hipErrorInvalidValue;
     const bool fs = !lockstep;
     const bool nt = !ql && n_qblocks == 1;
@@ -379,7 +491,7 @@ hipError_t launch_scan8(int prec, int metric, int KP, const float* Xq, const flo
                                    : nullptr;
     if (!unit || metric < 0 || metric > 1) return hipErrorInvalidValue;
     return unit(KP, Xq, rinit, mask, Qq, lsl, qscal, G8, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt,
-                gl_cap, gthr, pace, pace_tag, nt, ql, fs, q4, gate, st);
+                gl_cap, gthr, pace, pace_tag, nt, ql, fs, q4, gate, chkp, chk_ld, st);
 }
 
 }  // namespace vdb

@@ -211,7 +211,8 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
              const float* __restrict__ Qq, const float* __restrict__ lsl, const float* __restrict__ qscal, int G_arg,
              int64_t N, int B, int64_t n_steps, int steps_per_wg, int n_qb, float* __restrict__ gl_s,
              uint32_t* __restrict__ gl_i, uint32_t* __restrict__ gl_cnt, int64_t gl_cap, uint32_t* __restrict__ gthr,
-             uint32_t* __restrict__ pace, uint32_t pace_tag, const int* __restrict__ gate) {
+             uint32_t* __restrict__ pace, uint32_t pace_tag, const int* __restrict__ gate,
+             uint32_t* __restrict__ chkp, int chk_ld) {
     // a gated launch (the device-memory re-pass, vdb_api.cpp): nothing to do when its count is 0
     if (gate && *gate == 0) return;
     constexpr int RT = RT_, NW = scan8_nw(PREC, METRIC, QT);
@@ -231,6 +232,7 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
     __shared__ int s_cnt[QB];
     __shared__ float s_thr[QB];
     __shared__ int s_need, s_done;
+    __shared__ uint32_t s_chk[HL ? 2 : 1][QB];  // the checksum's per-query sums of this workgroup
     __shared__ uint32_t s_pend[NW][8][64];  // per wave and tile: each lane's entries left for a compaction round
     extern __shared__ __attribute__((aligned(16))) float s_q[];  // QLDS: [G][LQP planes][QT][256]
 
@@ -252,6 +254,8 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
     for (int i = threadIdx.x; i < QB; i += 64 * NW) {
         s_cnt[i] = 0;
         s_thr[i] = -INFINITY;
+        s_chk[0][i] = 0u;
+        if constexpr (HL) s_chk[HL ? 1 : 0][i] = 0u;
     }
     const float uH = qscal[0], uL = qscal[1], invU = qscal[2];
     float qsl[QT];  // per query: bound of |L uL| (the prefilter's slack)
@@ -306,6 +310,11 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
         }
     };
     f32x4 rin[NRI][4];
+    // The checksum (ABFT, vdb_scan8.hip): per lane and query tile, the sum (mod 2^32) of every H
+    // (and L) accumulator of rows < N this wave produced -- the same registers the tile tests read
+    uint32_t ckh[QT], ckl[QT];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) ckh[qt] = ckl[qt] = 0u;
     if (s_begin < s_end) {
         load_epi(s_begin, rin);  // before the slots: PX * LPS loads younger than these
         const float* xs = Xq + corpus_block((uint64_t)((s_begin * NW + wv) * RT), 0, 0, G);
@@ -446,6 +455,40 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
             continue;
         }
 #endif
+        // ---- checksum: every accumulator of a row < N (a wave-uniform test per step; only the
+        // last step of the corpus holds rows past N) ----
+        if (chkp) {
+            if ((t0 + RT) * 32 <= N) {
+#pragma unroll
+                for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+                    for (int qt = 0; qt < QT; ++qt) {
+                        uint32_t a = ckh[qt];
+#pragma unroll
+                        for (int v = 0; v < 16; v += 2) a += (uint32_t)aH[rt][qt][v] + (uint32_t)aH[rt][qt][v + 1];
+                        ckh[qt] = a;
+                        if constexpr (HL) {
+                            uint32_t c = ckl[qt];
+#pragma unroll
+                            for (int v = 0; v < 16; v += 2) c += (uint32_t)aL[rt][qt][v] + (uint32_t)aL[rt][qt][v + 1];
+                            ckl[qt] = c;
+                        }
+                    }
+            } else {
+#pragma unroll
+                for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+                    for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+                        for (int v = 0; v < 16; ++v) {
+                            const int64_t row = (t0 + rt) * 32 + 8 * (v >> 2) + 4 * (lane >> 5) + (v & 3);
+                            if (row < N) {
+                                ckh[qt] += (uint32_t)aH[rt][qt][v];
+                                if constexpr (HL) ckl[qt] += (uint32_t)aL[rt][qt][v];
+                            }
+                        }
+            }
+        }
         // ---- epilogue ----
         int thi[QT];
         bool qok[QT];
@@ -649,8 +692,28 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
         __syncthreads();  // B2
     }
 
+    // the checksum's partial sums: lane halves of a query column, then the waves through LDS,
+    // one word per (plane, workgroup, query) -- no atomics on global memory, summed by the finish
+    if (chkp) {
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) {
+            const uint32_t h = ckh[qt] + (uint32_t)__shfl_xor((int)ckh[qt], 32, 64);
+            const uint32_t l = ckl[qt] + (uint32_t)__shfl_xor((int)ckl[qt], 32, 64);
+            if (lane < 32) {
+                atomicAdd(&s_chk[0][qt * 32 + lane], h);
+                if constexpr (HL) atomicAdd(&s_chk[HL ? 1 : 0][qt * 32 + lane], l);
+            }
+        }
+    }
     // ---- flush: entries above the shared bound -> global per-query lists ----
     __syncthreads();
+    if (chkp) {
+        const int nwg8 = (int)(gridDim.x / (unsigned)n_qb);
+        for (int i = threadIdx.x; i < (HL ? 2 : 1) * QB; i += 64 * NW) {
+            const int pl = i / QB, q = i - pl * QB;
+            chkp[((size_t)pl * nwg8 + wg) * (size_t)chk_ld + (size_t)qb * QB + q] = s_chk[pl][q];
+        }
+    }
     uint32_t tkey = 0;
     if (lane < QPW && qb * QB + wv + NW * lane < B) {
         const int q = wv + NW * lane;
@@ -682,7 +745,7 @@ static hipError_t scan8_launch_g(const float* Xq, const float* rinit, const uint
                                  const float* lsl, const float* qscal, int G, int64_t N, int B, int n_qblocks,
                                  int64_t n_steps, int n_wg, int spw, float* gl_s, uint32_t* gl_i, uint32_t* gl_cnt,
                                  int64_t gl_cap, uint32_t* gthr, uint32_t* pace, uint32_t pace_tag, const int* gate,
-                                 hipStream_t st) {
+                                 uint32_t* chkp, int chk_ld, hipStream_t st) {
     auto k = scan8_kernel<P, M, QT, PX, KP, CAP, NT, QL, FS, GC, RT_, KW>;
     const size_t lds = QL ? (size_t)G * Planes8<P>::QPL * QT * 1024 : 0;
     if (QL) {
@@ -697,7 +760,7 @@ static hipError_t scan8_launch_g(const float* Xq, const float* rinit, const uint
     const int n_wg8 = (n_wg + 7) / 8 * 8;
     hipLaunchKernelGGL(k, dim3(n_wg8 * n_qblocks), dim3(64 * scan8_nw(P, M, QT)), lds, st, Xq, rinit, mask, Qq, lsl, qscal, G, N, B,
                        n_steps, spw, n_qblocks, gl_s, gl_i, gl_cnt, gl_cap, gthr, n_qblocks > 1 ? pace : nullptr,
-                       pace_tag, gate);
+                       pace_tag, gate, chkp, chk_ld);
     return hipGetLastError();
 }
 
@@ -707,12 +770,13 @@ static hipError_t scan8_launch(const float* Xq, const float* rinit, const uint32
                                const float* lsl, const float* qscal, int G, int64_t N, int B, int n_qblocks,
                                int64_t n_steps, int n_wg, int spw, float* gl_s, uint32_t* gl_i, uint32_t* gl_cnt,
                                int64_t gl_cap, uint32_t* gthr, uint32_t* pace, uint32_t pace_tag, const int* gate,
-                               hipStream_t st) {
+                               uint32_t* chkp, int chk_ld, hipStream_t st) {
     if constexpr (QL) {
         if (G == 4)  // D = 128: the group loop unrolls, and the whole next step is in flight
             return scan8_launch_g<P, M, QT, 4, KP, CAP, NT, QL, FS, 4, RT_, KW>(Xq, rinit, mask, Qq, lsl, qscal, G, N, B,
                                                                         n_qblocks, n_steps, n_wg, spw, gl_s, gl_i,
-                                                                        gl_cnt, gl_cap, gthr, pace, pace_tag, gate, st);
+                                                                        gl_cnt, gl_cap, gthr, pace, pace_tag, gate,
+                                                                        chkp, chk_ld, st);
     }
     // the step loop takes the groups PX at a time: Dp / 32 groups is only even (D = 192: 6), so
     // where PX does not divide them the 2-deep variant runs (4 deep, the tail's refills would read
@@ -721,11 +785,11 @@ static hipError_t scan8_launch(const float* Xq, const float* rinit, const uint32
         if (G % PX != 0)
             return scan8_launch_g<P, M, QT, 2, KP, CAP, NT, QL, FS, 0, RT_, KW>(
                 Xq, rinit, mask, Qq, lsl, qscal, G, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap,
-                gthr, pace, pace_tag, gate, st);
+                gthr, pace, pace_tag, gate, chkp, chk_ld, st);
     }
     return scan8_launch_g<P, M, QT, PX, KP, CAP, NT, QL, FS, 0, RT_, KW>(Xq, rinit, mask, Qq, lsl, qscal, G, N, B, n_qblocks,
                                                                 n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr,
-                                                                pace, pace_tag, gate, st);
+                                                                pace, pace_tag, gate, chkp, chk_ld, st);
 }
 
 // The query block in LDS takes the query operand off each wave's vector-memory path (from L2,
@@ -737,10 +801,13 @@ static hipError_t scan8_launch(const float* Xq, const float* rinit, const uint32
 constexpr int scan8_rows_q4() { return 1 * S8_NW * 32; }
 inline bool scan8_q4_fits(int G8, int prec) { return S8_NW == 4 && (size_t)G8 * (prec == PREC_I8X3 ? 2 : 1) * 4 * 1024 <= 32 * 1024; }
 inline int scan8_cap(int KP, bool ql) { return KP == 128 ? 192 : KP == 256 ? (ql ? 96 : 128) : 128; }  // as S8_KP
-inline bool scan8_qlds(int G8, int KP, int prec, bool small) {
+inline bool scan8_qlds(int G8, int KP, int prec, int metric, bool small) {
     const size_t q = (size_t)G8 * (prec == PREC_I8X3 ? 2 : 1) * 2 * 1024;
     if (small) return q <= 32 * 1024;
-    const size_t lists = (size_t)64 * scan8_cap(KP, true) * 8 + 8 * 2048 + 1024;  // s_pend of up to 8 waves
+    // lists, s_pend of this shape's waves (the 8-wave I8X3 L2 shape: 16 KiB; counted at 8 waves for
+    // every shape, C3's 96 KiB query block stopped fitting beside its 48 KiB of lists at the end of
+    // round 4), counters and the checksum's sums
+    const size_t lists = (size_t)64 * scan8_cap(KP, true) * 8 + (size_t)scan8_nw(prec, metric) * 2048 + 1536;
     return lists + q <= 160 * 1024;
 }
 
@@ -749,9 +816,11 @@ inline bool scan8_qlds(int G8, int KP, int prec, bool small) {
     int KP, const float *Xq, const float *rinit, const uint32_t *mask, const float *Qq, const float *lsl,          \
         const float *qscal, int G, int64_t N, int B, int n_qblocks, int64_t n_steps, int n_wg, int spw,           \
         float *gl_s, uint32_t *gl_i, uint32_t *gl_cnt, int64_t gl_cap, uint32_t *gthr, uint32_t *pace,            \
-        uint32_t pace_tag, bool nt, bool ql, bool fs, bool q4, const int *gate, hipStream_t st
+        uint32_t pace_tag, bool nt, bool ql, bool fs, bool q4, const int *gate, uint32_t *chkp, int chk_ld,      \
+        hipStream_t st
 #define S8_ARGS \
-    Xq, rinit, mask, Qq, lsl, qscal, G, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, pace, pace_tag, gate, st
+    Xq, rinit, mask, Qq, lsl, qscal, G, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, pace, pace_tag, gate, \
+        chkp, chk_ld, st
 #define S8_ONE(P, M, KPV, QTV, PXV, CAPV, NTV, QLV, FSV, KWV)   \
     if (KP == KPV && nt == NTV && ql == QLV && fs == FSV && !q4) \
         return scan8_launch<P, M, QTV, PXV, KPV, CAPV, NTV, QLV, FSV, KWV>(S8_ARGS);

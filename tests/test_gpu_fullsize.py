@@ -246,4 +246,7 @@ def test_c5_graph_5m_x_384(vdb):
     _, ei, _ = ref_cpu.exact_search(Q, V, k, "cosine")
     recall = np.mean([len(set(a) & set(b)) / k for a, b in zip(lab.tolist(), ei.tolist())])
     _report("c5.json", {"recall_at_10": recall, "build_s": build_s, "teams": TEAMS, "ef": ef})
-    assert recall >= 0.2  # parity for the graph is recall, not equality
+    # parity for the graph is recall, not equality.  The build and search are
+    # deterministic on this data: every run since round 2 measured 0.397 (profiles/r0*/reports/
+    # c5.json); the bar is that minus 0.025, so a regression of the graph shows
+    assert recall >= 0.37, recall

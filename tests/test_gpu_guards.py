@@ -7,6 +7,8 @@
   case runs in its own process (tests/_first_search_case.py).
 * The finish kernel's approx-vs-exact consistency guard: a planted stale L2 start value (the
   operand class of the round-3 failure) makes the query flagged, not certified.
+* The int8 pass's checksum (its H / L accumulator sums against the column sums of the stored
+  operands): a planted UNDER-scoring corpus operand, which the guard above cannot see, is flagged.
 * A device-memory search queued on a side stream while an add re-derives the int8 setup
   (the add must wait for it).
 
@@ -48,8 +50,24 @@ def test_first_search_in_a_fresh_process(precision, metric, qlds, D):
     assert "FIRST OK" in r.stdout
 
 
+@pytest.fixture
+def debug_knobs(monkeypatch):
+    """The test-only corruption knobs (debug_*) are refused unless VDB_DEBUG_KNOBS=1."""
+    monkeypatch.setenv("VDB_DEBUG_KNOBS", "1")
+
+
+def test_debug_knobs_refused_without_opt_in(vdb, monkeypatch):
+    monkeypatch.delenv("VDB_DEBUG_KNOBS", raising=False)
+    ix = vdb.NativeIndex(32, "euclidean")
+    ix.add(np.random.default_rng(3).random((100, 32), dtype=np.float32))
+    with pytest.raises(Exception, match="test-only"):
+        ix.set_param("debug_stale_rinit", 5)
+    with pytest.raises(Exception, match="test-only"):
+        ix.set_param("debug_negate_row8", 5)
+
+
 @pytest.mark.parametrize("precision", ["i8", "i8x3", "bf16x3"])
-def test_consistency_guard_flags_a_planted_stale_operand(vdb, precision):
+def test_consistency_guard_flags_a_planted_stale_operand(vdb, precision, debug_knobs):
     """A row whose L2 start value is stale (-|x|^2/2 read as 0) over-scores by |x|^2 in the
     candidate pass.  It lands in the rerank set, where its exact key disagrees with its
     approximate score by far more than eps: the finish flags the query (exact path) instead of
@@ -73,6 +91,43 @@ def test_consistency_guard_flags_a_planted_stale_operand(vdb, precision):
     np.testing.assert_array_equal(kk, ek)
     assert ix.stat("inconsistent_queries") >= 1
     assert ix.stat("fallback_queries") > f0
+
+
+@pytest.mark.parametrize("precision", ["i8", "i8x3"])
+@pytest.mark.parametrize("metric", ["cosine", "euclidean"])
+def test_checksum_flags_a_planted_under_scoring_operand(vdb, precision, metric, debug_knobs):
+    """the blind side of the approx-vs-exact guard.  Each query's true top-1
+    row has its int8 planes negated (debug_negate_row8: the column sums stay, as for a corpus
+    operand the pass reads wrong), so the pass UNDER-scores it: it never becomes a candidate, and
+    the finish's consistency check -- which sees only the rerank set -- has nothing to compare.
+    With the pass's checksum off the search returns wrong, certified results (the blind side,
+    shown); with it on (the default) every query's H (L) accumulator sums disagree with the
+    operands' column sums, every query is flagged, and the exact path returns exact results."""
+    rng = np.random.default_rng(43)
+    N, D, B, k = 20000, 96, 16, 10
+    V = rng.random((N, D), dtype=np.float32)
+    Q = rng.random((B, D), dtype=np.float32)
+    es, ei, ek = ref_cpu.exact_search(Q, V, k, metric)
+    ix = vdb.NativeIndex(D, metric, precision=precision)
+    ix.add(V)
+    _, i, kk = ix.search(Q, k, with_keys=True)
+    np.testing.assert_array_equal(i, ei)
+    assert ix.stat("inconsistent_queries") == 0
+    for r in sorted(set(ei[:, 0].tolist())):
+        ix.set_param("debug_negate_row8", int(r))
+    ix.set_param("scan_checksum", 0)
+    f0 = ix.stat("fallback_queries")
+    _, i, kk = ix.search(Q, k, with_keys=True)
+    wrong = int((i != ei).any(axis=1).sum())
+    print(f"{precision} {metric}: checksum off -> {wrong} of {B} queries wrong, "
+          f"{ix.stat('inconsistent_queries')} flagged inconsistent")
+    assert wrong >= 1 and ix.stat("inconsistent_queries") == 0  # nothing else sees it
+    ix.set_param("scan_checksum", 1)
+    _, i, kk = ix.search(Q, k, with_keys=True)
+    np.testing.assert_array_equal(i, ei)
+    np.testing.assert_array_equal(kk, ek)
+    assert ix.stat("inconsistent_queries") == B, ix.stat("inconsistent_queries")
+    assert ix.stat("fallback_queries") - f0 >= B
 
 
 def test_add_waits_for_queued_device_search_before_rederiving(vdb):

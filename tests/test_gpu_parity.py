@@ -1014,3 +1014,88 @@ def test_i8_narrow_kp_on_small_indexes(vdb, mem):
     ix2.set_param("i8_narrow", 0)
     with pytest.raises(Exception):
         ix2.set_param("i8_narrow", 1)
+
+
+def test_split_copy_allocated_lazily_under_auto(vdb):
+    """under auto (int8 candidate pass) the split-bf16 copy is allocated only when a
+    search first runs a split pass -- here the host re-pass of a query the int8 pass leaves
+    uncertified (BF16X3) -- so an index that never needs it holds 7 B per element (fp32 rows 4,
+    int8 planes 2, row-major xh 1) + 20 B per row.  Results exact before and after."""
+    rng = np.random.default_rng(61)
+    N, D, B, k = 30000, 128, 32, 10
+    V = rng.random((N, D), dtype=np.float32)
+    V[2000:2300] = _graded_neighbours(rng, V[3], 300)
+    ix = vdb.NativeIndex(D, "cosine")
+    ix.add(V)
+    cap = ix.stat("capacity")
+    Dp = (D + 63) // 64 * 64
+    assert ix.stat("split_copy") == 0
+    assert ix.stat("device_bytes") == 7 * cap * Dp + 20 * cap, ix.stat("device_bytes")
+    Q = rng.random((B, D), dtype=np.float32)
+    _, ei, ek = ref_cpu.exact_search(Q, V, k, "cosine")
+    _, i, kk = ix.search(Q, k, with_keys=True)
+    np.testing.assert_array_equal(i, ei)
+    np.testing.assert_array_equal(kk, ek)
+    assert ix.stat("split_copy") == 0  # nothing needed it
+    Q[4] = V[3]  # 300 rows the int8 pass cannot separate: host re-pass in BF16X3
+    _, ei, ek = ref_cpu.exact_search(Q, V, k, "cosine")
+    _, i, kk = ix.search(Q, k, with_keys=True)
+    np.testing.assert_array_equal(i, ei)
+    np.testing.assert_array_equal(kk, ek)
+    assert ix.stat("repass_queries") >= 1
+    assert ix.stat("split_copy") == 1 and ix.stat("split_copy_builds") == 1
+    assert ix.stat("device_bytes") == 11 * cap * Dp + 20 * cap
+    # the copy is now kept up to date by adds (and grows with the index)
+    V2 = rng.random((40000, D), dtype=np.float32)
+    ix.add(V2)
+    ix.set_param("precision", 1)  # bf16x3: reads the split copy on every search
+    Va = np.concatenate([V, V2])
+    _, ei, ek = ref_cpu.exact_search(Q, Va, k, "cosine")
+    _, i, kk = ix.search(Q, k, with_keys=True)
+    np.testing.assert_array_equal(i, ei)
+    np.testing.assert_array_equal(kk, ek)
+    assert ix.stat("split_copy_builds") == 1
+    # a bf16x3 index allocates it up front
+    ix3 = vdb.NativeIndex(D, "euclidean", precision="bf16x3")
+    ix3.add(V)
+    assert ix3.stat("split_copy") == 1
+    _, ei, ek = ref_cpu.exact_search(Q, V, k, "euclidean")
+    _, i, kk = ix3.search(Q, k, with_keys=True)
+    np.testing.assert_array_equal(i, ei)
+    np.testing.assert_array_equal(kk, ek)
+
+
+def test_device_repass_after_a_search_of_another_shape(vdb):
+    """the device re-pass's gathered-query block has slots past the gathered
+    count; they are zeroed, not left holding an earlier search's workspace bytes (which would set
+    the batch's int8 scale).  L2, a search of another batch size and k on the same stream first,
+    then a batch with one query among 300 close rows: re-passed (not the exact path), exact."""
+    import torch
+    rng = np.random.default_rng(67)
+    N, D = 40000, 128
+    V = rng.random((N, D), dtype=np.float32) * 4.0
+    V[1000:1300] = _graded_neighbours(rng, V[11], 300)
+    ix = vdb.NativeIndex(D, "euclidean")
+    ix.set_param("device_repass", 1)
+    ix.add(V)
+    st = torch.cuda.Stream()
+    st.wait_stream(torch.cuda.current_stream())
+    Q0 = (rng.random((48, D), dtype=np.float32) * 50.0).astype(np.float32)  # large |q|: big workspace values
+    q0 = torch.from_numpy(Q0).cuda()
+    o0 = [torch.empty((48, 30), dtype=t, device="cuda") for t in (torch.float32, torch.int64, torch.float64)]
+    ix.search_device(q0.data_ptr(), 48, 30, o0[0].data_ptr(), o0[1].data_ptr(), o0[2].data_ptr(), stream=st.cuda_stream)
+    B, k = 64, 10
+    Q = rng.random((B, D), dtype=np.float32) * 4.0
+    Q[5] = V[11]
+    qd = torch.from_numpy(Q).cuda()
+    sd = torch.empty((B, k), dtype=torch.float32, device="cuda")
+    idd = torch.empty((B, k), dtype=torch.int64, device="cuda")
+    kd = torch.empty((B, k), dtype=torch.float64, device="cuda")
+    ix.search_device(qd.data_ptr(), B, k, sd.data_ptr(), idd.data_ptr(), kd.data_ptr(), stream=st.cuda_stream)
+    torch.cuda.synchronize()
+    _, ei0, ek0 = ref_cpu.exact_search(Q0, V, 30, "euclidean")
+    np.testing.assert_array_equal(o0[1].cpu().numpy(), ei0)
+    _, ei, ek = ref_cpu.exact_search(Q, V, k, "euclidean")
+    np.testing.assert_array_equal(idd.cpu().numpy(), ei)
+    np.testing.assert_array_equal(kd.cpu().numpy(), ek)
+    assert ix.stat("fallback_queries") == 0, ix.stat("fallback_queries")
