@@ -288,6 +288,15 @@ hipError_t read_i8_stats(vdb_index* ix, hipStream_t st) {
     return e;
 }
 
+// Device memory zeroed and the zeroing finished when this returns, so work on ANY stream after it
+// sees zeros.  (hipMemset enqueues on the null stream, which the library's and the callers'
+// non-blocking streams are not ordered after.)
+hipError_t zero_now(void* p, size_t bytes, hipStream_t st) {
+    hipError_t e = hipMemsetAsync(p, 0, bytes, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    return e;
+}
+
 bool debug_knobs_enabled() {
     const char* e = std::getenv("VDB_DEBUG_KNOBS");
     return e && std::strcmp(e, "1") == 0;
@@ -679,11 +688,11 @@ int32_t vdb_index_create(int32_t dim, int32_t metric, int32_t device, vdb_index*
     if (const char* a8 = std::getenv("VDB_AUTO_I8")) ix->auto_i8 = std::atoi(a8) != 0;
     hipError_t e = hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMalloc(&ix->d_xmax, 64);
-    if (e == hipSuccess) e = hipMemset(ix->d_xmax, 0, 64);
+    if (e == hipSuccess) e = zero_now(ix->d_xmax, 64, ix->stream);
     if (e == hipSuccess) e = hipMalloc(&ix->d_i8, 64);
-    if (e == hipSuccess) e = hipMemset(ix->d_i8, 0, 64);
+    if (e == hipSuccess) e = zero_now(ix->d_i8, 64, ix->stream);
     if (e == hipSuccess) e = hipMalloc(&ix->d_csum, (size_t)2 * ix->Dp * sizeof(uint32_t));
-    if (e == hipSuccess) e = hipMemset(ix->d_csum, 0, (size_t)2 * ix->Dp * sizeof(uint32_t));
+    if (e == hipSuccess) e = zero_now(ix->d_csum, (size_t)2 * ix->Dp * sizeof(uint32_t), ix->stream);
     if (e != hipSuccess) {
         delete ix;
         return set_error(VDB_ERR_HIP, "index setup failed: %s", hipGetErrorString(e));
@@ -866,17 +875,18 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
     } else if (n.rfind("debug_", 0) == 0 && !debug_knobs_enabled()) {
         // test-only knobs corrupt the index on purpose: only with VDB_DEBUG_KNOBS=1
         return set_error(VDB_ERR_INVALID, "'%s' is a test-only knob (set VDB_DEBUG_KNOBS=1)", name);
-    } else if (n == "debug_negate_row8") {
-        // TEST ONLY: negates both int8 planes of row `value` (the column sums untouched): a corpus
-        // operand the int8 pass reads wrong, which under-scores a row that matches the query --
-        // the side the finish's approx-vs-exact check cannot see; the pass's checksum flags it
+    } else if (n == "debug_sink_row8") {
+        // TEST ONLY: both int8 planes of row `value` := -127 (the column sums untouched): a corpus
+        // operand the int8 pass reads wrong that UNDER-scores the row (for queries with
+        // non-negative components) -- the side the finish's approx-vs-exact check cannot see; the
+        // pass's checksum flags it
         HIP_TRY(hipSetDevice(ix->device));
         std::unique_lock<std::shared_mutex> g(ix->mu);
         if (value < 0 || value >= ix->count || !ix->Xq)
-            return set_error(VDB_ERR_INVALID, "debug_negate_row8: no int8 row %lld", (long long)value);
+            return set_error(VDB_ERR_INVALID, "debug_sink_row8: no int8 row %lld", (long long)value);
         const int wr = wait_idle(ix);
         if (wr) return wr;
-        HIP_TRY(launch_negate_row8(ix->Xq, value, ix->G / 4, ix->stream));
+        HIP_TRY(launch_sink_row8(ix->Xq, value, ix->G / 4, ix->stream));
         HIP_TRY(hipStreamSynchronize(ix->stream));
     } else if (n == "scan_checksum") {
         if (value < 0 || value > 1) return set_error(VDB_ERR_INVALID, "scan_checksum must be 0 or 1");
@@ -1761,7 +1771,11 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
                         unsigned long long* d = nullptr;
                         // flagged, overflowed, flagged in a one-plane pass, re-passed on the device
                         HIP_TRY(hipMalloc(&d, 4 * sizeof(unsigned long long)));
-                        HIP_TRY(hipMemset(d, 0, 4 * sizeof(unsigned long long)));
+                        // zeroed and COMPLETE before any search stream can use it: a plain hipMemset
+                        // runs on the null stream, which a non-blocking caller stream does not order
+                        // after -- the first search's device re-pass count could land before the
+                        // zeroing and be wiped (GPUTEST_r04: repass_queries 2 of 3 on a side stream)
+                        HIP_TRY(zero_now(d, 4 * sizeof(unsigned long long), ix->stream));
                         ix->d_totals = d;
                     }
                 }
@@ -2012,7 +2026,7 @@ int graph_upload(vdb_index* ix, int R, int64_t n, const int32_t* nbr_host, const
     hipError_t e = hipMalloc(&g->nbr, (size_t)g->cap * R * sizeof(int32_t));
     if (e == hipSuccess) e = hipMalloc(&g->entries, (size_t)std::max(n_ent, 1) * sizeof(int32_t));
     if (e == hipSuccess) e = hipMalloc(&g->d_stats, 64);
-    if (e == hipSuccess) e = hipMemset(g->d_stats, 0, 64);
+    if (e == hipSuccess) e = zero_now(g->d_stats, 64, ix->stream);
     if (e == hipSuccess && n > 0) e = hipMemcpy(g->nbr, nbr_host, (size_t)n * R * sizeof(int32_t), hipMemcpyHostToDevice);
     if (e == hipSuccess && n_ent > 0)
         e = hipMemcpy(g->entries, ent_host, (size_t)n_ent * sizeof(int32_t), hipMemcpyHostToDevice);

@@ -51,10 +51,10 @@ hipError_t launch_prep8(const float* Q, const double* qn64, const float* qmax, i
                         const uint32_t* csum = nullptr, uint32_t* chke = nullptr);
 // The int8 pass's checksum (vdb_scan8.hip): column sums of the int8 copy's two planes over rows
 // [row0, row0 + n) added into csum [2][Dp]; the L2 start values' sum for a batch (*out +=); and a
-// test-only corpus fault (one row's planes negated, the column sums left as they were)
+// test-only corpus fault (one row's planes set to -127, the column sums left as they were)
 hipError_t launch_colsum8(const float* Xq, int64_t row0, int64_t n, int G8, uint32_t* csum, hipStream_t st);
 hipError_t launch_rinsum8(const float* rinit, int64_t N, const float* qscal, uint32_t* out, hipStream_t st);
-hipError_t launch_negate_row8(float* Xq, int64_t row, int G8, hipStream_t st);
+hipError_t launch_sink_row8(float* Xq, int64_t row, int G8, hipStream_t st);
 hipError_t launch_pilot8(int prec, int metric, const float* Xq, const float* rinit, const uint32_t* mask,
                          const float* Qq, const float* qscal, int G8, int64_t N, int B, int n_qblocks, int QB,
                          int n_sample, uint32_t* pslots, hipStream_t st);

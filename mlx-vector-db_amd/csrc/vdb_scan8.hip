@@ -214,30 +214,22 @@ hipError_t launch_rinsum8(const float* rinit, int64_t N, const float* qscal, uin
     return hipGetLastError();
 }
 
-// TEST ONLY (index knob debug_negate_row8, behind VDB_DEBUG_KNOBS=1): negates both planes of one
-// row of the int8 copy without touching the column sums -- a corpus operand the pass reads
-// wrong, which under-scores a row that matched the query (tests/test_gpu_guards.py)
-__global__ void __launch_bounds__(64) negate_row8_kernel(float* __restrict__ Xq, int64_t r, int G8) {
+// TEST ONLY (index knob debug_sink_row8, behind VDB_DEBUG_KNOBS=1): sets both planes of one row of
+// the int8 copy to -127 without touching the column sums -- a corpus operand the pass reads wrong
+// that UNDER-scores the row for every query with non-negative components (the benchmark's data)
+__global__ void __launch_bounds__(64) sink_row8_kernel(float* __restrict__ Xq, int64_t r, int G8) {
     const int nc = 2 * G8;
+    const float v = __uint_as_float(0x81818181u);  // four int8 -127
     for (int t = threadIdx.x; t < 2 * nc; t += 64) {
         const int pl = t / nc, c = t - pl * nc;
         float* p = Xq + corpus_block((uint64_t)r >> 5, c >> 1, 0, G8) + (size_t)((r & 31) + 32 * (c & 1)) * 4 +
                    (pl ? corpus_plane(G8) : 0);
-        f32x4 v = *(f32x4*)p;
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {
-            const uint32_t u = __float_as_uint(v[w]);
-            uint32_t o = 0u;
-#pragma unroll
-            for (int bt = 0; bt < 4; ++bt) o |= ((uint32_t)(-(int)(int8_t)((u >> (8 * bt)) & 255u)) & 255u) << (8 * bt);
-            v[w] = __uint_as_float(o);
-        }
-        *(f32x4*)p = v;
+        *(f32x4*)p = f32x4{v, v, v, v};
     }
 }
 
-hipError_t launch_negate_row8(float* Xq, int64_t row, int G8, hipStream_t st) {
-    hipLaunchKernelGGL(negate_row8_kernel, dim3(1), dim3(64), 0, st, Xq, row, G8);
+hipError_t launch_sink_row8(float* Xq, int64_t row, int G8, hipStream_t st) {
+    hipLaunchKernelGGL(sink_row8_kernel, dim3(1), dim3(64), 0, st, Xq, row, G8);
     return hipGetLastError();
 }
 

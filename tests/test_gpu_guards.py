@@ -63,7 +63,7 @@ def test_debug_knobs_refused_without_opt_in(vdb, monkeypatch):
     with pytest.raises(Exception, match="test-only"):
         ix.set_param("debug_stale_rinit", 5)
     with pytest.raises(Exception, match="test-only"):
-        ix.set_param("debug_negate_row8", 5)
+        ix.set_param("debug_sink_row8", 5)
 
 
 @pytest.mark.parametrize("precision", ["i8", "i8x3", "bf16x3"])
@@ -97,8 +97,9 @@ def test_consistency_guard_flags_a_planted_stale_operand(vdb, precision, debug_k
 @pytest.mark.parametrize("metric", ["cosine", "euclidean"])
 def test_checksum_flags_a_planted_under_scoring_operand(vdb, precision, metric, debug_knobs):
     """the blind side of the approx-vs-exact guard.  Each query's true top-1
-    row has its int8 planes negated (debug_negate_row8: the column sums stay, as for a corpus
-    operand the pass reads wrong), so the pass UNDER-scores it: it never becomes a candidate, and
+    row has its int8 planes set to -127 (debug_sink_row8: the column sums stay, as for a corpus
+    operand the pass reads wrong), so the pass UNDER-scores it for every query (the data are
+    non-negative): it never becomes a candidate of any query, and
     the finish's consistency check -- which sees only the rerank set -- has nothing to compare.
     With the pass's checksum off the search returns wrong, certified results (the blind side,
     shown); with it on (the default) every query's H (L) accumulator sums disagree with the
@@ -114,7 +115,7 @@ def test_checksum_flags_a_planted_under_scoring_operand(vdb, precision, metric, 
     np.testing.assert_array_equal(i, ei)
     assert ix.stat("inconsistent_queries") == 0
     for r in sorted(set(ei[:, 0].tolist())):
-        ix.set_param("debug_negate_row8", int(r))
+        ix.set_param("debug_sink_row8", int(r))
     ix.set_param("scan_checksum", 0)
     f0 = ix.stat("fallback_queries")
     _, i, kk = ix.search(Q, k, with_keys=True)
