@@ -466,6 +466,8 @@ def main():
                     help="device re-pass of uncertified queries: -1 auto (armed after a fallback), 0 off, 1 always")
     ap.add_argument("--scan-pace", type=int, default=None, help="int8 pass: 1 pace the query blocks of a row range, "
                     "0 off (default; tuning)")
+    ap.add_argument("--scan-checksum", type=int, default=None,
+                    help="int8 pass checksum checked by the finish: 1 on (default), 0 off (A/B of its cost)")
     ap.add_argument("--rows", type=int, default=None, help="override the corpus rows (exploration only)")
     ap.add_argument("--batch", type=int, default=None,
                     help="override the batch (exploration only: e.g. one rank's shape of a weak-scaled run)")
@@ -589,6 +591,8 @@ def bench_brute(cfg, args, world, rank, local, dev, primary=True):
         ix.set_param("device_repass", args.device_repass)
     if args.i8_refine is not None:
         ix.set_param("i8_refine", args.i8_refine)
+    if args.scan_checksum is not None:
+        ix.set_param("scan_checksum", args.scan_checksum)
     if args.no_fallback:
         ix.set_param("no_fallback", 1)
     ix.reserve(n_local)

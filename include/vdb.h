@@ -27,8 +27,11 @@
  *     several threads overlap on the device) and return when the results are
  *     in host memory.
  *   - The library never frees caller memory.  An index owns its device-resident
- *     corpus (row-major fp32 rows + a split-bf16 candidate copy in MFMA operand
- *     tiles) and a per-call workspace pool.
+ *     corpus: row-major fp32 rows (the exact rerank), the int8
+ *     candidate copy in MFMA operand tiles (two planes, the default pass) with
+ *     its row-major hi plane and column sums, and -- for the bf16 / fp32
+ *     precisions, or under auto only once a search first runs a split pass --
+ *     a split-bf16 (fp32) candidate copy; plus a per-call workspace pool.
  *   - All entry points are thread-safe; searches on one index may run from
  *     several threads at once (the reference serves from a 4-thread executor,
  *     api/routes/vectors.py:43).

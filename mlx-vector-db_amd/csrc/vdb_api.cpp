@@ -1600,8 +1600,9 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     float* q8err2 = i8_refine ? c.take<float>(Bp) : nullptr;
     uint32_t* pace = c.take<uint32_t>((size_t)(n_wg + 7) / 8 * 8 * n_qblocks + 64);
     uint32_t* chkp = chk ? c.take<uint32_t>((size_t)2 * n_wg8 * Bp) : nullptr;
-    uint32_t* chke = chk ? c.take<uint32_t>((size_t)2 * Bp) : nullptr;
     uint32_t* chkr = chk && ix->metric == 1 ? c.take<uint32_t>(64) : nullptr;
+    // (the pilot writes the checksum's expectations when it runs; else the finish computes them)
+    uint32_t* chke = chk && n_pilot > 0 ? c.take<uint32_t>((size_t)2 * Bp) : nullptr;
     float* rep_q = mem == VDB_MEM_DEVICE ? c.take<float>((size_t)R_rep * D) : nullptr;
     float* rep_s = mem == VDB_MEM_DEVICE ? c.take<float>((size_t)R_rep * k) : nullptr;
     int64_t* rep_i = mem == VDB_MEM_DEVICE ? c.take<int64_t>((size_t)R_rep * k) : nullptr;
@@ -1639,7 +1640,7 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
             c8.xl_max = ix->i8st[5];
             c8.rmax_half = 0.5 * ix->xmax * ix->xmax;
             HIP_TRY(launch_prep8(Qd, qn64, q8max, B, Bp, D, Gs, ix->metric, prec, c8, Qt, q8lsl, q8err, q8scal, st,
-                                 q8res, q8err2, chk ? ix->d_csum : nullptr, chke));
+                                 q8res, q8err2));
             if (chkr) {  // L2: the start values' sum at this batch's scale
                 HIP_TRY(hipMemsetAsync(chkr, 0, sizeof(uint32_t), st));
                 HIP_TRY(launch_rinsum8(ix->rinit32, N, q8scal, chkr, st));
@@ -1666,7 +1667,8 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
             if (n_pilot > 0) {
                 if (i8_pass) {
                     HIP_TRY(launch_pilot8(prec, ix->metric, Xscan, ix->rinit32, md, Qt, q8scal, Gs, N, B,
-                                          (B + QB_pilot - 1) / QB_pilot, QB_pilot, n_pilot, pslots, st));
+                                          (B + QB_pilot - 1) / QB_pilot, QB_pilot, n_pilot, pslots, st,
+                                          chke ? ix->d_csum : nullptr, chke));
                     HIP_TRY(launch_pilot_bound(pslots, B, pilot_rank, gthr, st));
                 } else if (split_pass) {
                     HIP_TRY(launch_pilot2(prec, ix->metric, pilot_rank, Xscan, ix->rinit32, md, Qt, Gs, N, B,
@@ -1750,6 +1752,9 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
                 fa.chkp = chkp;
                 fa.chke = chke;
                 fa.chkr = chkr;
+                fa.chk_q = Qt;
+                fa.chk_csum = ix->d_csum;
+                fa.chk_g8 = Gs;
                 fa.chk_nw = n_wg8;
                 fa.chk_ld = Bp;
                 fa.chk_l = prec == PREC_I8X3;

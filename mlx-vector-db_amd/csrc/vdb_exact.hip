@@ -346,27 +346,46 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
     if (a.gate && b >= *a.gate) return;  // device re-pass: a slot past the gathered count
     FIN_STAMP(0);
     // The int8 pass's checksum (vdb_scan8.hip): the workgroups' partial sums of this query's H (and
-    // L) accumulators against the value the stored operands imply.  Read first, decided last.
+    // L) accumulators ([plane][query][workgroup], one coalesced read per lane), loaded here and
+    // compared at the end against the value the stored operands imply.
     __shared__ int s_ckbad;
+    uint32_t ck_h = 0u, ck_l = 0u, ck_eh = 0u, ck_el = 0u;
     if (a.chkp && tid < 64) {
-        uint32_t h = 0u, l = 0u;
         for (int w = tid; w < a.chk_nw; w += 64) {
-            h += a.chkp[(size_t)w * a.chk_ld + b];
-            if (a.chk_l) l += a.chkp[((size_t)a.chk_nw + w) * a.chk_ld + b];
+            ck_h += a.chkp[(size_t)b * a.chk_nw + w];
+            if (a.chk_l) ck_l += a.chkp[((size_t)a.chk_ld + b) * a.chk_nw + w];
         }
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {
-            h += (uint32_t)__shfl_xor((int)h, off, 64);
-            l += (uint32_t)__shfl_xor((int)l, off, 64);
+        if (a.chke && tid == 0) {  // the expectations the pilot computed
+            ck_eh = a.chke[2 * (size_t)b];
+            ck_el = a.chke[2 * (size_t)b + 1];
         }
-        if (tid == 0) {
-            const uint32_t eh = a.chke[2 * (size_t)b] + (a.chkr ? *a.chkr : 0u);
-            s_ckbad = h != eh || (a.chk_l && l != a.chke[2 * (size_t)b + 1]);
-        }
-    } else if (tid == 0) {
-        s_ckbad = 0;
     }
-    __syncthreads();
+    if (tid == 0) s_ckbad = 0;
+    // ... or, without a pilot (a gated re-pass sub-search), computed here by the second wave:
+    // sum_d CH[d] qh[d] (+ for L: CH ql + CL qh) from the query's int8 tiles (prep8 layout: s2_blk
+    // of vdb_scan2_kernel.h, G8 + QG_EXTRA groups)
+    if (a.chkp && !a.chke && tid >= 64 && tid < 128) {
+        const int l = tid - 64, G8 = a.chk_g8, GQ = G8 + QG_EXTRA, Dp = 32 * G8;
+        for (int cc = l; cc < 2 * G8; cc += 64) {
+            const int g = cc >> 1, h = cc & 1, d0 = 32 * g + 16 * h;
+            const float* src = a.chk_q + ((((size_t)(b >> 5) >> 2) * GQ + g) * 8 + ((b >> 5) & 3)) * BLOCK_FLOATS +
+                               (size_t)((b & 31) + 32 * h) * 4;
+            const f32x4 qh4 = *(const f32x4*)src;
+            const f32x4 ql4 = a.chk_l ? *(const f32x4*)(src + 4 * BLOCK_FLOATS) : qh4;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                const uint32_t uh = __float_as_uint(qh4[w]), ul = __float_as_uint(ql4[w]);
+#pragma unroll
+                for (int bt = 0; bt < 4; ++bt) {
+                    const int d = d0 + 4 * w + bt;
+                    const uint32_t hv = (uint32_t)(int)(int8_t)((uh >> (8 * bt)) & 255u);
+                    const uint32_t ch = a.chk_csum[d];
+                    ck_eh += hv * ch;
+                    if (a.chk_l) ck_el += (uint32_t)(int)(int8_t)((ul >> (8 * bt)) & 255u) * ch + hv * a.chk_csum[Dp + d];
+                }
+            }
+        }
+    }
     const int64_t c = min((int64_t)a.gl_cnt[b], a.gl_cap);
 #ifdef VDB_STAMP
     if (threadIdx.x == 0) g_fin_stamps[b][7] = (unsigned long long)c;
@@ -625,8 +644,32 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
     // up in the rows it over-scored).  s_epsb = eps without the L2 rounding term in |approx|.
     __shared__ double s_epsb;
     __shared__ int s_fl0, s_bad;
+    __shared__ uint32_t s_ckeh, s_ckel;
+    if (a.chkp && tid < 128) {  // the checksum's verdict (its loads were issued at the start)
+        // wave 0: the pass's sums (+ the pilot's expectations in lane 0); wave 1: the expectations
+        // when there was no pilot
+        const bool w1 = tid >= 64;
+        uint32_t x = w1 ? ck_eh : ck_h, y = w1 ? ck_el : ck_l;
+        if (w1 && a.chke) x = y = 0u;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            x += (uint32_t)__shfl_xor((int)x, off, 64);
+            y += (uint32_t)__shfl_xor((int)y, off, 64);
+        }
+        if (tid == 64 && !a.chke) {
+            s_ckeh = x;
+            s_ckel = y;
+        }
+        ck_h = x;
+        ck_l = y;
+    }
     __syncthreads();
     if (tid == 0) {
+        if (a.chkp) {
+            const uint32_t eh = (a.chke ? ck_eh : s_ckeh) + (a.chkr ? *a.chkr : 0u);
+            const uint32_t el = a.chke ? ck_el : s_ckel;
+            s_ckbad = ck_h != eh || (a.chk_l && ck_l != el);
+        }
         const bool full = m == KP;
         const double T = (double)key_to_float(a.gthr[b]);
         const bool have_k = m >= a.k;

@@ -47,17 +47,19 @@ hipError_t launch_quant_rows(const float* X, const float* inv32, const float* mu
 // queries -> int8 tiles Qq (G8 + QG_EXTRA groups), per query lsl / qerr, per batch qscal[3]
 hipError_t launch_prep8(const float* Q, const double* qn64, const float* qmax, int B, int Bp, int D, int G8,
                         int metric, int prec, const Int8Consts& c, float* Qq, float* lsl, float* qerr, float* qscal,
-                        hipStream_t st, float* qres = nullptr, float* qerr2 = nullptr,
-                        const uint32_t* csum = nullptr, uint32_t* chke = nullptr);
+                        hipStream_t st, float* qres = nullptr, float* qerr2 = nullptr);
 // The int8 pass's checksum (vdb_scan8.hip): column sums of the int8 copy's two planes over rows
 // [row0, row0 + n) added into csum [2][Dp]; the L2 start values' sum for a batch (*out +=); and a
 // test-only corpus fault (one row's planes set to -127, the column sums left as they were)
 hipError_t launch_colsum8(const float* Xq, int64_t row0, int64_t n, int G8, uint32_t* csum, hipStream_t st);
 hipError_t launch_rinsum8(const float* rinit, int64_t N, const float* qscal, uint32_t* out, hipStream_t st);
 hipError_t launch_sink_row8(float* Xq, int64_t row, int G8, hipStream_t st);
+// (csum / chke, optional: the first workgroup of each query block also writes the int8 pass's
+// checksum expectations per query, chke [B][2] -- see FinishArgs::chke)
 hipError_t launch_pilot8(int prec, int metric, const float* Xq, const float* rinit, const uint32_t* mask,
                          const float* Qq, const float* qscal, int G8, int64_t N, int B, int n_qblocks, int QB,
-                         int n_sample, uint32_t* pslots, hipStream_t st);
+                         int n_sample, uint32_t* pslots, hipStream_t st, const uint32_t* csum = nullptr,
+                         uint32_t* chke = nullptr);
 int scan8_rows_per_step(int prec, int metric, bool q4 = false);
 int scan8_qb(int KP, bool q4 = false);  // queries per block of the int8 pass
 bool scan8_q4_ok(int G8, int prec);     // the 128-query shape fits (short rows)
@@ -229,12 +231,15 @@ struct FinishArgs {
     double* sx_ek = nullptr; uint32_t* sx_ck = nullptr; uint32_t* sx_cr = nullptr; int* sx_n = nullptr;
     int* done = nullptr;
     // optional, the int8 pass's checksum (vdb_scan8.hip): per-workgroup partial sums of the H (and
-    // L) accumulators chkp [2][chk_nw][chk_ld], the expected values chke [Bp][2] (prep8) and, for
-    // L2, the start values' sum *chkr; a mismatch flags the query (exact path)
+    // L) accumulators chkp [2][chk_ld][chk_nw]; the value the operands imply is computed here from
+    // the query's int8 tiles chk_q (prep8's, chk_g8 32-dim groups) and the copy's column sums
+    // chk_csum [2][Dp], plus for L2 the start values' sum *chkr; a mismatch flags the query
     const uint32_t* chkp = nullptr;
-    const uint32_t* chke = nullptr;
+    const uint32_t* chke = nullptr;  // the expectations from the pilot (else computed here from chk_q)
     const uint32_t* chkr = nullptr;
-    int chk_nw = 0, chk_ld = 0;
+    const float* chk_q = nullptr;
+    const uint32_t* chk_csum = nullptr;
+    int chk_nw = 0, chk_ld = 0, chk_g8 = 0;
     bool chk_l = false;
 };
 hipError_t launch_finish(int metric, int KP, const FinishArgs& a, int B, hipStream_t st);

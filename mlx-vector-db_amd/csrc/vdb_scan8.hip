@@ -244,8 +244,7 @@ __global__ void __launch_bounds__(256) prep8_kernel(const float* __restrict__ Q,
                                                     int metric, int prec, Int8Consts c, float* __restrict__ Qq,
                                                     float* __restrict__ lsl, float* __restrict__ qerr,
                                                     float* __restrict__ qscal, float* __restrict__ qres,
-                                                    float* __restrict__ qerr2, const uint32_t* __restrict__ csum,
-                                                    uint32_t* __restrict__ chke) {
+                                                    float* __restrict__ qerr2) {
     const int lane = threadIdx.x & 63;
     const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (b >= Bp) return;
@@ -270,8 +269,6 @@ __global__ void __launch_bounds__(256) prep8_kernel(const float* __restrict__ Q,
     const float isq = 1.0f / sq;
     const int GQ = G8 + QG_EXTRA;
     double s_rq = 0.0, s_r8 = 0.0, s_ql = 0.0, s_qh = 0.0;
-    uint32_t eh = 0u, el = 0u;  // the checksum's query terms: sum_d CH qh, sum_d CH ql + CL qh (mod 2^32)
-    const int Dp = 32 * G8;
     for (int cc = lane; cc < 2 * GQ; cc += 64) {
         const int g = cc >> 1, h = cc & 1;
         const int d0 = 32 * (g % G8) + 16 * h;
@@ -281,11 +278,6 @@ __global__ void __launch_bounds__(256) prep8_kernel(const float* __restrict__ Q,
             const int d = d0 + j;
             const float qv = (real && d < D) ? q[d] * scale : 0.0f;
             split_i8(qv * isq, hv[j], lv[j]);
-            if (csum && g < G8) {
-                const uint32_t ch = csum[d], cl = csum[Dp + d];
-                eh += (uint32_t)hv[j] * ch;
-                el += (uint32_t)lv[j] * ch + (uint32_t)hv[j] * cl;
-            }
             if (g < G8) {
                 const double qh = (double)sq * hv[j], ql = (double)sq * lv[j] / 256.0;
                 const double r8 = (double)qv - qh, rq = r8 - ql;
@@ -317,15 +309,6 @@ __global__ void __launch_bounds__(256) prep8_kernel(const float* __restrict__ Q,
     s_r8 = wave_sum_butterfly(s_r8);
     s_ql = wave_sum_butterfly(s_ql);
     s_qh = wave_sum_butterfly(s_qh);
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        eh += (uint32_t)__shfl_xor((int)eh, off, 64);
-        el += (uint32_t)__shfl_xor((int)el, off, 64);
-    }
-    if (chke && lane == 0) {
-        chke[2 * b] = eh;
-        chke[2 * b + 1] = el;
-    }
     if (lane == 0) {
         const bool x3 = prec == PREC_I8X3;
         const double za = c.zmax_h + (x3 ? c.xl_max : 0.0);  // bound of |z~|
@@ -346,9 +329,9 @@ __global__ void __launch_bounds__(256) prep8_kernel(const float* __restrict__ Q,
 
 hipError_t launch_prep8(const float* Q, const double* qn64, const float* qmax, int B, int Bp, int D, int G8,
                         int metric, int prec, const Int8Consts& c, float* Qq, float* lsl, float* qerr, float* qscal,
-                        hipStream_t st, float* qres, float* qerr2, const uint32_t* csum, uint32_t* chke) {
+                        hipStream_t st, float* qres, float* qerr2) {
     hipLaunchKernelGGL(prep8_kernel, dim3((Bp + 3) / 4), dim3(256), 0, st, Q, qn64, qmax, B, Bp, D, G8, metric, prec, c,
-                       Qq, lsl, qerr, qscal, qres, qerr2, csum, chke);
+                       Qq, lsl, qerr, qscal, qres, qerr2);
     return hipGetLastError();
 }
 
@@ -363,11 +346,49 @@ template <int PREC, int METRIC, int QT>
 __global__ void __launch_bounds__(64 * PILOT8_WAVES)
 pilot8_scores_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, const uint32_t* __restrict__ mask,
                      const float* __restrict__ Qq, const float* __restrict__ qscal, int G, int64_t N, int B,
-                     int64_t n_tiles, int n_sample, uint32_t* __restrict__ pslots) {
+                     int64_t n_tiles, int n_sample, uint32_t* __restrict__ pslots,
+                     const uint32_t* __restrict__ csum, uint32_t* __restrict__ chke) {
     constexpr int QB = 32 * QT;
     constexpr int XPL = Planes8<PREC>::XPL;
     constexpr size_t GSTEP = 8 * BLOCK_FLOATS, PLANE = 4 * BLOCK_FLOATS;
     constexpr bool HL = Planes8<PREC>::L;
+    // The checksum's expected values for this query block (vdb_scan8_kernel.h; the first pilot
+    // workgroup of each block, off the scan's path): per query sum_d CH[d] qh[d] (+ L: CH ql + CL qh)
+    if (chke && blockIdx.x == 0) {
+        const int wv_ = threadIdx.x >> 6, ln = threadIdx.x & 63;
+        const int GQ = G + QG_EXTRA, Dp = 32 * G;
+        for (int qq = wv_; qq < QB; qq += PILOT8_WAVES) {
+            const int q = blockIdx.y * QB + qq;
+            uint32_t eh = 0u, el = 0u;
+            for (int cc = ln; cc < 2 * G; cc += 64) {
+                const int g = cc >> 1, h = cc & 1, d0 = 32 * g + 16 * h;
+                const float* src = Qq + s2_blk((uint64_t)(q >> 5), g, GQ) + (size_t)((q & 31) + 32 * h) * 4;
+                const f32x4 qh4 = *(const f32x4*)src;
+                const f32x4 ql4 = *(const f32x4*)(src + PLANE);
+#pragma unroll
+                for (int w = 0; w < 4; ++w) {
+                    const uint32_t uh = __float_as_uint(qh4[w]), ul = __float_as_uint(ql4[w]);
+#pragma unroll
+                    for (int bt = 0; bt < 4; ++bt) {
+                        const int d = d0 + 4 * w + bt;
+                        const uint32_t hv = (uint32_t)(int)(int8_t)((uh >> (8 * bt)) & 255u);
+                        const uint32_t ch = csum[d];
+                        eh += hv * ch;
+                        if (HL) el += (uint32_t)(int)(int8_t)((ul >> (8 * bt)) & 255u) * ch + hv * csum[Dp + d];
+                    }
+                }
+            }
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) {
+                eh += (uint32_t)__shfl_xor((int)eh, off, 64);
+                el += (uint32_t)__shfl_xor((int)el, off, 64);
+            }
+            if (ln == 0 && q < B) {
+                chke[2 * (size_t)q] = eh;
+                chke[2 * (size_t)q + 1] = el;
+            }
+        }
+    }
     __shared__ int s_part[PILOT8_WAVES][HL ? 2 : 1][QT][16][64];  // (I8: 32 KiB, room beside a scan)
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
@@ -438,7 +459,7 @@ pilot8_scores_kernel(const float* __restrict__ Xq, const float* __restrict__ rin
 
 hipError_t launch_pilot8(int prec, int metric, const float* Xq, const float* rinit, const uint32_t* mask,
                          const float* Qq, const float* qscal, int G8, int64_t N, int B, int n_qblocks, int QB,
-                         int n_sample, uint32_t* pslots, hipStream_t st) {
+                         int n_sample, uint32_t* pslots, hipStream_t st, const uint32_t* csum, uint32_t* chke) {
     const int64_t n_tiles = (N + 31) / 32;
     if (n_sample > n_tiles) n_sample = (int)n_tiles;
     if (n_sample <= 0) return hipSuccess;
@@ -448,7 +469,7 @@ hipError_t launch_pilot8(int prec, int metric, const float* Xq, const float* rin
 #define VDB_PILOT8(P, M, QTV)                                                                                    \
     if (!launched && prec == P && metric == M && QB == 32 * QTV) {                                               \
         hipLaunchKernelGGL((pilot8_scores_kernel<P, M, QTV>), grid, dim3(64 * PILOT8_WAVES), 0, st, Xq, rinit,   \
-                           mask, Qq, qscal, G8, N, B, n_tiles, n_sample, pslots);                                \
+                           mask, Qq, qscal, G8, N, B, n_tiles, n_sample, pslots, csum, chke);                   \
         launched = true;                                                                                         \
     }
     VDB_PILOT8(PREC_I8, 0, 2) VDB_PILOT8(PREC_I8, 1, 2) VDB_PILOT8(PREC_I8, 0, 1) VDB_PILOT8(PREC_I8, 1, 1)

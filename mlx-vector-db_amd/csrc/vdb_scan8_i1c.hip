@@ -12,6 +12,6 @@ S8_UNIT(launch_scan8_i1c, PREC_I8, 0, VDB_S8_PX1, 4)
 
 #ifdef VDB_STAMP8
 extern "C" int vdb_debug_scan8_stamps_i1c(unsigned long long* out, int n_waves) {
-    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(vdb::g_scan8_stamps), (size_t)n_waves * 10 * sizeof(unsigned long long));
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(vdb::g_scan8_stamps), (size_t)n_waves * 12 * sizeof(unsigned long long));
 }
 #endif

@@ -71,7 +71,7 @@ constexpr int scan8_nw(int prec, int metric, int QT = 2) {
 // Diagnostic build only (make variant VDEFS=-DVDB_STAMP8): per-wave cycles of scan8_kernel:
 // [0] total, [1] in the stream waits (s8_wait), [2] K-loop (step start to the last group's
 // refill, waits included), [3] epilogue, [4] steps, [5] start time (absolute)
-static __device__ unsigned long long g_scan8_stamps[1 << 16][10];
+static __device__ unsigned long long g_scan8_stamps[1 << 16][12];
 #define S8_NOW() __builtin_amdgcn_s_memtime()
 #define S8_STAMP(...) __VA_ARGS__
 #else
@@ -104,20 +104,41 @@ template <int PREC, int RT, int QT>
 __device__ __forceinline__ void group_mfma8(const f32x4 (&x)[RT][Planes8<PREC>::XPL],
                                             const f32x4 (&q)[QT][Planes8<PREC>::QPL], i32x16 (&aH)[RT][QT],
                                             i32x16 (&aL)[RT][QT]) {
+    // every H product first, then the L ones (I8X3): the tile tests after the step's last group
+    // read H alone, so H is complete while the group's L MFMAs still run; and each L set's two
+    // dependent MFMAs are not issued back to back
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-        for (int qt = 0; qt < QT; ++qt) {
-            const i32x4 xh = __builtin_bit_cast(i32x4, x[rt][0]);
-            const i32x4 qh = __builtin_bit_cast(i32x4, q[qt][0]);
-            aH[rt][qt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(xh, qh, aH[rt][qt], 0, 0, 0);
-            if constexpr (PREC == PREC_I8X3) {
-                const i32x4 ql = __builtin_bit_cast(i32x4, q[qt][Planes8<PREC>::QPL - 1]);
-                aL[rt][qt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(xh, ql, aL[rt][qt], 0, 0, 0);
-                aL[rt][qt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(__builtin_bit_cast(i32x4, x[rt][Planes8<PREC>::XPL - 1]),
-                                                                   qh, aL[rt][qt], 0, 0, 0);
-            }
-        }
+        for (int qt = 0; qt < QT; ++qt)
+            aH[rt][qt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(__builtin_bit_cast(i32x4, x[rt][0]),
+                                                               __builtin_bit_cast(i32x4, q[qt][0]), aH[rt][qt], 0, 0, 0);
+    if constexpr (PREC == PREC_I8X3) {
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt)
+                aL[rt][qt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(
+                    __builtin_bit_cast(i32x4, x[rt][0]), __builtin_bit_cast(i32x4, q[qt][Planes8<PREC>::QPL - 1]),
+                    aL[rt][qt], 0, 0, 0);
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt)
+                aL[rt][qt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(
+                    __builtin_bit_cast(i32x4, x[rt][Planes8<PREC>::XPL - 1]), __builtin_bit_cast(i32x4, q[qt][0]),
+                    aL[rt][qt], 0, 0, 0);
+    }
+}
+
+// the sum of 16 accumulators mod 2^32 as a depth-3 tree of v_add3_u32 (the checksum)
+__device__ __forceinline__ uint32_t hsum16(const i32x16& a) {
+    const uint32_t s0 = (uint32_t)a[0] + (uint32_t)a[1] + (uint32_t)a[2];
+    const uint32_t s1 = (uint32_t)a[3] + (uint32_t)a[4] + (uint32_t)a[5];
+    const uint32_t s2 = (uint32_t)a[6] + (uint32_t)a[7] + (uint32_t)a[8];
+    const uint32_t s3 = (uint32_t)a[9] + (uint32_t)a[10] + (uint32_t)a[11];
+    const uint32_t s4 = (uint32_t)a[12] + (uint32_t)a[13] + (uint32_t)a[14];
+    return (s0 + s1 + s2) + (s3 + s4 + (uint32_t)a[15]);
 }
 
 __device__ __forceinline__ int imax16(const i32x16& a) {  // a depth-3 tree of v_max3_i32
@@ -239,7 +260,7 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
     const int lane = threadIdx.x & 63;
     const int lane4 = lane * 4;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    S8_STAMP(const unsigned long long st_t0 = S8_NOW(), st_r0 = __builtin_amdgcn_s_memrealtime(); unsigned long long st_w = 0, st_k = 0, st_e = 0, st_n = 0, st_x = 0, st_y = 0, st_z = 0;)
+    S8_STAMP(const unsigned long long st_t0 = S8_NOW(), st_r0 = __builtin_amdgcn_s_memrealtime(); unsigned long long st_w = 0, st_k = 0, st_e = 0, st_n = 0, st_x = 0, st_y = 0, st_z = 0, st_q = 0, st_f = 0;)
     int wg, qb;
     xcd_map(n_qb, wg, qb);
     const uint32_t ptag = pace_tag & 0xFFFu;
@@ -455,40 +476,6 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
             continue;
         }
 #endif
-        // ---- checksum: every accumulator of a row < N (a wave-uniform test per step; only the
-        // last step of the corpus holds rows past N) ----
-        if (chkp) {
-            if ((t0 + RT) * 32 <= N) {
-#pragma unroll
-                for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-                    for (int qt = 0; qt < QT; ++qt) {
-                        uint32_t a = ckh[qt];
-#pragma unroll
-                        for (int v = 0; v < 16; v += 2) a += (uint32_t)aH[rt][qt][v] + (uint32_t)aH[rt][qt][v + 1];
-                        ckh[qt] = a;
-                        if constexpr (HL) {
-                            uint32_t c = ckl[qt];
-#pragma unroll
-                            for (int v = 0; v < 16; v += 2) c += (uint32_t)aL[rt][qt][v] + (uint32_t)aL[rt][qt][v + 1];
-                            ckl[qt] = c;
-                        }
-                    }
-            } else {
-#pragma unroll
-                for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-                    for (int qt = 0; qt < QT; ++qt)
-#pragma unroll
-                        for (int v = 0; v < 16; ++v) {
-                            const int64_t row = (t0 + rt) * 32 + 8 * (v >> 2) + 4 * (lane >> 5) + (v & 3);
-                            if (row < N) {
-                                ckh[qt] += (uint32_t)aH[rt][qt][v];
-                                if constexpr (HL) ckl[qt] += (uint32_t)aL[rt][qt][v];
-                            }
-                        }
-            }
-        }
         // ---- epilogue ----
         int thi[QT];
         bool qok[QT];
@@ -508,6 +495,28 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
 #pragma unroll
             for (int qt = 0; qt < QT; ++qt)
                 todo |= __any(qok[qt] && imax16(aH[rt][qt]) > thi[qt]) ? 1u << (rt * QT + qt) : 0u;
+        // ---- checksum: every accumulator of a row < N (a wave-uniform test per step; only the
+        // last step of the corpus holds rows past N).  After the tile tests, so their ballot is not
+        // held up behind it; pairwise trees, not one dependent chain per tile ----
+        if (chkp) {
+            if ((t0 + RT) * 32 <= N) {
+#pragma unroll
+                for (int qt = 0; qt < QT; ++qt) {
+#pragma unroll
+                    for (int rt = 0; rt < RT; ++rt) ckh[qt] += hsum16(aH[rt][qt]);
+                }
+            } else {
+#pragma unroll
+                for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+                    for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+                        for (int v = 0; v < 16; ++v) {
+                            const int64_t row = (t0 + rt) * 32 + 8 * (v >> 2) + 4 * (lane >> 5) + (v & 3);
+                            if (row < N) ckh[qt] += (uint32_t)aH[rt][qt][v];
+                        }
+            }
+        }
         S8_STAMP(const unsigned long long st_d = S8_NOW(); st_z += st_d - st_c; st_x += (todo != 0u) + ((unsigned long long)__builtin_popcount(todo) << 20);)
         // The rare insertions: one tile at a time through ONE copy of the insertion code (the tile's
         // registers picked by a wave-uniform switch), lanes whose fp32 (half-)score H uH (+ L uL)
@@ -624,7 +633,7 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
                     pmask |= 1u << t;
                 }
             }
-            S8_STAMP(if (!joined) st_y += (S8_NOW() - st_c) << 20;)
+            S8_STAMP(if (!joined) { st_y += (S8_NOW() - st_c) << 20; st_f -= S8_NOW(); })
             // compaction rounds (as scan2): lockstep = a workgroup barrier per step; FLAGSYNC = a
             // wave with leftovers raises s_need and the others join at their step end
             if constexpr (!FLAGSYNC) {
@@ -645,6 +654,29 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
             todo = pmask;
             pmask = 0;
         }
+        // the checksum's L sums (I8X3), at the end of the epilogue: the tile tests read only H,
+        // so a step without passing tiles never waited for its last L MFMAs -- summing L beside
+        // the H sums made every C4 step wait for the shared matrix pipe's drain (scan +7%)
+        if constexpr (HL) {
+            if (chkp) {
+                if ((t0 + RT) * 32 <= N) {
+#pragma unroll
+                    for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+                        for (int rt = 0; rt < RT; ++rt) ckl[qt] += hsum16(aL[rt][qt]);
+                } else {
+#pragma unroll
+                    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+                        for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+                            for (int v = 0; v < 16; ++v) {
+                                const int64_t row = (t0 + rt) * 32 + 8 * (v >> 2) + 4 * (lane >> 5) + (v & 3);
+                                if (row < N) ckl[qt] += (uint32_t)aL[rt][qt][v];
+                            }
+                }
+            }
+        }
         if (pace && s + 1 < s_end) {
             const uint32_t done = (uint32_t)(s - s_begin + 1);
             if (wv == 0 && lane == 0) s8_st_u32(pace, pbase + (uint32_t)qb * 4u, (ptag << 20) | min(done, 0xFFFFFu));
@@ -660,8 +692,9 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
         }
         // the next step's start values (issued before the tail's PX * LPS refills; younger
         // epilogue accesses only make this wait stricter) land before the back-edge
+        S8_STAMP(const unsigned long long st_g = S8_NOW(); st_f += st_g;)
         if constexpr (METRIC == 1) s8_wait<PX * LPS>(rin);
-        S8_STAMP(st_e += S8_NOW() - st_c;)
+        S8_STAMP(st_q += S8_NOW() - st_g; st_e += S8_NOW() - st_c;)
     }
 
     // The last step's tail refilled the slots (and, global operand, the query tiles) with loads
@@ -678,12 +711,22 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
     }
     if constexpr (METRIC == 1) s8_tie(rin);
 
-    // FLAGSYNC: keep answering compaction rounds until every wave is past its last step
+    // FLAGSYNC: keep answering compaction rounds until every wave is past its last step.  A wave
+    // past its last step polls (sleeping) for either: every wave done, or a round some running
+    // wave called (s_need) -- then it joins that round's barriers.  (Round 4 called a round itself
+    // on every poll, so once one wave of a workgroup had finished, every remaining step of the
+    // others ended in two barriers: 139 rounds per wave at C4 against ~0 the lists needed.)
     if (FLAGSYNC && lane == 0) atomicAdd(&s_done, 1);
     for (; FLAGSYNC;) {
-        if (lane == 0) lds_flag_st(&s_need, 1);
-        __syncthreads();  // B1
-        if (__builtin_amdgcn_readfirstlane(lds_flag_ld(&s_done)) == NW) break;
+        int need = 0;
+        for (;;) {
+            const int done = __builtin_amdgcn_readfirstlane(lds_flag_ld(&s_done));
+            need = __builtin_amdgcn_readfirstlane(lds_flag_ld(&s_need));
+            if (done == NW || need) break;
+            __builtin_amdgcn_s_sleep(4);
+        }
+        if (!need) break;  // every wave is done: nobody can call a round any more
+        __syncthreads();  // B1 (the round a running wave called)
         for (int q = wv; q < QB; q += NW)
             if (s_cnt[q] >= CAP)
                 compact_query<KW, CAP>(s_sc + q * CAP, s_ix + q * CAP, s_cnt + q, s_thr + q,
@@ -711,7 +754,7 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
         const int nwg8 = (int)(gridDim.x / (unsigned)n_qb);
         for (int i = threadIdx.x; i < (HL ? 2 : 1) * QB; i += 64 * NW) {
             const int pl = i / QB, q = i - pl * QB;
-            chkp[((size_t)pl * nwg8 + wg) * (size_t)chk_ld + (size_t)qb * QB + q] = s_chk[pl][q];
+            chkp[((size_t)pl * chk_ld + (size_t)qb * QB + q) * nwg8 + wg] = s_chk[pl][q];
         }
     }
     uint32_t tkey = 0;
@@ -729,10 +772,10 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
     {
         const int w = blockIdx.x * NW + wv;
         if (lane == 0 && w < (1 << 16)) {
-            const unsigned long long v[10] = {S8_NOW() - st_t0, st_w, st_k, st_e, st_n, st_r0, st_x, st_y, st_z,
-                                              __builtin_amdgcn_s_memrealtime()};
+            const unsigned long long v[12] = {S8_NOW() - st_t0, st_w, st_k, st_e, st_n, st_r0, st_x, st_y, st_z,
+                                              __builtin_amdgcn_s_memrealtime(), st_q, st_f};
 #pragma unroll
-            for (int i = 0; i < 10; ++i) g_scan8_stamps[w][i] = v[i];
+            for (int i = 0; i < 12; ++i) g_scan8_stamps[w][i] = v[i];
         }
     }
 #endif

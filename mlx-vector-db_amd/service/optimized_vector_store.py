@@ -7,13 +7,15 @@ that existing callers — the REST routes (api/routes/vectors.py:57-64, :193,
 unchanged with ``mlx-vector-db_amd/`` first on ``sys.path``.
 
 What differs underneath:
-  * the corpus lives on the GPU as row-major fp32 rows plus a split-bf16 copy
-    (hi / lo planes in MFMA operand tiles), with norms computed once at ingest
-    (the reference re-normalises every row on every query,
+  * the corpus lives on the GPU as row-major fp32 rows plus an int8 copy of the
+    centred rows (two planes in MFMA operand tiles; a split-bf16 copy is built
+    only if a search needs one), with norms computed once at ingest (the
+    reference re-normalises every row on every query,
     service/optimized_vector_store.py:31-41);
-  * search is a fused bf16-MFMA candidate pass (the hi plane; bf16x3 re-pass of
-    uncertified queries) + exact fp64 rerank and certificate instead of a full
-    argsort (:176-183); ranking is exact with ties to the lower row;
+  * search is a fused int8-MFMA candidate pass (I8 for k <= 16, I8X3 above;
+    uncertified queries re-passed or sent to the exact scan) + exact fp64 rerank
+    and certificate instead of a full argsort (:176-183); ranking is exact with
+    ties to the lower row;
   * ``batch_query``, ``optimize`` and ``health_check`` exist (callers expect
     them: api/routes/vectors.py:291, api/routes/admin.py:230, tests/demo.py:134,
     :248, :254) and the functional API of tests/test_vector_store.py:15-18.

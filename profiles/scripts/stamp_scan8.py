@@ -17,6 +17,8 @@ prec = sys.argv[2] if len(sys.argv) > 2 else "i8"
 N, D, B, k, metric, _ = bench.CONFIGS[cfg]
 unit = {("i8", "cosine"): "i1c", ("i8x3", "euclidean"): "i3l"}[(prec, metric)]
 ix = _vdb.NativeIndex(D, metric, precision=prec)
+if os.environ.get("STAMP_CHK") is not None:  # the int8 pass's checksum on / off (A/B)
+    ix.set_param("scan_checksum", int(os.environ["STAMP_CHK"]))
 ix.reserve(N)
 for s in range(0, N, 1 << 19):
     ix.add(bench.corpus_rows(N, D, s, min(s + (1 << 19), N)))
@@ -25,9 +27,9 @@ for _ in range(4):
     ix.search(Q, k)
 lib = _vdb.load_library()
 n = 1 << 16
-buf = (ctypes.c_ulonglong * (n * 10))()
+buf = (ctypes.c_ulonglong * (n * 12))()
 getattr(lib, f"vdb_debug_scan8_stamps_{unit}")(buf, n)
-raw = np.array(buf, dtype=np.uint64).reshape(n, 10)
+raw = np.array(buf, dtype=np.uint64).reshape(n, 12)
 out = os.environ.get("STAMP_OUT")
 if out:
     np.save(out, raw)
@@ -45,6 +47,8 @@ print(f"  steps with a passing tile {(x & 0xFFFFF).astype(float).mean() / sn:.3f
       f"{(x >> 20).astype(float).mean() / sn:.3f}; compaction rounds per wave {(y & 0xFFFFF).astype(float).mean():.1f}")
 print(f"  tile tests per step {a[:, 8].mean() / sn:10.0f}; tests + insertions (before the compaction check) per step "
       f"{(y >> 20).astype(float).mean() / sn:10.0f}")
+print(f"  after the first insertion round: flag checks / rounds / pacing per step {a[:, 11].mean() / sn:10.0f}; "
+      f"the start-value wait per step {a[:, 10].mean() / sn:10.0f}")
 print(f"  start spread {t0.max() / 100:.1f} us, end spread {(end.max() - end.min()) / 100:.1f} us, span {end.max() / 100:.1f} us")
 
 # drift between the query blocks of a row range (xcd_map: block L -> j = L / 8, qb = j % n_qb,
@@ -52,7 +56,7 @@ print(f"  start spread {t0.max() / 100:.1f} us, end spread {(end.max() - end.min
 n_qb = (B + 63) // 64
 if n_qb > 1:
     w = np.nonzero(live)[0]
-    L = w // 4
+    L = w // int(os.environ.get('STAMP_NW', '8' if prec == 'i8x3' and metric == 'euclidean' else '4'))
     j = L // 8
     rng_id = 8 * (j // n_qb) + L % 8
     endt = a[:, 9]

@@ -895,9 +895,12 @@ def _graded_neighbours(rng, x, n, lo=1e-3, hi=4e-3):
 def test_device_repass_of_uncertified_queries(vdb, metric):
     """in a device-memory search (the bench's and a GPU-resident server's path)
     the few queries auto's int8 pass leaves uncertified are gathered ON THE DEVICE into a gated
-    BF16X3 sub-search on the same stream (device_repass 1) -- no exact scan, no host wait.  A
-    batch of 64 with one query that has 300 close rows (cosine 1 - [1e-3, 4e-3]) searched three times
-    back to back: every result exact, no fallback, one re-passed query per batch."""
+    I8X3 sub-search (KP 128) on the same stream (device_repass 1) -- no exact scan, no host wait.
+    A batch of 64 with one query that has 300 close rows (cosine 1 - [1e-3, 4e-3]) searched three
+    times back to back on a side stream: every result exact, no fallback, one re-passed query per
+    batch.  (GPUTEST_r04 once counted 2: the re-pass counter was zeroed by a hipMemset on the null
+    stream, which this non-blocking stream is not ordered after, so the first search's count could
+    land first and be wiped -- now zeroed and completed before any search uses it.)"""
     import torch
     rng = np.random.default_rng(47)
     N, D, B, k = 40000, 128, 64, 10
