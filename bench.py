@@ -253,7 +253,8 @@ def main_graph(args, world, rank, local, dev):
         if keep_host:
             parts.append(part)
     t0 = time.perf_counter()
-    g = _vdb.NativeGraph.build(ix, degree=R, knn=knn, n_entries=N_ENTRIES)
+    n_ent = args.graph_entries or N_ENTRIES
+    g = _vdb.NativeGraph.build(ix, degree=R, knn=knn, n_entries=n_ent)
     build_s = time.perf_counter() - t0
     g.set_param("teams", args.teams)
     nq = args.warmup + args.steps
@@ -360,7 +361,7 @@ def main_graph(args, world, rank, local, dev):
                      "dimension (corpus seed 0 per 65536-row chunk; queries the same distribution, seed 1)"),
             "config": {"workload": f"c5: {desc}" + (" [clustered data]" if clustered else ""), "n_rows": N, "dim": D,
                        "global_batch": 1, "k": k,
-                       "metric": metric, "ef": GRAPH_EF, "degree": R, "build_knn": knn, "entries": N_ENTRIES,
+                       "metric": metric, "ef": GRAPH_EF, "degree": R, "build_knn": knn, "entries": n_ent,
                        "teams": args.teams,
                        "parallelism": f"replicas x{world}" if world > 1 else "single GPU"},
             "build_s": build_s,
@@ -481,6 +482,8 @@ def main():
                     help="diagnostics only (kernel-variant timing): skip the exact fallback; results may be wrong")
     ap.add_argument("--graph-knn", type=int, default=None, help="c5: kNN candidates per row for the build")
     ap.add_argument("--teams", type=int, default=64, help="c5: workgroups per query (vdb_graph_set_param teams)")
+    ap.add_argument("--graph-entries", type=int, default=None,
+                    help="c5: entry rows of the graph (default performance/hnsw_index.py N_ENTRIES)")
     ap.add_argument("--teams-sweep", default="1,16,256", help="c5: extra teams settings reported beside the line")
     ap.add_argument("--data", default="uniform", choices=["uniform", "clustered"],
                     help="c5: the corpus (BASELINE's uniform [0,1) rows, or rows around cluster centres: the "

@@ -889,7 +889,7 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
         HIP_TRY(launch_sink_row8(ix->Xq, value, ix->G / 4, ix->stream));
         HIP_TRY(hipStreamSynchronize(ix->stream));
     } else if (n == "scan_checksum") {
-        if (value < 0 || value > 1) return set_error(VDB_ERR_INVALID, "scan_checksum must be 0 or 1");
+        if (value < 0 || value > 2) return set_error(VDB_ERR_INVALID, "scan_checksum must be 0, 1 or 2");
         ix->scan_checksum = value;
     } else if (n == "debug_stale_rinit") {
         // TEST ONLY: plants a stale L2 start value, -|x|^2/2 := 0 for row `value` (the operand a
@@ -1520,6 +1520,9 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     bytes += ((size_t)(n_wg + 7) / 8 * 8 * n_qblocks + 64) * 4; // int8 pass: pacing counters
     // the int8 pass's checksum: partial sums [2][n_wg8][Bp], expected values [Bp][2], L2 start sum
     const bool chk = i8_pass && !exact_all && ix->scan_checksum && ix->d_csum && N > 0;
+    // the L sums of I8X3 too (scan_checksum 2): +5% on C4's scan over H alone (the xh plane, the
+    // query's hi plane and the start values; an L operand moves a score by at most the slack lsl)
+    const bool chk_l = chk && prec == PREC_I8X3 && ix->scan_checksum == 2;
     const int n_wg8 = (n_wg + 7) / 8 * 8;
     bytes += chk ? ((size_t)2 * n_wg8 * Bp + (size_t)2 * Bp + 64) * 4 + 768 : 0;
     const bool priv = !exact_all && !split_pass && !i8_pass && scan_priv(prec, variant, KP);
@@ -1690,7 +1693,7 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
                 HIP_TRY(launch_scan8(prec, ix->metric, KP, Xscan, ix->rinit32, md, Qt, q8lsl, q8scal, Gs, N, B,
                                      n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr,
                                      ix->scan_pace ? pace : nullptr, ix->pace_seq.fetch_add(1) + 1, lockstep,
-                                     (int)ix->scan_qlds, st, opt.gate, q4_8, chkp, Bp));
+                                     (int)ix->scan_qlds, st, opt.gate, q4_8, chkp, Bp, chk_l ? 1 : 0));
             else if (use_s3)
                 HIP_TRY(launch_scan3(prec, ix->metric, Xscan, ix->rinit32, md, Qt, Gs, N, B, n_qb3, steps3, n_wg3, spw3,
                                      gl_s, gl_i, gl_cnt, gl_cap, gthr, st));
@@ -1757,7 +1760,7 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
                 fa.chk_g8 = Gs;
                 fa.chk_nw = n_wg8;
                 fa.chk_ld = Bp;
-                fa.chk_l = prec == PREC_I8X3;
+                fa.chk_l = chk_l;
             }
             fa.qconst = fa.mu == q_mu && fa.dir == q_dir ? qconst : nullptr;  // (prep_queries' constants)
             fa.split = fin_split; fa.sx_ek = fx_ek; fa.sx_ck = fx_ck; fa.sx_cr = fx_cr; fa.sx_n = fx_n; fa.done = done;
@@ -2137,12 +2140,17 @@ std::vector<int32_t> knn_candidates(const std::vector<int64_t>& kid, int64_t r0,
 
 extern "C" {
 
+// entry rows of a graph: up to 256 every search team scores all of them; more (up to this many)
+// are split into one spread slice of <= 256 per team (vdb_graph.hip)
+constexpr int kGraphEntriesMax = 1 << 20;
+
 int32_t vdb_graph_build(vdb_index* ix, int32_t degree, int32_t knn, int32_t n_entries, vdb_graph** out) {
     if (!ix || !out) return set_error(VDB_ERR_INVALID, "NULL argument");
     *out = nullptr;
     if (degree < 2 || degree > 64 || (degree & 1)) return set_error(VDB_ERR_INVALID, "degree must be even in [2, 64]");
     if (knn < degree / 2 || knn > 200) return set_error(VDB_ERR_INVALID, "knn must be in [degree/2, 200]");
-    if (n_entries < 1 || n_entries > 256) return set_error(VDB_ERR_INVALID, "n_entries must be in [1, 256]");
+    if (n_entries < 1 || n_entries > kGraphEntriesMax)
+        return set_error(VDB_ERR_INVALID, "n_entries must be in [1, %d]", kGraphEntriesMax);
     HIP_TRY(hipSetDevice(ix->device));
     const int64_t N = ix->count;
     if (N > 0x7FFFFFFF) return set_error(VDB_ERR_INVALID, "graph rows are int32");
@@ -2315,7 +2323,8 @@ int32_t vdb_graph_import(vdb_index* ix, int32_t degree, int64_t n, const int32_t
     *out = nullptr;
     if (degree < 1 || degree > 64) return set_error(VDB_ERR_INVALID, "degree must be in [1, 64]");
     if (n != ix->count) return set_error(VDB_ERR_INVALID, "graph has %lld rows, index %lld", (long long)n, (long long)ix->count);
-    if (n_entries < 0 || n_entries > 256) return set_error(VDB_ERR_INVALID, "n_entries must be in [0, 256]");
+    if (n_entries < 0 || n_entries > kGraphEntriesMax)
+        return set_error(VDB_ERR_INVALID, "n_entries must be in [0, %d]", kGraphEntriesMax);
     for (int64_t i = 0; i < n * degree; ++i)
         if (nbr[i] < -1 || nbr[i] >= n) return set_error(VDB_ERR_INVALID, "neighbour id out of range at %lld", (long long)i);
     for (int i = 0; i < n_entries; ++i)

@@ -136,24 +136,36 @@ __global__ void __launch_bounds__(64 * GS_WAVES) graph_search_kernel(GraphSearch
     }
     __syncthreads();
 
-    // entry set: scored by all waves, the best min(ef, E) start the beam
-    const int E = a.n_entries < GS_ENT_MAX ? a.n_entries : GS_ENT_MAX;
+    // Entry set.  Up to GS_ENT_MAX entries: every team scores all of them and takes the ranks
+    // r with r mod T == team (the teams start from interleaved ranks).  A larger set (round 5):
+    // each team scores its own spread, disjoint slice of at most GS_ENT_MAX entries (entry
+    // (j T + team) step) and starts from its best -- with T teams the query meets T x 256
+    // entries, so on clustered data (a kNN graph has no edges between clusters) some team
+    // starts inside the query's cluster.
+    const bool sliced = a.n_entries > GS_ENT_MAX;
+    const int E = !sliced ? a.n_entries : min(GS_ENT_MAX, (a.n_entries + T - 1) / T);
+    const int64_t step = sliced ? max<int64_t>(1, (int64_t)a.n_entries / ((int64_t)T * E)) : 1;
     __shared__ float s_es[GS_ENT_MAX];
     __shared__ int32_t s_ei[GS_ENT_MAX];
-    for (int e0 = wv * 32; e0 < E; e0 += GS_WAVES * 32) {
-        const int n = min(32, E - e0);
-        wave_score_rows<METRIC>(qs, a.rows, Dp, a.rowscale, a.entries + e0, n, s_es + e0, lane);
-        if (lane < n) s_ei[e0 + lane] = a.entries[e0 + lane];
+    for (int e = tid; e < E; e += 64 * GS_WAVES) {
+        const int64_t src = sliced ? ((int64_t)e * T + team) * step : e;
+        s_ei[e] = src < a.n_entries ? a.entries[src] : -1;
+    }
+    __syncthreads();
+    const int Ev = sliced ? (int)min<int64_t>(E, ((int64_t)a.n_entries / step - team + T - 1) / T) : E;  // valid slots
+    for (int e0 = wv * 32; e0 < Ev; e0 += GS_WAVES * 32) {
+        const int n = min(32, Ev - e0);
+        wave_score_rows<METRIC>(qs, a.rows, Dp, a.rowscale, s_ei + e0, n, s_es + e0, lane);
     }
     __syncthreads();
     const int ef = a.ef;
-    for (int e = tid; e < E; e += 64 * GS_WAVES) {
+    for (int e = tid; e < Ev; e += 64 * GS_WAVES) {
         const float sv = s_es[e];
         const int32_t iv = s_ei[e];
         int rank = 0;
-        for (int j = 0; j < E; ++j) rank += better(s_es[j], (uint32_t)s_ei[j], sv, (uint32_t)iv) ? 1 : 0;
-        if (rank % T == team) {
-            const int pos = rank / T;
+        for (int j = 0; j < Ev; ++j) rank += better(s_es[j], (uint32_t)s_ei[j], sv, (uint32_t)iv) ? 1 : 0;
+        if (sliced || rank % T == team) {
+            const int pos = sliced ? rank : rank / T;
             if (pos < ef) {
                 s_bs[0][pos] = sv;
                 s_bi[0][pos] = iv;
@@ -163,7 +175,7 @@ __global__ void __launch_bounds__(64 * GS_WAVES) graph_search_kernel(GraphSearch
         }
     }
     if (tid == 0) {
-        const int mine = (E - team + T - 1) / T;
+        const int mine = sliced ? Ev : (E - team + T - 1) / T;
         s_bn = mine < ef ? mine : ef;
         s_cur = 0;
         s_scored = (unsigned)E;

@@ -68,7 +68,7 @@ hipError_t launch_scan8(int prec, int metric, int KP, const float* Xq, const flo
                         int n_qblocks, int64_t n_steps, int n_wg, int spw, float* gl_s, uint32_t* gl_i,
                         uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr, uint32_t* pace, uint32_t pace_tag,
                         int lockstep, int qlds, hipStream_t st, const int* gate = nullptr, bool q4 = false,
-                        uint32_t* chkp = nullptr, int chk_ld = 0);
+                        uint32_t* chkp = nullptr, int chk_ld = 0, int chk_l = 0);
 
 // Ingest: row-major fp32 [n][D] (device) -> the index's row-major fp32 copy X [cap][Dp]
 // (zero padded to Dp = 8 G; read by the exact paths, export and the graph) rows [row0, row0+n),

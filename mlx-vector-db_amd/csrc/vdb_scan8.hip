@@ -352,13 +352,15 @@ pilot8_scores_kernel(const float* __restrict__ Xq, const float* __restrict__ rin
     constexpr int XPL = Planes8<PREC>::XPL;
     constexpr size_t GSTEP = 8 * BLOCK_FLOATS, PLANE = 4 * BLOCK_FLOATS;
     constexpr bool HL = Planes8<PREC>::L;
-    // The checksum's expected values for this query block (vdb_scan8_kernel.h; the first pilot
-    // workgroup of each block, off the scan's path): per query sum_d CH[d] qh[d] (+ L: CH ql + CL qh)
-    if (chke && blockIdx.x == 0) {
+    // The checksum's expected values for this query block (vdb_scan8_kernel.h), one query per wave
+    // of the first QB / PILOT8_WAVES pilot workgroups of the block (a dependent load chain each:
+    // one workgroup looping over the block's 64 queries held the pilot -- and the scan after it --
+    // ~8 us at C6): per query sum_d CH[d] qh[d] (+ L: CH ql + CL qh)
+    if (chke && blockIdx.x < QB / PILOT8_WAVES) {
         const int wv_ = threadIdx.x >> 6, ln = threadIdx.x & 63;
         const int GQ = G + QG_EXTRA, Dp = 32 * G;
-        for (int qq = wv_; qq < QB; qq += PILOT8_WAVES) {
-            const int q = blockIdx.y * QB + qq;
+        {
+            const int q = blockIdx.y * QB + blockIdx.x * PILOT8_WAVES + wv_;
             uint32_t eh = 0u, el = 0u;
             for (int cc = ln; cc < 2 * G; cc += 64) {
                 const int g = cc >> 1, h = cc & 1, d0 = 32 * g + 16 * h;
@@ -464,7 +466,10 @@ hipError_t launch_pilot8(int prec, int metric, const float* Xq, const float* rin
     if (n_sample > n_tiles) n_sample = (int)n_tiles;
     if (n_sample <= 0) return hipSuccess;
     const int tpb = PILOT8_WAVES / pilot8_w(G8);
-    const dim3 grid((n_sample + tpb - 1) / tpb, n_qblocks);
+    // (with the checksum's expectations: at least QB / PILOT8_WAVES workgroups per query block,
+    // one query per wave; past n_sample they score nothing)
+    const int gx = (n_sample + tpb - 1) / tpb;
+    const dim3 grid(chke ? std::max(gx, QB / PILOT8_WAVES) : gx, n_qblocks);
     bool launched = false;
 #define VDB_PILOT8(P, M, QTV)                                                                                    \
     if (!launched && prec == P && metric == M && QB == 32 * QTV) {                                               \
@@ -490,7 +495,7 @@ hipError_t launch_scan8(int prec, int metric, int KP, const float* Xq, const flo
                         const float* Qq, const float* lsl, const float* qscal, int G8, int64_t N, int B,
                         int n_qblocks, int64_t n_steps, int n_wg, int spw, float* gl_s, uint32_t* gl_i,
                         uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr, uint32_t* pace, uint32_t pace_tag,
-                        int lockstep, int qlds, hipStream_t st, const int* gate, bool q4, uint32_t* chkp, int chk_ld) {
+                        int lockstep, int qlds, hipStream_t st, const int* gate, bool q4, uint32_t* chkp, int chk_ld, int chk_l) {
     // the query block in LDS (scan8_qlds): qlds 1 = the round-3 rule (short rows), 2 = whenever
     // it fits, -1 = auto (rule 2 past VDB_S8_QLDS_BIG_G8 groups), 0 = never -- except for rows of fewer 32-dim groups
     // than the global-operand variants keep in flight (PX = 4)
@@ -504,7 +509,7 @@ hipError_t launch_scan8(int prec, int metric, int KP, const float* Xq, const flo
                                    : nullptr;
     if (!unit || metric < 0 || metric > 1) return hipErrorInvalidValue;
     return unit(KP, Xq, rinit, mask, Qq, lsl, qscal, G8, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt,
-                gl_cap, gthr, pace, pace_tag, nt, ql, fs, q4, gate, chkp, chk_ld, st);
+                gl_cap, gthr, pace, pace_tag, nt, ql, fs, q4, gate, chkp, chk_ld, chk_l, st);
 }
 
 }  // namespace vdb

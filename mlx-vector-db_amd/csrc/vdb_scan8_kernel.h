@@ -233,7 +233,7 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
              int64_t N, int B, int64_t n_steps, int steps_per_wg, int n_qb, float* __restrict__ gl_s,
              uint32_t* __restrict__ gl_i, uint32_t* __restrict__ gl_cnt, int64_t gl_cap, uint32_t* __restrict__ gthr,
              uint32_t* __restrict__ pace, uint32_t pace_tag, const int* __restrict__ gate,
-             uint32_t* __restrict__ chkp, int chk_ld) {
+             uint32_t* __restrict__ chkp, int chk_ld, int chk_l) {
     // a gated launch (the device-memory re-pass, vdb_api.cpp): nothing to do when its count is 0
     if (gate && *gate == 0) return;
     constexpr int RT = RT_, NW = scan8_nw(PREC, METRIC, QT);
@@ -658,7 +658,7 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
         // so a step without passing tiles never waited for its last L MFMAs -- summing L beside
         // the H sums made every C4 step wait for the shared matrix pipe's drain (scan +7%)
         if constexpr (HL) {
-            if (chkp) {
+            if (chkp && chk_l) {
                 if ((t0 + RT) * 32 <= N) {
 #pragma unroll
                     for (int qt = 0; qt < QT; ++qt)
@@ -788,7 +788,7 @@ static hipError_t scan8_launch_g(const float* Xq, const float* rinit, const uint
                                  const float* lsl, const float* qscal, int G, int64_t N, int B, int n_qblocks,
                                  int64_t n_steps, int n_wg, int spw, float* gl_s, uint32_t* gl_i, uint32_t* gl_cnt,
                                  int64_t gl_cap, uint32_t* gthr, uint32_t* pace, uint32_t pace_tag, const int* gate,
-                                 uint32_t* chkp, int chk_ld, hipStream_t st) {
+                                 uint32_t* chkp, int chk_ld, int chk_l, hipStream_t st) {
     auto k = scan8_kernel<P, M, QT, PX, KP, CAP, NT, QL, FS, GC, RT_, KW>;
     const size_t lds = QL ? (size_t)G * Planes8<P>::QPL * QT * 1024 : 0;
     if (QL) {
@@ -803,7 +803,7 @@ static hipError_t scan8_launch_g(const float* Xq, const float* rinit, const uint
     const int n_wg8 = (n_wg + 7) / 8 * 8;
     hipLaunchKernelGGL(k, dim3(n_wg8 * n_qblocks), dim3(64 * scan8_nw(P, M, QT)), lds, st, Xq, rinit, mask, Qq, lsl, qscal, G, N, B,
                        n_steps, spw, n_qblocks, gl_s, gl_i, gl_cnt, gl_cap, gthr, n_qblocks > 1 ? pace : nullptr,
-                       pace_tag, gate, chkp, chk_ld);
+                       pace_tag, gate, chkp, chk_ld, chk_l);
     return hipGetLastError();
 }
 
@@ -813,13 +813,13 @@ static hipError_t scan8_launch(const float* Xq, const float* rinit, const uint32
                                const float* lsl, const float* qscal, int G, int64_t N, int B, int n_qblocks,
                                int64_t n_steps, int n_wg, int spw, float* gl_s, uint32_t* gl_i, uint32_t* gl_cnt,
                                int64_t gl_cap, uint32_t* gthr, uint32_t* pace, uint32_t pace_tag, const int* gate,
-                               uint32_t* chkp, int chk_ld, hipStream_t st) {
+                               uint32_t* chkp, int chk_ld, int chk_l, hipStream_t st) {
     if constexpr (QL) {
         if (G == 4)  // D = 128: the group loop unrolls, and the whole next step is in flight
             return scan8_launch_g<P, M, QT, 4, KP, CAP, NT, QL, FS, 4, RT_, KW>(Xq, rinit, mask, Qq, lsl, qscal, G, N, B,
                                                                         n_qblocks, n_steps, n_wg, spw, gl_s, gl_i,
                                                                         gl_cnt, gl_cap, gthr, pace, pace_tag, gate,
-                                                                        chkp, chk_ld, st);
+                                                                        chkp, chk_ld, chk_l, st);
     }
     // the step loop takes the groups PX at a time: Dp / 32 groups is only even (D = 192: 6), so
     // where PX does not divide them the 2-deep variant runs (4 deep, the tail's refills would read
@@ -828,11 +828,11 @@ static hipError_t scan8_launch(const float* Xq, const float* rinit, const uint32
         if (G % PX != 0)
             return scan8_launch_g<P, M, QT, 2, KP, CAP, NT, QL, FS, 0, RT_, KW>(
                 Xq, rinit, mask, Qq, lsl, qscal, G, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap,
-                gthr, pace, pace_tag, gate, chkp, chk_ld, st);
+                gthr, pace, pace_tag, gate, chkp, chk_ld, chk_l, st);
     }
     return scan8_launch_g<P, M, QT, PX, KP, CAP, NT, QL, FS, 0, RT_, KW>(Xq, rinit, mask, Qq, lsl, qscal, G, N, B, n_qblocks,
                                                                 n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr,
-                                                                pace, pace_tag, gate, chkp, chk_ld, st);
+                                                                pace, pace_tag, gate, chkp, chk_ld, chk_l, st);
 }
 
 // The query block in LDS takes the query operand off each wave's vector-memory path (from L2,
@@ -859,11 +859,11 @@ inline bool scan8_qlds(int G8, int KP, int prec, int metric, bool small) {
     int KP, const float *Xq, const float *rinit, const uint32_t *mask, const float *Qq, const float *lsl,          \
         const float *qscal, int G, int64_t N, int B, int n_qblocks, int64_t n_steps, int n_wg, int spw,           \
         float *gl_s, uint32_t *gl_i, uint32_t *gl_cnt, int64_t gl_cap, uint32_t *gthr, uint32_t *pace,            \
-        uint32_t pace_tag, bool nt, bool ql, bool fs, bool q4, const int *gate, uint32_t *chkp, int chk_ld,      \
+        uint32_t pace_tag, bool nt, bool ql, bool fs, bool q4, const int *gate, uint32_t *chkp, int chk_ld, int chk_l, \
         hipStream_t st
 #define S8_ARGS \
     Xq, rinit, mask, Qq, lsl, qscal, G, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, pace, pace_tag, gate, \
-        chkp, chk_ld, st
+        chkp, chk_ld, chk_l, st
 #define S8_ONE(P, M, KPV, QTV, PXV, CAPV, NTV, QLV, FSV, KWV)   \
     if (KP == KPV && nt == NTV && ql == QLV && fs == FSV && !q4) \
         return scan8_launch<P, M, QTV, PXV, KPV, CAPV, NTV, QLV, FSV, KWV>(S8_ARGS);
