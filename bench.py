@@ -235,7 +235,9 @@ def main_graph(args, world, rank, local, dev):
     """C5: the graph path at batch 1.  N>1 runs independent replicas (SURVEY.md §8e:
     each GPU holds the whole graph and serves its own queries); value = all queries
     served / the slowest rank's time."""
-    from performance.hnsw_index import N_ENTRIES
+    from performance.hnsw_index import N_ENTRIES, TEAMS
+    if args.teams is None:
+        args.teams = TEAMS
     N, D, B, k, metric, desc = CONFIGS["c5"]
     N = args.rows or N
     R = 2 * GRAPH_M
@@ -481,10 +483,11 @@ def main():
     ap.add_argument("--no-fallback", action="store_true",
                     help="diagnostics only (kernel-variant timing): skip the exact fallback; results may be wrong")
     ap.add_argument("--graph-knn", type=int, default=None, help="c5: kNN candidates per row for the build")
-    ap.add_argument("--teams", type=int, default=64, help="c5: workgroups per query (vdb_graph_set_param teams)")
+    ap.add_argument("--teams", type=int, default=None,
+                    help="c5: workgroups per query (vdb_graph_set_param teams; default performance/hnsw_index.py TEAMS)")
     ap.add_argument("--graph-entries", type=int, default=None,
                     help="c5: entry rows of the graph (default performance/hnsw_index.py N_ENTRIES)")
-    ap.add_argument("--teams-sweep", default="1,16,256", help="c5: extra teams settings reported beside the line")
+    ap.add_argument("--teams-sweep", default="16,64", help="c5: extra teams settings reported beside the line")
     ap.add_argument("--data", default="uniform", choices=["uniform", "clustered"],
                     help="c5: the corpus (BASELINE's uniform [0,1) rows, or rows around cluster centres: the "
                          "structured data a graph index is for)")

@@ -14,8 +14,9 @@ neighbour heuristic selects <= M out-edges, then <= 2M of out- and in-edges —
 instead of hnswlib's one-at-a-time insertion, so ``ef_construction`` and
 ``num_threads`` have nothing to control; rows added later are inserted as a batch
 (``add_rows``, vdb_graph_add) instead of rebuilding; the upper levels' job (a good
-start) is done by scoring 256 spread entry rows, and each query is searched by TEAMS
-workgroups from disjoint slices of them.
+start) is done by scoring spread entry rows -- N_ENTRIES of them, each of the TEAMS
+workgroups that search a query scoring its own spread slice of <= 256 (the kNN graph of
+clustered rows has no edges between clusters: the entries must reach the query's).
 The file is ``hnsw_graph.npz`` (neighbour array + entry rows); hnswlib's
 ``hnsw_index.bin`` format is not produced (its compatibility is unpinned,
 SURVEY.md §8f).  The graph refers to the corpus rows of a device index: ``build``
@@ -36,11 +37,14 @@ from service import _vdb
 logger = logging.getLogger("mlx_hnsw_lib")
 
 GRAPH_FILE = "hnsw_graph.npz"
-N_ENTRIES = 256
-# workgroups per query (include/vdb.h vdb_graph_set_param "teams"): at batch 1 the
-# query gets 64 CUs, each searching from its own slice of the entry rows
-# (5M x 384, ef 128: recall@10 0.06 -> 0.39 for p50 0.54 -> 0.66 ms)
-TEAMS = 64
+# entry rows (capped at the row count): 256 teams x 256 per team's slice
+N_ENTRIES = 65536
+# workgroups per query (include/vdb.h vdb_graph_set_param "teams"): at batch 1 the query
+# gets every CU, each searching from its own slice of the entry rows.  5M x 384, ef 128
+# (profiles/r05_c5): clustered rows recall@10 0.997 at p50 0.56 ms (the exact path 0.66 ms;
+# 256 entries: 0.03); BASELINE's uniform rows 0.56 at 0.76 ms (64 teams 0.39 at 0.63 ms; the
+# exact path 0.41 ms: on such data it is the right tool)
+TEAMS = 256
 
 
 class ProductionHNSWIndex:

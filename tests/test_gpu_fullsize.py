@@ -247,6 +247,8 @@ def test_c5_graph_5m_x_384(vdb):
     recall = np.mean([len(set(a) & set(b)) / k for a, b in zip(lab.tolist(), ei.tolist())])
     _report("c5.json", {"recall_at_10": recall, "build_s": build_s, "teams": TEAMS, "ef": ef})
     # parity for the graph is recall, not equality.  The build and search are
-    # deterministic on this data: every run since round 2 measured 0.397 (profiles/r0*/reports/
-    # c5.json); the bar is that minus 0.025, so a regression of the graph shows
-    assert recall >= 0.37, recall
+    # deterministic on this data: rounds 2-4 measured 0.397 at 64 teams over 256 entries
+    # (profiles/r0*/reports/c5.json); round 5's store setting (65536 entries, 256 teams) 0.556
+    # (profiles/r05_c5); the bar is that minus 0.05, so a regression of the graph shows
+    # 
+    assert recall >= 0.50, recall

@@ -249,3 +249,34 @@ def test_graph_teams_explore_more(vdb, metric):
     np.testing.assert_array_equal(single, lab[:4])  # deterministic, batch-independent
     with pytest.raises(ValueError):
         g.set_param("teams", 0)
+
+
+@pytest.mark.parametrize("metric", ["cosine", "euclidean"])
+def test_graph_clustered_rows_need_spread_entries(vdb, metric):
+    """on rows drawn around cluster centres a kNN graph has no edges between
+    clusters, so a search reaches only the clusters its entry rows fall in: 256 entries over 2000
+    clusters leave most queries without their cluster.  Entry sets past 256 are split into one
+    spread slice per team (vdb_graph.hip): 65536 entries over 256 teams start some team inside
+    every query's cluster, and recall@10 recovers."""
+    rng = np.random.default_rng(83)
+    C, per, D, nq, k = 2000, 50, 64, 200, 10
+    centres = rng.random((C, D), dtype=np.float32)
+    lab = np.repeat(np.arange(C), per)
+    rng.shuffle(lab)
+    V = (centres[lab] + 0.05 * rng.standard_normal((C * per, D))).astype(np.float32)
+    Q = (centres[rng.integers(0, C, nq)] + 0.05 * rng.standard_normal((nq, D))).astype(np.float32)
+    ix = vdb.NativeIndex(D, metric)
+    ix.add(V)
+    _, ei, _ = ref_cpu.exact_search(Q, V, k, metric)
+    few = vdb.NativeGraph.build(ix, degree=32, knn=32, n_entries=256)
+    few.set_param("teams", 64)
+    r_few = _recall(few.search(Q, k, ef=128)[0], ei)
+    many = vdb.NativeGraph.build(ix, degree=32, knn=32, n_entries=65536)
+    assert many.info() == (C * per, 32, 65536)
+    many.set_param("teams", 256)
+    labels, dist = many.search(Q, k, ef=128)
+    r_many = _recall(labels, ei)
+    print(f"{metric}: recall@10 with 256 entries {r_few:.3f}, with 65536 entries over 256 teams {r_many:.3f}")
+    assert r_few < 0.5 and r_many >= 0.95, (r_few, r_many)
+    keys = ref_cpu.exact_keys(Q[0], V[labels[0]], metric)
+    np.testing.assert_allclose(dist[0], 1.0 - keys if metric == "cosine" else -keys, rtol=1e-4, atol=1e-5)
