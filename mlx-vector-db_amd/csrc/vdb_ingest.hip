@@ -260,9 +260,9 @@ __global__ void __launch_bounds__(256) prep_queries_kernel(const float* __restri
     if (lane == 0 && gthr) gthr[b] = 0u;
     if (lane == 0 && gl_cnt) gl_cnt[b] = 0u;
     if (lane == 0 && done) done[b] = 0;
-    if (gslots)  // [Bp][KP_MAX] publish slots, then [Bp][PILOT_SLOTS] pilot slots
+    if (gslots)  // [Bp][KP_MAX] publish slots, then the pilot slots (pslot_at: slot-major over B)
         for (int j = lane; j < KP_MAX + PILOT_SLOTS; j += 64)
-            gslots[j < KP_MAX ? (size_t)b * KP_MAX + j : (size_t)Bp * KP_MAX + (size_t)b * PILOT_SLOTS + j - KP_MAX] = 0u;
+            gslots[j < KP_MAX ? (size_t)b * KP_MAX + j : (size_t)Bp * KP_MAX + pslot_at(b, j - KP_MAX, B)] = 0u;
     const int Dp = G * GROUP_DIMS;
     const int np = (D + 255) / 256;
     const bool real = b < B;

@@ -104,7 +104,11 @@ hipError_t launch_unpack_rows(const float* X, int G, int D, int64_t row0, int64_
 // gslots[B][KP_MAX]: per-query slots of published workgroup bests; both zeroed by
 // prep_queries (see the publish step of scan_topk_kernel).
 constexpr int KP_MAX = 256;
-constexpr int PILOT_SLOTS = 256;  // pilot bound slots per query (pslots [Bp][PILOT_SLOTS])
+constexpr int PILOT_SLOTS = 256;  // pilot bound slots per query
+// pslots layout: slot-major, [PILOT_SLOTS][B] (a pilot wave's 32 queries of one tile -> one 128-byte
+// segment per atomic instruction; query-major, each went to 32 cache lines: the guide's
+// 17x-slower scattered-atomic shape, ~100 us of C4's 219 us pilot)
+__host__ __device__ inline size_t pslot_at(int q, int slot, int B) { return (size_t)slot * B + q; }
 // Queries: row-major [B][D] -> tiled Qt [Bp/32 tiles] with G + QG_EXTRA groups
 // (the first QG_EXTRA groups repeated at the end; cosine: pre-normalised in
 // fp32; zero padding written) and/or the split-bf16 tiles Qs (G/2 + QG_EXTRA

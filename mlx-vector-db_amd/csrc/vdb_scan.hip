@@ -934,7 +934,8 @@ __global__ void __launch_bounds__(64) pilot_scores_kernel(const float* __restric
             const bool ok = ((mword >> ro) & 1u) && ((int64_t)t * 32 + ro < N);
             best = ok ? fmaxf(best, sc) : best;
         }
-        if (q < B && best != -INFINITY) atomicMax(pslots + (size_t)q * PILOT_SLOTS + (i % PILOT_SLOTS), order_key(best));
+        best = fmaxf(best, __shfl_xor(best, 32, 64));  // the tile's two row halves (lane, lane + 32)
+        if (lane < 32 && q < B && best != -INFINITY) atomicMax(pslots + pslot_at(q, i % PILOT_SLOTS, B), order_key(best));
     }
 }
 
@@ -947,7 +948,7 @@ __global__ void __launch_bounds__(64) pilot_bound_kernel(const uint32_t* __restr
     constexpr int E = PILOT_SLOTS / 64;
     uint32_t v[E];
 #pragma unroll
-    for (int i = 0; i < E; ++i) v[i] = pslots[(size_t)q * PILOT_SLOTS + i * 64 + lane];
+    for (int i = 0; i < E; ++i) v[i] = pslots[pslot_at(q, i * 64 + lane, B)];
     int filled = 0;
 #pragma unroll
     for (int i = 0; i < E; ++i) filled += __popcll(__ballot(v[i] != 0u));

@@ -93,8 +93,8 @@ pilot2_scores_kernel(const float* __restrict__ Xs, const float* __restrict__ rin
 #pragma unroll
         for (int v = 0; v < 16; ++v) best = ((valid >> v) & 1u) ? fmaxf(best, acc[0][qt][v]) : best;
         if (METRIC == 1) best = 2.0f * best;
-        if (q < B && best != -INFINITY)
-            atomicMax(pslots + (size_t)q * PILOT_SLOTS + (i % PILOT_SLOTS), order_key(best));
+        best = fmaxf(best, __shfl_xor(best, 32, 64));  // the tile's two row halves (lane, lane + 32)
+        if (lane < 32 && q < B && best != -INFINITY) atomicMax(pslots + pslot_at(q, i % PILOT_SLOTS, B), order_key(best));
     }
 }
 

@@ -214,7 +214,7 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
         for (int i = 0; i < QW; ++i) {
             const int q = qb * QB + wv + NW * i;
 #pragma unroll
-            for (int e = 0; e < PILOT_E; ++e) pv[i][e] = q < B ? pslots[(size_t)q * PILOT_SLOTS + e * 64 + lane] : 0u;
+            for (int e = 0; e < PILOT_E; ++e) pv[i][e] = q < B ? pslots[pslot_at(q, e * 64 + lane, B)] : 0u;
         }
 #pragma unroll
         for (int i = 0; i < QW; ++i) {

@@ -5,9 +5,11 @@
 
 // scan_qlds auto (-1): the query block in LDS for short rows (rule 1) and, past 768 dims,
 // whenever it fits (rule 2).  Measured (profiles/r04_qlds, same box): C3 (D = 1536) scan 0.625
-// -> 0.572 ms with rule 2; C2 (D = 768) 0.153 -> 0.161 ms (slower: kept on rule 1); C6 equal.
+// -> 0.572 ms with rule 2; C2 (D = 768) 0.153 -> 0.161 ms (slower then: that shape did not load
+// the corpus nt, VDB_S8_NTQL).  With nt loads (round 5) C2 runs 0.148 -> 0.143 ms with the block
+// in LDS, so rule 2 starts past 16 groups (profiles/r05_ab/ab8_ntql.log).
 #ifndef VDB_S8_QLDS_BIG_G8
-#define VDB_S8_QLDS_BIG_G8 24
+#define VDB_S8_QLDS_BIG_G8 16
 #endif
 
 namespace vdb {
@@ -198,18 +200,41 @@ hipError_t launch_colsum8(const float* Xq, int64_t row0, int64_t n, int G8, uint
 // accumulator start values, as scan8_kernel computes them (qscal[2] from prep8)
 __global__ void __launch_bounds__(256) rinsum8_kernel(const float* __restrict__ rinit, int64_t N,
                                                       const float* __restrict__ qscal, uint32_t* __restrict__ out) {
+    // 16-byte loads, four in flight per lane (the start values are 16-byte aligned, allocation
+    // granularity; the last N % 4 by the first threads)
     const float invU = qscal[2];
     uint32_t s = 0u;
-    for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < N; r += (int64_t)gridDim.x * 256)
-        s += (uint32_t)__float2int_rn(rinit[r] * invU);
+    const int64_t n4 = N >> 2, tid = (int64_t)blockIdx.x * 256 + threadIdx.x, nt = (int64_t)gridDim.x * 256;
+    const f32x4* r4 = (const f32x4*)rinit;
+    int64_t r = tid;
+    for (; r + 3 * nt < n4; r += 4 * nt) {
+        f32x4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = r4[r + u * nt];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) s += (uint32_t)__float2int_rn(v[u][j] * invU);
+    }
+    for (; r < n4; r += nt) {
+        const f32x4 v = r4[r];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s += (uint32_t)__float2int_rn(v[j] * invU);
+    }
+    if (tid < (N & 3)) s += (uint32_t)__float2int_rn(rinit[4 * n4 + tid] * invU);
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) s += (uint32_t)__shfl_xor((int)s, off, 64);
-    if ((threadIdx.x & 63) == 0) atomicAdd(out, s);
+    // one atomic per workgroup: every one of them goes to the same word, and same-address
+    // atomics serialise at the memory side (4 per workgroup over 2048 workgroups: 98 us)
+    __shared__ uint32_t s_w[4];
+    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(out, s_w[0] + s_w[1] + s_w[2] + s_w[3]);
 }
 
 hipError_t launch_rinsum8(const float* rinit, int64_t N, const float* qscal, uint32_t* out, hipStream_t st) {
     if (N <= 0) return hipSuccess;
-    const int64_t blocks = std::min<int64_t>(1024, (N + 255) / 256);
+    const int64_t blocks = std::min<int64_t>(512, std::max<int64_t>(1, ((N >> 2) + 1023) / 1024));
     hipLaunchKernelGGL(rinsum8_kernel, dim3((unsigned)blocks), dim3(256), 0, st, rinit, N, qscal, out);
     return hipGetLastError();
 }
@@ -340,27 +365,27 @@ hipError_t launch_prep8(const float* Q, const double* qn64, const float* qmax, i
 // tile and query into the pilot slots; L2 adds the exact fp32 start value per row.
 // =============================================================================
 constexpr int PILOT8_WAVES = 4;
-__host__ __device__ inline int pilot8_w(int G8) { return G8 >= 8 ? 4 : G8 >= 3 ? 2 : 1; }
+// waves per sampled tile (each takes every W-th group): short rows one (no LDS exchange: C4 / C6)
+__host__ __device__ inline int pilot8_w(int G8) { return G8 >= 16 ? 4 : G8 >= 8 ? 2 : 1; }
 
 template <int PREC, int METRIC, int QT>
 __global__ void __launch_bounds__(64 * PILOT8_WAVES)
 pilot8_scores_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, const uint32_t* __restrict__ mask,
-                     const float* __restrict__ Qq, const float* __restrict__ qscal, int G, int64_t N, int B,
+                     const float* __restrict__ Qq, const float* __restrict__ qscal, int G, int64_t N, int B, int n_qb,
                      int64_t n_tiles, int n_sample, uint32_t* __restrict__ pslots,
                      const uint32_t* __restrict__ csum, uint32_t* __restrict__ chke) {
     constexpr int QB = 32 * QT;
     constexpr int XPL = Planes8<PREC>::XPL;
     constexpr size_t GSTEP = 8 * BLOCK_FLOATS, PLANE = 4 * BLOCK_FLOATS;
     constexpr bool HL = Planes8<PREC>::L;
-    // The checksum's expected values for this query block (vdb_scan8_kernel.h), one query per wave
-    // of the first QB / PILOT8_WAVES pilot workgroups of the block (a dependent load chain each:
-    // one workgroup looping over the block's 64 queries held the pilot -- and the scan after it --
-    // ~8 us at C6): per query sum_d CH[d] qh[d] (+ L: CH ql + CL qh)
-    if (chke && blockIdx.x < QB / PILOT8_WAVES) {
+    // The checksum's expected values (vdb_scan8_kernel.h), one query per wave of the first
+    // B / PILOT8_WAVES workgroups (a dependent load chain each: one workgroup looping over a block's
+    // 64 queries held the pilot -- and the scan after it -- ~8 us at C6): per query
+    // sum_d CH[d] qh[d] (+ L: CH ql + CL qh)
+    if (chke) {
         const int wv_ = threadIdx.x >> 6, ln = threadIdx.x & 63;
         const int GQ = G + QG_EXTRA, Dp = 32 * G;
-        {
-            const int q = blockIdx.y * QB + blockIdx.x * PILOT8_WAVES + wv_;
+        for (int q = blockIdx.x * PILOT8_WAVES + wv_; q < B; q += gridDim.x * PILOT8_WAVES) {
             uint32_t eh = 0u, el = 0u;
             for (int cc = ln; cc < 2 * G; cc += 64) {
                 const int g = cc >> 1, h = cc & 1, d0 = 32 * g + 16 * h;
@@ -385,77 +410,99 @@ pilot8_scores_kernel(const float* __restrict__ Xq, const float* __restrict__ rin
                 eh += (uint32_t)__shfl_xor((int)eh, off, 64);
                 el += (uint32_t)__shfl_xor((int)el, off, 64);
             }
-            if (ln == 0 && q < B) {
+            if (ln == 0) {
                 chke[2 * (size_t)q] = eh;
                 chke[2 * (size_t)q + 1] = el;
             }
         }
     }
-    __shared__ int s_part[PILOT8_WAVES][HL ? 2 : 1][QT][16][64];  // (I8: 32 KiB, room beside a scan)
+    // the group partials of waves part > 0 (W > 1 only: dynamic, so a one-wave-per-tile launch
+    // holds no LDS and keeps 8 workgroups per CU; I8: 32 KiB, I8X3 64)
+    extern __shared__ int s_pdyn[];
+    typedef int PartT[HL ? 2 : 1][QT][16][64];
+    PartT* s_part = (PartT*)s_pdyn;
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
     const int W = pilot8_w(G);
     const int part = wv % W;
     const int i = blockIdx.x * (PILOT8_WAVES / W) + wv / W;
-    const int qb = blockIdx.y;
     const bool live = i < n_sample;
     const uint64_t t = live ? (uint64_t)((int64_t)i * n_tiles / n_sample) : 0;
     const float* xs = Xq + corpus_block(t, 0, 0, G) + lane * 4;
     const size_t XGSTEP = corpus_gstep(), XPLANE = corpus_plane(G);
-    const float* qs = Qq + s2_blk((uint64_t)(qb * QT), 0, G + QG_EXTRA) + lane * 4;
-    i32x16 aH[1][QT], aL[1][QT];
-#pragma unroll
-    for (int qt = 0; qt < QT; ++qt)
-#pragma unroll
-        for (int v = 0; v < 16; ++v) aH[0][qt][v] = aL[0][qt][v] = 0;
-    for (int g = part; g < G; g += W) {
-        constexpr int QPL = Planes8<PREC>::QPL;
-        f32x4 xr[1][XPL], qr[QT][QPL];
-#pragma unroll
-        for (int pl = 0; pl < XPL; ++pl) xr[0][pl] = *(const f32x4*)(xs + g * XGSTEP + pl * XPLANE);
-#pragma unroll
-        for (int qt = 0; qt < QT; ++qt)
-#pragma unroll
-            for (int pl = 0; pl < QPL; ++pl) qr[qt][pl] = *(const f32x4*)(qs + g * GSTEP + pl * PLANE + qt * BLOCK_FLOATS);
-        group_mfma8<PREC, 1, QT>(xr, qr, aH, aL);
-    }
-    if (part > 0) {
-#pragma unroll
-        for (int qt = 0; qt < QT; ++qt)
-#pragma unroll
-            for (int v = 0; v < 16; ++v) {
-                s_part[wv][0][qt][v][lane] = aH[0][qt][v];
-                if constexpr (HL) s_part[wv][HL ? 1 : 0][qt][v][lane] = aL[0][qt][v];
-            }
-    }
-    __syncthreads();
-    if (part > 0 || !live) return;
-    for (int w = 1; w < W; ++w)
-#pragma unroll
-        for (int qt = 0; qt < QT; ++qt)
-#pragma unroll
-            for (int v = 0; v < 16; ++v) {
-                aH[0][qt][v] += s_part[wv + w][0][qt][v][lane];
-                if constexpr (HL) aL[0][qt][v] += s_part[wv + w][HL ? 1 : 0][qt][v][lane];
-            }
     const float uH = qscal[0], uL = qscal[1];
-    const uint32_t valid = tile_valid16(mask, (int64_t)t, N, lane);
+    const uint32_t valid = live ? tile_valid16(mask, (int64_t)t, N, lane) : 0u;
     float rr[16];
 #pragma unroll
     for (int v = 0; v < 16; ++v)
-        rr[v] = METRIC == 1 ? rinit[t * 32 + (v & 3) + 8 * (v >> 2) + 4 * (lane >> 5)] : 0.0f;
+        rr[v] = METRIC == 1 && live && part == 0 ? rinit[t * 32 + (v & 3) + 8 * (v >> 2) + 4 * (lane >> 5)] : 0.0f;
+    // Every query block of the batch against this wave's sampled tile: the tile and its start
+    // values are read once (round 4 ran one workgroup per (tile, query block): C4's 8 blocks read
+    // each sampled tile 8 times over 16 K workgroups, 219 us per batch with one stream)
+    for (int qb = 0; qb < n_qb; ++qb) {
+        const float* qs = Qq + s2_blk((uint64_t)(qb * QT), 0, G + QG_EXTRA) + lane * 4;
+        i32x16 aH[1][QT], aL[1][QT];
 #pragma unroll
-    for (int qt = 0; qt < QT; ++qt) {
-        const int q = qb * QB + qt * 32 + (lane & 31);
-        float best = -INFINITY;
+        for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
-        for (int v = 0; v < 16; ++v) {
-            const float sv = fmaf((float)aH[0][qt][v], uH, (float)aL[0][qt][v] * uL) + rr[v];
-            best = ((valid >> v) & 1u) ? fmaxf(best, sv) : best;
+            for (int v = 0; v < 16; ++v) aH[0][qt][v] = aL[0][qt][v] = 0;
+        // the wave's groups PC at a time: every load of a chunk issued before its first MFMA
+        constexpr int PC = 4;
+        for (int g0 = part; g0 < G; g0 += W * PC) {
+            constexpr int QPL = Planes8<PREC>::QPL;
+            f32x4 xr[PC][1][XPL], qr[PC][QT][QPL];
+#pragma unroll
+            for (int j = 0; j < PC; ++j) {
+                const int g = g0 + W * j < G ? g0 + W * j : g0;
+#pragma unroll
+                for (int pl = 0; pl < XPL; ++pl) xr[j][0][pl] = *(const f32x4*)(xs + g * XGSTEP + pl * XPLANE);
+#pragma unroll
+                for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+                    for (int pl = 0; pl < QPL; ++pl)
+                        qr[j][qt][pl] = *(const f32x4*)(qs + g * GSTEP + pl * PLANE + qt * BLOCK_FLOATS);
+            }
+#pragma unroll
+            for (int j = 0; j < PC; ++j)
+                if (g0 + W * j < G) group_mfma8<PREC, 1, QT>(xr[j], qr[j], aH, aL);
         }
-        if (METRIC == 1) best = 2.0f * best;
-        if (q < B && best != -INFINITY)
-            atomicMax(pslots + (size_t)q * PILOT_SLOTS + (i % PILOT_SLOTS), order_key(best));
+        if (W > 1) {  // (W is uniform over the workgroup: every wave reaches both barriers)
+            if (part > 0) {
+#pragma unroll
+                for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+                    for (int v = 0; v < 16; ++v) {
+                        s_part[wv][0][qt][v][lane] = aH[0][qt][v];
+                        if constexpr (HL) s_part[wv][HL ? 1 : 0][qt][v][lane] = aL[0][qt][v];
+                    }
+            }
+            __syncthreads();
+            if (part == 0)
+                for (int w = 1; w < W; ++w)
+#pragma unroll
+                    for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+                        for (int v = 0; v < 16; ++v) {
+                            aH[0][qt][v] += s_part[wv + w][0][qt][v][lane];
+                            if constexpr (HL) aL[0][qt][v] += s_part[wv + w][HL ? 1 : 0][qt][v][lane];
+                        }
+            __syncthreads();
+        }
+        if (part > 0 || !live) continue;
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) {
+            const int q = qb * QB + qt * 32 + (lane & 31);
+            float best = -INFINITY;
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+                const float sv = fmaf((float)aH[0][qt][v], uH, (float)aL[0][qt][v] * uL) + rr[v];
+                best = ((valid >> v) & 1u) ? fmaxf(best, sv) : best;
+            }
+            if (METRIC == 1) best = 2.0f * best;
+            best = fmaxf(best, __shfl_xor(best, 32, 64));  // the tile's two row halves (lane, lane + 32)
+            if (lane < 32 && q < B && best != -INFINITY)
+                atomicMax(pslots + pslot_at(q, i % PILOT_SLOTS, B), order_key(best));
+        }
     }
 }
 
@@ -466,15 +513,16 @@ hipError_t launch_pilot8(int prec, int metric, const float* Xq, const float* rin
     if (n_sample > n_tiles) n_sample = (int)n_tiles;
     if (n_sample <= 0) return hipSuccess;
     const int tpb = PILOT8_WAVES / pilot8_w(G8);
-    // (with the checksum's expectations: at least QB / PILOT8_WAVES workgroups per query block,
-    // one query per wave; past n_sample they score nothing)
+    // (with the checksum's expectations: at least B / PILOT8_WAVES workgroups, one query per wave;
+    // past n_sample they score nothing)
     const int gx = (n_sample + tpb - 1) / tpb;
-    const dim3 grid(chke ? std::max(gx, QB / PILOT8_WAVES) : gx, n_qblocks);
+    const dim3 grid(chke ? std::max(gx, (B + PILOT8_WAVES - 1) / PILOT8_WAVES) : gx);
     bool launched = false;
 #define VDB_PILOT8(P, M, QTV)                                                                                    \
     if (!launched && prec == P && metric == M && QB == 32 * QTV) {                                               \
-        hipLaunchKernelGGL((pilot8_scores_kernel<P, M, QTV>), grid, dim3(64 * PILOT8_WAVES), 0, st, Xq, rinit,   \
-                           mask, Qq, qscal, G8, N, B, n_tiles, n_sample, pslots, csum, chke);                   \
+        const size_t lds = pilot8_w(G8) > 1 ? (size_t)PILOT8_WAVES * (P == PREC_I8X3 ? 2 : 1) * QTV * 16 * 64 * 4 : 0; \
+        hipLaunchKernelGGL((pilot8_scores_kernel<P, M, QTV>), grid, dim3(64 * PILOT8_WAVES), lds, st, Xq, rinit, \
+                           mask, Qq, qscal, G8, N, B, n_qblocks, n_tiles, n_sample, pslots, csum, chke);        \
         launched = true;                                                                                         \
     }
     VDB_PILOT8(PREC_I8, 0, 2) VDB_PILOT8(PREC_I8, 1, 2) VDB_PILOT8(PREC_I8, 0, 1) VDB_PILOT8(PREC_I8, 1, 1)
@@ -503,7 +551,7 @@ hipError_t launch_scan8(int prec, int metric, int KP, const float* Xq, const flo
     const bool ql = q4 || (mode != 0 && scan8_qlds(G8, KP, prec, metric, mode == 1)) || G8 < 4;
     if (q4 && (KP != 128 || !scan8_q4_ok(G8, prec))) return hipErrorInvalidValue;
     const bool fs = !lockstep;
-    const bool nt = !ql && n_qblocks == 1;
+    const bool nt = (!ql || (VDB_S8_NTQL && fs && !q4)) && n_qblocks == 1;
     auto* unit = prec == PREC_I8X3 ? (metric == 0 ? launch_scan8_i3c : launch_scan8_i3l)
                  : prec == PREC_I8 ? (metric == 0 ? launch_scan8_i1c : launch_scan8_i1l)
                                    : nullptr;

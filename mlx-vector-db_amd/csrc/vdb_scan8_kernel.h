@@ -54,6 +54,12 @@ constexpr int scan8_nw(int prec, int metric, int QT = 2) {
     return prec == PREC_I8X3 && metric == 1 && QT != 4 ? VDB_S8_NW_X3L : S8_NW;
 }
 // the step's group loop: one loop with the tail selected inside (1) or the tail peeled (0)
+// the corpus loads non-temporal with the query block in LDS (one query block, flag-gated): C6
+// scan 0.243 -> 0.219 ms, C2 (with the block in LDS past 16 groups) 0.148 -> 0.143 ms
+// (profiles/r05_ab/ab8_ntql.log; before, only the L2-operand shapes loaded nt)
+#ifndef VDB_S8_NTQL
+#define VDB_S8_NTQL 1
+#endif
 #ifndef VDB_S8_ONELOOP
 #define VDB_S8_ONELOOP 0
 #endif
@@ -887,11 +893,17 @@ inline bool scan8_qlds(int G8, int KP, int prec, int metric, bool small) {
     S8_ONE(P, M, 64, 2, PXV, 128, NTV, QLV, FSV, 64)   \
     S8_ONE(P, M, 128, 2, PXV, 192, NTV, QLV, FSV, 128) \
     S8_ONE(P, M, 256, 2, PXV, (QLV ? 96 : 128), NTV, QLV, FSV, 64)
+// one query block with the query block in LDS: the corpus loads non-temporal too (VDB_S8_NTQL)
+#if VDB_S8_NTQL
+#define S8_KP_NTQL(P, M, PXL) S8_KP(P, M, PXL, true, true, true)
+#else
+#define S8_KP_NTQL(P, M, PXL)
+#endif
 #define S8_MODES(P, M, PXV, PXL)                                               \
     S8_KP(P, M, PXV, false, false, false) S8_KP(P, M, PXV, true, false, false) \
     S8_KP(P, M, PXL, false, true, false) S8_KP(P, M, PXL, false, true, true)   \
     S8_KP(P, M, PXV, false, false, true) S8_KP(P, M, PXV, true, false, true)   \
-    S8_ONE4(P, M, false) S8_ONE4(P, M, true)
+    S8_KP_NTQL(P, M, PXL) S8_ONE4(P, M, false) S8_ONE4(P, M, true)
 #define S8_UNIT(NAME, P, M, PXV, PXL)  \
     hipError_t NAME(S8_UNIT_PARAMS) {  \
         S8_MODES(P, M, PXV, PXL)       \
