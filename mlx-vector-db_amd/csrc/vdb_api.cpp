@@ -1512,6 +1512,9 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     bytes += (size_t)Bp * 4 + 256;                          // shared thresholds
     bytes += (size_t)Bp * (KP_MAX + PILOT_SLOTS) * 4 + 256;  // shared threshold slots + pilot slots
     bytes += (size_t)Bp * 12 + 1024;                          // int8 pass: qmax, lsl, qerr [Bp]; qscal
+    // int8 L2 pass: the batch's integer accumulator start values (vdb_scan8.hip rstart8)
+    const bool rs8_on = i8_pass && !exact_all && ix->metric == 1;
+    bytes += rs8_on ? (size_t)round_up(N, 32) * 4 + 256 : 0;
     const bool i8_refine = prec == PREC_I8 && ix->Xh &&  // the finish's I8 refinement
                            (ix->i8_refine == 1 || (ix->i8_refine == -1 && ix->Dp >= kRefineMinDp));
     bytes += i8_refine ? (size_t)Bp * (ix->Dp + 1) * 4 + 512 : 0;  // query residuals [Bp][Dp] + qerr2 [Bp]
@@ -1604,6 +1607,7 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     uint32_t* pace = c.take<uint32_t>((size_t)(n_wg + 7) / 8 * 8 * n_qblocks + 64);
     uint32_t* chkp = chk ? c.take<uint32_t>((size_t)2 * n_wg8 * Bp) : nullptr;
     uint32_t* chkr = chk && ix->metric == 1 ? c.take<uint32_t>(64) : nullptr;
+    int* rs8 = rs8_on ? c.take<int>((size_t)round_up(N, 32)) : nullptr;
     // (the pilot writes the checksum's expectations when it runs; else the finish computes them)
     uint32_t* chke = chk && n_pilot > 0 ? c.take<uint32_t>((size_t)2 * Bp) : nullptr;
     float* rep_q = mem == VDB_MEM_DEVICE ? c.take<float>((size_t)R_rep * D) : nullptr;
@@ -1644,9 +1648,9 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
             c8.rmax_half = 0.5 * ix->xmax * ix->xmax;
             HIP_TRY(launch_prep8(Qd, qn64, q8max, B, Bp, D, Gs, ix->metric, prec, c8, Qt, q8lsl, q8err, q8scal, st,
                                  q8res, q8err2));
-            if (chkr) {  // L2: the start values' sum at this batch's scale
-                HIP_TRY(hipMemsetAsync(chkr, 0, sizeof(uint32_t), st));
-                HIP_TRY(launch_rinsum8(ix->rinit32, N, q8scal, chkr, st));
+            if (rs8) {  // L2: the start values at this batch's scale (+ their sum, the checksum's)
+                if (chkr) HIP_TRY(hipMemsetAsync(chkr, 0, sizeof(uint32_t), st));
+                HIP_TRY(launch_rstart8(ix->rinit32, N, q8scal, rs8, chkr, st));
             }
         }
         int n_flag = 0;
@@ -1690,7 +1694,7 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
             if (use_s3) ix->n_scan3++;
             if ((q4 && !use_s3) || q4_8) ix->n_q4++;
             if (i8_pass)
-                HIP_TRY(launch_scan8(prec, ix->metric, KP, Xscan, ix->rinit32, md, Qt, q8lsl, q8scal, Gs, N, B,
+                HIP_TRY(launch_scan8(prec, ix->metric, KP, Xscan, (const float*)rs8, md, Qt, q8lsl, q8scal, Gs, N, B,
                                      n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr,
                                      ix->scan_pace ? pace : nullptr, ix->pace_seq.fetch_add(1) + 1, lockstep,
                                      (int)ix->scan_qlds, st, opt.gate, q4_8, chkp, Bp, chk_l ? 1 : 0));

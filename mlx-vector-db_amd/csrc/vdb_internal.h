@@ -52,7 +52,7 @@ hipError_t launch_prep8(const float* Q, const double* qn64, const float* qmax, i
 // [row0, row0 + n) added into csum [2][Dp]; the L2 start values' sum for a batch (*out +=); and a
 // test-only corpus fault (one row's planes set to -127, the column sums left as they were)
 hipError_t launch_colsum8(const float* Xq, int64_t row0, int64_t n, int G8, uint32_t* csum, hipStream_t st);
-hipError_t launch_rinsum8(const float* rinit, int64_t N, const float* qscal, uint32_t* out, hipStream_t st);
+hipError_t launch_rstart8(const float* rinit, int64_t N, const float* qscal, int* rs, uint32_t* sum, hipStream_t st);
 hipError_t launch_sink_row8(float* Xq, int64_t row, int G8, hipStream_t st);
 // (csum / chke, optional: the first workgroup of each query block also writes the int8 pass's
 // checksum expectations per query, chke [B][2] -- see FinishArgs::chke)

@@ -196,32 +196,39 @@ hipError_t launch_colsum8(const float* Xq, int64_t row0, int64_t n, int G8, uint
     return hipGetLastError();
 }
 
-// *out += sum over rows r < N of rint(rinit[r] * (1 / (s_x s_q))) (mod 2^32): the L2 pass's
-// accumulator start values, as scan8_kernel computes them (qscal[2] from prep8)
-__global__ void __launch_bounds__(256) rinsum8_kernel(const float* __restrict__ rinit, int64_t N,
-                                                      const float* __restrict__ qscal, uint32_t* __restrict__ out) {
-    // 16-byte loads, four in flight per lane (the start values are 16-byte aligned, allocation
-    // granularity; the last N % 4 by the first threads)
+// The L2 pass's accumulator start values at this batch's scale, rs[r] = rint(rinit[r] * (1 / (s_x
+// s_q))) (qscal[2] from prep8; 0 past N), which scan8_kernel loads as its H accumulators' start
+// (round 4 converted them in the pass: 16 x (mul, round, convert) per wave-step, with the register
+// copies ~20% of C4's vector instructions), and *sum += their sum (mod 2^32), the checksum's term
+__global__ void __launch_bounds__(256) rstart8_kernel(const float* __restrict__ rinit, int64_t N, int64_t Np,
+                                                      const float* __restrict__ qscal, int* __restrict__ rs,
+                                                      uint32_t* __restrict__ out) {
+    // 16-byte loads and stores, four in flight per lane (both arrays 16-byte aligned: allocation
+    // granularity, Np a multiple of 32); rows N..Np-1 (the last tile's padding) start at 0
     const float invU = qscal[2];
     uint32_t s = 0u;
-    const int64_t n4 = N >> 2, tid = (int64_t)blockIdx.x * 256 + threadIdx.x, nt = (int64_t)gridDim.x * 256;
+    const int64_t n4 = Np >> 2, tid = (int64_t)blockIdx.x * 256 + threadIdx.x, nt = (int64_t)gridDim.x * 256;
     const f32x4* r4 = (const f32x4*)rinit;
+    i32x4* o4 = (i32x4*)rs;
+    auto conv = [&](const f32x4& v, int64_t r) {
+        i32x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            o[j] = 4 * r + j < N ? __float2int_rn(v[j] * invU) : 0;
+            s += (uint32_t)o[j];
+        }
+        return o;
+    };
     int64_t r = tid;
     for (; r + 3 * nt < n4; r += 4 * nt) {
         f32x4 v[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) v[u] = r4[r + u * nt];
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) s += (uint32_t)__float2int_rn(v[u][j] * invU);
+        for (int u = 0; u < 4; ++u) o4[r + u * nt] = conv(v[u], r + u * nt);
     }
-    for (; r < n4; r += nt) {
-        const f32x4 v = r4[r];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) s += (uint32_t)__float2int_rn(v[j] * invU);
-    }
-    if (tid < (N & 3)) s += (uint32_t)__float2int_rn(rinit[4 * n4 + tid] * invU);
+    for (; r < n4; r += nt) o4[r] = conv(r4[r], r);
+    if (!out) return;
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) s += (uint32_t)__shfl_xor((int)s, off, 64);
     // one atomic per workgroup: every one of them goes to the same word, and same-address
@@ -232,10 +239,11 @@ __global__ void __launch_bounds__(256) rinsum8_kernel(const float* __restrict__ 
     if (threadIdx.x == 0) atomicAdd(out, s_w[0] + s_w[1] + s_w[2] + s_w[3]);
 }
 
-hipError_t launch_rinsum8(const float* rinit, int64_t N, const float* qscal, uint32_t* out, hipStream_t st) {
+hipError_t launch_rstart8(const float* rinit, int64_t N, const float* qscal, int* rs, uint32_t* sum, hipStream_t st) {
     if (N <= 0) return hipSuccess;
-    const int64_t blocks = std::min<int64_t>(512, std::max<int64_t>(1, ((N >> 2) + 1023) / 1024));
-    hipLaunchKernelGGL(rinsum8_kernel, dim3((unsigned)blocks), dim3(256), 0, st, rinit, N, qscal, out);
+    const int64_t Np = (N + 31) / 32 * 32;
+    const int64_t blocks = std::min<int64_t>(512, std::max<int64_t>(1, ((Np >> 2) + 1023) / 1024));
+    hipLaunchKernelGGL(rstart8_kernel, dim3((unsigned)blocks), dim3(256), 0, st, rinit, N, Np, qscal, rs, sum);
     return hipGetLastError();
 }
 

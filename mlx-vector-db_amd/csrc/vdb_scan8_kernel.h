@@ -222,12 +222,12 @@ __device__ __forceinline__ uint32_t s8_pace_min(uint32_t v, uint32_t tag, int la
 // The smallest H that can still pass threshold th (half units) given |L uL| <= slack, minus a
 // margin for the fp32 evaluation: H <= the result means the tile's scores are all <= th.
 __device__ __forceinline__ int h_floor(float th, float slack, float invU) {
-    if (!(th > -INFINITY)) return INT_MIN;
+    // (selects, not branches: the compiler made each test an exec-mask branch, three per query tile
+    // and step)
     const float t = (th - slack) * invU;
     const float m = t - fabsf(t) * 1e-5f - 4.0f;
-    if (m <= -2.0e9f) return INT_MIN;
-    if (m >= 2.0e9f) return 2000000000;
-    return (int)floorf(m);
+    const int r = (int)floorf(fminf(fmaxf(m, -2.0e9f), 2.0e9f));
+    return th > -INFINITY && m > -2.0e9f ? r : INT_MIN;
 }
 
 // Per-batch scalars written by prep8 (device): [0] uH = s_x s_q, [1] uL = uH / 256, [2] 1 / uH.
@@ -322,7 +322,8 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
     // loads per slot (group) of the streams: corpus tiles, + query tiles from global memory
     constexpr int LPS = RT * XPL + (QLDS ? 0 : QT * QPL);
     const uint32_t voff = (uint32_t)lane * 16u;
-    // L2: the next step's start values, loaded one step ahead, before the tail groups' refills
+    // L2: the next step's start values (the batch's integer H starts, vdb_scan8.hip rstart8), loaded
+    // one step ahead, before the tail groups' refills
     // (lane half h holds -|x|^2/2 of rows 32 t + 8 a + 4 h + b, a, b = 0..3, of each tile: the
     // rows of its accumulator registers 4 a + b)
     constexpr int NRI = METRIC == 1 ? RT : 1;
@@ -371,6 +372,30 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
         if constexpr (METRIC == 1) s8_wait<PX * LPS>(rin);
     }
 
+    // The tile tests' integer thresholds (flag-gated shapes with the query block in LDS): computed
+    // here and again after each compaction round this wave takes part in -- nothing else changes
+    // s_thr (gk is read once) -- not in every step's epilogue (an LDS read and ~20 vector
+    // instructions per query tile and step).  (The other shapes recompute them per step: carried
+    // across the loop there, the extra live registers moved asm-loaded slots through AGPRs before
+    // their waits, tools/vmcnt_check.py.)
+    constexpr bool THC = FLAGSYNC && QLDS;
+    int thc[QT];
+    auto thr_of = [&](int qt, float& thf_) {
+        const int ql = qt * 32 + (lane & 31);
+        const float thr = fmaxf(s_thr[ql], key_to_float(gk[qt]));
+        thf_ = METRIC == 0 ? thr : 0.5f * thr;
+        return h_floor(thf_, qsl[qt], invU);
+    };
+    auto refresh_thr = [&]() {
+        if constexpr (THC) {
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt) {
+                float f;
+                thc[qt] = thr_of(qt, f);
+            }
+        }
+    };
+    refresh_thr();
     for (int64_t s = s_begin; s < s_end; ++s) {
         S8_STAMP(const unsigned long long st_a = S8_NOW(); ++st_n;)
         const int64_t t0 = (s * NW + wv) * RT;
@@ -386,7 +411,7 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
 #pragma unroll
                 for (int a = 0; a < 4; ++a)
 #pragma unroll
-                    for (int b2 = 0; b2 < 4; ++b2) init[4 * a + b2] = __float2int_rn(rin[METRIC == 1 ? rt : 0][a][b2] * invU);
+                    for (int b2 = 0; b2 < 4; ++b2) init[4 * a + b2] = __float_as_int(rin[METRIC == 1 ? rt : 0][a][b2]);
             }
 #pragma unroll
             for (int qt = 0; qt < QT; ++qt) {
@@ -485,14 +510,19 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
         // ---- epilogue ----
         int thi[QT];
         bool qok[QT];
-        float thf[QT];  // the (half-)score thresholds: s_thr changes only in compaction rounds
+        float thf[QT];  // the (half-)score thresholds (INS2 / INSTHR builds)
 #pragma unroll
         for (int qt = 0; qt < QT; ++qt) {
-            const int ql = qt * 32 + (lane & 31);
-            const float thr = fmaxf(s_thr[ql], key_to_float(gk[qt]));
-            thf[qt] = METRIC == 0 ? thr : 0.5f * thr;
-            thi[qt] = h_floor(thf[qt], qsl[qt], invU);
-            qok[qt] = qb * QB + ql < B;
+            qok[qt] = qb * QB + qt * 32 + (lane & 31) < B;
+            if constexpr (THC) {
+                thi[qt] = thc[qt];
+                thf[qt] = 0.0f;
+#if VDB_S8_INS2 || VDB_S8_INSTHR
+                thi[qt] = thr_of(qt, thf[qt]);
+#endif
+            } else {
+                thi[qt] = thr_of(qt, thf[qt]);
+            }
         }
         // The hot path: every tile's H maximum against the integer floor of its threshold
         uint32_t todo = 0;  // wave-uniform: bit rt * QT + qt = some lane of tile (rt, qt) passes
@@ -657,6 +687,7 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
                                            KW == KP && qb * QB + q < B ? gthr + qb * QB + q : nullptr);
             if (FLAGSYNC && threadIdx.x == 0) lds_flag_st(&s_need, 0);
             __syncthreads();  // B2
+            refresh_thr();  // the round raised s_thr
             todo = pmask;
             pmask = 0;
         }
