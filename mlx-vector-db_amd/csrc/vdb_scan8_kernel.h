@@ -321,6 +321,9 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the compiler's loads are done before the streams start
     // loads per slot (group) of the streams: corpus tiles, + query tiles from global memory
     constexpr int LPS = RT * XPL + (QLDS ? 0 : QT * QPL);
+    // loads issued after a step's start values (for the next step) within that step: the tail
+    // groups' refills after the first (one loop: all of them)
+    constexpr int RIN_YOUNGER = VDB_S8_ONELOOP ? PX * LPS : (PX - 1) * LPS;
     const uint32_t voff = (uint32_t)lane * 16u;
     // L2: the next step's start values (the batch's integer H starts, vdb_scan8.hip rstart8), loaded
     // one step ahead, before the tail groups' refills
@@ -487,10 +490,17 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
         // the siblings' counts: issued only where the epilogue waits for them (an asm load never
         // waited for could land in a register the compiler has reused)
         if (pace && s + 1 < s_end) pv = s8_ld_u32(pace, poff);
-        if (s + 1 < s_end) load_epi(s + 1, rin);
+        // L2: the next step's start values after the first tail group, whose MFMAs are the last
+        // reads of this step's (D = 128: the first group of the step), so they can land in the
+        // same registers: issued before the tail, both sets were live at once and every step
+        // copied 16 registers twice (v_mov_b64 x 16, C4).  Waits: a tail group p >= 1 has the
+        // same loads younger than its slot as before ((PX - 1) slots + the start values); the
+        // start values have (PX - 1) slots after them (the step-end wait below)
 #pragma unroll
-        for (int p = 0; p < PX; ++p)
+        for (int p = 0; p < PX; ++p) {
             group(p, gb + p, xn + (size_t)p * XGSTEP, Qbase + (size_t)(gb + p + PQ) * GSTEP);
+            if (p == 0 && s + 1 < s_end) load_epi(s + 1, rin);
+        }
 #endif
 
         S8_STAMP(const unsigned long long st_c = S8_NOW(); st_k += st_c - st_a;)
@@ -503,7 +513,7 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
                 for (int qt = 0; qt < QT; ++qt) f += imax16(aH[rt][qt]);
             if (f == 123456789) gl_s[0] = (float)f;
             if (pace && s + 1 < s_end) asm volatile("s_waitcnt vmcnt(%1)" : "+v"(pv) : "n"(PX * LPS + (METRIC == 1 ? RT * 4 : 0)));
-            if constexpr (METRIC == 1) s8_wait<PX * LPS>(rin);
+            if constexpr (METRIC == 1) s8_wait<RIN_YOUNGER>(rin);
             continue;
         }
 #endif
@@ -727,10 +737,10 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
                 slow = s8_pace_min(v, ptag, lane, n_qb);
             }
         }
-        // the next step's start values (issued before the tail's PX * LPS refills; younger
-        // epilogue accesses only make this wait stricter) land before the back-edge
+        // the next step's start values (RIN_YOUNGER refills issued after them; younger epilogue
+        // accesses only make this wait stricter) land before the back-edge
         S8_STAMP(const unsigned long long st_g = S8_NOW(); st_f += st_g;)
-        if constexpr (METRIC == 1) s8_wait<PX * LPS>(rin);
+        if constexpr (METRIC == 1) s8_wait<RIN_YOUNGER>(rin);
         S8_STAMP(st_q += S8_NOW() - st_g; st_e += S8_NOW() - st_c;)
     }
 
