@@ -826,7 +826,7 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
         if (value < 0 || value > 1) return set_error(VDB_ERR_INVALID, "graph_fill must be 0 or 1");
         ix->graph_fill = value;
     } else if (n == "pilot_tiles") {
-        if (value < -1 || value > 4096) return set_error(VDB_ERR_INVALID, "pilot_tiles must be in [-1, 4096]");
+        if (value < -1 || value > 32768) return set_error(VDB_ERR_INVALID, "pilot_tiles must be in [-1, 32768]");
         ix->pilot_tiles = value;
     } else if (n == "timing") {
         ix->timing = value != 0;

@@ -178,7 +178,10 @@ constexpr int FIN_NB4 = VDB_FIN_WAVES > 8 ? 3 : 6;  // rows per wave per batch o
 // of row pieces in flight per wave; the loop form below keeps one 1 KiB piece per row in flight
 // and ran C3's exact keys at 150 us for 256 candidates x 256 queries, profiles/r04 fin stamps)
 constexpr int FIN_MP8 = 8;
-constexpr int FIN_NB8 = 1;
+#ifndef VDB_FIN_NB8
+#define VDB_FIN_NB8 1
+#endif
+constexpr int FIN_NB8 = VDB_FIN_NB8;
 
 template <int METRIC, int KP>
 __global__ void __launch_bounds__(64 * RERANK_WAVES) rerank_kernel(RerankArgs a) {
@@ -735,7 +738,10 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
     if (refine) {
         if (tid == 0) s_cbmax = 0u;
         __syncthreads();
-        constexpr int NBR = FIN_WAVES > 8 ? 4 : 8;  // candidates per wave per batch (row loads in flight together)
+#ifndef VDB_FIN_NBR
+#define VDB_FIN_NBR (FIN_WAVES > 8 ? 4 : 8)
+#endif
+        constexpr int NBR = VDB_FIN_NBR;  // candidates per wave per batch (row loads in flight together)
         const float* rq = a.qres + (size_t)b * a.Dp;
         const float fsx = (METRIC == 0 ? 1.0f : 2.0f) * a.sx;
         const float qmx = 127.0f * a.qscal[0] / a.sx;  // s_q * 127 = max |q'|
