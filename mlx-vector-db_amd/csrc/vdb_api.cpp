@@ -1540,7 +1540,15 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     // each workgroup inserts (C6, 10 M rows, int8 pass: 512 -> 2048 tiles, scan 0.329 -> 0.259 ms,
     // 200 K -> 250 K QPS; C2 / C3, 1 M rows: larger samples only add pilot time,
     // profiles/r03_i8/pilot).
-    const int64_t pilot_def = std::min<int64_t>(4096, std::max<int64_t>(512 * std::max(1, k / 12), N / (32 * 160)));
+    // Rows of 4 groups (D <= 128: the int8 pass's register-resident pilot, vdb_scan8.hip
+    // pilot8_g4) take twice the k-based sample, up to 8192 tiles where the rows are many (at most
+    // ~2.5% of them): C4 (k = 100) 4096 -> 8192, scan 2.32 -> 2.19 ms, 213 K -> 220 K QPS with
+    // the pilot at ~50 -> ~90 us (profiles/r05_ab/ab20)
+    const bool cheap_pilot = i8_pass && Gs == 4;
+    const int64_t pilot_cap = cheap_pilot ? std::max<int64_t>(4096, std::min<int64_t>(8192, N / (32 * 40))) : 4096;
+    const int64_t pilot_def = std::min<int64_t>(pilot_cap,
+                                                std::max<int64_t>((cheap_pilot ? 1024 : 512) * std::max(1, k / 12),
+                                                                  N / (32 * 160)));
     const int n_pilot = opt.gate ? 0  // a gated re-pass sub-search: no pilot (few queries; its launches stay light)
                                  : (int)std::min<int64_t>(ix->pilot_tiles >= 0 ? ix->pilot_tiles : pilot_def,
                                                           round_up(N, 32) / 32);

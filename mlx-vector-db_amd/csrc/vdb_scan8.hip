@@ -376,6 +376,49 @@ constexpr int PILOT8_WAVES = 4;
 // waves per sampled tile (each takes every W-th group): short rows one (no LDS exchange: C4 / C6)
 __host__ __device__ inline int pilot8_w(int G8) { return G8 >= 16 ? 4 : G8 >= 8 ? 2 : 1; }
 
+// The checksum's expected values (vdb_scan8_kernel.h), one query per wave of the pilot's first
+// B / PILOT8_WAVES workgroups (a dependent load chain each: one workgroup looping over a block's
+// 64 queries held the pilot -- and the scan after it -- ~8 us at C6): per query
+// sum_d CH[d] qh[d] (+ L: CH ql + CL qh)
+template <int PREC>
+__device__ __forceinline__ void pilot8_chke(const float* __restrict__ Qq, int G, int B,
+                                            const uint32_t* __restrict__ csum, uint32_t* __restrict__ chke) {
+    constexpr size_t PLANE = 4 * BLOCK_FLOATS;
+    constexpr bool HL = Planes8<PREC>::L;
+    const int wv_ = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    const int GQ = G + QG_EXTRA, Dp = 32 * G;
+    for (int q = blockIdx.x * PILOT8_WAVES + wv_; q < B; q += gridDim.x * PILOT8_WAVES) {
+        uint32_t eh = 0u, el = 0u;
+        for (int cc = ln; cc < 2 * G; cc += 64) {
+            const int g = cc >> 1, h = cc & 1, d0 = 32 * g + 16 * h;
+            const float* src = Qq + s2_blk((uint64_t)(q >> 5), g, GQ) + (size_t)((q & 31) + 32 * h) * 4;
+            const f32x4 qh4 = *(const f32x4*)src;
+            const f32x4 ql4 = *(const f32x4*)(src + PLANE);
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                const uint32_t uh = __float_as_uint(qh4[w]), ul = __float_as_uint(ql4[w]);
+#pragma unroll
+                for (int bt = 0; bt < 4; ++bt) {
+                    const int d = d0 + 4 * w + bt;
+                    const uint32_t hv = (uint32_t)(int)(int8_t)((uh >> (8 * bt)) & 255u);
+                    const uint32_t ch = csum[d];
+                    eh += hv * ch;
+                    if (HL) el += (uint32_t)(int)(int8_t)((ul >> (8 * bt)) & 255u) * ch + hv * csum[Dp + d];
+                }
+            }
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            eh += (uint32_t)__shfl_xor((int)eh, off, 64);
+            el += (uint32_t)__shfl_xor((int)el, off, 64);
+        }
+        if (ln == 0) {
+            chke[2 * (size_t)q] = eh;
+            chke[2 * (size_t)q + 1] = el;
+        }
+    }
+}
+
 template <int PREC, int METRIC, int QT>
 __global__ void __launch_bounds__(64 * PILOT8_WAVES)
 pilot8_scores_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, const uint32_t* __restrict__ mask,
@@ -386,44 +429,7 @@ pilot8_scores_kernel(const float* __restrict__ Xq, const float* __restrict__ rin
     constexpr int XPL = Planes8<PREC>::XPL;
     constexpr size_t GSTEP = 8 * BLOCK_FLOATS, PLANE = 4 * BLOCK_FLOATS;
     constexpr bool HL = Planes8<PREC>::L;
-    // The checksum's expected values (vdb_scan8_kernel.h), one query per wave of the first
-    // B / PILOT8_WAVES workgroups (a dependent load chain each: one workgroup looping over a block's
-    // 64 queries held the pilot -- and the scan after it -- ~8 us at C6): per query
-    // sum_d CH[d] qh[d] (+ L: CH ql + CL qh)
-    if (chke) {
-        const int wv_ = threadIdx.x >> 6, ln = threadIdx.x & 63;
-        const int GQ = G + QG_EXTRA, Dp = 32 * G;
-        for (int q = blockIdx.x * PILOT8_WAVES + wv_; q < B; q += gridDim.x * PILOT8_WAVES) {
-            uint32_t eh = 0u, el = 0u;
-            for (int cc = ln; cc < 2 * G; cc += 64) {
-                const int g = cc >> 1, h = cc & 1, d0 = 32 * g + 16 * h;
-                const float* src = Qq + s2_blk((uint64_t)(q >> 5), g, GQ) + (size_t)((q & 31) + 32 * h) * 4;
-                const f32x4 qh4 = *(const f32x4*)src;
-                const f32x4 ql4 = *(const f32x4*)(src + PLANE);
-#pragma unroll
-                for (int w = 0; w < 4; ++w) {
-                    const uint32_t uh = __float_as_uint(qh4[w]), ul = __float_as_uint(ql4[w]);
-#pragma unroll
-                    for (int bt = 0; bt < 4; ++bt) {
-                        const int d = d0 + 4 * w + bt;
-                        const uint32_t hv = (uint32_t)(int)(int8_t)((uh >> (8 * bt)) & 255u);
-                        const uint32_t ch = csum[d];
-                        eh += hv * ch;
-                        if (HL) el += (uint32_t)(int)(int8_t)((ul >> (8 * bt)) & 255u) * ch + hv * csum[Dp + d];
-                    }
-                }
-            }
-#pragma unroll
-            for (int off = 32; off >= 1; off >>= 1) {
-                eh += (uint32_t)__shfl_xor((int)eh, off, 64);
-                el += (uint32_t)__shfl_xor((int)el, off, 64);
-            }
-            if (ln == 0) {
-                chke[2 * (size_t)q] = eh;
-                chke[2 * (size_t)q + 1] = el;
-            }
-        }
-    }
+    if (chke) pilot8_chke<PREC>(Qq, G, B, csum, chke);
     // the group partials of waves part > 0 (W > 1 only: dynamic, so a one-wave-per-tile launch
     // holds no LDS and keeps 8 workgroups per CU; I8: 32 KiB, I8X3 64)
     extern __shared__ int s_pdyn[];
@@ -514,19 +520,107 @@ pilot8_scores_kernel(const float* __restrict__ Xq, const float* __restrict__ rin
     }
 }
 
+// Short rows (4 groups of 32 dims, D <= 128: C4 / C6): one wave per sampled tile holds the tile
+// in registers, and the next query block's tiles are loaded while the current block's MFMAs and
+// epilogue run (the generic loop waited for every block's loads: C4, 4096 tiles x 8 blocks,
+// 116 us with one stream, ~10x its MFMA time) -- a cheaper pilot affords a larger sample, whose
+// bound then spares the scan more insertions (C4, 16 K tiles: scan 2.32 -> 2.11 ms)
+template <int PREC, int METRIC, int QT>
+__global__ void __launch_bounds__(64 * PILOT8_WAVES)
+pilot8_g4_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, const uint32_t* __restrict__ mask,
+                 const float* __restrict__ Qq, const float* __restrict__ qscal, int64_t N, int B, int n_qb,
+                 int64_t n_tiles, int n_sample, uint32_t* __restrict__ pslots, const uint32_t* __restrict__ csum,
+                 uint32_t* __restrict__ chke) {
+    constexpr int G = 4, QB = 32 * QT;
+    constexpr int XPL = Planes8<PREC>::XPL, QPL = Planes8<PREC>::QPL;
+    constexpr size_t GSTEP = 8 * BLOCK_FLOATS, PLANE = 4 * BLOCK_FLOATS;
+    if (chke) pilot8_chke<PREC>(Qq, G, B, csum, chke);
+    const int lane = threadIdx.x & 63;
+    const int i = blockIdx.x * PILOT8_WAVES + (threadIdx.x >> 6);
+    if (i >= n_sample) return;  // (no barriers below)
+    const uint64_t t = (uint64_t)((int64_t)i * n_tiles / n_sample);
+    const float* xs = Xq + corpus_block(t, 0, 0, G) + lane * 4;
+    const size_t XGSTEP = corpus_gstep(), XPLANE = corpus_plane(G);
+    f32x4 xr[G][1][XPL];
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int pl = 0; pl < XPL; ++pl) xr[g][0][pl] = *(const f32x4*)(xs + g * XGSTEP + pl * XPLANE);
+    float rr[16];
+    if constexpr (METRIC == 1) {
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+            const f32x4 r4 = *(const f32x4*)(rinit + t * 32 + 8 * a + 4 * (lane >> 5));
+#pragma unroll
+            for (int b = 0; b < 4; ++b) rr[4 * a + b] = r4[b];
+        }
+    } else {
+#pragma unroll
+        for (int v = 0; v < 16; ++v) rr[v] = 0.0f;
+    }
+    const uint32_t valid = tile_valid16(mask, (int64_t)t, N, lane);
+    const float uH = qscal[0], uL = qscal[1];
+    auto load_q = [&](int qb, f32x4 (&q)[G][QT][QPL]) {
+        const float* qs = Qq + s2_blk((uint64_t)(qb * QT), 0, G + QG_EXTRA) + lane * 4;
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+                for (int pl = 0; pl < QPL; ++pl) q[g][qt][pl] = *(const f32x4*)(qs + g * GSTEP + pl * PLANE + qt * BLOCK_FLOATS);
+    };
+    f32x4 qa[G][QT][QPL], qn[G][QT][QPL];
+    load_q(0, qa);
+    for (int qb = 0; qb < n_qb; ++qb) {
+        if (qb + 1 < n_qb) load_q(qb + 1, qn);
+        i32x16 aH[1][QT], aL[1][QT];
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+            for (int v = 0; v < 16; ++v) aH[0][qt][v] = aL[0][qt][v] = 0;
+#pragma unroll
+        for (int g = 0; g < G; ++g) group_mfma8<PREC, 1, QT>(xr[g], qa[g], aH, aL);
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) {
+            const int q = qb * QB + qt * 32 + (lane & 31);
+            float best = -INFINITY;
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+                const float sv = fmaf((float)aH[0][qt][v], uH, (float)aL[0][qt][v] * uL) + rr[v];
+                best = ((valid >> v) & 1u) ? fmaxf(best, sv) : best;
+            }
+            if (METRIC == 1) best = 2.0f * best;
+            best = fmaxf(best, __shfl_xor(best, 32, 64));  // the tile's two row halves (lane, lane + 32)
+            if (lane < 32 && q < B && best != -INFINITY)
+                atomicMax(pslots + pslot_at(q, i % PILOT_SLOTS, B), order_key(best));
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+                for (int pl = 0; pl < QPL; ++pl) qa[g][qt][pl] = qn[g][qt][pl];
+    }
+}
+
 hipError_t launch_pilot8(int prec, int metric, const float* Xq, const float* rinit, const uint32_t* mask,
                          const float* Qq, const float* qscal, int G8, int64_t N, int B, int n_qblocks, int QB,
                          int n_sample, uint32_t* pslots, hipStream_t st, const uint32_t* csum, uint32_t* chke) {
     const int64_t n_tiles = (N + 31) / 32;
     if (n_sample > n_tiles) n_sample = (int)n_tiles;
     if (n_sample <= 0) return hipSuccess;
-    const int tpb = PILOT8_WAVES / pilot8_w(G8);
+    const int tpb = G8 == 4 ? PILOT8_WAVES : PILOT8_WAVES / pilot8_w(G8);
     // (with the checksum's expectations: at least B / PILOT8_WAVES workgroups, one query per wave;
     // past n_sample they score nothing)
     const int gx = (n_sample + tpb - 1) / tpb;
     const dim3 grid(chke ? std::max(gx, (B + PILOT8_WAVES - 1) / PILOT8_WAVES) : gx);
     bool launched = false;
 #define VDB_PILOT8(P, M, QTV)                                                                                    \
+    if (!launched && prec == P && metric == M && QB == 32 * QTV && G8 == 4) {                                    \
+        hipLaunchKernelGGL((pilot8_g4_kernel<P, M, QTV>), grid, dim3(64 * PILOT8_WAVES), 0, st, Xq, rinit, mask, Qq, \
+                           qscal, N, B, n_qblocks, n_tiles, n_sample, pslots, csum, chke);                      \
+        launched = true;                                                                                         \
+    }                                                                                                            \
     if (!launched && prec == P && metric == M && QB == 32 * QTV) {                                               \
         const size_t lds = pilot8_w(G8) > 1 ? (size_t)PILOT8_WAVES * (P == PREC_I8X3 ? 2 : 1) * QTV * 16 * 64 * 4 : 0; \
         hipLaunchKernelGGL((pilot8_scores_kernel<P, M, QTV>), grid, dim3(64 * PILOT8_WAVES), lds, st, Xq, rinit, \
