@@ -461,7 +461,10 @@ pilot8_scores_kernel(const float* __restrict__ Xq, const float* __restrict__ rin
 #pragma unroll
             for (int v = 0; v < 16; ++v) aH[0][qt][v] = aL[0][qt][v] = 0;
         // the wave's groups PC at a time: every load of a chunk issued before its first MFMA
-        constexpr int PC = 4;
+#ifndef VDB_PILOT8_PC
+#define VDB_PILOT8_PC 4
+#endif
+        constexpr int PC = VDB_PILOT8_PC;
         for (int g0 = part; g0 < G; g0 += W * PC) {
             constexpr int QPL = Planes8<PREC>::QPL;
             f32x4 xr[PC][1][XPL], qr[PC][QT][QPL];
