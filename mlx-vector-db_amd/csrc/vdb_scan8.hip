@@ -373,8 +373,17 @@ hipError_t launch_prep8(const float* Q, const double* qn64, const float* qmax, i
 // tile and query into the pilot slots; L2 adds the exact fp32 start value per row.
 // =============================================================================
 constexpr int PILOT8_WAVES = 4;
-// waves per sampled tile (each takes every W-th group): short rows one (no LDS exchange: C4 / C6)
-__host__ __device__ inline int pilot8_w(int G8) { return G8 >= 16 ? 4 : G8 >= 8 ? 2 : 1; }
+// waves per sampled tile (each takes every W-th group, partials through LDS): one for short rows
+// (C4 / C6) and for long ones (> 24 groups): there the scan's query block leaves < 32 KiB of LDS
+// beside it, and an LDS-free pilot runs on the CUs beside another batch's scan instead of after
+// it (C3: 411.5 K -> 419-422 K QPS, profiles/r05_ab/ab25_pilot_w1.log; C2's W = 4 pilot fits
+// beside its scan: unchanged)
+#ifndef VDB_PILOT8_W1
+#define VDB_PILOT8_W1 0
+#endif
+__host__ __device__ inline int pilot8_w(int G8) {
+    return VDB_PILOT8_W1 || G8 > 24 ? 1 : G8 >= 16 ? 4 : G8 >= 8 ? 2 : 1;
+}
 
 // The checksum's expected values (vdb_scan8_kernel.h), one query per wave of the pilot's first
 // B / PILOT8_WAVES workgroups (a dependent load chain each: one workgroup looping over a block's
