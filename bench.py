@@ -439,7 +439,7 @@ def main():
     ap.add_argument("--scaling", default=None, choices=["weak", "strong"],
                     help="N>1: weak = global batch B*N (fixed work per GPU), strong = global batch B "
                          "(default: strong for c4 / c6, whose BASELINE batch is sharded, weak otherwise)")
-    ap.add_argument("--precision", default="auto", choices=["auto", "bf16x3", "bf16", "fp32", "i8", "i8x3"],
+    ap.add_argument("--precision", default="auto", choices=["auto", "bf16x3", "bf16", "fp32", "i8", "i8x3", "i8q"],
                     help="candidate-pass arithmetic (results identical; DESIGN.md §3)")
     ap.add_argument("--scan-variant", type=int, default=None, help="candidate-pass kernel variant (tuning)")
     ap.add_argument("--n-wg", type=int, default=None, help="candidate-pass workgroups (tuning)")
@@ -480,6 +480,8 @@ def main():
     ap.add_argument("--streams", type=int, default=3,
                     help="single GPU: batches queued round-robin on this many HIP streams (a server's request "
                          "streams; each batch still runs the whole search)")
+    ap.add_argument("--auto-i8q", type=int, default=None,
+                    help="auto's L2 pass for 16 < k <= 100: 1 the xh plane x 16-bit query (default), 0 I8X3")
     ap.add_argument("--no-fallback", action="store_true",
                     help="diagnostics only (kernel-variant timing): skip the exact fallback; results may be wrong")
     ap.add_argument("--graph-knn", type=int, default=None, help="c5: kNN candidates per row for the build")
@@ -601,6 +603,8 @@ def bench_brute(cfg, args, world, rank, local, dev, primary=True):
         ix.set_param("scan_checksum", args.scan_checksum)
     if args.no_fallback:
         ix.set_param("no_fallback", 1)
+    if args.auto_i8q is not None:
+        ix.set_param("auto_i8q", args.auto_i8q)
     ix.reserve(n_local)
     host_parts = []
     # --plant-close P (one GPU): P query targets, each with 300 rows closer to it than the int8
@@ -664,7 +668,7 @@ def bench_brute(cfg, args, world, rank, local, dev, primary=True):
     ev_in_loop = bool(args.timing) and n_str == 1
     ix.set_param("timing", int(ev_in_loop))
     scan0, pipe0, n0 = ix.stat("scan_ns"), ix.stat("pipeline_ns"), ix.stat("timed_searches")
-    by_prec0 = {p: ix.stat(f"searches_{p}") for p in ("fp32", "bf16x3", "bf16", "i8", "i8x3")}
+    by_prec0 = {p: ix.stat(f"searches_{p}") for p in ("fp32", "bf16x3", "bf16", "i8", "i8x3", "i8q")}
     fb0 = ix.stat("fallback_queries")
     if world > 1:
         dist.barrier()
@@ -728,13 +732,13 @@ def bench_brute(cfg, args, world, rank, local, dev, primary=True):
         #     launch time is not a fraction of any roofline (it exceeded 1); the
         #     roofline fraction is the implementation's, above.
         Dp = (D + 63) // 64 * 64
-        elem = {"i8": 1, "i8x3": 2, "bf16": 2}.get(prec, 4)
-        q_elem = {"i8": 1, "i8x3": 2}.get(prec, 4)  # query tiles (i8: the hi plane; i8x3: both 1-byte planes)
+        elem = {"i8": 1, "i8x3": 2, "i8q": 1, "bf16": 2}.get(prec, 4)
+        q_elem = {"i8": 1, "i8x3": 2, "i8q": 2}.get(prec, 4)  # query tiles (i8: the hi plane; i8x3 / i8q: both 1-byte planes)
         hbm_bytes = n_local * Dp * elem + (n_local * 4 if metric == "euclidean" else 0) + Bg * Dp * q_elem
-        n_mfma = {"fp32": 1, "bf16x3": 3, "bf16": 2, "i8": 1, "i8x3": 3}[prec]
+        n_mfma = {"fp32": 1, "bf16x3": 3, "bf16": 2, "i8": 1, "i8x3": 3, "i8q": 2}[prec]
         mfma_flops = n_mfma * 2.0 * Bg * n_local * D
         mfma_peak = {"fp32": FP32_MFMA_PEAK_TFLOPS, "bf16x3": BF16_MFMA_PEAK_TFLOPS, "bf16": BF16_MFMA_PEAK_TFLOPS,
-                     "i8": I8_MFMA_PEAK_TOPS, "i8x3": I8_MFMA_PEAK_TOPS}[prec]
+                     "i8": I8_MFMA_PEAK_TOPS, "i8x3": I8_MFMA_PEAK_TOPS, "i8q": I8_MFMA_PEAK_TOPS}[prec]
         t_hbm = hbm_bytes / (HBM_PEAK_GBS * 1e9)
         t_mfma = mfma_flops / (mfma_peak * 1e12)
         achieved_gbs = hbm_bytes / (scan_ms * 1e-3) / 1e9
@@ -747,7 +751,7 @@ def bench_brute(cfg, args, world, rank, local, dev, primary=True):
                     "frac": achieved_tf / mfma_peak}
         roof["basis"] = (f"implementation: {elem} B per corpus element read once + queries; "
                          f"{n_mfma} MFMA product(s) per fp32 product "
-                         f"({ {'fp32': 'fp32', 'i8': 'int8', 'i8x3': 'int8'}.get(prec, 'bf16')} peak)")
+                         f"({ {'fp32': 'fp32', 'i8': 'int8', 'i8x3': 'int8', 'i8q': 'int8'}.get(prec, 'bf16')} peak)")
         s_flops = 2.0 * Bg * n_local * D
         s_bytes = n_local * D * (2 if cfg == "c3" else 4) + 4 * n_local + 4 * Bg * D + 12 * Bg * k
         fp32_eq = {"flops_per_launch": s_flops, "bytes_per_launch": s_bytes,
@@ -784,14 +788,15 @@ def bench_brute(cfg, args, world, rank, local, dev, primary=True):
             "dtype": {"fp32": "f32", "bf16x3": "f32 (bf16x3 split MFMA candidates, fp64 exact rerank)",
                       "bf16": "f32 (bf16 corpus x split query MFMA candidates, fp64 exact rerank)",
                       "i8": "f32 (int8 centred corpus x int8 query integer-MFMA candidates, fp64 exact rerank)",
-                      "i8x3": "f32 (16-bit fixed-point corpus x query integer-MFMA candidates, fp64 exact rerank)"}[prec],
+                      "i8x3": "f32 (16-bit fixed-point corpus x query integer-MFMA candidates, fp64 exact rerank)",
+                      "i8q": "f32 (8-bit centred corpus x 16-bit query integer-MFMA candidates, fp64 exact rerank)"}[prec],
             "data": "synthetic uniform [0,1) fp32 (numpy PCG64, corpus seed 0 per 65536-row chunk, queries seed 1)",
             "config": {"workload": f"{cfg}: {desc}", "n_rows": N, "dim": D, "global_batch": Bg,
                        "batch_per_gpu_equiv": B, "k": k,
                        "metric": metric, "parallelism": f"row-shard x{world}" if world > 1 else "single GPU",
                        "rows_per_gpu": n_local},
             "roofline": dict(roof, traffic=traffic,
-                             kernel={"fp32": "scan_topk", "i8": "scan8_kernel", "i8x3": "scan8_kernel"}.get(prec, "scan2_kernel"),
+                             kernel={"fp32": "scan_topk", "i8": "scan8_kernel", "i8x3": "scan8_kernel", "i8q": "scan8_kernel"}.get(prec, "scan2_kernel"),
                              fp32_equivalent=fp32_eq, precision=prec,
                              precision_requested=args.precision, searches_by_precision=by_prec,
                              traffic_source=traffic_src, algorithmic_bytes=hbm_bytes, algorithmic_flops=mfma_flops,

@@ -204,12 +204,16 @@ struct vdb_index {
     // flags a query, then 256 for good (i8_wide).  Knob "i8_narrow": -1 auto, 0 off.
     int64_t i8_narrow = -1;
     std::atomic<bool> i8_wide{false};
+    // auto's L2 pass for 16 < k <= 100: PREC_I8Q (the xh plane against the 16-bit query) unless
+    // "auto_i8q" = 0, or once a batch flagged more than 1/8 of its queries (i8q_off: I8X3 after)
+    bool auto_i8q = true;
+    std::atomic<bool> i8q_off{false};
     std::atomic<uint32_t> pace_seq{0};  // launch tag of the pacing counters
     int64_t scan_q4 = -1;      // split pass 128-query shape (D <= 128, KP = 128, B >= 256): -1 auto, 0 off, 1 on
     // stats
     std::atomic<int64_t> n_searches{0}, n_queries{0}, n_fallback{0}, n_overflow{0}, n_incons{0}, n_repass{0}, n_scan3{0}, n_q4{0};
     std::atomic<int64_t> n_xs_builds{0};  // lazy builds of the split copy (ensure_xs)
-    std::atomic<int64_t> n_by_prec[N_PREC] = {{0}, {0}, {0}, {0}, {0}};  // candidate passes per PREC_* (VDB_PREC_AUTO's choices)
+    std::atomic<int64_t> n_by_prec[N_PREC] = {{0}, {0}, {0}, {0}, {0}, {0}};  // candidate passes per PREC_* (VDB_PREC_AUTO's choices)
     std::atomic<int64_t> scan_ns{0}, pipe_ns{0}, n_timed{0};
     unsigned long long* d_totals = nullptr;  // device: flagged / overflowed / flagged-in-bf16 queries of device-gated searches
     std::shared_mutex mu;  // add/clear/reserve exclusive; search shared
@@ -245,11 +249,12 @@ int wait_idle(vdb_index* ix);
 enum XsKind { kXsNone = -1, kXsFp32 = 0, kXsSplit = 1 };
 int xs_kind(int64_t precision) {
     if (precision == VDB_PREC_FP32) return kXsFp32;
-    if (precision == VDB_PREC_I8 || precision == VDB_PREC_I8X3) return kXsNone;
+    if (precision == VDB_PREC_I8 || precision == VDB_PREC_I8X3 || precision == VDB_PREC_I8Q) return kXsNone;
     return kXsSplit;
 }
 bool needs_i8(int64_t precision, bool auto_i8) {
-    return precision == VDB_PREC_I8 || precision == VDB_PREC_I8X3 || (precision == VDB_PREC_AUTO && auto_i8);
+    return precision == VDB_PREC_I8 || precision == VDB_PREC_I8X3 || precision == VDB_PREC_I8Q ||
+           (precision == VDB_PREC_AUTO && auto_i8);
 }
 // Settings whose candidate pass reads Xs on every search keep it allocated and up to date from the
 // start; AUTO with the int8 copy reads it only for holds, host re-passes and retries, so it is
@@ -757,12 +762,12 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
     std::string n(name);
     if (n == "precision") {
         if (value != VDB_PREC_FP32 && value != VDB_PREC_BF16X3 && value != VDB_PREC_BF16 && value != VDB_PREC_AUTO &&
-            value != VDB_PREC_I8 && value != VDB_PREC_I8X3)
+            value != VDB_PREC_I8 && value != VDB_PREC_I8X3 && value != VDB_PREC_I8Q)
             return set_error(VDB_ERR_INVALID,
-                             "precision must be %d (fp32), %d (bf16x3), %d (bf16), %d (auto), %d (i8) or %d (i8x3), "
-                             "got %lld",
+                             "precision must be %d (fp32), %d (bf16x3), %d (bf16), %d (auto), %d (i8), %d (i8x3) or "
+                             "%d (i8q), got %lld",
                              VDB_PREC_FP32, VDB_PREC_BF16X3, VDB_PREC_BF16, VDB_PREC_AUTO, VDB_PREC_I8, VDB_PREC_I8X3,
-                             (long long)value);
+                             VDB_PREC_I8Q, (long long)value);
         HIP_TRY(hipSetDevice(ix->device));
         std::unique_lock<std::shared_mutex> g(ix->mu);
         if (value == ix->precision) return VDB_OK;
@@ -786,6 +791,8 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
             HIP_TRY(build_candidate_rows(ix, 0, ix->count, ix->stream, xs && !built, xq));
             HIP_TRY(read_i8_stats(ix, ix->stream));
         }
+    } else if (n == "auto_i8q") {
+        ix->auto_i8q = value != 0;
     } else if (n == "auto_int8") {  // VDB_PREC_AUTO's candidate copy: 1 int8, 0 split-bf16
         HIP_TRY(hipSetDevice(ix->device));
         std::unique_lock<std::shared_mutex> g(ix->mu);
@@ -951,6 +958,9 @@ int32_t vdb_index_get_stat(const vdb_index* cix, const char* name, int64_t* valu
     else if (n == "searches_i8") *value = ix->n_by_prec[PREC_I8].load();
     else if (n == "searches_i8x3") *value = ix->n_by_prec[PREC_I8X3].load();
     else if (n == "auto_int8") *value = ix->auto_i8 ? 1 : 0;
+    else if (n == "auto_i8q") *value = ix->auto_i8q ? 1 : 0;
+    else if (n == "i8q_off") *value = ix->i8q_off.load() ? 1 : 0;
+    else if (n == "searches_i8q") *value = ix->n_by_prec[PREC_I8Q].load();
     else if (n == "i8_wide") *value = ix->i8_wide ? 1 : 0;
     else if (n == "device_bytes") {  // the row buffers actually allocated
         const int64_t xb = (int64_t)(ix->cap_rows / 32) * ix->G * BLOCK_FLOATS * 4;  // fp32 X: 4 B per element
@@ -1371,14 +1381,19 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     const bool hold8 = auto_prec && ix->auto_i8 && approx && (x3_i8 || !auto_x3) && auto_take_hold8(ix);
     const bool auto_8 = auto_prec && !auto_x3 && ix->auto_i8 && !hold8;
     const bool auto_8x3 = x3_i8 && !hold8;
+    // L2, 16 < k <= 100: the xh plane against the 16-bit query (two MFMAs per group, half the
+    // corpus bytes of I8X3; its 8-bit corpus bound certifies at KP = 256)
+    const bool auto_8q = auto_8x3 && ix->metric == 1 && k <= 100 && ix->auto_i8q && !ix->i8q_off;
     const bool force_8x3 = auto_prec && opt.force_i8x3 && ix->auto_i8 && ix->Xq;
     const int prec_req = !ix->X ? PREC_FP32
                          : force_8x3 ? PREC_I8X3
                          : ix->precision == VDB_PREC_BF16X3 ? PREC_BF16X3
                          : ix->precision == VDB_PREC_BF16 ? PREC_BF16
                          : ix->precision == VDB_PREC_I8X3 ? PREC_I8X3
+                         : ix->precision == VDB_PREC_I8Q ? (ix->metric == 1 ? PREC_I8Q : PREC_I8X3)
                          : ix->precision == VDB_PREC_I8 ? PREC_I8
-                         : auto_prec ? (auto_x3 ? (auto_8x3 ? PREC_I8X3 : PREC_BF16X3) : auto_8 ? PREC_I8 : PREC_BF16)
+                         : auto_prec ? (auto_x3 ? (auto_8x3 ? (auto_8q ? PREC_I8Q : PREC_I8X3) : PREC_BF16X3)
+                                                 : auto_8 ? PREC_I8 : PREC_BF16)
                                      : PREC_FP32;
     if (auto_prec && approx && (!auto_x3 || x3_i8)) ix->last_i8 = auto_8 || auto_8x3;
     // (a device re-pass's gated sub-search is counted by the device: repass_queries)
@@ -1405,6 +1420,8 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     const bool i8_narrow = auto_prec && ix->i8_narrow != 0 && !ix->i8_wide &&
                            (N <= kI8NarrowRows || (ix->Dp <= 128 && N <= kI8NarrowRowsShort));
     if (prec_req == PREC_I8) margin_def = std::max(16, (i8_narrow ? 128 : 256) - k);
+    // I8Q (the 8-bit corpus's bound, as I8's): KP = 256
+    if (prec_req == PREC_I8Q) margin_def = std::max(16, 256 - k);
     // a re-pass sub-search (host or device) takes KP = 128: its few queries are the ones whose
     // rows sit closer together than the one-plane pass could separate, so they need the wider
     // gap between the k-th and the KP-th candidate (C2 with 300 rows in a 3e-3 cosine band:
@@ -1744,9 +1761,9 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
             fa.dir = prec == PREC_BF16 && ix->dir_set && !ix->no_dir_bound ? ix->d_dir : nullptr;
             fa.dres = 1.01 * ix->xres_dir;
             if (i8_pass) {  // the int8 copy's rounding of the centred rows (absolute: cosine rows are unit)
-                fa.xres = 1.01 * ix->i8st[prec == PREC_I8 ? 0 : 2] + 1e-300;
+                fa.xres = 1.01 * ix->i8st[prec == PREC_I8X3 ? 2 : 0] + 1e-300;  // (I8 / I8Q: the xh plane's)
                 fa.dir = ix->dir_set && !ix->no_dir_bound ? ix->d_dir : nullptr;
-                fa.dres = 1.01 * ix->i8st[prec == PREC_I8 ? 1 : 3];
+                fa.dres = 1.01 * ix->i8st[prec == PREC_I8X3 ? 3 : 1];
                 fa.qerr = q8err;
                 fa.mu = ix->d_mu;
                 if (i8_refine) {
@@ -1799,13 +1816,14 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
                         ix->d_totals = d;
                     }
                 }
-                unsigned long long* htot = auto_prec && (one_plane || prec == PREC_I8X3) ? ix->h_totals : nullptr;
+                unsigned long long* htot =
+                    auto_prec && (one_plane || prec == PREC_I8X3 || prec == PREC_I8Q) ? ix->h_totals : nullptr;
                 // The device re-pass: up to kRepassDev uncertified queries gathered on the
                 // device into a BF16X3 sub-search on this stream, gated on their count (its candidate
                 // pass and finish exit at once when nothing was flagged), its rows scattered back;
                 // the rest, if any, take the gated exact path.  Like the host re-pass (repass_flagged)
                 // for auto's one-plane / I8X3 passes, with the split copy kept beside the int8 one.
-                const bool can_rep = !opt.repass && auto_prec && (one_plane || prec == PREC_I8X3) &&
+                const bool can_rep = !opt.repass && auto_prec && (one_plane || prec == PREC_I8X3 || prec == PREC_I8Q) &&
                                      xs_kind(VDB_PREC_BF16X3) == xs_kind(ix->precision) && rep_q &&
                                      k <= kMaxApproxK;
                 bool rep = can_rep && ix->device_repass == 1;
@@ -1865,6 +1883,8 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
             // auto's I8X3 pass: a failure the size of the one-plane passes' retries holds BF16X3
             // for the next searches (this batch's uncertified queries take the exact path below)
             if (auto_prec && prec == PREC_I8X3 && n_flag > std::max(1, B / 8) && !ix->no_fallback) auto_fail8(ix);
+            // auto's I8Q pass: such a failure turns it off for this index (I8X3 from then on)
+            if (auto_prec && prec == PREC_I8Q && n_flag > std::max(1, B / 8) && !ix->no_fallback) ix->i8q_off = true;
             if (timed) {
                 const int frc = flush_timing(ix, w);
                 if (frc) return frc;

@@ -25,10 +25,13 @@ constexpr int PREC_BF16 = 2;
 //   PREC_I8     int8 copy of the centred rows (vdb_scan8_kernel.h): x ~ s_x xh (1 byte per element),
 //               query s_q qh (8 bits): one v_mfma_i32_32x32x32_i8 per 32-dim group
 //   PREC_I8X3   both planes of the int8 copy, x ~ s_x (xh + xl/256), query 16 bits: three per group
+//   PREC_I8Q    the xh plane (8 bits, 1 byte per element) against the 16-bit query: xh.qh + xh.ql /
+//               256, two per group (L2, 16 < k <= 100: C4)
 constexpr int PREC_I8 = 3;
 constexpr int PREC_I8X3 = 4;
-constexpr int N_PREC = 5;
-inline bool prec_is_i8(int p) { return p == PREC_I8 || p == PREC_I8X3; }
+constexpr int PREC_I8Q = 5;
+constexpr int N_PREC = 6;
+inline bool prec_is_i8(int p) { return p == PREC_I8 || p == PREC_I8X3 || p == PREC_I8Q; }
 
 // Per-index constants of the int8 pass (vdb_api.cpp): the quantisation step s_x of the centred
 // rows, max |s_x xh| and max |s_x xl / 256| over the rows (row norms), max |x|^2 / 2 (L2 start)

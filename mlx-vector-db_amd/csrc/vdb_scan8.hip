@@ -343,14 +343,15 @@ __global__ void __launch_bounds__(256) prep8_kernel(const float* __restrict__ Q,
     s_ql = wave_sum_butterfly(s_ql);
     s_qh = wave_sum_butterfly(s_qh);
     if (lane == 0) {
-        const bool x3 = prec == PREC_I8X3;
-        const double za = c.zmax_h + (x3 ? c.xl_max : 0.0);  // bound of |z~|
-        // I8X3: |L uL| <= |s_x xh| |s_q ql / 256| + |s_x xl / 256| |s_q qh| (I8 has no L)
-        const double sl = x3 ? c.zmax_h * sqrt(s_ql) + c.xl_max * sqrt(s_qh) : 0.0;
+        const bool x3 = prec == PREC_I8X3, q16 = x3 || prec == PREC_I8Q;
+        const double za = c.zmax_h + (x3 ? c.xl_max : 0.0);  // bound of |z~| (I8 / I8Q: s_x xh alone)
+        // I8X3: |L uL| <= |s_x xh| |s_q ql / 256| + |s_x xl / 256| |s_q qh|; I8Q the first term
+        // alone (I8 has no L)
+        const double sl = q16 ? c.zmax_h * sqrt(s_ql) + (x3 ? c.xl_max * sqrt(s_qh) : 0.0) : 0.0;
         // approx - z.q' = -(z - z~).q' (the corpus term, finish) - z~.(q' - q~) (q~ = s_q qh for
-        // I8, s_q (qh + ql / 256) for I8X3) - [I8X3: the dropped s_x s_q xl.ql / 65536] (+ L2: the
-        // rounding of H's start, <= 0.5 uH, 1 uH with the fp32 product before it)
-        double e = za * sqrt(x3 ? s_rq : s_r8) + (x3 ? c.xl_max * sqrt(s_ql) : 0.0) + (metric == 1 ? (double)uH : 0.0);
+        // I8, s_q (qh + ql / 256) for I8X3 / I8Q) - [I8X3: the dropped s_x s_q xl.ql / 65536]
+        // (+ L2: the rounding of H's start, <= 0.5 uH, 1 uH with the fp32 product before it)
+        double e = za * sqrt(q16 ? s_rq : s_r8) + (x3 ? c.xl_max * sqrt(s_ql) : 0.0) + (metric == 1 ? (double)uH : 0.0);
         e = 1.01 * (metric == 0 ? e : 2.0 * e);
         lsl[b] = real ? (float)(1.01 * sl) * (1.0f + 1e-5f) + 1e-30f : 0.0f;
         qerr[b] = real ? (float)e * (1.0f + 1e-5f) : 0.0f;
@@ -412,7 +413,7 @@ __device__ __forceinline__ void pilot8_chke(const float* __restrict__ Qq, int G,
                     const uint32_t hv = (uint32_t)(int)(int8_t)((uh >> (8 * bt)) & 255u);
                     const uint32_t ch = csum[d];
                     eh += hv * ch;
-                    if (HL) el += (uint32_t)(int)(int8_t)((ul >> (8 * bt)) & 255u) * ch + hv * csum[Dp + d];
+                    if (HL) el += (uint32_t)(int)(int8_t)((ul >> (8 * bt)) & 255u) * ch + (PREC == PREC_I8X3 ? hv * csum[Dp + d] : 0u);
                 }
             }
         }
@@ -634,13 +635,14 @@ hipError_t launch_pilot8(int prec, int metric, const float* Xq, const float* rin
         launched = true;                                                                                         \
     }                                                                                                            \
     if (!launched && prec == P && metric == M && QB == 32 * QTV) {                                               \
-        const size_t lds = pilot8_w(G8) > 1 ? (size_t)PILOT8_WAVES * (P == PREC_I8X3 ? 2 : 1) * QTV * 16 * 64 * 4 : 0; \
+        const size_t lds = pilot8_w(G8) > 1 ? (size_t)PILOT8_WAVES * (P == PREC_I8 ? 1 : 2) * QTV * 16 * 64 * 4 : 0; \
         hipLaunchKernelGGL((pilot8_scores_kernel<P, M, QTV>), grid, dim3(64 * PILOT8_WAVES), lds, st, Xq, rinit, \
                            mask, Qq, qscal, G8, N, B, n_qblocks, n_tiles, n_sample, pslots, csum, chke);        \
         launched = true;                                                                                         \
     }
     VDB_PILOT8(PREC_I8, 0, 2) VDB_PILOT8(PREC_I8, 1, 2) VDB_PILOT8(PREC_I8, 0, 1) VDB_PILOT8(PREC_I8, 1, 1)
     VDB_PILOT8(PREC_I8X3, 0, 2) VDB_PILOT8(PREC_I8X3, 1, 2) VDB_PILOT8(PREC_I8X3, 0, 1) VDB_PILOT8(PREC_I8X3, 1, 1)
+    VDB_PILOT8(PREC_I8Q, 1, 2) VDB_PILOT8(PREC_I8Q, 1, 1)
 #undef VDB_PILOT8
     if (!launched) return hipErrorInvalidValue;
     return hipGetLastError();
@@ -668,6 +670,7 @@ hipError_t launch_scan8(int prec, int metric, int KP, const float* Xq, const flo
     const bool nt = (!ql || (VDB_S8_NTQL && fs && !q4)) && n_qblocks == 1;
     auto* unit = prec == PREC_I8X3 ? (metric == 0 ? launch_scan8_i3c : launch_scan8_i3l)
                  : prec == PREC_I8 ? (metric == 0 ? launch_scan8_i1c : launch_scan8_i1l)
+                 : prec == PREC_I8Q && metric == 1 ? launch_scan8_iql  // (L2 only: vdb_api.cpp)
                                    : nullptr;
     if (!unit || metric < 0 || metric > 1) return hipErrorInvalidValue;
     return unit(KP, Xq, rinit, mask, Qq, lsl, qscal, G8, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt,

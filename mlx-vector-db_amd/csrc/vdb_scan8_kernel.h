@@ -51,7 +51,7 @@ constexpr int S8_NW = VDB_S8_NW;
 #endif
 // (the 128-query shape, QT = 4, keeps S8_NW: its host-side rows per step are scan8_rows_q4)
 constexpr int scan8_nw(int prec, int metric, int QT = 2) {
-    return prec == PREC_I8X3 && metric == 1 && QT != 4 ? VDB_S8_NW_X3L : S8_NW;
+    return (prec == PREC_I8X3 || prec == PREC_I8Q) && metric == 1 && QT != 4 ? VDB_S8_NW_X3L : S8_NW;
 }
 // the step's group loop: one loop with the tail selected inside (1) or the tail peeled (0)
 // the corpus loads non-temporal with the query block in LDS (one query block, flag-gated): C6
@@ -93,17 +93,17 @@ static __device__ unsigned long long g_scan8_stamps[1 << 16][12];
 #endif
 // (the 8-wave I8X3 L2 shape: one row tile per wave, the same rows per step with 256 registers)
 constexpr int scan8_rt(int prec, int metric) {
-    return prec == PREC_I8X3 && metric == 1 && VDB_S8_NW_X3L == 8 ? 1
-           : prec == PREC_I8X3 || metric == 1                   ? VDB_S8_RT3
+    return (prec == PREC_I8X3 || prec == PREC_I8Q) && metric == 1 && VDB_S8_NW_X3L == 8 ? 1
+           : prec == PREC_I8X3 || prec == PREC_I8Q || metric == 1                   ? VDB_S8_RT3
                                                                 : VDB_S8_RT1;
 }
 constexpr int scan8_rows(int prec, int metric) { return scan8_rt(prec, metric) * scan8_nw(prec, metric) * 32; }
 
 template <int PREC>
 struct Planes8 {
-    static constexpr int XPL = PREC == PREC_I8X3 ? 2 : 1;  // corpus planes read
-    static constexpr int QPL = PREC == PREC_I8X3 ? 2 : 1;  // query planes read
-    static constexpr bool L = PREC == PREC_I8X3;  // the L accumulator set
+    static constexpr int XPL = PREC == PREC_I8X3 ? 2 : 1;                       // corpus planes read
+    static constexpr int QPL = PREC == PREC_I8X3 || PREC == PREC_I8Q ? 2 : 1;   // query planes read
+    static constexpr bool L = PREC == PREC_I8X3 || PREC == PREC_I8Q;            // the L accumulator set
 };
 
 template <int PREC, int RT, int QT>
@@ -119,6 +119,15 @@ __device__ __forceinline__ void group_mfma8(const f32x4 (&x)[RT][Planes8<PREC>::
         for (int qt = 0; qt < QT; ++qt)
             aH[rt][qt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(__builtin_bit_cast(i32x4, x[rt][0]),
                                                                __builtin_bit_cast(i32x4, q[qt][0]), aH[rt][qt], 0, 0, 0);
+    if constexpr (PREC == PREC_I8Q) {  // L = xh.ql alone (the corpus's 8 bits)
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt)
+                aL[rt][qt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(
+                    __builtin_bit_cast(i32x4, x[rt][0]), __builtin_bit_cast(i32x4, q[qt][Planes8<PREC>::QPL - 1]),
+                    aL[rt][qt], 0, 0, 0);
+    }
     if constexpr (PREC == PREC_I8X3) {
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt)
@@ -889,10 +898,11 @@ static hipError_t scan8_launch(const float* Xq, const float* rinit, const uint32
 // with CAP 96): 96 + 56.5 KiB.  `small` keeps the round-3 rule (block <= 32 KiB: short rows).
 // rows per step of the 128-query shape (one row tile per wave)
 constexpr int scan8_rows_q4() { return 1 * S8_NW * 32; }
-inline bool scan8_q4_fits(int G8, int prec) { return S8_NW == 4 && (size_t)G8 * (prec == PREC_I8X3 ? 2 : 1) * 4 * 1024 <= 32 * 1024; }
+inline int scan8_qpl(int prec) { return prec == PREC_I8X3 || prec == PREC_I8Q ? 2 : 1; }
+inline bool scan8_q4_fits(int G8, int prec) { return S8_NW == 4 && (size_t)G8 * scan8_qpl(prec) * 4 * 1024 <= 32 * 1024; }
 inline int scan8_cap(int KP, bool ql) { return KP == 128 ? 192 : KP == 256 ? (ql ? 96 : 128) : 128; }  // as S8_KP
 inline bool scan8_qlds(int G8, int KP, int prec, int metric, bool small) {
-    const size_t q = (size_t)G8 * (prec == PREC_I8X3 ? 2 : 1) * 2 * 1024;
+    const size_t q = (size_t)G8 * scan8_qpl(prec) * 2 * 1024;
     if (small) return q <= 32 * 1024;
     // lists, s_pend of this shape's waves (the 8-wave I8X3 L2 shape: 16 KiB; counted at 8 waves for
     // every shape, C3's 96 KiB query block stopped fitting beside its 48 KiB of lists at the end of
@@ -954,5 +964,6 @@ hipError_t launch_scan8_i1c(S8_UNIT_PARAMS);
 hipError_t launch_scan8_i1l(S8_UNIT_PARAMS);
 hipError_t launch_scan8_i3c(S8_UNIT_PARAMS);
 hipError_t launch_scan8_i3l(S8_UNIT_PARAMS);
+hipError_t launch_scan8_iql(S8_UNIT_PARAMS);
 
 }  // namespace vdb

@@ -28,7 +28,7 @@ VDB_ERR_NODEVICE = -6
 
 METRIC_IDS = {"cosine": 0, "euclidean": 1}
 # candidate-pass arithmetic (include/vdb.h VDB_PREC_*); results are identical, speed differs
-PRECISION_IDS = {"fp32": 0, "bf16x3": 1, "bf16": 2, "auto": 3, "i8": 4, "i8x3": 5}
+PRECISION_IDS = {"fp32": 0, "bf16x3": 1, "bf16": 2, "auto": 3, "i8": 4, "i8x3": 5, "i8q": 6}
 MEM_HOST = 0
 MEM_DEVICE = 1
 # largest beam (ef) vdb_graph_search accepts (csrc/vdb_graph.hip GS_EF_MAX)

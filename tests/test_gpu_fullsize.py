@@ -118,7 +118,7 @@ def test_c2_exact_vs_reference_fp32_order(vdb):
     np.testing.assert_allclose(s[sub], rs, atol=1e-4, rtol=0)
     assert ix.stat("fallback_queries") == 0
     rep.update(precision=ix.precision,
-               searches_by_precision={p: ix.stat(f"searches_{p}") for p in ("bf16", "bf16x3", "fp32", "i8", "i8x3")})
+               searches_by_precision={p: ix.stat(f"searches_{p}") for p in ("bf16", "bf16x3", "fp32", "i8", "i8x3", "i8q")})
     _report("c2_fp32_ref.json", rep)
 
 
@@ -145,7 +145,7 @@ def test_c3_1m_x_1536_b256(vdb):
             assert i[b, 0] == r and s[b, 0] > 0.9999
         np.testing.assert_array_equal(i[sub], ei)
         np.testing.assert_array_equal(kk[sub], ek)
-    by_prec = {p: ix.stat(f"searches_{p}") for p in ("bf16", "bf16x3", "fp32", "i8", "i8x3")}
+    by_prec = {p: ix.stat(f"searches_{p}") for p in ("bf16", "bf16x3", "fp32", "i8", "i8x3", "i8q")}
     _report("c3.json", {"fallback_queries_per_search": fbs, "host_search_s": dts, "searches_by_precision": by_prec})
     rep, rs = _fp32_order(Q, V, i, sub, k, "cosine")
     np.testing.assert_allclose(s[sub], rs, atol=1e-4, rtol=0)
@@ -178,7 +178,7 @@ def test_c4_10m_x_128_l2_b512_top100(vdb, sync):
             assert i[b, 0] == r and s[b, 0] == 0.0
         np.testing.assert_array_equal(i[sub], ei)
         np.testing.assert_array_equal(kk[sub], ek)
-    by_prec = {p: ix.stat(f"searches_{p}") for p in ("bf16", "bf16x3", "fp32", "i8", "i8x3")}
+    by_prec = {p: ix.stat(f"searches_{p}") for p in ("bf16", "bf16x3", "fp32", "i8", "i8x3", "i8q")}
     _report(f"c4_sync{sync}.json", {"fallback_queries_per_search": fbs, "searches_by_precision": by_prec})
     assert fbs[-1] <= B // 50
     if sync == 0:
@@ -212,7 +212,7 @@ def test_c6_10m_x_128_cosine_b64_top10(vdb):
             assert i[b, 0] == r and s[b, 0] > 0.9999
         np.testing.assert_array_equal(i[sub], ei)
         np.testing.assert_array_equal(kk[sub], ek)
-    by_prec = {p: ix.stat(f"searches_{p}") for p in ("bf16", "bf16x3", "fp32", "i8", "i8x3")}
+    by_prec = {p: ix.stat(f"searches_{p}") for p in ("bf16", "bf16x3", "fp32", "i8", "i8x3", "i8q")}
     _report("c6.json", {"fallback_queries_per_search": fbs, "searches_by_precision": by_prec})
     assert fbs[-1] <= max(1, B // 50)
     rep, rs = _fp32_order(Q, V, i, sub, k, "cosine")

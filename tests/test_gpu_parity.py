@@ -31,7 +31,7 @@ def _mask_words(mask_bool):
     return np.packbits(bits, bitorder="little").view("<u4").astype(np.uint32)
 
 
-PRECISIONS = ["bf16x3", "bf16", "fp32", "auto", "i8", "i8x3"]
+PRECISIONS = ["bf16x3", "bf16", "fp32", "auto", "i8", "i8x3", "i8q"]  # (i8q: L2; cosine indexes run i8x3)
 
 
 def _check(vdb, V, Q, k, metric, mask=None, force_exact=False, margin=None, chunked_add=False, precision="bf16x3",
@@ -365,6 +365,46 @@ def test_auto_hold8_holds_bf16_until_the_rows_change(vdb):
     assert ix.stat("auto_hold8") == 0
     ix.search(Q, k)
     assert ix.stat("searches_i8") == 2
+
+
+def test_auto_l2_k_above_16_runs_i8q_and_turns_it_off_after_a_failure(vdb):
+    """L2 with 16 < k <= 100: auto's pass is I8Q (the int8 copy's xh plane against the 16-bit
+    query, KP = 256), exact through the certificate.  Rows its 8-bit corpus cannot separate (two
+    tight clusters far apart: one quantisation step spans a cluster) leave most queries
+    uncertified: the batch takes the exact path and the index runs I8X3 from then on (i8q_off)."""
+    rng = np.random.default_rng(53)
+    D, N, B, k = 128, 6000, 16, 40
+    V = rng.random((N, D), dtype=np.float32)
+    Q = rng.random((B, D), dtype=np.float32)
+    ix = vdb.NativeIndex(D, "euclidean")
+    assert ix.stat("auto_i8q") == 1
+    ix.add(V)
+    es, ei, ek = ref_cpu.exact_search(Q, V, k, "euclidean")
+    s, i, kk = ix.search(Q, k, with_keys=True)
+    np.testing.assert_array_equal(i, ei)
+    np.testing.assert_array_equal(kk, ek)
+    assert ix.stat("searches_i8q") == 1 and ix.stat("searches_i8x3") == 0
+    assert ix.stat("fallback_queries") == 0 and ix.stat("i8q_off") == 0
+    s, i, kk = ix.search(Q, 120, with_keys=True)  # k > 100: I8X3
+    assert ix.stat("searches_i8x3") == 1
+    ix.close()
+
+    b1, b2 = rng.random(D, dtype=np.float32), rng.random(D, dtype=np.float32)
+    side = rng.random(N) < 0.5
+    V = (np.where(side[:, None], b1, b2) + 1e-5 * rng.standard_normal((N, D))).astype(np.float32)
+    Q = (V[rng.integers(0, N, B)] + 1e-6 * rng.standard_normal((B, D))).astype(np.float32)
+    ix = vdb.NativeIndex(D, "euclidean")
+    ix.add(V)
+    es, ei, ek = ref_cpu.exact_search(Q, V, k, "euclidean")
+    s, i, kk = ix.search(Q, k, with_keys=True)
+    np.testing.assert_array_equal(i, ei)
+    np.testing.assert_array_equal(kk, ek)
+    assert ix.stat("searches_i8q") == 1 and ix.stat("fallback_queries") > B // 8
+    assert ix.stat("i8q_off") == 1
+    s, i, kk = ix.search(Q, k, with_keys=True)
+    np.testing.assert_array_equal(kk, ek)
+    assert ix.stat("searches_i8q") == 1 and ix.stat("searches_i8x3") + ix.stat("searches_bf16x3") >= 1
+    ix.close()
 
 
 def test_auto_k_above_16_runs_i8x3_and_holds_bf16x3_after_a_failure(vdb):
