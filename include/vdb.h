@@ -107,9 +107,9 @@ enum { VDB_MEM_HOST = 0, VDB_MEM_DEVICE = 1 };
  *                    next search starts the hold.  Stats "repass_queries", "auto_hold",
  *                    "auto_hold8". */
 /*   VDB_PREC_I8Q     the int8 copy's xh plane (1 byte per element) against the 16-bit query:
- *                    xh.qh + xh.ql / 256, two int8 MFMAs per group (L2 only; cosine indexes run
- *                    I8X3).  AUTO's pass for L2 with 16 < k <= 100 (KP = 256) until a batch
- *                    flags more than 1/8 of its queries (then I8X3 for good, stat "i8q_off"). */
+ *                    xh.qh + xh.ql / 256, two int8 MFMAs per group.  AUTO's pass for L2 with
+ *                    16 < k <= 100 (KP = 256) until a batch flags more than 1/8 of its queries
+ *                    (then I8X3 for good, stat "i8q_off"). */
 enum { VDB_PREC_FP32 = 0, VDB_PREC_BF16X3 = 1, VDB_PREC_BF16 = 2, VDB_PREC_AUTO = 3, VDB_PREC_I8 = 4, VDB_PREC_I8X3 = 5,
        VDB_PREC_I8Q = 6 };
 

@@ -1390,7 +1390,7 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
                          : ix->precision == VDB_PREC_BF16X3 ? PREC_BF16X3
                          : ix->precision == VDB_PREC_BF16 ? PREC_BF16
                          : ix->precision == VDB_PREC_I8X3 ? PREC_I8X3
-                         : ix->precision == VDB_PREC_I8Q ? (ix->metric == 1 ? PREC_I8Q : PREC_I8X3)
+                         : ix->precision == VDB_PREC_I8Q ? PREC_I8Q
                          : ix->precision == VDB_PREC_I8 ? PREC_I8
                          : auto_prec ? (auto_x3 ? (auto_8x3 ? (auto_8q ? PREC_I8Q : PREC_I8X3) : PREC_BF16X3)
                                                  : auto_8 ? PREC_I8 : PREC_BF16)

@@ -642,7 +642,7 @@ hipError_t launch_pilot8(int prec, int metric, const float* Xq, const float* rin
     }
     VDB_PILOT8(PREC_I8, 0, 2) VDB_PILOT8(PREC_I8, 1, 2) VDB_PILOT8(PREC_I8, 0, 1) VDB_PILOT8(PREC_I8, 1, 1)
     VDB_PILOT8(PREC_I8X3, 0, 2) VDB_PILOT8(PREC_I8X3, 1, 2) VDB_PILOT8(PREC_I8X3, 0, 1) VDB_PILOT8(PREC_I8X3, 1, 1)
-    VDB_PILOT8(PREC_I8Q, 1, 2) VDB_PILOT8(PREC_I8Q, 1, 1)
+    VDB_PILOT8(PREC_I8Q, 0, 2) VDB_PILOT8(PREC_I8Q, 1, 2) VDB_PILOT8(PREC_I8Q, 0, 1) VDB_PILOT8(PREC_I8Q, 1, 1)
 #undef VDB_PILOT8
     if (!launched) return hipErrorInvalidValue;
     return hipGetLastError();
@@ -670,7 +670,7 @@ hipError_t launch_scan8(int prec, int metric, int KP, const float* Xq, const flo
     const bool nt = (!ql || (VDB_S8_NTQL && fs && !q4)) && n_qblocks == 1;
     auto* unit = prec == PREC_I8X3 ? (metric == 0 ? launch_scan8_i3c : launch_scan8_i3l)
                  : prec == PREC_I8 ? (metric == 0 ? launch_scan8_i1c : launch_scan8_i1l)
-                 : prec == PREC_I8Q && metric == 1 ? launch_scan8_iql  // (L2 only: vdb_api.cpp)
+                 : prec == PREC_I8Q ? (metric == 0 ? launch_scan8_iqc : launch_scan8_iql)
                                    : nullptr;
     if (!unit || metric < 0 || metric > 1) return hipErrorInvalidValue;
     return unit(KP, Xq, rinit, mask, Qq, lsl, qscal, G8, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt,

@@ -964,6 +964,7 @@ hipError_t launch_scan8_i1c(S8_UNIT_PARAMS);
 hipError_t launch_scan8_i1l(S8_UNIT_PARAMS);
 hipError_t launch_scan8_i3c(S8_UNIT_PARAMS);
 hipError_t launch_scan8_i3l(S8_UNIT_PARAMS);
+hipError_t launch_scan8_iqc(S8_UNIT_PARAMS);
 hipError_t launch_scan8_iql(S8_UNIT_PARAMS);
 
 }  // namespace vdb

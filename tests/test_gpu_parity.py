@@ -31,7 +31,7 @@ def _mask_words(mask_bool):
     return np.packbits(bits, bitorder="little").view("<u4").astype(np.uint32)
 
 
-PRECISIONS = ["bf16x3", "bf16", "fp32", "auto", "i8", "i8x3", "i8q"]  # (i8q: L2; cosine indexes run i8x3)
+PRECISIONS = ["bf16x3", "bf16", "fp32", "auto", "i8", "i8x3", "i8q"]
 
 
 def _check(vdb, V, Q, k, metric, mask=None, force_exact=False, margin=None, chunked_add=False, precision="bf16x3",
