@@ -1,4 +1,4 @@
-// vdb_scan8_kernel.h — the int8 candidate pass (PREC_I8 / PREC_I8X3) and its launch templates
+// vdb_scan8_kernel.h — the int8 candidate pass (PREC_I8 / PREC_I8Q / PREC_I8X3) and its launch templates
 // (included by vdb_scan8.hip and the per-(precision, metric) instantiation units
 // vdb_scan8_{i1,i3}{c,l}.hip, which the build compiles in parallel).
 //
@@ -8,6 +8,7 @@
 // The query block q (cosine: normalised) is quantised the same way per batch, q ~ s_q (qh + ql /
 // 256) (vdb_scan8.hip prep8).  Per 32-dim group and (row tile, query tile) the pass issues
 //   PREC_I8    xh.qh -> H                                   1 v_mfma_i32_32x32x32_i8
+//   PREC_I8Q   xh.qh -> H, xh.ql -> L                       2 (the 8-bit corpus x the 16-bit query)
 //   PREC_I8X3  xh.qh -> H, xh.ql + xl.qh -> L               3 v_mfma_i32_32x32x32_i8
 // and the (half-)score is H s_x s_q (+ L s_x s_q / 256): integer sums are exact, an i8 MFMA does
 // twice the K of a bf16 one in the same cycles, and the I8 pass reads one byte per element
