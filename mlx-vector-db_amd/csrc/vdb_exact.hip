@@ -274,7 +274,10 @@ hipError_t launch_rerank(int metric, int KP, const RerankArgs& a, int B, hipStre
 // at C2 bf16) get exact fp64 keys, all waves, batched NB candidates per wave so the corpus
 // loads of a batch are in flight together; exact ranks come from counting (no sort),
 // several threads per candidate.  A list longer than FIN_CAP goes to the exact scan.
-constexpr int FIN_CAP = 16384;  // 128 KiB of (key, row) in LDS
+#ifndef VDB_FIN_CAP
+#define VDB_FIN_CAP 16384
+#endif
+constexpr int FIN_CAP = VDB_FIN_CAP;  // 128 KiB of (key, row) in LDS
 constexpr int FIN_NB = 2;        // candidates per wave per batch
 constexpr int FIN_WAVES = VDB_FIN_WAVES;
 
@@ -329,8 +332,13 @@ __device__ __forceinline__ void exact_keys_batch(const float* __restrict__ q, do
     }
 }
 
-template <int METRIC, int KP>
-__global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
+// FW waves per workgroup: 16 (FIN_WAVES), or 8 for rows of more than 1024 dims (no spills at the
+// 8-piece exact keys: C3 400-413 K -> 419-421 K QPS; C2 / C4 / C6 -0.5..-1% at 8, so they keep 16;
+// profiles/r05_ab/ab34_finish_waves.log)
+template <int METRIC, int KP, int FW = FIN_WAVES>
+__global__ void __launch_bounds__(64 * FW) finish_kernel(FinishArgs a) {
+    constexpr int FIN_WAVES = FW;  // (shadows the default inside this kernel)
+    constexpr int FIN_NB4 = FW > 8 ? 3 : 6;
     __shared__ uint32_t s_key[FIN_CAP];
     __shared__ uint32_t s_row[FIN_CAP];
     __shared__ __attribute__((aligned(16))) uint32_t s_ck[KP];
@@ -1087,10 +1095,14 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) finish_kernel(FinishArgs a) {
 hipError_t launch_finish(int metric, int KP, const FinishArgs& a, int B, hipStream_t st) {
     if (a.split < 1 || (a.split > 1 && (!a.sx_ek || !a.sx_ck || !a.sx_cr || !a.sx_n || !a.done)))
         return hipErrorInvalidValue;
-#define VDB_FIN(M, KPV)                                                                         \
-    if (metric == M && KP == KPV) {                                                             \
-        hipLaunchKernelGGL((finish_kernel<M, KPV>), dim3(B, a.split), dim3(64 * FIN_WAVES), 0, st, a); \
-        return hipGetLastError();                                                               \
+    const bool w8 = FIN_WAVES > 8 && a.D > 1024;
+#define VDB_FIN(M, KPV)                                                                                    \
+    if (metric == M && KP == KPV) {                                                                        \
+        if (w8)                                                                                            \
+            hipLaunchKernelGGL((finish_kernel<M, KPV, 8>), dim3(B, a.split), dim3(64 * 8), 0, st, a);      \
+        else                                                                                               \
+            hipLaunchKernelGGL((finish_kernel<M, KPV>), dim3(B, a.split), dim3(64 * FIN_WAVES), 0, st, a); \
+        return hipGetLastError();                                                                          \
     }
     VDB_FIN(0, 32) VDB_FIN(0, 64) VDB_FIN(0, 128) VDB_FIN(0, 256)
     VDB_FIN(1, 32) VDB_FIN(1, 64) VDB_FIN(1, 128) VDB_FIN(1, 256)
