@@ -80,7 +80,7 @@ def test_golden_fixtures(vdb, path, precision):
 @pytest.mark.parametrize("metric", ["cosine", "euclidean"])
 @pytest.mark.parametrize("N,D,B,k", [(5000, 384, 7, 10), (3000, 100, 3, 5), (4096, 128, 64, 100),
                                      (1234, 33, 65, 32), (700, 1536, 9, 10), (20000, 768, 130, 10),
-                                     (9000, 64, 40, 200)])
+                                     (9000, 64, 40, 200), (2500, 1100, 17, 150)])
 def test_random_uniform(vdb, metric, N, D, B, k, precision):
     rng = np.random.default_rng(N + D)
     V = rng.random((N, D), dtype=np.float32)
@@ -109,6 +109,19 @@ def test_finish_split(vdb, split, metric):
     _check(vdb, V, Q, 25, metric, params={"finish_split": split})
     _check(vdb, V, Q, 25, metric, precision="bf16", params={"finish_split": split})
     _check(vdb, V, Q, 25, metric, precision="i8", params={"finish_split": split})
+
+
+@pytest.mark.parametrize("split", [1, 3])
+@pytest.mark.parametrize("metric", ["cosine", "euclidean"])
+def test_finish_long_rows(vdb, split, metric):
+    """Rows of more than 1024 dims take the 8-wave finish (vdb_exact.hip, launch_finish): ragged
+    D = 1090 at KP 64 / 256 (k 25 / 120), alone and split across workgroups."""
+    rng = np.random.default_rng(1090 + split)
+    V = rng.standard_normal((6000, 1090)).astype(np.float32)
+    Q = rng.standard_normal((24, 1090)).astype(np.float32)
+    for k in (25, 120):
+        _check(vdb, V, Q, k, metric, params={"finish_split": split})
+        _check(vdb, V, Q, k, metric, precision="i8", params={"finish_split": split})
 
 
 @pytest.mark.parametrize("precision", ["bf16x3", "bf16"])
