@@ -111,14 +111,15 @@ def test_finish_split(vdb, split, metric):
     _check(vdb, V, Q, 25, metric, precision="i8", params={"finish_split": split})
 
 
-@pytest.mark.parametrize("split", [1, 3])
+@pytest.mark.parametrize("split,D", [(1, 1090), (3, 1090), (1, 1024), (1, 1025)])
 @pytest.mark.parametrize("metric", ["cosine", "euclidean"])
-def test_finish_long_rows(vdb, split, metric):
+def test_finish_long_rows(vdb, split, D, metric):
     """Rows of more than 1024 dims take the 8-wave finish (vdb_exact.hip, launch_finish): ragged
-    D = 1090 at KP 64 / 256 (k 25 / 120), alone and split across workgroups."""
-    rng = np.random.default_rng(1090 + split)
-    V = rng.standard_normal((6000, 1090)).astype(np.float32)
-    Q = rng.standard_normal((24, 1090)).astype(np.float32)
+    D = 1090 at KP 64 / 256 (k 25 / 120), alone and split across workgroups, and both sides of
+    the switch (1024: 16 waves, 1025: 8)."""
+    rng = np.random.default_rng(D + split)
+    V = rng.standard_normal((6000, D)).astype(np.float32)
+    Q = rng.standard_normal((24, D)).astype(np.float32)
     for k in (25, 120):
         _check(vdb, V, Q, k, metric, params={"finish_split": split})
         _check(vdb, V, Q, k, metric, precision="i8", params={"finish_split": split})
