@@ -206,8 +206,12 @@ struct vdb_index {
     std::atomic<bool> i8_wide{false};
     // auto's L2 pass for 16 < k <= 100: PREC_I8Q (the xh plane against the 16-bit query) unless
     // "auto_i8q" = 0, or once a batch flagged more than 1/8 of its queries (i8q_off: I8X3 after)
-    bool auto_i8q = true;
+    std::atomic<bool> auto_i8q{true};
     std::atomic<bool> i8q_off{false};
+    // the last auto pass was I8Q, and its batch size: a device-memory search sees its flags a
+    // search or more late (h_totals), and turns I8Q off by the same 1/8 rule
+    std::atomic<bool> last_i8q{false};
+    std::atomic<int> last_i8q_b{0};
     std::atomic<uint32_t> pace_seq{0};  // launch tag of the pacing counters
     int64_t scan_q4 = -1;      // split pass 128-query shape (D <= 128, KP = 128, B >= 256): -1 auto, 0 off, 1 on
     // stats
@@ -692,8 +696,10 @@ int32_t vdb_index_create(int32_t dim, int32_t metric, int32_t device, vdb_index*
     if (const char* q4 = std::getenv("VDB_SCAN_Q4")) ix->scan_q4 = std::min(1, std::max(-1, std::atoi(q4)));
     if (const char* a8 = std::getenv("VDB_AUTO_I8")) ix->auto_i8 = std::atoi(a8) != 0;
     hipError_t e = hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipMalloc(&ix->d_xmax, 64);
-    if (e == hipSuccess) e = zero_now(ix->d_xmax, 64, ix->stream);
+    // d_xmax: [0, 32) the residual maxima, [32, 36) the non-finite count, [64, 96) and
+    // [128, 192) an add's snapshot of the maxima and of d_i8 (restored when the add is rejected)
+    if (e == hipSuccess) e = hipMalloc(&ix->d_xmax, 192);
+    if (e == hipSuccess) e = zero_now(ix->d_xmax, 192, ix->stream);
     if (e == hipSuccess) e = hipMalloc(&ix->d_i8, 64);
     if (e == hipSuccess) e = zero_now(ix->d_i8, 64, ix->stream);
     if (e == hipSuccess) e = hipMalloc(&ix->d_csum, (size_t)2 * ix->Dp * sizeof(uint32_t));
@@ -1046,6 +1052,11 @@ int32_t vdb_index_add(vdb_index* ix, const float* vectors, int64_t n, int32_t me
         if (wr) return wr;
     }
     HIP_TRY(hipMemsetAsync(ix->d_nonfinite, 0, sizeof(int), st));
+    // snapshot of the row statistics the kernels below raise over the new rows: a rejected add
+    // puts them back (its rows must leave no trace in any statistic or column sum)
+    char* bak = reinterpret_cast<char*>(ix->d_xmax);
+    HIP_TRY(hipMemcpyAsync(bak + 64, ix->d_xmax, 32, hipMemcpyDeviceToDevice, st));
+    HIP_TRY(hipMemcpyAsync(bak + 128, ix->d_i8, 64, hipMemcpyDeviceToDevice, st));
     if (mem == VDB_MEM_DEVICE) {
         // the rows may still be being written on the caller's stream (NULL = the null stream):
         // ingest (on the index's own stream) starts after that work
@@ -1100,6 +1111,16 @@ int32_t vdb_index_add(vdb_index* ix, const float* vectors, int64_t n, int32_t me
             HIP_TRY(hipMemsetAsync(ix->d_i8, 0, 64, st));
             HIP_TRY(hipStreamSynchronize(st));
             std::memset(ix->i8st, 0, sizeof(ix->i8st));
+        } else {
+            // the rejected rows' statistics and column sums came in with them: the maxima and the
+            // int8 statistics go back to the snapshot, the column sums are rebuilt over [0, count)
+            HIP_TRY(hipMemcpyAsync(ix->d_xmax, bak + 64, 32, hipMemcpyDeviceToDevice, st));
+            HIP_TRY(hipMemcpyAsync(ix->d_i8, bak + 128, 64, hipMemcpyDeviceToDevice, st));
+            if (ix->Xq && needs_i8(ix->precision, ix->auto_i8)) {
+                HIP_TRY(hipMemsetAsync(ix->d_csum, 0, (size_t)2 * ix->Dp * sizeof(uint32_t), st));
+                HIP_TRY(launch_colsum8(ix->Xq, 0, ix->count, ix->G / 4, ix->d_csum, st));
+            }
+            HIP_TRY(read_i8_stats(ix, st));  // (synchronises)
         }
         return set_error(VDB_ERR_NONFINITE, "%d row(s) contain NaN or Inf; nothing was added", nonfinite);
     }
@@ -1356,6 +1377,8 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
         const unsigned long long seen = ix->h_totals[0];
         const unsigned long long prev = ix->auto_seen.exchange(seen);
         if (seen > prev) {
+            if (ix->last_i8q && seen - prev > (unsigned long long)std::max(1, ix->last_i8q_b.load() / 8))
+                ix->i8q_off = true;
             if (ix->last_i8) {
                 auto_fail8(ix);
                 ix->i8_wide = true;
@@ -1395,7 +1418,11 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
                          : auto_prec ? (auto_x3 ? (auto_8x3 ? (auto_8q ? PREC_I8Q : PREC_I8X3) : PREC_BF16X3)
                                                  : auto_8 ? PREC_I8 : PREC_BF16)
                                      : PREC_FP32;
-    if (auto_prec && approx && (!auto_x3 || x3_i8)) ix->last_i8 = auto_8 || auto_8x3;
+    if (auto_prec && approx && (!auto_x3 || x3_i8)) {
+        ix->last_i8 = auto_8 || auto_8x3;
+        ix->last_i8q = prec_req == PREC_I8Q;
+        ix->last_i8q_b = (int)B;
+    }
     // (a device re-pass's gated sub-search is counted by the device: repass_queries)
     if (approx && !opt.gate) ix->n_by_prec[prec_req]++;
     // the "one plane" precisions (a wide certificate: KP = 128 for small k) and their re-pass

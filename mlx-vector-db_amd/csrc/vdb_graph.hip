@@ -178,7 +178,7 @@ __global__ void __launch_bounds__(64 * GS_WAVES) graph_search_kernel(GraphSearch
         const int mine = sliced ? Ev : (E - team + T - 1) / T;
         s_bn = mine < ef ? mine : ef;
         s_cur = 0;
-        s_scored = (unsigned)E;
+        s_scored = (unsigned)(sliced ? Ev : E);
     }
     __syncthreads();
 

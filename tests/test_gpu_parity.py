@@ -542,6 +542,37 @@ def test_nonfinite_rejected(vdb):
         ix.search(np.full((1, 4), np.inf, np.float32), 1)
 
 
+@pytest.mark.parametrize("metric", ["cosine", "euclidean"])
+@pytest.mark.parametrize("precision", ["i8", "i8x3", "auto"])
+def test_rejected_add_leaves_no_trace(vdb, metric, precision):
+    """an add rejected for a NaN row after good rows must leave the int8 copy's
+    column sums (the pass's checksum) and the row statistics as they were: the next searches
+    certify in the int8 pass with no flagged / inconsistent query, and stay exact after a
+    further good add."""
+    from oracle import ref_cpu
+    rng = np.random.default_rng(41)
+    D = 96
+    V = rng.random((6000, D), dtype=np.float32)
+    Q = rng.random((16, D), dtype=np.float32)
+    ix = vdb.NativeIndex(D, metric, precision=precision)
+    ix.add(V[:4000])
+    bad = rng.random((500, D), dtype=np.float32) * 50.0  # large rows: they would raise the maxima
+    bad[321, 7] = np.nan
+    with pytest.raises(ValueError):
+        ix.add(bad)
+    assert ix.count() == 4000
+    for rows in (4000, 6000):
+        if rows == 6000:
+            ix.add(V[4000:])
+        _, i, kk = ix.search(Q, 10, with_keys=True)
+        _, ei, ek = ref_cpu.exact_search(Q, V[:rows], 10, metric)
+        np.testing.assert_array_equal(i, ei)
+        np.testing.assert_array_equal(kk, ek)
+    assert ix.stat("inconsistent_queries") == 0
+    assert ix.stat("fallback_queries") == 0
+    ix.close()
+
+
 def test_export_roundtrip(vdb):
     rng = np.random.default_rng(9)
     V = rng.standard_normal((1000, 77)).astype(np.float32)
