@@ -449,6 +449,8 @@ def main():
     ap.add_argument("--scan-qring", type=int, default=None, help="1: query operand through an LDS ring (tuning)")
     ap.add_argument("--scan-qlds", type=int, default=None, help="0: query block never in LDS (tuning)")
     ap.add_argument("--scan-q4", type=int, default=None, help="128-query shape: -1 auto, 0 off, 1 on (tuning)")
+    ap.add_argument("--scan-wide", type=int, default=None,
+                    help="wide int8 pass (D <= 128, B > 256): -1 auto, 0 off, 1 on (tuning)")
     ap.add_argument("--scan-realign", type=int, default=None,
                     help="flag-gated step ends: a workgroup barrier every n steps (tuning)")
     ap.add_argument("--dir-bound", type=int, default=None,
@@ -581,6 +583,8 @@ def bench_brute(cfg, args, world, rank, local, dev, primary=True):
         ix.set_param("scan_qlds", args.scan_qlds)
     if args.scan_q4 is not None:
         ix.set_param("scan_q4", args.scan_q4)
+    if args.scan_wide is not None:
+        ix.set_param("scan_wide", args.scan_wide)
     if args.dir_bound is not None:
         ix.set_param("dir_bound", args.dir_bound)
     if args.scan_publish is not None:

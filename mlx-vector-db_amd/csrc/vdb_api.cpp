@@ -214,8 +214,12 @@ struct vdb_index {
     std::atomic<int> last_i8q_b{0};
     std::atomic<uint32_t> pace_seq{0};  // launch tag of the pacing counters
     int64_t scan_q4 = -1;      // split pass 128-query shape (D <= 128, KP = 128, B >= 256): -1 auto, 0 off, 1 on
+    // the wide int8 pass (vdb_scan8w.hip: rows of 4 groups, B > 256): -1 auto (from kWideMinRows
+    // rows), 0 off, 1 at any row count
+    int64_t scan_wide = -1;
     // stats
     std::atomic<int64_t> n_searches{0}, n_queries{0}, n_fallback{0}, n_overflow{0}, n_incons{0}, n_repass{0}, n_scan3{0}, n_q4{0};
+    std::atomic<int64_t> n_wide{0};  // searches through the wide int8 pass
     std::atomic<int64_t> n_xs_builds{0};  // lazy builds of the split copy (ensure_xs)
     std::atomic<int64_t> n_by_prec[N_PREC] = {{0}, {0}, {0}, {0}, {0}, {0}};  // candidate passes per PREC_* (VDB_PREC_AUTO's choices)
     std::atomic<int64_t> scan_ns{0}, pipe_ns{0}, n_timed{0};
@@ -854,6 +858,9 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
     } else if (n == "scan_qlds") {
         if (value < -1 || value > 2) return set_error(VDB_ERR_INVALID, "scan_qlds must be -1 (auto), 0, 1 or 2");
         ix->scan_qlds = value;
+    } else if (n == "scan_wide") {
+        if (value < -1 || value > 1) return set_error(VDB_ERR_INVALID, "scan_wide must be -1, 0 or 1");
+        ix->scan_wide = value;
     } else if (n == "scan_q4") {
         if (value < -1 || value > 1) return set_error(VDB_ERR_INVALID, "scan_q4 must be -1, 0 or 1");
         ix->scan_q4 = value;
@@ -948,6 +955,7 @@ int32_t vdb_index_get_stat(const vdb_index* cix, const char* name, int64_t* valu
     else if (n == "repass_queries") *value = ix->n_repass.load() + (int64_t)dt[3];  // + device re-passes
     else if (n == "searches_scan3") *value = ix->n_scan3.load();
     else if (n == "searches_q4") *value = ix->n_q4.load();
+    else if (n == "searches_wide") *value = ix->n_wide.load();
     else if (n == "auto_hold") *value = ix->auto_hold.load();
     else if (n == "auto_hold8") *value = ix->auto_hold8.load();
     else if (n == "overflow_queries") *value = ix->n_overflow.load() + (int64_t)dt[1];
@@ -1243,6 +1251,10 @@ constexpr int kRepassArm = 256;
 // auto's I8 pass: KP = 128 up to this many rows (i8_narrow)
 constexpr int64_t kI8NarrowRows = 512 * 1024;
 constexpr int64_t kI8NarrowRowsShort = 4 * 1024 * 1024;  // rows of <= 128 dims
+// the wide int8 pass under scan_wide auto: from this many rows (smaller indexes: the 64-query shape)
+constexpr int64_t kWideMinRows = 65536;
+// the finish holds every segment's entries: at most FIN_CAP (16 K) / W8_CH segments
+constexpr int FIN_SEG_MAX = 512;
 // i8_refine auto: the finish refines I8 candidates' scores for padded rows of this many dims or more
 constexpr int64_t kRefineMinDp = 512;
 // VDB_PREC_AUTO uses the bf16 pass up to this k (its KP = next_pow2(k + 112) stays 128)
@@ -1477,6 +1489,13 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     // Opt-in (scan_q4 = 1): C4 ran 2.91 -> 3.08 ms with it (profiles/r04_q48, same box).
     const bool q4_8 = i8_pass && !exact_all && !opt.gate && KP == 128 && B >= 256 && scan8_q4_ok(Gs, prec) &&
                       ix->scan_q4 == 1;
+    // The wide int8 pass (vdb_scan8w.hip): rows of 4 groups (D <= 128) and batches of more than 256
+    // (C4, and each rank of its row-sharded run): all queries of a 512-query block in one
+    // workgroup, the corpus staged once through LDS; one workgroup per CU, tiles dealt round-robin
+    const int64_t n_tiles_all = round_up(N, 32) / 32;
+    const bool wide8 = i8_pass && !exact_all && !opt.gate && !q4_8 && scan8w_ok(Gs, B) && N > 0 &&
+                       (ix->scan_wide == 1 || (ix->scan_wide < 0 && N >= kWideMinRows));
+    const int n_seg8 = wide8 ? (int)std::min<int64_t>(FIN_SEG_MAX, round_up(std::min<int64_t>(ix->n_cu, n_tiles_all), 8)) : 0;
     // query rows per candidate-pass block: the int8 pass keeps 64 at KP = 256 (KW = 64 kept per
     // workgroup, vdb_scan8_kernel.h), the split pass 32 there
     const int QB = q4 ? 128 : i8_pass ? scan8_qb(KP, q4_8) : KP == 256 ? 32 : 64;
@@ -1570,12 +1589,14 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     // the L sums of I8X3 too (scan_checksum 2): +5% on C4's scan over H alone (the xh plane, the
     // query's hi plane and the start values; an L operand moves a score by at most the slack lsl)
     const bool chk_l = chk && prec == PREC_I8X3 && ix->scan_checksum == 2;
-    const int n_wg8 = (n_wg + 7) / 8 * 8;
+    const int n_wg8 = wide8 ? n_seg8 : (n_wg + 7) / 8 * 8;
+    bytes += wide8 ? (size_t)Bp * n_seg8 * 4 + 256 : 0;  // the wide pass's segment counts
     bytes += chk ? ((size_t)2 * n_wg8 * Bp + (size_t)2 * Bp + 64) * 4 + 768 : 0;
     const bool priv = !exact_all && !split_pass && !i8_pass && scan_priv(prec, variant, KP);
     // global per-query candidate lists: at most 512 entries per workgroup and query
     // (the largest LDS buffer of any variant; 4 x 64 for the wave-private one)
-    const int64_t gl_cap = exact_all ? 0 : use_s3 ? (int64_t)((n_wg3 + 7) / 8 * 8) * 64
+    const int64_t gl_cap = exact_all ? 0 : wide8 ? (int64_t)n_seg8 * W8_CH
+                                       : use_s3 ? (int64_t)((n_wg3 + 7) / 8 * 8) * 64
                                               : (int64_t)((n_wg + 7) / 8 * 8) * 512;
     bytes += (size_t)B * gl_cap * 8 + (size_t)Bp * 4 + 768;
     // Pilot sample: 512 row tiles, more for large k (its bound then saves more insert work than
@@ -1658,6 +1679,7 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     float* q8err2 = i8_refine ? c.take<float>(Bp) : nullptr;
     uint32_t* pace = c.take<uint32_t>((size_t)(n_wg + 7) / 8 * 8 * n_qblocks + 64);
     uint32_t* chkp = chk ? c.take<uint32_t>((size_t)2 * n_wg8 * Bp) : nullptr;
+    uint32_t* segc = wide8 ? c.take<uint32_t>((size_t)Bp * n_seg8) : nullptr;
     uint32_t* chkr = chk && ix->metric == 1 ? c.take<uint32_t>(64) : nullptr;
     int* rs8 = rs8_on ? c.take<int>((size_t)round_up(N, 32)) : nullptr;
     // (the pilot writes the checksum's expectations when it runs; else the finish computes them)
@@ -1745,7 +1767,11 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
             if (timed) HIP_TRY(hipEventRecord(tev[0], st));
             if (use_s3) ix->n_scan3++;
             if ((q4 && !use_s3) || q4_8) ix->n_q4++;
-            if (i8_pass)
+            if (wide8) ix->n_wide++;
+            if (wide8)
+                HIP_TRY(launch_scan8w(prec, ix->metric, Xscan, rs8, md, Qt, q8lsl, q8scal, Gs, N, B, Bp, n_seg8, gl_s, gl_i,
+                                      gl_cap, segc, gthr, chkp, Bp, chk_l ? 1 : 0, st));
+            else if (i8_pass)
                 HIP_TRY(launch_scan8(prec, ix->metric, KP, Xscan, (const float*)rs8, md, Qt, q8lsl, q8scal, Gs, N, B,
                                      n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr,
                                      ix->scan_pace ? pace : nullptr, ix->pace_seq.fetch_add(1) + 1, lockstep,
@@ -1819,6 +1845,8 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
                 fa.chk_l = chk_l;
             }
             fa.qconst = fa.mu == q_mu && fa.dir == q_dir ? qconst : nullptr;  // (prep_queries' constants)
+            fa.seg_cnt = segc;
+            fa.seg_n = n_seg8;
             fa.split = fin_split; fa.sx_ek = fx_ek; fa.sx_ck = fx_ck; fa.sx_cr = fx_cr; fa.sx_n = fx_n; fa.done = done;
             HIP_TRY(launch_finish(ix->metric, KP, fa, B, st));
             if (timed) HIP_TRY(hipEventRecord(tev[2], st));

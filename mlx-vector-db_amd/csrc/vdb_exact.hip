@@ -397,11 +397,11 @@ __global__ void __launch_bounds__(64 * FW) finish_kernel(FinishArgs a) {
             }
         }
     }
-    const int64_t c = min((int64_t)a.gl_cnt[b], a.gl_cap);
+    const int64_t c = a.seg_cnt ? 0 : min((int64_t)a.gl_cnt[b], a.gl_cap);
 #ifdef VDB_STAMP
     if (threadIdx.x == 0) g_fin_stamps[b][7] = (unsigned long long)c;
 #endif
-    if (c > FIN_CAP) {
+    if (!a.seg_cnt && c > FIN_CAP) {
         if (tid == 0 && sp == 0) {
             const int pos = atomicAdd(a.flag_count, 1);
             a.flag_list[pos] = b;
@@ -417,13 +417,36 @@ __global__ void __launch_bounds__(64 * FW) finish_kernel(FinishArgs a) {
     // appended by workgroups that flushed against older, lower bounds, so this typically
     // leaves about KP entries.
     const uint32_t tkey = a.gthr[b];
-    __shared__ int s_n;
+    __shared__ int s_n, s_ovf;
     if (tid == 0) {
         s_ak = 0;
         s_akp = 0;
         s_n = 0;
+        s_ovf = 0;
     }
     __syncthreads();
+    // the wide int8 pass's lists: one segment of W8_CH slots per scan workgroup, wave wv taking
+    // segments wv, wv + FW, ...; a segment that overflowed sends the query to the exact path
+    for (int sg = a.seg_cnt ? wv : a.seg_n; sg < a.seg_n; sg += FIN_WAVES) {
+        const uint32_t cnt = a.seg_cnt[(size_t)b * a.seg_n + sg];
+        if (cnt > (uint32_t)W8_CH) {
+            if (lane == 0) s_ovf = 1;
+            continue;
+        }
+        const bool in = lane < (int)cnt;
+        const uint32_t key = in ? order_key(ls[(size_t)sg * W8_CH + lane]) : 0u;
+        const uint32_t row = in ? li[(size_t)sg * W8_CH + lane] : 0u;
+        const bool keep = in && key >= tkey;
+        const unsigned long long bm = __ballot(keep);
+        int base = 0;
+        if (lane == 0 && bm) base = atomicAdd(&s_n, __popcll(bm));
+        base = __shfl(base, 0, 64);
+        if (keep) {
+            const int pos = base + __popcll(bm & ((1ull << lane) - 1ull));
+            s_key[pos] = key;
+            s_row[pos] = row;
+        }
+    }
     for (int e0 = wv * 64; e0 < c; e0 += 64 * FIN_WAVES) {
         const int e = e0 + lane;
         const uint32_t key = e < c ? order_key(ls[e]) : 0u;
@@ -440,6 +463,14 @@ __global__ void __launch_bounds__(64 * FW) finish_kernel(FinishArgs a) {
         }
     }
     __syncthreads();
+    if (s_ovf) {  // (uniform: every thread returns)
+        if (tid == 0 && sp == 0) {
+            const int pos = atomicAdd(a.flag_count, 1);
+            a.flag_list[pos] = b;
+            if (a.overflow_count) atomicAdd(a.overflow_count, 1);
+        }
+        return;
+    }
     FIN_STAMP(1);
     const int n = s_n;
     // Select the KP best by (approx key desc, row asc): T = the KP-th largest key by an 8-bit

@@ -66,6 +66,14 @@ hipError_t launch_pilot8(int prec, int metric, const float* Xq, const float* rin
 int scan8_rows_per_step(int prec, int metric, bool q4 = false);
 int scan8_qb(int KP, bool q4 = false);  // queries per block of the int8 pass
 bool scan8_q4_ok(int G8, int prec);     // the 128-query shape fits (short rows)
+// the wide int8 pass (vdb_scan8w.hip): rows of 4 groups, batches of more than 256; W8_CH slots per
+// (workgroup, query) segment of the candidate lists
+constexpr int W8_CH = 32;
+bool scan8w_ok(int G8, int B);
+hipError_t launch_scan8w(int prec, int metric, const float* Xq, const int* rs8, const uint32_t* mask, const float* Qq,
+                         const float* lsl, const float* qscal, int G8, int64_t N, int B, int Bp, int n_seg,
+                         float* gl_s, uint32_t* gl_i, int64_t gl_cap, uint32_t* seg_cnt, const uint32_t* gthr,
+                         uint32_t* chkp, int chk_ld, int chk_l, hipStream_t st);
 hipError_t launch_scan8(int prec, int metric, int KP, const float* Xq, const float* rinit, const uint32_t* mask,
                         const float* Qq, const float* lsl, const float* qscal, int G8, int64_t N, int B,
                         int n_qblocks, int64_t n_steps, int n_wg, int spw, float* gl_s, uint32_t* gl_i,
@@ -248,6 +256,10 @@ struct FinishArgs {
     const uint32_t* chk_csum = nullptr;
     int chk_nw = 0, chk_ld = 0, chk_g8 = 0;
     bool chk_l = false;
+    // optional, the wide int8 pass (vdb_scan8w.hip): the lists are seg_n segments of W8_CH slots
+    // per query, one per scan workgroup, with counts seg_cnt [B][seg_n] (> W8_CH: overflowed)
+    const uint32_t* seg_cnt = nullptr;
+    int seg_n = 0;
 };
 hipError_t launch_finish(int metric, int KP, const FinishArgs& a, int B, hipStream_t st);
 

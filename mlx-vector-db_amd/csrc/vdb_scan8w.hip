@@ -1,0 +1,329 @@
+// vdb_scan8w.hip — the int8 candidate pass for short rows and large batches (round 6): the
+// "wide" shape.  Used for D <= 128 (4 groups of 32 dims) and B > 256 (C4: 10M x 128 L2 top-100,
+// B = 512, and every rank of its 8-way row-sharded run).
+//
+// Why a second shape.  scan8_kernel (vdb_scan8_kernel.h) gives each workgroup ONE 64-query block
+// and streams the corpus through registers, so C4's 8 query blocks read every row 8 times (from
+// L2 when they stay close), with the query block in LDS beside per-query candidate lists.  A
+// build whose steps end after the K-loop ran C4's scan in 0.94 ms against 1.61 ms for the real
+// kernel and 0.52 ms of MFMA time (profiles/r06_ab): the K-loop alone waited on its L2 stream,
+// and the epilogue (tile tests, LDS lists, compaction flags) took the rest.
+//
+// Here one workgroup of 8 waves holds ALL of up to 512 queries, one 64-query block per wave, and
+// each wave keeps its block's int8 tiles in REGISTERS for the whole launch (D = 128: 4 groups x 2
+// query tiles x 2 planes = 64 VGPRs).  The corpus is read from HBM exactly once: row tiles are
+// staged into a two-slot LDS ring by LDS-DMA (global_load_lds_dwordx4, no VGPR destination), every
+// wave reads each staged tile's A operand from LDS (4 ds_read_b128 per tile), and the slots turn
+// over behind one workgroup barrier per stage of NTILE row tiles (16 for one corpus plane, 8 for
+// two: 64 KiB of corpus per slot).  The loads of stage m + 1 are issued right after stage m's
+// barrier, so a whole stage of MFMA work (NTILE x 16 MFMAs per wave) covers their latency.
+//
+// No LDS candidate lists: the shared bound is the pilot's (gthr, fixed for the launch), so a row
+// whose (half-)score passes it goes straight to its query's global list.  Each (workgroup, query)
+// owns a fixed segment of W8_CH slots of that list (no global atomics): the position comes from
+// an LDS counter of the wave that owns the query; the segment counts go to seg_cnt [B][n_seg]
+// and the finish reads the segments (vdb_exact.hip, seg mode).  A segment that would overflow
+// makes the finish send its query to the exact path (correct, slow).  Row tiles are dealt to the
+// workgroups one at a time (tile t -> workgroup t mod n_seg), so a run of similar rows spreads over
+// all segments: with C4's pilot bound ~2 entries per segment and query are expected.
+//
+// Certificate invariant (vdb_exact.hip finish_kernel): every row not in its query's list scored
+// (this arithmetic) <= the final shared bound (gthr, the pilot's), so acut = max(a_KP, T) holds.
+// The checksum (vdb_scan8.hip) is unchanged: per lane the sums of every H (and L) accumulator of
+// the rows < N this workgroup scored, one word per (plane, query, workgroup).
+#include "vdb_scan8_kernel.h"
+
+namespace vdb {
+
+constexpr int W8_NW = 8;   // waves per workgroup: one 64-query block each (two per SIMD)
+constexpr int W8_QT = 2;   // query tiles per wave
+constexpr int W8_G = 4;    // 32-dim groups (Dp = 128)
+constexpr int W8_QB = W8_NW * 64;  // queries per workgroup
+
+template <int PREC>
+__host__ __device__ constexpr int w8_ntile() { return Planes8<PREC>::XPL == 2 ? 8 : 16; }
+template <int PREC, int METRIC>
+__host__ __device__ constexpr size_t w8_slot_bytes() {
+    return (size_t)w8_ntile<PREC>() * W8_G * Planes8<PREC>::XPL * 1024 + (METRIC == 1 ? (size_t)w8_ntile<PREC>() * 128 : 0);
+}
+template <int PREC, int METRIC>
+__host__ __device__ constexpr size_t w8_lds_bytes() { return 2 * w8_slot_bytes<PREC, METRIC>() + (size_t)W8_NW * 64 * 4; }
+
+// the LDS byte address of a __shared__ object (the LDS-DMA destination base is an address, M0)
+__device__ __forceinline__ uint32_t w8_lds_addr(const void* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+
+// One LDS-DMA load: lane l's 16 bytes at gsrc go to LDS byte lds + 16 l.  M0 is compiler-reserved,
+// so it is saved and restored inside the same statement; the asm is invisible to hipcc's wait
+// counting: the stage barrier below waits vmcnt(0) for it.
+template <bool NT>
+__device__ __forceinline__ void w8_glds(const void* gsrc, uint32_t lds) {
+    uint32_t keep;
+    if constexpr (NT)
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(gsrc), "s"(lds) : "memory");
+    else
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(gsrc), "s"(lds) : "memory");
+}
+
+template <int PREC, int METRIC, bool NT>
+__global__ void __launch_bounds__(64 * W8_NW, 1)
+scan8w_kernel(const float* __restrict__ Xq, const int* __restrict__ rs8, const uint32_t* __restrict__ mask,
+              const float* __restrict__ Qq, const float* __restrict__ lsl, const float* __restrict__ qscal, int64_t N,
+              int B, int Bp, float* __restrict__ gl_s, uint32_t* __restrict__ gl_i, int64_t gl_cap,
+              uint32_t* __restrict__ seg_cnt, const uint32_t* __restrict__ gthr, uint32_t* __restrict__ chkp, int chk_ld,
+              int chk_l) {
+    constexpr int G = W8_G, QT = W8_QT, NW = W8_NW;
+    constexpr int XPL = Planes8<PREC>::XPL, QPL = Planes8<PREC>::QPL;
+    constexpr bool HL = Planes8<PREC>::L;
+    constexpr int NTILE = w8_ntile<PREC>();
+    constexpr size_t TILE_B = (size_t)G * XPL * 1024;
+    constexpr size_t CORP_B = NTILE * TILE_B;
+    constexpr size_t SLOT_B = w8_slot_bytes<PREC, METRIC>();
+    constexpr size_t GSTEP = 8 * BLOCK_FLOATS, PLANE = 4 * BLOCK_FLOATS;
+    static_assert(XPL * NTILE * G == 8 * NW, "8 corpus loads per wave and stage");
+    extern __shared__ __attribute__((aligned(16))) char s_dyn[];
+    int* s_seg = (int*)(s_dyn + 2 * SLOT_B);  // [NW][64]: this workgroup's entries per query
+
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int w = blockIdx.x, n_seg = gridDim.x;
+    const int q0 = (blockIdx.y * NW + wv) * 64;  // this wave's queries q0 .. q0 + 63
+    const bool active = q0 < Bp;                 // (wave-uniform: a block past the padded batch only loads)
+    const int64_t T = (N + 31) >> 5;
+    const int64_t my_tiles = T > w ? (T - 1 - w) / n_seg + 1 : 0;
+    const int64_t n_stages = (my_tiles + NTILE - 1) / NTILE;
+    const uint32_t ring = w8_lds_addr(s_dyn);
+    const size_t XPLANE = corpus_plane(G);
+
+    s_seg[wv * 64 + lane] = 0;
+
+    // This wave's share of stage m's LDS-DMA loads into slot sl: 8 corpus blocks (one row tile,
+    // or two, all groups and planes) and, L2, one 1 KiB piece of the batch's integer start values
+    // (8 row tiles x 128 B, a per-lane source address each)
+    auto issue = [&](int64_t m, int sl) {
+        const uint32_t sbase = ring + (uint32_t)(sl * SLOT_B);
+#pragma unroll
+        for (int u = 0; u < (XPL == 1 ? 2 : 1); ++u) {
+            const int i = wv + NW * u;
+            const int64_t t = (m * NTILE + i) * n_seg + w;
+            if (t < T) {
+#pragma unroll
+                for (int g = 0; g < G; ++g)
+#pragma unroll
+                    for (int pl = 0; pl < XPL; ++pl)
+                        w8_glds<NT>(Xq + corpus_block((uint64_t)t, g, pl, G) + lane * 4,
+                                    sbase + (uint32_t)(((i * G + g) * XPL + pl) * 1024));
+            }
+        }
+        if constexpr (METRIC == 1) {
+            if (wv < NTILE / 8) {
+                const int i = wv * 8 + (lane >> 3);
+                int64_t t = (m * NTILE + i) * n_seg + w;
+                if (t >= T) t = 0;  // (a tile no wave scores: any valid source)
+                w8_glds<NT>(rs8 + t * 32 + (lane & 7) * 4, sbase + (uint32_t)(CORP_B + wv * 1024));
+            }
+        }
+    };
+
+    // the query block's tiles, whole, in registers; per query tile the pilot's bound (fixed for
+    // the launch) as the (half-)score threshold and its integer floor for the tile tests
+    const float uH = qscal[0], uL = qscal[1], invU = qscal[2];
+    f32x4 qr[G][QT][QPL];
+    float thf[QT];
+    int thc[QT];
+    uint32_t ckh[QT], ckl[QT];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+        const int q = q0 + qt * 32 + (lane & 31);
+        const bool ok = active && q < B;
+        const float th = ok ? key_to_float(gthr[q]) : INFINITY;
+        thf[qt] = METRIC == 0 ? th : 0.5f * th;
+        thc[qt] = ok ? h_floor(thf[qt], lsl[q], invU) : INT_MAX;
+        ckh[qt] = ckl[qt] = 0u;
+    }
+    if (active) {
+        const float* qs = Qq + s2_blk((uint64_t)(q0 / 32), 0, G + QG_EXTRA) + lane * 4;
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+                for (int pl = 0; pl < QPL; ++pl) qr[g][qt][pl] = *(const f32x4*)(qs + g * GSTEP + pl * PLANE + qt * BLOCK_FLOATS);
+    }
+    if (n_stages > 0) issue(0, 0);
+
+    for (int64_t m = 0; m < n_stages; ++m) {
+        // this wave's loads of stage m have landed (vmcnt 0: nothing younger is in flight yet);
+        // after the barrier every wave's have, and every wave is done with stage m - 1, whose
+        // slot stage m + 1 now refills
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (m + 1 < n_stages) issue(m + 1, (int)((m + 1) & 1));
+        if (!active) continue;
+        const char* slot = s_dyn + (size_t)(m & 1) * SLOT_B;
+        for (int i = 0; i < NTILE; ++i) {
+            const int64_t t = (m * NTILE + i) * n_seg + w;
+            if (t >= T) break;
+            f32x4 xr[G][1][XPL];
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+#pragma unroll
+                for (int pl = 0; pl < XPL; ++pl)
+                    xr[g][0][pl] = *(const f32x4*)(slot + (size_t)i * TILE_B + (size_t)((g * XPL + pl) * 1024) + lane * 16);
+            i32x16 aH[1][QT], aL[1][QT];
+            {
+                i32x16 init;
+#pragma unroll
+                for (int v = 0; v < 16; ++v) init[v] = 0;
+                if constexpr (METRIC == 1) {
+                    // lane half h holds rows 32 t + 8 a + 4 h + b of its accumulator registers 4 a + b
+#pragma unroll
+                    for (int a = 0; a < 4; ++a) {
+                        const i32x4 r4 = *(const i32x4*)(slot + CORP_B + (size_t)i * 128 + (size_t)(8 * a + 4 * (lane >> 5)) * 4);
+#pragma unroll
+                        for (int b2 = 0; b2 < 4; ++b2) init[4 * a + b2] = r4[b2];
+                    }
+                }
+#pragma unroll
+                for (int qt = 0; qt < QT; ++qt) {
+                    aH[0][qt] = init;
+#pragma unroll
+                    for (int v = 0; v < 16; ++v) aL[0][qt][v] = 0;
+                }
+            }
+#pragma unroll
+            for (int g = 0; g < G; ++g) group_mfma8<PREC, 1, QT>(xr[g], qr[g], aH, aL);
+
+            // ---- epilogue: the tile tests (H only, minus the L term's slack), the checksum ----
+            uint32_t todo = 0;
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt)
+                todo |= __builtin_amdgcn_ballot_w64(imax16(aH[0][qt]) > thc[qt]) != 0ull ? 1u << qt : 0u;
+            if (chkp) {
+                if ((t + 1) * 32 <= N) {
+#pragma unroll
+                    for (int qt = 0; qt < QT; ++qt) ckh[qt] += hsum16(aH[0][qt]);
+                    if constexpr (HL) {
+                        if (chk_l) {
+#pragma unroll
+                            for (int qt = 0; qt < QT; ++qt) ckl[qt] += hsum16(aL[0][qt]);
+                        }
+                    }
+                } else {
+#pragma unroll
+                    for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+                        for (int v = 0; v < 16; ++v) {
+                            const int64_t row = t * 32 + 8 * (v >> 2) + 4 * (lane >> 5) + (v & 3);
+                            if (row < N) {
+                                ckh[qt] += (uint32_t)aH[0][qt][v];
+                                if (HL && chk_l) ckl[qt] += (uint32_t)aL[0][qt][v];
+                            }
+                        }
+                }
+            }
+            // ---- the rare insertions: straight into this (workgroup, query) segment ----
+            while (todo != 0u) {
+                const int qt = __builtin_amdgcn_readfirstlane(__builtin_ctz(todo));
+                todo &= todo - 1u;
+                const i32x16 h = qt == 0 ? aH[0][0] : aH[0][QT - 1];
+                i32x16 l;
+                if constexpr (HL) l = qt == 0 ? aL[0][0] : aL[0][QT - 1];
+                const int ql = qt * 32 + (lane & 31);
+                const int qg = q0 + ql;
+                const float th = qt == 0 ? thf[0] : thf[QT - 1];
+                const uint32_t cand = qg < B ? tile_valid16(mask, t, N, lane) : 0u;
+                float sv[16];
+                uint32_t pm = 0;
+#pragma unroll
+                for (int v = 0; v < 16; ++v) {
+                    sv[v] = HL ? fmaf((float)h[v], uH, (float)l[v] * uL) : (float)h[v] * uH;
+                    pm |= (sv[v] > th ? 1u : 0u) << v;
+                }
+                pm &= cand;
+                int pos = 0;
+                if (pm != 0u) pos = atomicAdd(&s_seg[wv * 64 + ql], __builtin_popcount(pm));
+                const uint32_t rb = (uint32_t)(t * 32) + 4u * (uint32_t)(lane >> 5);
+                float* ls = gl_s + (size_t)qg * gl_cap + (size_t)w * W8_CH;
+                uint32_t* li = gl_i + (size_t)qg * gl_cap + (size_t)w * W8_CH;
+                while (pm != 0u) {
+                    const int v = __builtin_ctz(pm);
+                    pm &= pm - 1u;
+                    float a_ = sv[0];
+#pragma unroll
+                    for (int u = 1; u < 16; ++u) a_ = v == u ? sv[u] : a_;
+                    if (pos < W8_CH) {
+                        ls[pos] = METRIC == 0 ? a_ : 2.0f * a_;
+                        li[pos] = rb + (uint32_t)((v & 3) + 8 * (v >> 2));
+                    }
+                    ++pos;
+                }
+            }
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!active) return;
+    // this workgroup's entries per query (the finish's segment counts; > W8_CH = overflowed)
+    if (q0 + lane < B) seg_cnt[(size_t)(q0 + lane) * n_seg + w] = (uint32_t)s_seg[wv * 64 + lane];
+    // the checksum's partial sums: the tile's two row halves (lanes l, l + 32), one word per
+    // (plane, query, workgroup)
+    if (chkp) {
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) {
+            const uint32_t hsum = ckh[qt] + (uint32_t)__shfl_xor((int)ckh[qt], 32, 64);
+            const uint32_t lsum = ckl[qt] + (uint32_t)__shfl_xor((int)ckl[qt], 32, 64);
+            const int q = q0 + qt * 32 + lane;
+            if (lane < 32 && q < B) {
+                chkp[(size_t)q * n_seg + w] = hsum;
+                if (HL && chk_l) chkp[((size_t)chk_ld + q) * n_seg + w] = lsum;
+            }
+        }
+    }
+}
+
+bool scan8w_ok(int G8, int B) { return G8 == W8_G && B > 256; }
+int scan8w_qblocks(int B) { return (B + W8_QB - 1) / W8_QB; }
+
+template <int P, int M, bool NT>
+static hipError_t scan8w_launch(const float* Xq, const int* rs8, const uint32_t* mask, const float* Qq, const float* lsl,
+                                const float* qscal, int64_t N, int B, int Bp, int n_seg, float* gl_s, uint32_t* gl_i,
+                                int64_t gl_cap, uint32_t* seg_cnt, const uint32_t* gthr, uint32_t* chkp, int chk_ld,
+                                int chk_l, hipStream_t st) {
+    auto k = scan8w_kernel<P, M, NT>;
+    constexpr size_t lds = w8_lds_bytes<P, M>();
+    static_assert(lds <= 160 * 1024, "LDS");
+    static std::atomic<bool> lds_set{false};
+    if (!lds_set.load()) {
+        const hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        lds_set = true;
+    }
+    hipLaunchKernelGGL(k, dim3((unsigned)n_seg, (unsigned)scan8w_qblocks(B)), dim3(64 * W8_NW), lds, st, Xq, rs8, mask, Qq,
+                       lsl, qscal, N, B, Bp, gl_s, gl_i, gl_cap, seg_cnt, gthr, chkp, chk_ld, chk_l);
+    return hipGetLastError();
+}
+
+hipError_t launch_scan8w(int prec, int metric, const float* Xq, const int* rs8, const uint32_t* mask, const float* Qq,
+                         const float* lsl, const float* qscal, int G8, int64_t N, int B, int Bp, int n_seg,
+                         float* gl_s, uint32_t* gl_i, int64_t gl_cap, uint32_t* seg_cnt, const uint32_t* gthr,
+                         uint32_t* chkp, int chk_ld, int chk_l, hipStream_t st) {
+    if (!scan8w_ok(G8, B) || n_seg <= 0 || gl_cap != (int64_t)n_seg * W8_CH || (metric == 1 && !rs8))
+        return hipErrorInvalidValue;
+    // the corpus is read once per query block: non-temporal with one (C4), default policy with
+    // several (they share each tile through the XCD's L2)
+    const bool nt = scan8w_qblocks(B) == 1;
+#define W8_CASE(P, M)                                                                                                 \
+    if (prec == P && metric == M)                                                                                     \
+        return nt ? scan8w_launch<P, M, true>(Xq, rs8, mask, Qq, lsl, qscal, N, B, Bp, n_seg, gl_s, gl_i, gl_cap,     \
+                                              seg_cnt, gthr, chkp, chk_ld, chk_l, st)                                 \
+                  : scan8w_launch<P, M, false>(Xq, rs8, mask, Qq, lsl, qscal, N, B, Bp, n_seg, gl_s, gl_i, gl_cap,    \
+                                               seg_cnt, gthr, chkp, chk_ld, chk_l, st);
+    W8_CASE(PREC_I8Q, 1) W8_CASE(PREC_I8X3, 1) W8_CASE(PREC_I8, 1)
+    W8_CASE(PREC_I8Q, 0) W8_CASE(PREC_I8X3, 0) W8_CASE(PREC_I8, 0)
+#undef W8_CASE
+    return hipErrorInvalidValue;
+}
+
+}  // namespace vdb
