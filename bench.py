@@ -134,21 +134,29 @@ def cpu_baseline(V, Q, k, metric="cosine", budget_s=10.0):
     res = {"unit": "queries/s", "cores": threads, "kind": "port"}
     parts = []
     batched_qps = 0.0
-    if metric == "cosine":
-        Bs = int(max(1, min(B, (64 << 20) // max(N, 1))))
+    if True:
+        # cosine: the reference's batched module; L2 (no batched L2 in the reference): the store's
+        # per-query L2 arithmetic over corpus chunks of 1 M rows with a running top-k merge
+        # instead of the full argsort, Bs queries at a time
+        Bs = int(max(1, min(B, (64 << 20) // max(N, 1)))) if metric == "cosine" else int(max(1, min(B, 2)))
         bt = []
         t0 = time.perf_counter()
         j = 0
         while not bt or (time.perf_counter() - t0 < budget_s and len(bt) < 50):
             t1 = time.perf_counter()
-            ref_cpu.reference_batch_search(Q[(j * Bs) % B:(j * Bs) % B + Bs], V, k)
+            qs = Q[(j * Bs) % B:(j * Bs) % B + Bs]
+            if metric == "cosine":
+                ref_cpu.reference_batch_search(qs, V, k)
+            else:
+                ref_cpu.reference_l2_batch_chunked(qs, V, k)
             bt.append(time.perf_counter() - t1)
             j += 1
         batched_qps = Bs / float(np.mean(bt))
         res["batched"] = {"qps": batched_qps, "p50_ms_per_batch": float(np.median(bt)) * 1e3, "batches": len(bt),
                           "queries_per_batch": Bs}
         parts.append(f"(ii) {len(bt)} batch(es) of {Bs} of the {B} queries x the full {N}x{V.shape[1]} corpus "
-                     f"({sum(bt):.1f} s)")
+                     f"({'batched cosine' if metric == 'cosine' else 'L2 in 1 M-row chunks, top-k merge'}, "
+                     f"{sum(bt):.1f} s)")
     qt = []
     t0 = time.perf_counter()
     i = 0
@@ -445,22 +453,14 @@ def main():
     ap.add_argument("--n-wg", type=int, default=None, help="candidate-pass workgroups (tuning)")
     ap.add_argument("--scan-sync", type=int, default=None,
                     help="candidate-pass step end: 1 lockstep barrier, 2 flag-gated rounds (tuning; default by D)")
-    ap.add_argument("--gate-div", type=int, default=None, help="gated fallback: n_cu / d workgroups (tuning)")
-    ap.add_argument("--scan-qring", type=int, default=None, help="1: query operand through an LDS ring (tuning)")
     ap.add_argument("--scan-qlds", type=int, default=None, help="0: query block never in LDS (tuning)")
     ap.add_argument("--scan-q4", type=int, default=None, help="128-query shape: -1 auto, 0 off, 1 on (tuning)")
     ap.add_argument("--scan-wide", type=int, default=None,
                     help="wide int8 pass (D <= 128, B > 256): -1 auto, 0 off, 1 on (tuning)")
-    ap.add_argument("--scan-realign", type=int, default=None,
-                    help="flag-gated step ends: a workgroup barrier every n steps (tuning)")
     ap.add_argument("--dir-bound", type=int, default=None,
                     help="bf16 certificate: 1 residual bound along the rows' mean direction (default), 0 Cauchy-Schwarz")
-    ap.add_argument("--scan-publish", type=int, default=None,
-                    help="split pass slot publishing: -1 auto, 0 off, 1 on (tuning)")
     ap.add_argument("--pilot-tiles", type=int, default=None, help="row tiles sampled by the pilot bound (tuning)")
     ap.add_argument("--margin", type=int, default=None, help="candidates beyond k (tuning; default per precision)")
-    ap.add_argument("--pilot-fused", type=int, default=None, help="split pass: 1 the scan derives the pilot bound, "
-                    "0 a separate bound kernel (tuning)")
     ap.add_argument("--pilot-rank", type=int, default=None, help="rank of the pilot bound (tuning; default: Poisson rule)")
     ap.add_argument("--k", type=int, default=None, help="tuning: the config at another k (not the config's line)")
     ap.add_argument("--finish-split", type=int, default=None, help="workgroups per query in the finish (tuning)")
@@ -469,8 +469,6 @@ def main():
                     help="one GPU: P queries per batch with 300 rows the int8 pass cannot separate (re-pass test)")
     ap.add_argument("--device-repass", type=int, default=None,
                     help="device re-pass of uncertified queries: -1 auto (armed after a fallback), 0 off, 1 always")
-    ap.add_argument("--scan-pace", type=int, default=None, help="int8 pass: 1 pace the query blocks of a row range, "
-                    "0 off (default; tuning)")
     ap.add_argument("--scan-checksum", type=int, default=None,
                     help="int8 pass checksum checked by the finish: 1 on (default), 0 off (A/B of its cost)")
     ap.add_argument("--rows", type=int, default=None, help="override the corpus rows (exploration only)")
@@ -535,7 +533,7 @@ def main():
             if rank == 0:
                 rec[key] = {k_: sub[k_] for k_ in ("value", "unit", "n_gpus", "steps", "ms_per_step", "p50_ms",
                                                    "scaling", "dtype", "config", "fallback_queries_timed",
-                                                   "fallback_queries_total")}
+                                                   "fallback_queries_total", "cpu_baseline") if k_ in sub}
                 rec[key]["roofline"] = {
                     k_: sub["roofline"][k_] for k_ in ("bound", "achieved", "peak", "unit", "frac", "traffic",
                                                        "traffic_source", "avg_launch_ms", "precision", "basis",
@@ -553,6 +551,8 @@ def bench_brute(cfg, args, world, rank, local, dev, primary=True):
     elsewhere).  primary=False: the compact secondary line (no CPU baseline / serving)."""
     rec = None
     N, D, B, k, metric, desc = CONFIGS[cfg]
+    if rank == 0:  # progress on stderr (a long default run stays visibly alive)
+        print(f"bench: {cfg} start", file=sys.stderr, flush=True)
     if args.k is not None:  # tuning: the config's rows and batch at another k (not a bench line)
         k = int(args.k)
         desc = f"{desc} [k = {k}]"
@@ -563,7 +563,8 @@ def bench_brute(cfg, args, world, rank, local, dev, primary=True):
     n_local = hi - lo
 
     # ---- data: this rank's shard of the corpus, replicated queries -------------------
-    keep_host = primary and world == 1 and rank == 0 and not args.no_cpu_baseline
+    # (every record at N = 1 carries its CPU baseline, VERDICT r5 #4: sub-records on a shorter budget)
+    keep_host = world == 1 and rank == 0 and not args.no_cpu_baseline
     ix = _vdb.NativeIndex(D, metric, local, precision=args.precision)
     if args.scan_variant is not None:
         ix.set_param("scan_variant" if args.precision == "fp32" else "scan_variant_bf16x3", args.scan_variant)
@@ -573,12 +574,6 @@ def bench_brute(cfg, args, world, rank, local, dev, primary=True):
         ix.set_param("scan_sync", args.scan_sync)
     if args.pilot_tiles is not None:
         ix.set_param("pilot_tiles", args.pilot_tiles)
-    if args.scan_realign is not None:
-        ix.set_param("scan_realign", args.scan_realign)
-    if args.gate_div is not None:
-        ix.set_param("gate_div", args.gate_div)
-    if args.scan_qring is not None:
-        ix.set_param("scan_qring", args.scan_qring)
     if args.scan_qlds is not None:
         ix.set_param("scan_qlds", args.scan_qlds)
     if args.scan_q4 is not None:
@@ -587,16 +582,10 @@ def bench_brute(cfg, args, world, rank, local, dev, primary=True):
         ix.set_param("scan_wide", args.scan_wide)
     if args.dir_bound is not None:
         ix.set_param("dir_bound", args.dir_bound)
-    if args.scan_publish is not None:
-        ix.set_param("scan_publish", args.scan_publish)
     if args.margin is not None:
         ix.set_param("margin", args.margin)
-    if args.pilot_fused is not None:
-        ix.set_param("pilot_fused", args.pilot_fused)
     if args.pilot_rank is not None:
         ix.set_param("pilot_rank", args.pilot_rank)
-    if args.scan_pace is not None:
-        ix.set_param("scan_pace", args.scan_pace)
     if args.finish_split is not None:
         ix.set_param("finish_split", args.finish_split)
     if args.device_repass is not None:
@@ -816,9 +805,10 @@ def bench_brute(cfg, args, world, rank, local, dev, primary=True):
         if keep_host:
             V = np.concatenate(host_parts) if len(host_parts) > 1 else host_parts[0]
             del host_parts
-            if cfg in ("c1", "c2") and not args.no_serving:
+            if primary and cfg in ("c1", "c2") and not args.no_serving:
                 rec["serving"] = serving_stats(V, metric, k, local)
-            rec["cpu_baseline"] = cpu_baseline(V, Q, k, metric)
+            print(f"bench: {cfg} cpu baseline", file=sys.stderr, flush=True)
+            rec["cpu_baseline"] = cpu_baseline(V, Q, k, metric, budget_s=10.0 if primary else 6.0)
     ix.close()
     return rec
 

@@ -175,22 +175,9 @@ struct vdb_index {
     int64_t scan_sync = 0;        // scan step end: 0 auto, 1 lockstep barrier, 2 flag-gated rounds
     int64_t no_fallback = 0;      // diagnostics only: skip the exact fallback (results may be wrong)
     int64_t pilot_rank_override = 0;  // tuning: rank of the pilot bound (0 = the Poisson rule)
-    // split pass: 1 = the scan's prologue derives the pilot bound (one launch fewer), 0 = the
-    // bound kernel.  Measured (profiles/r02_ab, C2): the prologue costs the scan ~25 us (bf16)
-    // / ~30 us (bf16x3) against ~5 us for the kernel, so 0 is the default.
-    int64_t pilot_fused = 0;
-    int64_t scan_publish = -1;    // split pass slot publishing: -1 auto (= off since round 3), 0 off, 1 on
     bool no_dir_bound = false;    // diagnostics: PREC_BF16 certificate with Cauchy-Schwarz only
-    int64_t scan_realign = 0;     // flag-gated step ends: a workgroup barrier every n steps (0 none)
-    int64_t scan_qring = 0;       // split pass, global query operand: query chunks through an LDS ring
-    int64_t gate_div = 1;         // gated exact fallback: n_cu / gate_div row ranges, one query slot each when > 1
     int64_t finish_split = 1;  // workgroups per query in the finish kernel (tuning)
-    int64_t scan3 = 0;         // large-batch candidate pass: -1 auto (B >= 128), 0 off, 1 always (vdb_scan3_kernel.h)
     int64_t scan_qlds = -1;    // split pass: query block in LDS when it fits (-1 auto), 0 never
-    // int8 pass: pace the query blocks of a row range (vdb_scan8_kernel.h), opt-in: it held C4's
-    // 8 blocks within 5 steps (from 26) and ran the scan at 4.99 ms against 2.90 without
-    // (the range at its slowest block's speed, the prefetch drained per sleep; profiles/r03_i8/pace)
-    bool scan_pace = false;
     // the finish's I8 refinement (i8_refine): -1 auto = rows of kRefineMinDp dims or more (C3 +6%,
     // C2 neutral, C6 -1%: shorter rows rerank cheaply; profiles/r04_mx1); 0 off; 1 on
     int i8_refine = -1;
@@ -212,13 +199,12 @@ struct vdb_index {
     // search or more late (h_totals), and turns I8Q off by the same 1/8 rule
     std::atomic<bool> last_i8q{false};
     std::atomic<int> last_i8q_b{0};
-    std::atomic<uint32_t> pace_seq{0};  // launch tag of the pacing counters
     int64_t scan_q4 = -1;      // split pass 128-query shape (D <= 128, KP = 128, B >= 256): -1 auto, 0 off, 1 on
     // the wide int8 pass (vdb_scan8w.hip: rows of 4 groups, B > 256): -1 auto (from kWideMinRows
     // rows), 0 off, 1 at any row count
     int64_t scan_wide = -1;
     // stats
-    std::atomic<int64_t> n_searches{0}, n_queries{0}, n_fallback{0}, n_overflow{0}, n_incons{0}, n_repass{0}, n_scan3{0}, n_q4{0};
+    std::atomic<int64_t> n_searches{0}, n_queries{0}, n_fallback{0}, n_overflow{0}, n_incons{0}, n_repass{0}, n_q4{0};
     std::atomic<int64_t> n_wide{0};  // searches through the wide int8 pass
     std::atomic<int64_t> n_xs_builds{0};  // lazy builds of the split copy (ensure_xs)
     std::atomic<int64_t> n_by_prec[N_PREC] = {{0}, {0}, {0}, {0}, {0}, {0}};  // candidate passes per PREC_* (VDB_PREC_AUTO's choices)
@@ -622,9 +608,9 @@ int run_exact(vdb_index* ix, Workspace* w, const float* Qd, const double* qn64, 
     const int KE = std::max(32, next_pow2(k));
     const int64_t N = ix->count;
     const bool gated = qcount_dev != nullptr;
-    // ~2 workgroups per CU of rows (gated: 1 / gate_div, since an empty gated launch still has to
-    // find free CUs beside the next batch's scan), at least 64 rows per wave
-    const int64_t wg_target = gated ? std::max<int64_t>(1, ix->n_cu / std::max<int64_t>(1, ix->gate_div)) : 2 * ix->n_cu;
+    // ~2 workgroups per CU of rows (gated: 1, since an empty gated launch still has to find free
+    // CUs beside the next batch's scan), at least 64 rows per wave
+    const int64_t wg_target = gated ? std::max<int64_t>(1, ix->n_cu) : 2 * ix->n_cu;
     int n_wg = (int)std::min<int64_t>(wg_target, std::max<int64_t>(1, N / 256));
     const int64_t rpw = (N + n_wg - 1) / n_wg;
     n_wg = (int)((N + rpw - 1) / rpw);
@@ -641,8 +627,7 @@ int run_exact(vdb_index* ix, Workspace* w, const float* Qd, const double* qn64, 
     if (gated && done_dev) {  // one launch: the last workgroup per query merges and writes (ExactTail)
         const ExactTail tail{done_dev, mk, mi, k, index_offset, out_s, out_i, out_k, row_ids, host_totals};
         HIP_TRY(launch_exact_scan(ix->metric, KE, Qd, qn64, qlist_dev, nq, ix->X, ix->G, ix->dim, ix->nrm64, mask_dev,
-                                  N, n_wg, rpw, lk, li, st, qcount_dev, ovf_dev, ix->d_totals, &tail,
-                                  ix->gate_div > 1 ? 1 : 4));
+                                  N, n_wg, rpw, lk, li, st, qcount_dev, ovf_dev, ix->d_totals, &tail, 4));
         return VDB_OK;
     }
     HIP_TRY(launch_exact_scan(ix->metric, KE, Qd, qn64, qlist_dev, nq, ix->X, ix->G, ix->dim, ix->nrm64, mask_dev, N,
@@ -692,11 +677,6 @@ int32_t vdb_index_create(int32_t dim, int32_t metric, int32_t device, vdb_index*
     ix->Dp = (int)round_up(dim, 64);  // G = Dp/8 is a multiple of the scan prefetch depth
     ix->G = ix->Dp / GROUP_DIMS;
     ix->n_cu = prop.multiProcessorCount;
-    // start value of the scan_qring parameter (A/B runs of whole test suites)
-    if (const char* qr = std::getenv("VDB_SCAN_QRING")) ix->scan_qring = std::atoi(qr) != 0;
-    if (const char* gd = std::getenv("VDB_GATE_DIV")) ix->gate_div = std::min(64, std::max(1, std::atoi(gd)));
-    // start value of the scan3 parameter (A/B runs of whole suites): -1 auto, 0 off, 1 always
-    if (const char* s3 = std::getenv("VDB_SCAN3")) ix->scan3 = std::min(1, std::max(-1, std::atoi(s3)));
     if (const char* q4 = std::getenv("VDB_SCAN_Q4")) ix->scan_q4 = std::min(1, std::max(-1, std::atoi(q4)));
     if (const char* a8 = std::getenv("VDB_AUTO_I8")) ix->auto_i8 = std::atoi(a8) != 0;
     hipError_t e = hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking);
@@ -852,9 +832,6 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
     } else if (n == "finish_split") {
         if (value < 1 || value > 8) return set_error(VDB_ERR_INVALID, "finish_split must be in [1, 8]");
         ix->finish_split = value;
-    } else if (n == "scan_pace") {
-        if (value < 0 || value > 1) return set_error(VDB_ERR_INVALID, "scan_pace must be 0 or 1");
-        ix->scan_pace = value != 0;
     } else if (n == "scan_qlds") {
         if (value < -1 || value > 2) return set_error(VDB_ERR_INVALID, "scan_qlds must be -1 (auto), 0, 1 or 2");
         ix->scan_qlds = value;
@@ -864,25 +841,8 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
     } else if (n == "scan_q4") {
         if (value < -1 || value > 1) return set_error(VDB_ERR_INVALID, "scan_q4 must be -1, 0 or 1");
         ix->scan_q4 = value;
-    } else if (n == "scan3") {
-        if (value < -1 || value > 1) return set_error(VDB_ERR_INVALID, "scan3 must be -1, 0 or 1");
-        ix->scan3 = value;
-    } else if (n == "gate_div") {
-        if (value < 1 || value > 64) return set_error(VDB_ERR_INVALID, "gate_div must be in [1, 64]");
-        ix->gate_div = value;
-    } else if (n == "scan_qring") {
-        if (value < 0 || value > 1) return set_error(VDB_ERR_INVALID, "scan_qring must be 0 or 1");
-        ix->scan_qring = value;
-    } else if (n == "scan_realign") {
-        if (value < 0 || value > 255) return set_error(VDB_ERR_INVALID, "scan_realign must be in [0, 255]");
-        ix->scan_realign = value;
     } else if (n == "dir_bound") {
         ix->no_dir_bound = value == 0;
-    } else if (n == "scan_publish") {
-        if (value < -1 || value > 1) return set_error(VDB_ERR_INVALID, "scan_publish must be -1, 0 or 1");
-        ix->scan_publish = value;
-    } else if (n == "pilot_fused") {
-        ix->pilot_fused = value != 0;
     } else if (n == "i8_refine") {
         if (value < -1 || value > 1) return set_error(VDB_ERR_INVALID, "i8_refine must be -1, 0 or 1");
         ix->i8_refine = (int)value;
@@ -953,7 +913,6 @@ int32_t vdb_index_get_stat(const vdb_index* cix, const char* name, int64_t* valu
     else if (n == "queries") *value = ix->n_queries.load();
     else if (n == "fallback_queries") *value = ix->n_fallback.load() + (int64_t)dt[0];
     else if (n == "repass_queries") *value = ix->n_repass.load() + (int64_t)dt[3];  // + device re-passes
-    else if (n == "searches_scan3") *value = ix->n_scan3.load();
     else if (n == "searches_q4") *value = ix->n_q4.load();
     else if (n == "searches_wide") *value = ix->n_wide.load();
     else if (n == "auto_hold") *value = ix->auto_hold.load();
@@ -1484,27 +1443,22 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     // each row range is re-read from L2 by half as many workgroups (C4: 8 -> 4 blocks)
     const bool q4 = split_pass && !exact_all && !opt.gate && KP == 128 && B >= 256 && Gs <= 8 &&
                     (ix->scan_q4 == 1 || (ix->scan_q4 < 0));
-    // The int8 pass's 128-query shape (vdb_scan8_kernel.h S8_ONE4): the same rule for short rows
-    // (D <= 128), KP = 128, batches of >= 256 (C4: I8X3, 8 -> 4 query blocks per row range)
-    // Opt-in (scan_q4 = 1): C4 ran 2.91 -> 3.08 ms with it (profiles/r04_q48, same box).
-    const bool q4_8 = i8_pass && !exact_all && !opt.gate && KP == 128 && B >= 256 && scan8_q4_ok(Gs, prec) &&
-                      ix->scan_q4 == 1;
     // The wide int8 pass (vdb_scan8w.hip): rows of 4 groups (D <= 128) and batches of more than 256
     // (C4, and each rank of its row-sharded run): all queries of a 512-query block in one
     // workgroup, the corpus staged once through LDS; one workgroup per CU, tiles dealt round-robin
     const int64_t n_tiles_all = round_up(N, 32) / 32;
-    const bool wide8 = i8_pass && !exact_all && !opt.gate && !q4_8 && scan8w_ok(Gs, B) && N > 0 &&
+    const bool wide8 = i8_pass && !exact_all && !opt.gate && scan8w_ok(Gs, B) && N > 0 &&
                        (ix->scan_wide == 1 || (ix->scan_wide < 0 && N >= kWideMinRows));
     const int n_seg8 = wide8 ? (int)std::min<int64_t>(FIN_SEG_MAX, round_up(std::min<int64_t>(ix->n_cu, n_tiles_all), 8)) : 0;
     // query rows per candidate-pass block: the int8 pass keeps 64 at KP = 256 (KW = 64 kept per
     // workgroup, vdb_scan8_kernel.h), the split pass 32 there
-    const int QB = q4 ? 128 : i8_pass ? scan8_qb(KP, q4_8) : KP == 256 ? 32 : 64;
+    const int QB = q4 ? 128 : i8_pass ? 64 : KP == 256 ? 32 : 64;
     const int QB_pilot = i8_pass ? 64 : KP == 256 ? 32 : 64;  // the pilot's own query blocks (instantiations)
     const int Bp = (int)round_up(B, 128);  // whole query super tiles (tiled layout)
     const int n_qblocks = (B + QB - 1) / QB;
     int variant = split_pass || i8_pass ? 0 : (int)ix->scan_variant;
     if (!split_pass && !i8_pass && !scan_variant_ok(prec, variant, Gs)) variant = 0;  // e.g. PX=8 needs Dp % 128 == 0
-    const int64_t step_rows = i8_pass ? scan8_rows_per_step(prec, ix->metric, q4_8)
+    const int64_t step_rows = i8_pass ? scan8_rows_per_step(prec, ix->metric)
                               : split_pass ? scan2_rows_per_step(q4) : scan_rows_per_step(prec, variant);
     const int64_t n_steps = std::max<int64_t>(1, round_up(N, step_rows) / step_rows);
     // one 4-wave workgroup per CU (1 wave per SIMD, all of its 512 registers):
@@ -1521,24 +1475,6 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     // under the others' loads (C2 366 -> 384 K QPS, C3 365 -> 401 K with its scan 0.576 -> 0.487 ms,
     // profiles/r04_ab/sync, same box).
     const int lockstep = ix->scan_sync == 0 ? (!i8_pass && ix->Dp > 128) : ix->scan_sync == 1;
-    // Slot publishing (shared bound from the workgroups' own bests, vdb_scan2.hip): round 2 found it
-    // paying off over many steps (C4: 610 per workgroup) and not over few (C2: 8, profiles/r02_ab/).
-    // Measured again in round 3 (profiles/r03_ab/publish): off is as fast or faster everywhere --
-    // C6 (10M x 128, one 64-query block, 77 steps per workgroup: 256 workgroups' same-address slot
-    // atomics for the same 64 queries) 0.92 -> 0.47 ms, C2 0.30 -> 0.29, C3 / C4 equal -- so auto
-    // is off (the knob stays for A/B)
-    const int publish = (ix->scan_publish >= 0 ? (int)ix->scan_publish : 0) | (int)(ix->scan_realign << 8);
-    // The large-batch pass (vdb_scan3_kernel.h): 256 queries per workgroup sharing each row
-    // group through LDS.  Auto: B >= 128 and enough workgroups per query block that no
-    // workgroup is likely to hold more than its KW = 32 best of a query's top k.
-    const int n_qb3 = (B + 255) / 256;
-    const int64_t steps3 = std::max<int64_t>(1, round_up(N, scan3_rows_per_step()) / scan3_rows_per_step());
-    const int wg3_target = ix->n_wg_override > 0 ? (int)ix->n_wg_override : std::max(1, ix->n_cu / n_qb3);
-    const int spw3 = (int)std::max<int64_t>(1, (steps3 + wg3_target - 1) / wg3_target);
-    const int n_wg3 = (int)((steps3 + spw3 - 1) / spw3);
-    // (a gated sub-search -- the device re-pass -- runs the gated 64-query shapes: ADVICE r4)
-    const bool use_s3 = split_pass && !exact_all && !opt.gate &&
-                        (ix->scan3 == 1 || (ix->scan3 < 0 && B >= 128 && n_wg3 >= std::max(8, 4 * k / 32)));
 
     Workspace* w = acquire_ws(ix, st, own_stream);
     if (own_stream) {
@@ -1583,7 +1519,6 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     bytes += i8_refine ? (size_t)Bp * (ix->Dp + 1) * 4 + 512 : 0;  // query residuals [Bp][Dp] + qerr2 [Bp]
     const int R_rep = std::min(B, kRepassDev);                // device re-pass: gathered queries + results
     bytes += mem == VDB_MEM_DEVICE ? (size_t)R_rep * (D * 4 + (size_t)k * 20) + 1024 : 0;
-    bytes += ((size_t)(n_wg + 7) / 8 * 8 * n_qblocks + 64) * 4; // int8 pass: pacing counters
     // the int8 pass's checksum: partial sums [2][n_wg8][Bp], expected values [Bp][2], L2 start sum
     const bool chk = i8_pass && !exact_all && ix->scan_checksum && ix->d_csum && N > 0;
     // the L sums of I8X3 too (scan_checksum 2): +5% on C4's scan over H alone (the xh plane, the
@@ -1596,7 +1531,6 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     // global per-query candidate lists: at most 512 entries per workgroup and query
     // (the largest LDS buffer of any variant; 4 x 64 for the wave-private one)
     const int64_t gl_cap = exact_all ? 0 : wide8 ? (int64_t)n_seg8 * W8_CH
-                                       : use_s3 ? (int64_t)((n_wg3 + 7) / 8 * 8) * 64
                                               : (int64_t)((n_wg + 7) / 8 * 8) * 512;
     bytes += (size_t)B * gl_cap * 8 + (size_t)Bp * 4 + 768;
     // Pilot sample: 512 row tiles, more for large k (its bound then saves more insert work than
@@ -1677,7 +1611,6 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     float* q8scal = c.take<float>(64);
     float* q8res = i8_refine ? c.take<float>((size_t)Bp * ix->Dp) : nullptr;
     float* q8err2 = i8_refine ? c.take<float>(Bp) : nullptr;
-    uint32_t* pace = c.take<uint32_t>((size_t)(n_wg + 7) / 8 * 8 * n_qblocks + 64);
     uint32_t* chkp = chk ? c.take<uint32_t>((size_t)2 * n_wg8 * Bp) : nullptr;
     uint32_t* segc = wide8 ? c.take<uint32_t>((size_t)Bp * n_seg8) : nullptr;
     uint32_t* chkr = chk && ix->metric == 1 ? c.take<uint32_t>(64) : nullptr;
@@ -1754,7 +1687,7 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
                 } else if (split_pass) {
                     HIP_TRY(launch_pilot2(prec, ix->metric, pilot_rank, Xscan, ix->rinit32, md, Qt, Gs, N, B,
                                           (B + QB_pilot - 1) / QB_pilot, QB_pilot, n_pilot, pslots, gthr, st));
-                    if (!ix->pilot_fused || use_s3 || q4) HIP_TRY(launch_pilot_bound(pslots, B, pilot_rank, gthr, st));
+                    HIP_TRY(launch_pilot_bound(pslots, B, pilot_rank, gthr, st));
                 }
                 else
                     HIP_TRY(launch_pilot(prec, ix->metric, pilot_rank, Xscan, rowscale, md, Qt, Gs, N, B,
@@ -1762,28 +1695,22 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
             }
             // scan_ns times the scan kernel alone (the roofline's kernel); pipeline_ns
             // everything from the pilot to the rerank
-            if (opt.gate && (use_s3 || q4 || !(split_pass || i8_pass)))  // only these passes are gated
+            if (opt.gate && (q4 || !(split_pass || i8_pass)))  // only these passes are gated
                 return set_error(VDB_ERR_INVALID, "device re-pass: the sub-search has no gated candidate pass");
             if (timed) HIP_TRY(hipEventRecord(tev[0], st));
-            if (use_s3) ix->n_scan3++;
-            if ((q4 && !use_s3) || q4_8) ix->n_q4++;
+            if (q4) ix->n_q4++;
             if (wide8) ix->n_wide++;
             if (wide8)
                 HIP_TRY(launch_scan8w(prec, ix->metric, Xscan, rs8, md, Qt, q8lsl, q8scal, Gs, N, B, Bp, n_seg8, gl_s, gl_i,
                                       gl_cap, segc, gthr, chkp, Bp, chk_l ? 1 : 0, st));
             else if (i8_pass)
                 HIP_TRY(launch_scan8(prec, ix->metric, KP, Xscan, (const float*)rs8, md, Qt, q8lsl, q8scal, Gs, N, B,
-                                     n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr,
-                                     ix->scan_pace ? pace : nullptr, ix->pace_seq.fetch_add(1) + 1, lockstep,
-                                     (int)ix->scan_qlds, st, opt.gate, q4_8, chkp, Bp, chk_l ? 1 : 0));
-            else if (use_s3)
-                HIP_TRY(launch_scan3(prec, ix->metric, Xscan, ix->rinit32, md, Qt, Gs, N, B, n_qb3, steps3, n_wg3, spw3,
-                                     gl_s, gl_i, gl_cnt, gl_cap, gthr, st));
+                                     n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, lockstep,
+                                     (int)ix->scan_qlds, st, opt.gate, chkp, Bp, chk_l ? 1 : 0));
             else if (split_pass)
                 HIP_TRY(launch_scan2(prec, ix->metric, KP, Xscan, ix->rinit32, md, Qt, Gs, N, B, n_qblocks, n_steps,
-                                     n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, pslots,
-                                     n_pilot > 0 && ix->pilot_fused && !q4 ? pilot_rank : 0, lockstep, publish,
-                                     (int)ix->scan_qring, st, q4, (int)ix->scan_qlds, opt.gate));
+                                     n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, lockstep, st, q4,
+                                     (int)ix->scan_qlds, opt.gate));
             else if (priv)
                 HIP_TRY(launch_scan_topk_priv(prec, ix->metric, KP, Xscan, rowscale, md, Qt, Gs, N, B, n_qblocks,
                                               n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, st));

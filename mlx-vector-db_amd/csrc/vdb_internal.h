@@ -63,9 +63,7 @@ hipError_t launch_pilot8(int prec, int metric, const float* Xq, const float* rin
                          const float* Qq, const float* qscal, int G8, int64_t N, int B, int n_qblocks, int QB,
                          int n_sample, uint32_t* pslots, hipStream_t st, const uint32_t* csum = nullptr,
                          uint32_t* chke = nullptr);
-int scan8_rows_per_step(int prec, int metric, bool q4 = false);
-int scan8_qb(int KP, bool q4 = false);  // queries per block of the int8 pass
-bool scan8_q4_ok(int G8, int prec);     // the 128-query shape fits (short rows)
+int scan8_rows_per_step(int prec, int metric);  // (64 queries per block of the int8 pass)
 // the wide int8 pass (vdb_scan8w.hip): rows of 4 groups, batches of more than 256; W8_CH slots per
 // (workgroup, query) segment of the candidate lists
 constexpr int W8_CH = 32;
@@ -77,8 +75,8 @@ hipError_t launch_scan8w(int prec, int metric, const float* Xq, const int* rs8, 
 hipError_t launch_scan8(int prec, int metric, int KP, const float* Xq, const float* rinit, const uint32_t* mask,
                         const float* Qq, const float* lsl, const float* qscal, int G8, int64_t N, int B,
                         int n_qblocks, int64_t n_steps, int n_wg, int spw, float* gl_s, uint32_t* gl_i,
-                        uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr, uint32_t* pace, uint32_t pace_tag,
-                        int lockstep, int qlds, hipStream_t st, const int* gate = nullptr, bool q4 = false,
+                        uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr,
+                        int lockstep, int qlds, hipStream_t st, const int* gate = nullptr,
                         uint32_t* chkp = nullptr, int chk_ld = 0, int chk_l = 0);
 
 // Ingest: row-major fp32 [n][D] (device) -> the index's row-major fp32 copy X [cap][Dp]
@@ -175,17 +173,9 @@ int scan2_qb(int KP);
 hipError_t launch_scan2(int prec, int metric, int KP, const float* Xs, const float* rinit, const uint32_t* mask,
                         const float* Qs, int G, int64_t N, int B, int n_qblocks, int64_t n_steps, int n_wg, int spw,
                         float* gl_s, uint32_t* gl_i, uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr,
-                        uint32_t* gslots, const uint32_t* pslots, int prank, int lockstep, int publish, int qring,
-                        hipStream_t st, bool q4 = false, int qlds = -1, const int* gate = nullptr);
-// The large-batch split pass (vdb_scan3_kernel.h): 256 queries per workgroup (n_qb blocks), row
-// groups shared by the waves through LDS, KW = 32 kept per query and workgroup (drop bound ->
-// gthr).  Steps of scan3_rows_per_step() rows; same inputs / outputs as launch_scan2.
-int scan3_rows_per_step();
-hipError_t launch_scan3(int prec, int metric, const float* Xs, const float* rinit, const uint32_t* mask,
-                        const float* Qs, int G, int64_t N, int B, int n_qb, int64_t n_steps, int n_wg, int spw,
-                        float* gl_s, uint32_t* gl_i, uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr, hipStream_t st);
-// Pilot scores for the split pass: fills pslots only; scan2 derives the bound (rank prank of
-// the slots) in its prologue, so there is no separate bound kernel.
+                        int lockstep, hipStream_t st, bool q4 = false, int qlds = -1, const int* gate = nullptr);
+// Pilot scores for the split pass: fills pslots only; the bound kernel (launch_pilot_bound) takes
+// the rank-th best of them into gthr.
 hipError_t launch_pilot2(int prec, int metric, int KP, const float* Xs, const float* rinit, const uint32_t* mask,
                          const float* Qs, int G, int64_t N, int B, int n_qblocks, int QB, int n_sample,
                          uint32_t* pslots, uint32_t* gthr, hipStream_t st);

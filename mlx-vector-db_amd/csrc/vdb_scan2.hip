@@ -1,7 +1,6 @@
 // vdb_scan2.hip — the split-bf16 candidate pass (PREC_BF16X3, the default, and PREC_BF16):
 // pilot kernel, dispatch to the instantiation units (kernel: vdb_scan2_kernel.h).
 #include "vdb_scan2_kernel.h"
-#include "vdb_scan3_kernel.h"
 
 namespace vdb {
 
@@ -126,36 +125,23 @@ hipError_t launch_pilot2(int prec, int metric, int KP, const float* Xs, const fl
 // Dispatch
 // =============================================================================
 int scan2_rows_per_step(bool q4) { return q4 ? 2 * S2_NW * 32 : S2_ROWS; }
-int scan3_rows_per_step() { return S3_ROWS; }
-
-hipError_t launch_scan3(int prec, int metric, const float* Xs, const float* rinit, const uint32_t* mask,
-                        const float* Qs, int G, int64_t N, int B, int n_qb, int64_t n_steps, int n_wg, int spw,
-                        float* gl_s, uint32_t* gl_i, uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr, hipStream_t st) {
-    auto* unit = prec == PREC_BF16X3 ? (metric == 0 ? launch_scan3_b3c : launch_scan3_b3l)
-                 : prec == PREC_BF16 ? (metric == 0 ? launch_scan3_b1c : launch_scan3_b1l)
-                                     : nullptr;
-    if (!unit || metric < 0 || metric > 1) return hipErrorInvalidValue;
-    return unit(Xs, rinit, mask, Qs, G, N, B, n_qb, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, st);
-}
 
 hipError_t launch_scan2(int prec, int metric, int KP, const float* Xs, const float* rinit, const uint32_t* mask,
                         const float* Qs, int G, int64_t N, int B, int n_qblocks, int64_t n_steps, int n_wg, int spw,
                         float* gl_s, uint32_t* gl_i, uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr,
-                        uint32_t* gslots, const uint32_t* pslots, int prank, int lockstep, int publish, int qring,
-                        hipStream_t st, bool q4, int qlds, const int* gate) {
+                        int lockstep, hipStream_t st, bool q4, int qlds, const int* gate) {
     // the query block in LDS: auto (qlds < 0) when it fits, 0 = from global memory (then, with one
     // query block, the corpus stream takes the non-temporal policy)
     const bool ql = q4 || (qlds != 0 && scan2_qlds(G, KP, q4));
     if (q4 && (!ql || KP != 128)) return hipErrorInvalidValue;
     const bool fs = !lockstep;
-    const bool qch = qring && !ql && !fs && G % S2_QCG == 0;
     const bool nt = !ql && n_qblocks == 1;
     auto* unit = prec == PREC_BF16X3 ? (metric == 0 ? launch_scan2_b3c : launch_scan2_b3l)
                  : prec == PREC_BF16 ? (metric == 0 ? launch_scan2_b1c : launch_scan2_b1l)
                                      : nullptr;
     if (!unit || metric < 0 || metric > 1) return hipErrorInvalidValue;
-    return unit(KP, Xs, rinit, mask, Qs, G, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr,
-                gslots, pslots, prank, nt, ql, fs, qch, q4, publish, gate, st);
+    return unit(KP, Xs, rinit, mask, Qs, G, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, nt,
+                ql, fs, q4, gate, st);
 }
 
 }  // namespace vdb

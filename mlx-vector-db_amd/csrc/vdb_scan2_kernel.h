@@ -36,7 +36,7 @@ namespace vdb {
 #ifdef VDB_STAMP
 // Diagnostic build only (make stamp): per-wave phase cycles of scan2_kernel:
 // [0] prologue, [1] k-loop, [2] epilogue (insert + compaction rounds), [3] total,
-// [4] publish, [5] flush, [6] steps, [7] start time (absolute)
+// [4] (unused), [5] flush, [6] steps, [7] start time (absolute)
 static __device__ unsigned long long g_scan2_stamps[1 << 16][8];
 #define S2_NOW() __builtin_amdgcn_s_memtime()
 #endif
@@ -133,10 +133,6 @@ __device__ __forceinline__ uint32_t pilot_slot_rank(uint32_t (&v)[PILOT_E], int 
 // GC > 0: the dimension groups as a compile-time constant (short rows, C4: 8), so the group
 // loop unrolls; the runtime loop made the register allocator copy 4 of the 8 accumulator
 // tiles between register sets on every step (256 v_accvgpr_mov per step at C4).
-// QCH: the global query operand goes through a double-buffered LDS ring of S2_QCG-group chunks,
-// loaded once per workgroup instead of once per wave (lockstep step ends only: one workgroup
-// barrier per chunk, which every wave reaches since all run the same steps).
-constexpr int S2_QCG = 4;
 // RT row tiles per wave (the default S2_RT = 4; the 128-query shape QT = 4 takes 2, so the
 // accumulators stay at 128 registers).  KW < KP: a workgroup keeps only its KW best per query
 // (smaller LDS buffers, which the 128-query blocks need); its compactions then do not raise
@@ -144,13 +140,12 @@ constexpr int S2_QCG = 4;
 // to its drop bound (its KW-th best), which keeps the certificate's invariant (rows outside the
 // lists score <= max(a_KP, final gthr)); the finish then certifies as usual.
 template <int PREC, int METRIC, int QT, int PX, int KP, int CAP, bool NT, bool QLDS, bool FLAGSYNC, int GC = 0,
-          bool QCH = false, int RT_ = S2_RT, int KW = KP>
+          int RT_ = S2_RT, int KW = KP>
 __global__ void __launch_bounds__(64 * S2_NW, 1)
 scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, const uint32_t* __restrict__ mask,
              const float* __restrict__ Qs, int G_arg, int64_t N, int B, int64_t n_steps, int steps_per_wg, int n_qb,
              float* __restrict__ gl_s, uint32_t* __restrict__ gl_i, uint32_t* __restrict__ gl_cnt, int64_t gl_cap,
-             uint32_t* __restrict__ gthr, uint32_t* __restrict__ gslots, const uint32_t* __restrict__ pslots,
-             int prank, int publish, const int* __restrict__ gate) {
+             uint32_t* __restrict__ gthr, const int* __restrict__ gate) {
     // a gated launch (the device-memory re-pass, vdb_api.cpp): nothing to do when its count is 0
     if (gate && *gate == 0) return;
     constexpr int RT = RT_, NW = S2_NW;
@@ -162,8 +157,7 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
 #ifndef VDB_S2_PQ
 #define VDB_S2_PQ 0
 #endif
-    static_assert(!QCH || (!QLDS && !FLAGSYNC), "query ring: global query operand, lockstep step ends");
-    constexpr int PQ = (QLDS || QCH) ? 1 : (VDB_S2_PQ > 0 && VDB_S2_PQ < PX && PX % (VDB_S2_PQ > 0 ? VDB_S2_PQ : 1) == 0 ? VDB_S2_PQ : PX);
+    constexpr int PQ = QLDS ? 1 : (VDB_S2_PQ > 0 && VDB_S2_PQ < PX && PX % (VDB_S2_PQ > 0 ? VDB_S2_PQ : 1) == 0 ? VDB_S2_PQ : PX);
     constexpr size_t GSTEP = 8 * BLOCK_FLOATS;  // query: consecutive groups of one super tile
     constexpr size_t PLANE = 4 * BLOCK_FLOATS;  // query: lo plane after hi
     constexpr size_t XGSTEP = corpus_gstep();   // corpus (vdb_common.h corpus_block)
@@ -173,9 +167,6 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
     __shared__ uint32_t s_ix[QB * CAP];
     __shared__ int s_cnt[QB];
     __shared__ float s_thr[QB];
-    __shared__ uint32_t s_best[NW][QB];
-    __shared__ uint32_t s_pub[NW][QB];
-    __shared__ uint32_t s_sh[QB];
     __shared__ int s_need, s_done;
     __shared__ uint32_t s_pend[NW][RT * QT][64];  // per wave and tile: each lane's entries left for a compaction round
     extern __shared__ __attribute__((aligned(16))) float s_q[];  // QLDS: [G][plane][QT][256]
@@ -185,7 +176,7 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 #ifdef VDB_STAMP
     const unsigned long long st_t0 = S2_NOW();
-    unsigned long long st_pro = 0, st_k = 0, st_e = 0, st_pub = 0, st_fl = 0, st_a = 0, st_n = 0;
+    unsigned long long st_pro = 0, st_k = 0, st_e = 0, st_fl = 0, st_a = 0, st_n = 0;
 #endif
     int wg, qb;
     xcd_map(n_qb, wg, qb);
@@ -195,37 +186,7 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
     }
     for (int i = threadIdx.x; i < QB; i += 64 * NW) {
         s_cnt[i] = 0;
-#pragma unroll
-        for (int w = 0; w < NW; ++w) {
-            s_best[w][i] = 0;
-            s_pub[w][i] = 0;
-        }
-        s_sh[i] = 0;
         s_thr[i] = -INFINITY;
-    }
-    // the pilot's bound (pilot2_scores_kernel filled the slots): every workgroup derives it for
-    // its query block into s_sh; range 0 also raises gthr, which the finish pass reads (it must
-    // cover every bound a workgroup dropped rows against)
-    if (prank > 0) {
-        __syncthreads();
-        constexpr int QW = QB / NW;  // queries per wave: all their slots loaded before the first
-        uint32_t pv[QW][PILOT_E];    // selection (one round trip, not QW of them)
-#pragma unroll
-        for (int i = 0; i < QW; ++i) {
-            const int q = qb * QB + wv + NW * i;
-#pragma unroll
-            for (int e = 0; e < PILOT_E; ++e) pv[i][e] = q < B ? pslots[pslot_at(q, e * 64 + lane, B)] : 0u;
-        }
-#pragma unroll
-        for (int i = 0; i < QW; ++i) {
-            const int ql = wv + NW * i;
-            if (qb * QB + ql >= B) break;
-            const uint32_t T = pilot_slot_rank(pv[i], prank);
-            if (lane == 0 && T != 0u) {
-                s_sh[ql] = T;
-                if (wg == 0) atomicMax(gthr + qb * QB + ql, T);
-            }
-        }
     }
     const float* Qbase = Qs + s2_blk((uint64_t)(qb * QT), 0, G + QG_EXTRA);
     if constexpr (QLDS) {
@@ -234,45 +195,9 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
             *(f32x4*)(s_q + (size_t)e * 4) = *(const f32x4*)(Qbase + g * GSTEP + pl * PLANE + qt * BLOCK_FLOATS + 4 * l);
         }
     }
-    // query ring (QCH): chunk c = groups [CG c, CG c + CG) in buffer c & 1 ([g][plane][QT][256]
-    // floats, as the QLDS block); each thread moves QNE float4 of a chunk
-    constexpr int CG = S2_QCG;
-    constexpr int CHF = CG * 2 * QT * 256;  // floats per chunk buffer
-    constexpr int QNE = QCH ? CG * 2 * QT * 64 / (64 * NW) : 1;
-    static_assert(!QCH || (CG * 2 * QT * 64) % (64 * NW) == 0, "query chunk not a whole number of float4 per thread");
-    f32x4 qc[QNE];
-    auto ring_load = [&](int g0) {  // chunk starting at group g0 -> qc
-#pragma unroll
-        for (int j = 0; j < QNE; ++j) {
-            const int e = (int)threadIdx.x + 64 * NW * j;
-            const int l = e & 63, qt = (e >> 6) % QT, pl = (e / (64 * QT)) & 1, gi = e / (128 * QT);
-            qc[j] = *(const f32x4*)(Qbase + (size_t)(g0 + gi) * GSTEP + pl * PLANE + qt * BLOCK_FLOATS + 4 * l);
-        }
-    };
-    auto ring_store = [&](int buf) {
-#pragma unroll
-        for (int j = 0; j < QNE; ++j) *(f32x4*)(s_q + (size_t)buf * CHF + ((int)threadIdx.x + 64 * NW * j) * 4) = qc[j];
-    };
-    int cpar = 0;  // buffer of the chunk the next q_ring read falls in
-    if constexpr (QCH) {
-        ring_load(0);
-        ring_store(0);
-        ring_load(CG % G);
-    }
     __syncthreads();
 
-    // slot publishing (as vdb_scan.hip): lane group pq_r of LPQ lanes serves query wv + NW (lane / LPQ)
     constexpr int QPW = QB / NW;
-    constexpr int LPQ = 64 / QPW;
-    constexpr int SL = KP / LPQ;
-    constexpr int SLV = SL / 4 > 0 ? SL / 4 : 1;
-    // publishing needs a lane group of >= NW lanes per query (QB <= 64); the 128-query shape
-    // runs without it (its bound: the pilot's, the compactions' own thresholds)
-    constexpr bool PUB = LPQ >= NW && KW == KP;
-    static_assert(SL % 4 == 0, "slots per lane must be whole uint4 loads");
-    const int pq_r = lane % LPQ;
-    const int pq = wv + NW * (lane / LPQ);
-    const int pqg = qb * QB + pq;
 
     const int64_t s_begin = (int64_t)wg * steps_per_wg;
     const int64_t s_end = s_begin + steps_per_wg < n_steps ? s_begin + steps_per_wg : n_steps;
@@ -285,13 +210,6 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
 #pragma unroll
             for (int pl = 0; pl < QPL; ++pl) q[qt][pl] = *(const f32x4*)(s_q + ((size_t)(g * 2 + pl) * QT + qt) * 256 + lane4);
     };
-    auto q_ring = [&](int g, f32x4 (&q)[QT][QPL]) {  // group g of the chunk in buffer cpar
-#pragma unroll
-        for (int qt = 0; qt < QT; ++qt)
-#pragma unroll
-            for (int pl = 0; pl < QPL; ++pl)
-                q[qt][pl] = *(const f32x4*)(s_q + (size_t)cpar * CHF + ((size_t)(g * 2 + pl) * QT + qt) * 256 + lane4);
-    };
     if (s_begin < s_end) {
         const float* xs = Xs + corpus_block((uint64_t)((s_begin * NW + wv) * RT), 0, 0, G);
 #pragma unroll
@@ -301,9 +219,7 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
 #pragma unroll
                 for (int pl = 0; pl < XPL; ++pl)
                     xr[p][rt][pl] = corpus_ld<NT>(xs + p * XGSTEP + pl * XPLANE + rt * BLOCK_FLOATS + lane4);
-        if constexpr (QCH) {
-            q_ring(0, qr[0]);
-        } else if constexpr (!QLDS) {
+        if constexpr (!QLDS) {
 #pragma unroll
             for (int p = 0; p < PQ; ++p)
 #pragma unroll
@@ -364,30 +280,7 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
         // one group: MFMAs of slot p, then refill slot p with the group PX ahead (this step's,
         // or the next step's first groups); refills pinned right behind the MFMAs
         auto group = [&](const int p, const int g, const float* xsrc, const float* qsrc) {
-            if constexpr (QCH) {
-                const int gn = g + 1 < G ? g + 1 : 0;
-                if (gn % CG == 0) {  // the next group opens a chunk: publish the prefetched one
-                    ring_store(cpar ^ 1);
-                    cpar ^= 1;
-                    __syncthreads();
-                    ring_load(gn + CG < G ? gn + CG : 0);
-                }
-                f32x4 qn[1][QT][QPL];
-                q_ring(gn % CG, qn[0]);
-                group_mfma<PREC, RT, QT>(xr[p], qr[0], acc);
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-                    for (int pl = 0; pl < XPL; ++pl)
-                        xr[p][rt][pl] = corpus_ld<NT>(xsrc + pl * XPLANE + rt * BLOCK_FLOATS + lane4);
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int qt = 0; qt < QT; ++qt)
-#pragma unroll
-                    for (int pl = 0; pl < QPL; ++pl) qr[0][qt][pl] = qn[0][qt][pl];
-                (void)qsrc;
-            } else if constexpr (QLDS) {
+if constexpr (QLDS) {
                 f32x4 qn[1][QT][QPL];
                 q_lds(g + 1 < G ? g + 1 : 0, qn[0]);
                 group_mfma<PREC, RT, QT>(xr[p], qr[0], acc);
@@ -466,7 +359,7 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
 #pragma unroll
         for (int qt = 0; qt < QT; ++qt) {
             const int ql = qt * 32 + (lane & 31);
-            const float thr = fmaxf(s_thr[ql], key_to_float(max(gk[qt], s_sh[ql])));
+            const float thr = fmaxf(s_thr[ql], key_to_float(gk[qt]));
             thrh[qt] = METRIC == 0 ? thr : 0.5f * thr;
             qok[qt] = qb * QB + ql < B;
         }
@@ -482,8 +375,7 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
         // independent compares, then one round per hit of the lane with the most hits -- with
         // one wave per SIMD a compare-ballot-branch chain per register cost ~140 cycles, ~2.9 K per
         // tile.  Only the lanes whose score passes append (one returning LDS atomic each);
-        // entries that find the buffer full wait in s_pend for a compaction round.  The lane's
-        // best appended score goes to s_best (publish).
+        // entries that find the buffer full wait in s_pend for a compaction round.
         uint32_t pmask = 0;  // wave-uniform: tiles with entries left in s_pend
         for (bool joined = false;; joined = true) {
             while (todo != 0u) {
@@ -511,7 +403,7 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
                         gkq = gk[q2];
                         ok = qok[q2];
                     }
-                const float thr = fmaxf(s_thr[ql], key_to_float(max(gkq, s_sh[ql])));
+                const float thr = fmaxf(s_thr[ql], key_to_float(gkq));
                 const float th = METRIC == 0 ? thr : 0.5f * thr;
                 const uint32_t cand = joined ? s_pend[wv][t][lane] : ok ? tile_valid16(mask, t0 + rt, N, lane) : 0u;
                 const uint32_t rb = (uint32_t)((t0 + rt) * 32) + 4u * (uint32_t)(lane >> 5);
@@ -520,7 +412,6 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
                 for (int v = 0; v < 16; ++v) pm |= (h[v] > th ? 1u : 0u) << v;
                 pm &= cand;
                 uint32_t left = 0;
-                float mx = -INFINITY;
                 while (__any(pm != 0u)) {
                     if (pm != 0u) {
                         const int v = __builtin_ctz(pm);
@@ -536,10 +427,8 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
                         } else {
                             left |= 1u << v;
                         }
-                        mx = fmaxf(mx, sc);
                     }
                 }
-                if (mx != -INFINITY) atomicMax(&s_best[wv][ql], order_key(mx));
                 if (__any(left != 0u)) {
                     s_pend[wv][t][lane] = left;
                     pmask |= 1u << t;
@@ -564,58 +453,12 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
             todo = pmask;
             pmask = 0;
         }
-        // ---- publish (as vdb_scan.hip): per-wave bests into KP slots per query; the slot
-        // minimum is a lower bound of the global KP-th best.  Only at steps 1, 2, 4, 8, ... and
-        // the last, so the slots are read back right away (a few waits per launch) instead of
-        // holding KP/4 registers per lane across the next step ----
 #ifdef VDB_STAMP
         {
             const unsigned long long t = S2_NOW();
             st_e += t - st_a;
             st_a = t;
         }
-#endif
-        const int64_t sd = s - s_begin + 1;
-        // flag-gated step ends: an optional plain barrier every `realign` steps (bits 8-15 of
-        // `publish`) bounds how far the waves drift apart (they share the query operand's lines)
-        if constexpr (FLAGSYNC) {
-            const int realign = (publish >> 8) & 255;
-            if (realign > 0 && sd % realign == 0) __syncthreads();
-        }
-#ifdef VDB_S2_NO_PUBLISH
-        if (false) {
-#else
-        if (PUB && (publish & 1) && ((sd & (sd - 1)) == 0 || s + 1 == s_end)) {
-#endif
-            int improved = 0;
-            if (pq_r < NW && pqg < B) {
-                const uint32_t best = s_best[pq_r][pq];
-                improved = best > s_pub[pq_r][pq];
-                if (improved) {
-                    s_pub[pq_r][pq] = best;
-                    atomicMax(gslots + (size_t)pqg * KP_MAX + ((wg * NW + pq_r) % KP), best);
-                }
-            }
-#pragma unroll
-            for (int off = 1; off < LPQ; off <<= 1) improved |= __shfl_xor(improved, off, 64);
-            if (improved) {
-                const uint32_t* sl = gslots + (size_t)pqg * KP_MAX + pq_r * SL;
-                uint32_t mn = 0xFFFFFFFFu;
-#pragma unroll
-                for (int j = 0; j < SLV; ++j) {
-                    const uint4 sv = *(const uint4*)(sl + 4 * j);
-                    mn = min(min(mn, min(sv.x, sv.y)), min(sv.z, sv.w));
-                }
-#pragma unroll
-                for (int off = 1; off < LPQ; off <<= 1) mn = min(mn, (uint32_t)__shfl_xor((int)mn, off, 64));
-                if (pq_r == 0 && pqg < B) {
-                    atomicMax(gthr + pqg, mn);
-                    atomicMax(&s_sh[pq], mn);
-                }
-            }
-        }
-#ifdef VDB_STAMP
-        st_pub += S2_NOW() - st_a;
 #endif
     }
 #ifdef VDB_STAMP
@@ -646,7 +489,7 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
             dk = s_thr[q] == -INFINITY ? 0u : order_key(s_thr[q]);
             if (dk) atomicMax(gthr + qb * QB + q, dk);
         }
-        tkey = max(max(gthr[qb * QB + q], s_sh[q]), dk);
+        tkey = max(gthr[qb * QB + q], dk);
     }
     append_flush<CAP>(s_sc, s_ix, s_cnt, wv, NW, QPW, qb * QB, B, tkey, gl_s, gl_i, gl_cnt, gl_cap);
 #ifdef VDB_STAMP
@@ -659,7 +502,7 @@ scan2_kernel(const float* __restrict__ Xs, const float* __restrict__ rinit, cons
             g_scan2_stamps[w][1] = st_k;
             g_scan2_stamps[w][2] = st_e;
             g_scan2_stamps[w][3] = t - st_t0;
-            g_scan2_stamps[w][4] = st_pub;
+            g_scan2_stamps[w][4] = 0;
             g_scan2_stamps[w][5] = st_fl;
             g_scan2_stamps[w][6] = st_n;
             g_scan2_stamps[w][7] = st_t0;
@@ -678,15 +521,15 @@ inline bool scan2_qlds(int G16, int KP, bool q4 = false) {
     return (size_t)G16 * 2 * (q4 ? 4 : scan2_qb(KP) / 32) * 1024 <= (q4 ? 64 : 32) * 1024;
 }
 
-template <int P, int M, int QT, int PX, int KP, int CAP, bool NT, bool QL, bool FS, int GC, bool QC = false,
-          int RT_ = S2_RT, int KW = KP>
+template <int P, int M, int QT, int PX, int KP, int CAP, bool NT, bool QL, bool FS, int GC, int RT_ = S2_RT,
+          int KW = KP>
 static hipError_t scan2_launch_g(const float* Xs, const float* rinit, const uint32_t* mask, const float* Qs, int G,
                                  int64_t N, int B, int n_qblocks, int64_t n_steps, int n_wg, int spw, float* gl_s,
-                                 uint32_t* gl_i, uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr, uint32_t* gslots,
-                                 const uint32_t* pslots, int prank, int publish, const int* gate, hipStream_t st) {
-    auto k = scan2_kernel<P, M, QT, PX, KP, CAP, NT, QL, FS, GC, QC, RT_, KW>;
-    const size_t lds = QL ? (size_t)G * 2 * QT * 1024 : QC ? (size_t)2 * S2_QCG * 2 * QT * 1024 : 0;
-    if (QL || QC) {
+                                 uint32_t* gl_i, uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr, const int* gate,
+                                 hipStream_t st) {
+    auto k = scan2_kernel<P, M, QT, PX, KP, CAP, NT, QL, FS, GC, RT_, KW>;
+    const size_t lds = QL ? (size_t)G * 2 * QT * 1024 : 0;
+    if (QL) {
         // the dynamic part (query block) plus the static top-k buffers must fit the 160 KiB of a
         // CU: raise the dynamic limit to what this call needs (monotone; racing calls only
         // raise it to values that fit)
@@ -700,7 +543,7 @@ static hipError_t scan2_launch_g(const float* Xs, const float* rinit, const uint
     }
     const int n_wg8 = (n_wg + 7) / 8 * 8;
     hipLaunchKernelGGL(k, dim3(n_wg8 * n_qblocks), dim3(64 * S2_NW), lds, st, Xs, rinit, mask, Qs, G, N, B, n_steps, spw,
-                       n_qblocks, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, pslots, prank, publish, gate);
+                       n_qblocks, gl_s, gl_i, gl_cnt, gl_cap, gthr, gate);
     return hipGetLastError();
 }
 
@@ -709,41 +552,30 @@ static hipError_t scan2_launch_g(const float* Xs, const float* rinit, const uint
 template <int P, int M, int QT, int PX, int KP, int CAP, bool NT, bool QL, bool FS, int RT_ = S2_RT, int KW = KP>
 static hipError_t scan2_launch(const float* Xs, const float* rinit, const uint32_t* mask, const float* Qs, int G,
                                int64_t N, int B, int n_qblocks, int64_t n_steps, int n_wg, int spw, float* gl_s,
-                               uint32_t* gl_i, uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr, uint32_t* gslots,
-                               const uint32_t* pslots, int prank, int publish, const int* gate, hipStream_t st) {
+                               uint32_t* gl_i, uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr, const int* gate,
+                               hipStream_t st) {
     if constexpr (QL) {
         if (G == 8)
-            return scan2_launch_g<P, M, QT, PX, KP, CAP, NT, QL, FS, 8, false, RT_, KW>(
-                Xs, rinit, mask, Qs, G, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots,
-                pslots, prank, publish, gate, st);
+            return scan2_launch_g<P, M, QT, PX, KP, CAP, NT, QL, FS, 8, RT_, KW>(
+                Xs, rinit, mask, Qs, G, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gate, st);
     }
-    return scan2_launch_g<P, M, QT, PX, KP, CAP, NT, QL, FS, 0, false, RT_, KW>(
-        Xs, rinit, mask, Qs, G, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, pslots,
-        prank, publish, gate, st);
+    return scan2_launch_g<P, M, QT, PX, KP, CAP, NT, QL, FS, 0, RT_, KW>(
+        Xs, rinit, mask, Qs, G, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gate, st);
 }
 
 // The argument list of one (precision, metric) unit's launcher (launch_scan2 dispatches).
 #define S2_UNIT_PARAMS                                                                                             \
     int KP, const float *Xs, const float *rinit, const uint32_t *mask, const float *Qs, int G, int64_t N, int B,    \
         int n_qblocks, int64_t n_steps, int n_wg, int spw, float *gl_s, uint32_t *gl_i, uint32_t *gl_cnt,          \
-        int64_t gl_cap, uint32_t *gthr, uint32_t *gslots, const uint32_t *pslots, int prank, bool nt, bool ql,     \
-        bool fs, bool qch, bool q4, int publish, const int *gate, hipStream_t st
-#define S2_ARGS Xs, rinit, mask, Qs, G, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gslots, \
-                pslots, prank, publish, gate, st
+        int64_t gl_cap, uint32_t *gthr, bool nt, bool ql, bool fs, bool q4, const int *gate, hipStream_t st
+#define S2_ARGS Xs, rinit, mask, Qs, G, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gate, st
 #define S2_ONE(P, M, KPV, QTV, PXV, CAPV, NTV, QLV, FSV)                 \
-    if (KP == KPV && nt == NTV && ql == QLV && fs == FSV && !qch && !q4) \
+    if (KP == KPV && nt == NTV && ql == QLV && fs == FSV && !q4) \
         return scan2_launch<P, M, QTV, PXV, KPV, CAPV, NTV, QLV, FSV>(S2_ARGS);
 // the 128-query shape (query block in LDS, 2 row tiles per wave, KW = 48 kept of KP = 128)
 #define S2_ONE4(P, M, PXV, FSV)                                               \
-    if (KP == 128 && ql && fs == FSV && !qch && q4)                           \
+    if (KP == 128 && ql && fs == FSV && q4)                                   \
         return scan2_launch<P, M, 4, PXV, 128, 64, false, true, FSV, 2, 48>(S2_ARGS);
-// query ring variants (global query operand, lockstep step ends)
-#define S2_ONEQ(P, M, KPV, QTV, PXV, CAPV, NTV)                                      \
-    if (KP == KPV && nt == NTV && !ql && !fs && qch)                                \
-        return scan2_launch_g<P, M, QTV, PXV, KPV, CAPV, NTV, false, false, 0, true>(S2_ARGS);
-#define S2_KPQ(P, M, PXV, NTV)                                                       \
-    S2_ONEQ(P, M, 32, 2, PXV, 128, NTV) S2_ONEQ(P, M, 64, 2, PXV, 128, NTV)         \
-    S2_ONEQ(P, M, 128, 2, PXV, 192, NTV) S2_ONEQ(P, M, 256, 1, PXV, 320, NTV)
 #define S2_KP(P, M, PXV, NTV, QLV, FSV)                    \
     S2_ONE(P, M, 32, 2, PXV, 128, NTV, QLV, FSV)           \
     S2_ONE(P, M, 64, 2, PXV, 128, NTV, QLV, FSV)           \
@@ -755,7 +587,6 @@ static hipError_t scan2_launch(const float* Xs, const float* rinit, const uint32
     S2_KP(P, M, PXV, false, false, false) S2_KP(P, M, PXV, true, false, false)     \
     S2_KP(P, M, PXL, false, true, false) S2_KP(P, M, PXL, false, true, true)       \
     S2_KP(P, M, PXV, false, false, true) S2_KP(P, M, PXV, true, false, true)       \
-    S2_KPQ(P, M, PXV, false) S2_KPQ(P, M, PXV, true)                              \
     S2_ONE4(P, M, PXL, false) S2_ONE4(P, M, PXL, true)
 #ifndef VDB_S2_QLDS_PX
 #define VDB_S2_QLDS_PX 2

@@ -651,30 +651,27 @@ hipError_t launch_pilot8(int prec, int metric, const float* Xq, const float* rin
 // =============================================================================
 // Dispatch
 // =============================================================================
-int scan8_rows_per_step(int prec, int metric, bool q4) { return q4 ? scan8_rows_q4() : scan8_rows(prec, metric); }
-int scan8_qb(int KP, bool q4) { (void)KP; return q4 ? 128 : 64; }  // every KP (KP = 256: KW = 64, S8_KP)
-bool scan8_q4_ok(int G8, int prec) { return G8 <= 4 && scan8_q4_fits(G8, prec); }
+int scan8_rows_per_step(int prec, int metric) { return scan8_rows(prec, metric); }
 
 hipError_t launch_scan8(int prec, int metric, int KP, const float* Xq, const float* rinit, const uint32_t* mask,
                         const float* Qq, const float* lsl, const float* qscal, int G8, int64_t N, int B,
                         int n_qblocks, int64_t n_steps, int n_wg, int spw, float* gl_s, uint32_t* gl_i,
-                        uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr, uint32_t* pace, uint32_t pace_tag,
-                        int lockstep, int qlds, hipStream_t st, const int* gate, bool q4, uint32_t* chkp, int chk_ld, int chk_l) {
+                        uint32_t* gl_cnt, int64_t gl_cap, uint32_t* gthr,
+                        int lockstep, int qlds, hipStream_t st, const int* gate, uint32_t* chkp, int chk_ld, int chk_l) {
     // the query block in LDS (scan8_qlds): qlds 1 = the round-3 rule (short rows), 2 = whenever
     // it fits, -1 = auto (rule 2 past VDB_S8_QLDS_BIG_G8 groups), 0 = never -- except for rows of fewer 32-dim groups
     // than the global-operand variants keep in flight (PX = 4)
     const int mode = qlds < 0 ? (G8 > VDB_S8_QLDS_BIG_G8 ? 2 : 1) : qlds;
-    const bool ql = q4 || (mode != 0 && scan8_qlds(G8, KP, prec, metric, mode == 1)) || G8 < 4;
-    if (q4 && (KP != 128 || !scan8_q4_ok(G8, prec))) return hipErrorInvalidValue;
+    const bool ql = (mode != 0 && scan8_qlds(G8, KP, prec, metric, mode == 1)) || G8 < 4;
     const bool fs = !lockstep;
-    const bool nt = (!ql || (VDB_S8_NTQL && fs && !q4)) && n_qblocks == 1;
+    const bool nt = (!ql || (VDB_S8_NTQL && fs)) && n_qblocks == 1;
     auto* unit = prec == PREC_I8X3 ? (metric == 0 ? launch_scan8_i3c : launch_scan8_i3l)
                  : prec == PREC_I8 ? (metric == 0 ? launch_scan8_i1c : launch_scan8_i1l)
                  : prec == PREC_I8Q ? (metric == 0 ? launch_scan8_iqc : launch_scan8_iql)
                                    : nullptr;
     if (!unit || metric < 0 || metric > 1) return hipErrorInvalidValue;
     return unit(KP, Xq, rinit, mask, Qq, lsl, qscal, G8, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt,
-                gl_cap, gthr, pace, pace_tag, nt, ql, fs, q4, gate, chkp, chk_ld, chk_l, st);
+                gl_cap, gthr, nt, ql, fs, gate, chkp, chk_ld, chk_l, st);
 }
 
 }  // namespace vdb

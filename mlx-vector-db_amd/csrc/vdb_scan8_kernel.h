@@ -50,7 +50,6 @@ constexpr int S8_NW = VDB_S8_NW;
 #ifndef VDB_S8_NW_X3L
 #define VDB_S8_NW_X3L 8
 #endif
-// (the 128-query shape, QT = 4, keeps S8_NW: its host-side rows per step are scan8_rows_q4)
 constexpr int scan8_nw(int prec, int metric, int QT = 2) {
     return (prec == PREC_I8X3 || prec == PREC_I8Q) && metric == 1 && QT != 4 ? VDB_S8_NW_X3L : S8_NW;
 }
@@ -196,38 +195,6 @@ __device__ __forceinline__ void s8_tie(f32x4 (&r)[A][C]) {  // after an s8_wait:
         for (int c = 0; c < C; ++c) asm volatile("" : "+v"(r[a][c]));
 }
 
-// Pacing of the query blocks that share a row range (n_qb > 1): their workgroups start together
-// on one XCD and read the same rows, so L2 serves all but the first -- while they stay within a
-// few steps of each other.  Their insert work differs, and over C4's 1221 steps they drifted 26
-// steps apart on average (48 at most; stamps, profiles/r03_i8/st4c), and the corpus came from HBM
-// 3.3x (8.55 GB per launch against 2.6).  Each workgroup publishes its step count (tagged with
-// the launch, so an earlier launch's counts read as "no information"); a wave more than
-// S8_PACE_W steps ahead of its range's slowest sibling sleeps, at most S8_PACE_SPIN times per
-// step -- a pacing hint only: nothing waits on a sibling that is not running.  Opt-in (index
-// knob "scan_pace"): it held C4's blocks within 5 steps and made the scan slower, 4.99 ms
-// against 2.90 -- the range runs at its slowest block's speed and each sleep drains the
-// prefetch; the L2 misses were not what bounded C4 (profiles/r03_i8/pace).
-#ifndef S8_PACE_W
-#define S8_PACE_W 6
-#endif
-#ifndef S8_PACE_SPIN
-#define S8_PACE_SPIN 64
-#endif
-__device__ __forceinline__ uint32_t s8_ld_u32(const uint32_t* base, uint32_t voff) {  // L2-coherent (sc1)
-    uint32_t r;
-    asm volatile("global_load_dword %0, %1, %2 sc1" : "=v"(r) : "v"(voff), "s"(base));
-    return r;
-}
-__device__ __forceinline__ void s8_st_u32(uint32_t* base, uint32_t voff, uint32_t v) {
-    asm volatile("global_store_dword %0, %1, %2 sc1" : : "v"(voff), "v"(v), "s"(base) : "memory");
-}
-// the slowest sibling's published step count, or 0xFFFFF where none is known (lanes < n_qb)
-__device__ __forceinline__ uint32_t s8_pace_min(uint32_t v, uint32_t tag, int lane, int n_qb) {
-    uint32_t m = (lane < n_qb && (v >> 20) == tag) ? (v & 0xFFFFFu) : 0xFFFFFu;
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) m = min(m, (uint32_t)__shfl_xor((int)m, off, 64));
-    return m;
-}
 
 // The smallest H that can still pass threshold th (half units) given |L uL| <= slack, minus a
 // margin for the fp32 evaluation: H <= the result means the tile's scores are all <= th.
@@ -248,8 +215,7 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
              const float* __restrict__ Qq, const float* __restrict__ lsl, const float* __restrict__ qscal, int G_arg,
              int64_t N, int B, int64_t n_steps, int steps_per_wg, int n_qb, float* __restrict__ gl_s,
              uint32_t* __restrict__ gl_i, uint32_t* __restrict__ gl_cnt, int64_t gl_cap, uint32_t* __restrict__ gthr,
-             uint32_t* __restrict__ pace, uint32_t pace_tag, const int* __restrict__ gate,
-             uint32_t* __restrict__ chkp, int chk_ld, int chk_l) {
+             const int* __restrict__ gate, uint32_t* __restrict__ chkp, int chk_ld, int chk_l) {
     // a gated launch (the device-memory re-pass, vdb_api.cpp): nothing to do when its count is 0
     if (gate && *gate == 0) return;
     constexpr int RT = RT_, NW = scan8_nw(PREC, METRIC, QT);
@@ -279,11 +245,6 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
     S8_STAMP(const unsigned long long st_t0 = S8_NOW(), st_r0 = __builtin_amdgcn_s_memrealtime(); unsigned long long st_w = 0, st_k = 0, st_e = 0, st_n = 0, st_x = 0, st_y = 0, st_z = 0, st_q = 0, st_f = 0;)
     int wg, qb;
     xcd_map(n_qb, wg, qb);
-    const uint32_t ptag = pace_tag & 0xFFFu;
-    const uint32_t pbase = (uint32_t)(wg * n_qb) * 4u;  // this range's counters, one per query block
-    const uint32_t poff = pbase + (uint32_t)(lane < n_qb ? lane : 0) * 4u;
-    if (pace && threadIdx.x == 0) s8_st_u32(pace, pbase + (uint32_t)qb * 4u, ptag << 20);
-    uint32_t pv = 0u;  // the siblings' counts, loaded in a step's tail, read in its epilogue
     if (threadIdx.x == 0) {
         s_need = 0;
         s_done = 0;
@@ -479,12 +440,7 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
         // 128 of them through VGPRs at the loop exit of every step (208 accvgpr moves, C2 I8).
         for (int gb = 0; gb < G; gb += PX) {
             const bool last = gb + PX >= G;
-            if (last) {
-                // the siblings' counts: issued only where the epilogue waits for them (an asm
-                // load never waited for could land in a register the compiler has reused)
-                if (pace && s + 1 < s_end) pv = s8_ld_u32(pace, poff);
-                if (s + 1 < s_end) load_epi(s + 1, rin);
-            }
+            if (last && s + 1 < s_end) load_epi(s + 1, rin);
 #pragma unroll
             for (int p = 0; p < PX; ++p)
                 group(p, gb + p, last ? xn + (size_t)p * XGSTEP : xs + (size_t)(gb + p + PX) * XGSTEP,
@@ -497,9 +453,6 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
             for (int p = 0; p < PX; ++p)
                 group(p, gb + p, xs + (size_t)(gb + p + PX) * XGSTEP, Qbase + (size_t)(gb + p + PQ) * GSTEP);
         }
-        // the siblings' counts: issued only where the epilogue waits for them (an asm load never
-        // waited for could land in a register the compiler has reused)
-        if (pace && s + 1 < s_end) pv = s8_ld_u32(pace, poff);
         // L2: the next step's start values after the first tail group, whose MFMAs are the last
         // reads of this step's (D = 128: the first group of the step), so they can land in the
         // same registers: issued before the tail, both sets were live at once and every step
@@ -522,7 +475,6 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
 #pragma unroll
                 for (int qt = 0; qt < QT; ++qt) f += imax16(aH[rt][qt]);
             if (f == 123456789) gl_s[0] = (float)f;
-            if (pace && s + 1 < s_end) asm volatile("s_waitcnt vmcnt(%1)" : "+v"(pv) : "n"(PX * LPS + (METRIC == 1 ? RT * 4 : 0)));
             if constexpr (METRIC == 1) s8_wait<RIN_YOUNGER>(rin);
             continue;
         }
@@ -734,19 +686,6 @@ scan8_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, cons
                 }
             }
         }
-        if (pace && s + 1 < s_end) {
-            const uint32_t done = (uint32_t)(s - s_begin + 1);
-            if (wv == 0 && lane == 0) s8_st_u32(pace, pbase + (uint32_t)qb * 4u, (ptag << 20) | min(done, 0xFFFFFu));
-            // younger than the counts: the L2 start values (RT x 4 loads) and the tail's refills
-            asm volatile("s_waitcnt vmcnt(%1)" : "+v"(pv) : "n"(PX * LPS + (METRIC == 1 ? RT * 4 : 0)));
-            uint32_t slow = s8_pace_min(pv, ptag, lane, n_qb);
-            for (int it = 0; it < S8_PACE_SPIN && done > slow + S8_PACE_W; ++it) {
-                __builtin_amdgcn_s_sleep(8);
-                uint32_t v = s8_ld_u32(pace, poff);
-                asm volatile("s_waitcnt vmcnt(0)" : "+v"(v));  // (the stream's loads too: this wave waits anyway)
-                slow = s8_pace_min(v, ptag, lane, n_qb);
-            }
-        }
         // the next step's start values (RIN_YOUNGER refills issued after them; younger epilogue
         // accesses only make this wait stricter) land before the back-edge
         S8_STAMP(const unsigned long long st_g = S8_NOW(); st_f += st_g;)
@@ -844,7 +783,7 @@ template <int P, int M, int QT, int PX, int KP, int CAP, bool NT, bool QL, bool 
 static hipError_t scan8_launch_g(const float* Xq, const float* rinit, const uint32_t* mask, const float* Qq,
                                  const float* lsl, const float* qscal, int G, int64_t N, int B, int n_qblocks,
                                  int64_t n_steps, int n_wg, int spw, float* gl_s, uint32_t* gl_i, uint32_t* gl_cnt,
-                                 int64_t gl_cap, uint32_t* gthr, uint32_t* pace, uint32_t pace_tag, const int* gate,
+                                 int64_t gl_cap, uint32_t* gthr, const int* gate,
                                  uint32_t* chkp, int chk_ld, int chk_l, hipStream_t st) {
     auto k = scan8_kernel<P, M, QT, PX, KP, CAP, NT, QL, FS, GC, RT_, KW>;
     const size_t lds = QL ? (size_t)G * Planes8<P>::QPL * QT * 1024 : 0;
@@ -859,8 +798,7 @@ static hipError_t scan8_launch_g(const float* Xq, const float* rinit, const uint
     }
     const int n_wg8 = (n_wg + 7) / 8 * 8;
     hipLaunchKernelGGL(k, dim3(n_wg8 * n_qblocks), dim3(64 * scan8_nw(P, M, QT)), lds, st, Xq, rinit, mask, Qq, lsl, qscal, G, N, B,
-                       n_steps, spw, n_qblocks, gl_s, gl_i, gl_cnt, gl_cap, gthr, n_qblocks > 1 ? pace : nullptr,
-                       pace_tag, gate, chkp, chk_ld, chk_l);
+                       n_steps, spw, n_qblocks, gl_s, gl_i, gl_cnt, gl_cap, gthr, gate, chkp, chk_ld, chk_l);
     return hipGetLastError();
 }
 
@@ -869,13 +807,13 @@ template <int P, int M, int QT, int PX, int KP, int CAP, bool NT, bool QL, bool 
 static hipError_t scan8_launch(const float* Xq, const float* rinit, const uint32_t* mask, const float* Qq,
                                const float* lsl, const float* qscal, int G, int64_t N, int B, int n_qblocks,
                                int64_t n_steps, int n_wg, int spw, float* gl_s, uint32_t* gl_i, uint32_t* gl_cnt,
-                               int64_t gl_cap, uint32_t* gthr, uint32_t* pace, uint32_t pace_tag, const int* gate,
+                               int64_t gl_cap, uint32_t* gthr, const int* gate,
                                uint32_t* chkp, int chk_ld, int chk_l, hipStream_t st) {
     if constexpr (QL) {
         if (G == 4)  // D = 128: the group loop unrolls, and the whole next step is in flight
             return scan8_launch_g<P, M, QT, 4, KP, CAP, NT, QL, FS, 4, RT_, KW>(Xq, rinit, mask, Qq, lsl, qscal, G, N, B,
                                                                         n_qblocks, n_steps, n_wg, spw, gl_s, gl_i,
-                                                                        gl_cnt, gl_cap, gthr, pace, pace_tag, gate,
+                                                                        gl_cnt, gl_cap, gthr, gate,
                                                                         chkp, chk_ld, chk_l, st);
     }
     // the step loop takes the groups PX at a time: Dp / 32 groups is only even (D = 192: 6), so
@@ -885,11 +823,11 @@ static hipError_t scan8_launch(const float* Xq, const float* rinit, const uint32
         if (G % PX != 0)
             return scan8_launch_g<P, M, QT, 2, KP, CAP, NT, QL, FS, 0, RT_, KW>(
                 Xq, rinit, mask, Qq, lsl, qscal, G, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap,
-                gthr, pace, pace_tag, gate, chkp, chk_ld, chk_l, st);
+                gthr, gate, chkp, chk_ld, chk_l, st);
     }
     return scan8_launch_g<P, M, QT, PX, KP, CAP, NT, QL, FS, 0, RT_, KW>(Xq, rinit, mask, Qq, lsl, qscal, G, N, B, n_qblocks,
                                                                 n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr,
-                                                                pace, pace_tag, gate, chkp, chk_ld, chk_l, st);
+                                                                gate, chkp, chk_ld, chk_l, st);
 }
 
 // The query block in LDS takes the query operand off each wave's vector-memory path (from L2,
@@ -897,10 +835,7 @@ static hipError_t scan8_launch(const float* Xq, const float* rinit, const uint32
 // (64 queries x D bytes per plane; I8 reads qh alone) plus the static LDS (64 queries x CAP x
 // 8 B of lists, s_pend 8 KiB, counters) is within the CU's 160 KiB: C3 (D = 1536, I8, KP = 256
 // with CAP 96): 96 + 56.5 KiB.  `small` keeps the round-3 rule (block <= 32 KiB: short rows).
-// rows per step of the 128-query shape (one row tile per wave)
-constexpr int scan8_rows_q4() { return 1 * S8_NW * 32; }
 inline int scan8_qpl(int prec) { return prec == PREC_I8X3 || prec == PREC_I8Q ? 2 : 1; }
-inline bool scan8_q4_fits(int G8, int prec) { return S8_NW == 4 && (size_t)G8 * scan8_qpl(prec) * 4 * 1024 <= 32 * 1024; }
 inline int scan8_cap(int KP, bool ql) { return KP == 128 ? 192 : KP == 256 ? (ql ? 96 : 128) : 128; }  // as S8_KP
 inline bool scan8_qlds(int G8, int KP, int prec, int metric, bool small) {
     const size_t q = (size_t)G8 * scan8_qpl(prec) * 2 * 1024;
@@ -916,27 +851,15 @@ inline bool scan8_qlds(int G8, int KP, int prec, int metric, bool small) {
 #define S8_UNIT_PARAMS                                                                                             \
     int KP, const float *Xq, const float *rinit, const uint32_t *mask, const float *Qq, const float *lsl,          \
         const float *qscal, int G, int64_t N, int B, int n_qblocks, int64_t n_steps, int n_wg, int spw,           \
-        float *gl_s, uint32_t *gl_i, uint32_t *gl_cnt, int64_t gl_cap, uint32_t *gthr, uint32_t *pace,            \
-        uint32_t pace_tag, bool nt, bool ql, bool fs, bool q4, const int *gate, uint32_t *chkp, int chk_ld, int chk_l, \
+        float *gl_s, uint32_t *gl_i, uint32_t *gl_cnt, int64_t gl_cap, uint32_t *gthr, bool nt, bool ql, bool fs,  \
+        const int *gate, uint32_t *chkp, int chk_ld, int chk_l,                                                     \
         hipStream_t st
 #define S8_ARGS \
-    Xq, rinit, mask, Qq, lsl, qscal, G, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, pace, pace_tag, gate, \
+    Xq, rinit, mask, Qq, lsl, qscal, G, N, B, n_qblocks, n_steps, n_wg, spw, gl_s, gl_i, gl_cnt, gl_cap, gthr, gate, \
         chkp, chk_ld, chk_l, st
 #define S8_ONE(P, M, KPV, QTV, PXV, CAPV, NTV, QLV, FSV, KWV)   \
-    if (KP == KPV && nt == NTV && ql == QLV && fs == FSV && !q4) \
+    if (KP == KPV && nt == NTV && ql == QLV && fs == FSV)        \
         return scan8_launch<P, M, QTV, PXV, KPV, CAPV, NTV, QLV, FSV, KWV>(S8_ARGS);
-// The 128-query shape (scan8_q4, short rows, KP = 128): the query block (128 x D x planes) in
-// LDS, ONE row tile per wave and step (the I8X3 H and L sets of 4 query tiles: 128 registers),
-// a workgroup keeps KW = 48 of KP = 128 per query (CAP 64: 64 KiB of lists).  Twice the MFMAs
-// per corpus byte of the 64-query shape, and half the query blocks re-reading each row range
-// (C4, 10M x 128, B = 512: 8 -> 4 blocks).
-#if VDB_S8_NW == 4
-#define S8_ONE4(P, M, FSV)                    \
-    if (KP == 128 && ql && fs == FSV && q4)   \
-        return scan8_launch<P, M, 4, 4, 128, 64, false, true, FSV, 48, 1>(S8_ARGS);
-#else  // (4 waves only: scan8_q4_fits says no)
-#define S8_ONE4(P, M, FSV)
-#endif
 // KP = 256 keeps 64-query blocks: a workgroup keeps its best KW = 64 per query (LDS 64 KiB, 48
 // with the query block in LDS beside it; the drop bound -> gthr, vdb_scan2_kernel.h), so a
 // 64-query batch reads the corpus once
@@ -955,7 +878,7 @@ inline bool scan8_qlds(int G8, int KP, int prec, int metric, bool small) {
     S8_KP(P, M, PXV, false, false, false) S8_KP(P, M, PXV, true, false, false) \
     S8_KP(P, M, PXL, false, true, false) S8_KP(P, M, PXL, false, true, true)   \
     S8_KP(P, M, PXV, false, false, true) S8_KP(P, M, PXV, true, false, true)   \
-    S8_KP_NTQL(P, M, PXL) S8_ONE4(P, M, false) S8_ONE4(P, M, true)
+    S8_KP_NTQL(P, M, PXL)
 #define S8_UNIT(NAME, P, M, PXV, PXL)  \
     hipError_t NAME(S8_UNIT_PARAMS) {  \
         S8_MODES(P, M, PXV, PXL)       \

@@ -35,10 +35,33 @@
 
 namespace vdb {
 
-constexpr int W8_NW = 8;   // waves per workgroup: one 64-query block each (two per SIMD)
-constexpr int W8_QT = 2;   // query tiles per wave
+// waves per workgroup and query tiles (32 queries) per wave: 8 x 2 (two waves per SIMD, 64
+// queries each) by default; 16 x 1 (four per SIMD) an A/B build
+#ifndef VDB_W8_NW
+#define VDB_W8_NW 8
+#endif
+#ifndef VDB_W8_QT
+#define VDB_W8_QT 2
+#endif
+// A/B build knobs: VDB_W8_PF 1 = the next tile's operands read from LDS before this tile's
+// MFMAs; VDB_W8_STAGGER n = the second wave of each SIMD starts every stage ~64 n cycles late
+#ifndef VDB_W8_PF
+#define VDB_W8_PF 0
+#endif
+#ifndef VDB_W8_STAGGER
+#define VDB_W8_STAGGER 0
+#endif
+// VDB_W8_HFIRST 1 (default): a tile's H products (the tile tests' operand) issued before its L
+// products, so the tile tests run under the wave's own L MFMAs (C4 scan -1..2%, r06_wide7)
+#ifndef VDB_W8_HFIRST
+#define VDB_W8_HFIRST 1
+#endif
+constexpr int W8_NW = VDB_W8_NW;
+constexpr int W8_QT = VDB_W8_QT;
 constexpr int W8_G = 4;    // 32-dim groups (Dp = 128)
-constexpr int W8_QB = W8_NW * 64;  // queries per workgroup
+constexpr int W8_QW = W8_QT * 32;    // queries per wave
+constexpr int W8_QB = W8_NW * W8_QW;  // queries per workgroup
+static_assert(W8_QB == 512, "512 queries per workgroup");
 
 template <int PREC>
 __host__ __device__ constexpr int w8_ntile() { return Planes8<PREC>::XPL == 2 ? 8 : 16; }
@@ -47,7 +70,7 @@ __host__ __device__ constexpr size_t w8_slot_bytes() {
     return (size_t)w8_ntile<PREC>() * W8_G * Planes8<PREC>::XPL * 1024 + (METRIC == 1 ? (size_t)w8_ntile<PREC>() * 128 : 0);
 }
 template <int PREC, int METRIC>
-__host__ __device__ constexpr size_t w8_lds_bytes() { return 2 * w8_slot_bytes<PREC, METRIC>() + (size_t)W8_NW * 64 * 4; }
+__host__ __device__ constexpr size_t w8_lds_bytes() { return 2 * w8_slot_bytes<PREC, METRIC>() + (size_t)W8_QB * 4; }
 
 // the LDS byte address of a __shared__ object (the LDS-DMA destination base is an address, M0)
 __device__ __forceinline__ uint32_t w8_lds_addr(const void* p) {
@@ -83,40 +106,36 @@ scan8w_kernel(const float* __restrict__ Xq, const int* __restrict__ rs8, const u
     constexpr size_t CORP_B = NTILE * TILE_B;
     constexpr size_t SLOT_B = w8_slot_bytes<PREC, METRIC>();
     constexpr size_t GSTEP = 8 * BLOCK_FLOATS, PLANE = 4 * BLOCK_FLOATS;
-    static_assert(XPL * NTILE * G == 8 * NW, "8 corpus loads per wave and stage");
+    constexpr int QW = W8_QW;
+    constexpr int LPW = XPL * NTILE * G / NW;  // corpus loads per wave and stage
+    static_assert(XPL * NTILE * G == LPW * NW, "corpus loads spread evenly over the waves");
     extern __shared__ __attribute__((aligned(16))) char s_dyn[];
-    int* s_seg = (int*)(s_dyn + 2 * SLOT_B);  // [NW][64]: this workgroup's entries per query
+    int* s_seg = (int*)(s_dyn + 2 * SLOT_B);  // [NW][QW]: this workgroup's entries per query
 
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int w = blockIdx.x, n_seg = gridDim.x;
-    const int q0 = (blockIdx.y * NW + wv) * 64;  // this wave's queries q0 .. q0 + 63
+    const int q0 = (blockIdx.y * NW + wv) * QW;  // this wave's queries q0 .. q0 + QW - 1
     const bool active = q0 < Bp;                 // (wave-uniform: a block past the padded batch only loads)
     const int64_t T = (N + 31) >> 5;
     const int64_t my_tiles = T > w ? (T - 1 - w) / n_seg + 1 : 0;
     const int64_t n_stages = (my_tiles + NTILE - 1) / NTILE;
     const uint32_t ring = w8_lds_addr(s_dyn);
-    const size_t XPLANE = corpus_plane(G);
 
-    s_seg[wv * 64 + lane] = 0;
+    if (lane < QW) s_seg[wv * QW + lane] = 0;
 
-    // This wave's share of stage m's LDS-DMA loads into slot sl: 8 corpus blocks (one row tile,
-    // or two, all groups and planes) and, L2, one 1 KiB piece of the batch's integer start values
-    // (8 row tiles x 128 B, a per-lane source address each)
+    // This wave's share of stage m's LDS-DMA loads into slot sl: LPW of the stage's 64 corpus
+    // blocks (1 KiB each: row tile, group, plane) and, L2, waves 0 .. NTILE / 8 - 1 one 1 KiB piece
+    // of the batch's integer start values each (8 row tiles x 128 B, a per-lane source address)
     auto issue = [&](int64_t m, int sl) {
         const uint32_t sbase = ring + (uint32_t)(sl * SLOT_B);
 #pragma unroll
-        for (int u = 0; u < (XPL == 1 ? 2 : 1); ++u) {
-            const int i = wv + NW * u;
+        for (int u = 0; u < LPW; ++u) {
+            const int j = wv * LPW + u;  // (tile, group, plane) block j of the stage
+            const int i = j / (G * XPL), g = (j / XPL) % G, pl = j % XPL;
             const int64_t t = (m * NTILE + i) * n_seg + w;
-            if (t < T) {
-#pragma unroll
-                for (int g = 0; g < G; ++g)
-#pragma unroll
-                    for (int pl = 0; pl < XPL; ++pl)
-                        w8_glds<NT>(Xq + corpus_block((uint64_t)t, g, pl, G) + lane * 4,
-                                    sbase + (uint32_t)(((i * G + g) * XPL + pl) * 1024));
-            }
+            if (t < T)
+                w8_glds<NT>(Xq + corpus_block((uint64_t)t, g, pl, G) + lane * 4, sbase + (uint32_t)(j * 1024));
         }
         if constexpr (METRIC == 1) {
             if (wv < NTILE / 8) {
@@ -162,30 +181,48 @@ scan8w_kernel(const float* __restrict__ Xq, const int* __restrict__ rs8, const u
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
         if (m + 1 < n_stages) issue(m + 1, (int)((m + 1) & 1));
         if (!active) continue;
+#if VDB_W8_STAGGER > 0
+        // the waves sharing a SIMD (w, w + 4, ...: a workgroup's waves go to the SIMDs in a fixed
+        // cyclic order) start the stage a fraction of a tile apart, so one's epilogue runs under
+        // the other's MFMAs instead of all of them leaving the matrix pipe idle together
+        for (int z = 0; z < (wv >> 2) * VDB_W8_STAGGER / (NW >> 2); ++z) __builtin_amdgcn_s_sleep(1);
+#endif
         const char* slot = s_dyn + (size_t)(m & 1) * SLOT_B;
-        for (int i = 0; i < NTILE; ++i) {
-            const int64_t t = (m * NTILE + i) * n_seg + w;
-            if (t >= T) break;
-            f32x4 xr[G][1][XPL];
+        const int n_here = (int)min<int64_t>(NTILE, my_tiles - m * NTILE);  // this stage's tiles
+        // a tile's operands from the slot: the A blocks and (L2) the rows' integer start values
+        // (lane half h holds rows 32 t + 8 a + 4 h + b of its accumulator registers 4 a + b)
+        auto ld_tile = [&](int i, f32x4 (&x)[G][1][XPL], i32x4 (&r)[4]) {
 #pragma unroll
             for (int g = 0; g < G; ++g)
 #pragma unroll
                 for (int pl = 0; pl < XPL; ++pl)
-                    xr[g][0][pl] = *(const f32x4*)(slot + (size_t)i * TILE_B + (size_t)((g * XPL + pl) * 1024) + lane * 16);
+                    x[g][0][pl] = *(const f32x4*)(slot + (size_t)i * TILE_B + (size_t)((g * XPL + pl) * 1024) + lane * 16);
+            if constexpr (METRIC == 1) {
+#pragma unroll
+                for (int a = 0; a < 4; ++a)
+                    r[a] = *(const i32x4*)(slot + CORP_B + (size_t)i * 128 + (size_t)(8 * a + 4 * (lane >> 5)) * 4);
+            }
+        };
+#if VDB_W8_PF
+        f32x4 xr[G][1][XPL];
+        i32x4 rr[4];
+        ld_tile(0, xr, rr);
+#endif
+        for (int i = 0; i < n_here; ++i) {
+            const int64_t t = (m * NTILE + i) * n_seg + w;
+#if VDB_W8_PF
+            f32x4 xn[G][1][XPL];
+            i32x4 rn[4];
+#else
+            f32x4 xr[G][1][XPL];
+            i32x4 rr[4];
+            ld_tile(i, xr, rr);
+#endif
             i32x16 aH[1][QT], aL[1][QT];
             {
                 i32x16 init;
 #pragma unroll
-                for (int v = 0; v < 16; ++v) init[v] = 0;
-                if constexpr (METRIC == 1) {
-                    // lane half h holds rows 32 t + 8 a + 4 h + b of its accumulator registers 4 a + b
-#pragma unroll
-                    for (int a = 0; a < 4; ++a) {
-                        const i32x4 r4 = *(const i32x4*)(slot + CORP_B + (size_t)i * 128 + (size_t)(8 * a + 4 * (lane >> 5)) * 4);
-#pragma unroll
-                        for (int b2 = 0; b2 < 4; ++b2) init[4 * a + b2] = r4[b2];
-                    }
-                }
+                for (int v = 0; v < 16; ++v) init[v] = METRIC == 1 ? rr[v >> 2][v & 3] : 0;
 #pragma unroll
                 for (int qt = 0; qt < QT; ++qt) {
                     aH[0][qt] = init;
@@ -193,9 +230,60 @@ scan8w_kernel(const float* __restrict__ Xq, const int* __restrict__ rs8, const u
                     for (int v = 0; v < 16; ++v) aL[0][qt][v] = 0;
                 }
             }
+#if VDB_W8_HFIRST
+            // every H product of the tile first, then the L ones: the tile tests read H alone, so
+            // they run while the wave's own L MFMAs still execute
 #pragma unroll
-            for (int g = 0; g < G; ++g) group_mfma8<PREC, 1, QT>(xr[g], qr[g], aH, aL);
+            for (int g = 0; g < G; ++g)
+#pragma unroll
+                for (int qt = 0; qt < QT; ++qt)
+                    aH[0][qt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(__builtin_bit_cast(i32x4, xr[g][0][0]),
+                                                                      __builtin_bit_cast(i32x4, qr[g][qt][0]), aH[0][qt], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);  // (the scheduler would interleave them again)
+            if constexpr (HL) {
+#pragma unroll
+                for (int g = 0; g < G; ++g)
+#pragma unroll
+                    for (int qt = 0; qt < QT; ++qt) {
+                        aL[0][qt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(__builtin_bit_cast(i32x4, xr[g][0][0]),
+                                                                          __builtin_bit_cast(i32x4, qr[g][qt][QPL - 1]), aL[0][qt], 0, 0, 0);
+                        if constexpr (PREC == PREC_I8X3)
+                            aL[0][qt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(__builtin_bit_cast(i32x4, xr[g][0][XPL - 1]),
+                                                                              __builtin_bit_cast(i32x4, qr[g][qt][0]), aL[0][qt], 0, 0, 0);
+                    }
+            }
+            if (false)
+#endif
+            group_mfma8<PREC, 1, QT>(xr[0], qr[0], aH, aL);
+#if VDB_W8_PF
+            // the next tile's operands, read after this tile's first MFMAs issued: their LDS
+            // latency runs under this tile's MFMAs (read before them, hipcc's loop-header wait
+            // for the operands in flight waited for these too: lgkmcnt(0) before the first MFMA)
+            __builtin_amdgcn_sched_barrier(0);
+            if (i + 1 < n_here) ld_tile(i + 1, xn, rn);
+            __builtin_amdgcn_sched_barrier(0);
+#endif
+#pragma unroll
+            for (int g = 1; g < G; ++g)
+                if (!VDB_W8_HFIRST) group_mfma8<PREC, 1, QT>(xr[g], qr[g], aH, aL);
+#if VDB_W8_PF
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+#pragma unroll
+                for (int pl = 0; pl < XPL; ++pl) xr[g][0][pl] = xn[g][0][pl];
+#pragma unroll
+            for (int a = 0; a < 4; ++a) rr[a] = rn[a];
+#endif
 
+#ifdef VDB_SCAN8W_KLOOP_ONLY
+            {  // diagnostic build (make wvariant): the K-loop alone, results are garbage
+                int f = 0;
+#pragma unroll
+                for (int qt = 0; qt < QT; ++qt) f += imax16(aH[0][qt]) + (HL ? imax16(aL[0][qt]) : 0);
+                if (f == 123456789) gl_s[0] = (float)f;
+                continue;
+            }
+#endif
             // ---- epilogue: the tile tests (H only, minus the L term's slack), the checksum ----
             uint32_t todo = 0;
 #pragma unroll
@@ -224,6 +312,10 @@ scan8w_kernel(const float* __restrict__ Xq, const int* __restrict__ rs8, const u
                         }
                 }
             }
+#ifdef VDB_SCAN8W_NOINS
+            if (todo == 0xdeadu) gl_s[1] = 0.0f;  // diagnostic build: tile tests without insertions
+            todo = 0;
+#endif
             // ---- the rare insertions: straight into this (workgroup, query) segment ----
             while (todo != 0u) {
                 const int qt = __builtin_amdgcn_readfirstlane(__builtin_ctz(todo));
@@ -244,7 +336,7 @@ scan8w_kernel(const float* __restrict__ Xq, const int* __restrict__ rs8, const u
                 }
                 pm &= cand;
                 int pos = 0;
-                if (pm != 0u) pos = atomicAdd(&s_seg[wv * 64 + ql], __builtin_popcount(pm));
+                if (pm != 0u) pos = atomicAdd(&s_seg[wv * QW + ql], __builtin_popcount(pm));
                 const uint32_t rb = (uint32_t)(t * 32) + 4u * (uint32_t)(lane >> 5);
                 float* ls = gl_s + (size_t)qg * gl_cap + (size_t)w * W8_CH;
                 uint32_t* li = gl_i + (size_t)qg * gl_cap + (size_t)w * W8_CH;
@@ -266,7 +358,7 @@ scan8w_kernel(const float* __restrict__ Xq, const int* __restrict__ rs8, const u
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (!active) return;
     // this workgroup's entries per query (the finish's segment counts; > W8_CH = overflowed)
-    if (q0 + lane < B) seg_cnt[(size_t)(q0 + lane) * n_seg + w] = (uint32_t)s_seg[wv * 64 + lane];
+    if (lane < QW && q0 + lane < B) seg_cnt[(size_t)(q0 + lane) * n_seg + w] = (uint32_t)s_seg[wv * QW + lane];
     // the checksum's partial sums: the tile's two row halves (lanes l, l + 32), one word per
     // (plane, query, workgroup)
     if (chkp) {

@@ -124,6 +124,39 @@ def reference_batch_search(queries, vectors, k=10):
     return idx.astype(np.int64), np.take_along_axis(S, idx, axis=1)
 
 
+def reference_l2_batch_chunked(queries, vectors, k=10, chunk_rows=1 << 20):
+    """A batch of the store's L2 queries (`_compiled_euclidean_distance`,
+    service/optimized_vector_store.py:43-48: sqrt(sum((x - q)^2)) per row, fp32) with the full
+    stable argsort of `_brute_force_search` (:176-183) replaced by a running top-k over corpus
+    chunks (C4's [512, 10M] distance matrix would be 20 GB).  Merging by
+    (distance asc, row asc) keeps exactly the rows the full stable argsort's [:k] would, in the
+    same order.  Returns (indices int64 [B, k'], distances fp32 [B, k']), k' = min(k, N)."""
+    Q = np.asarray(queries, dtype=np.float32)
+    V = np.asarray(vectors, dtype=np.float32)
+    B, N = Q.shape[0], V.shape[0]
+    kk = min(k, N)
+    best_d = np.full((B, 0), np.inf, np.float32)
+    best_i = np.zeros((B, 0), np.int64)
+    for r0 in range(0, N, chunk_rows):
+        C = V[r0:r0 + chunk_rows]
+        d = np.empty((B, C.shape[0]), np.float32)
+        for b in range(B):
+            diff = C - Q[b]
+            d[b] = np.sqrt(np.sum(diff * diff, axis=1, dtype=np.float32))
+        kc = min(kk, C.shape[0])
+        vk = np.partition(d, kc - 1, axis=1)[:, kc - 1]  # every row <= the chunk's kc-th distance (ties kept)
+        nd = np.full((B, kk), np.inf, np.float32)
+        ni = np.zeros((B, kk), np.int64)
+        for b in range(B):
+            sel = np.flatnonzero(d[b] <= vk[b])
+            cd = np.concatenate([best_d[b], d[b, sel]])
+            ci = np.concatenate([best_i[b], sel.astype(np.int64) + r0])
+            order = np.lexsort((ci, cd))[:kk]  # (distance asc, row asc): lexsort's last key is primary
+            nd[b, :order.size], ni[b, :order.size] = cd[order], ci[order]
+        best_d, best_i = nd, ni
+    return best_i, best_d
+
+
 # =============================================================================
 # 2. The exact ranking contract (fp64, canonical order) the GPU path must match
 # =============================================================================

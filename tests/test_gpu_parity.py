@@ -125,24 +125,6 @@ def test_finish_long_rows(vdb, split, D, metric):
         _check(vdb, V, Q, k, metric, precision="i8", params={"finish_split": split})
 
 
-@pytest.mark.parametrize("precision", ["bf16x3", "bf16"])
-@pytest.mark.parametrize("metric", ["cosine", "euclidean"])
-@pytest.mark.parametrize("D,B,k", [(320, 150, 100), (768, 40, 10), (1000, 20, 150)])
-def test_scan_query_ring(vdb, precision, metric, D, B, k):
-    """The candidate pass with the query operand through the per-workgroup LDS ring
-    (index param scan_qring: chunks of 4 dim groups, double-buffered, one barrier per chunk):
-    several query blocks, KP 32 to 256 (k 10 / 100 / 150 plus the margin), ragged D; the
-    overflowing data of test_scan_step_sync_modes keeps the compaction rounds busy."""
-    rng = np.random.default_rng(D + B)
-    N = 40000
-    Q = rng.random((B, D), dtype=np.float32)
-    t = (np.arange(N, dtype=np.float32) / N)[:, None]
-    V = (Q[rng.integers(0, B, N)] * t + rng.random((N, D), dtype=np.float32) * (1.0 - t)).astype(np.float32)
-    ix, _, _ = _check(vdb, V, Q, k, metric, precision=precision, params={"scan_qring": 1})
-    with pytest.raises(Exception):
-        ix.set_param("scan_qring", 2)
-
-
 @pytest.mark.parametrize("precision", ["bf16x3", "i8", "i8x3"])
 @pytest.mark.parametrize("sync", [1, 2])
 @pytest.mark.parametrize("metric", ["cosine", "euclidean"])
@@ -760,52 +742,6 @@ def test_full_size_c2_subset(vdb, precision):
 
 
 @pytest.mark.parametrize("metric", ["cosine", "euclidean"])
-@pytest.mark.parametrize("precision", ["bf16", "bf16x3"])
-def test_scan3_large_batch_pass(vdb, metric, precision):
-    """The large-batch candidate pass (vdb_scan3_kernel.h, knob "scan3" = 1): query blocks of 256
-    over rows shared through LDS, KW = 32 kept per query and workgroup.  Bit-exact vs the oracle
-    for ragged batches (1, 64, 300: two blocks, the second partial), k up to 100, D in {128 (the
-    compile-time group count), 200 (ragged), 768}, a filter mask, and a corpus whose clustered
-    rows put more than KW of a query's top k into one workgroup (the drop bound then sends that
-    query to the exact path, still exact)."""
-    rng = np.random.default_rng(61)
-    for D, N in ((128, 70_000), (200, 30_011), (768, 20_000)):
-        V = rng.random((N, D), dtype=np.float32)
-        Q = rng.random((300, D), dtype=np.float32)
-        Q[7], Q[299] = V[N - 1], V[12345]
-        ix = vdb.NativeIndex(D, metric, precision=precision)
-        ix.set_param("scan3", 1)
-        ix.add(V)
-        for B, k in ((300, 10), (64, 100), (1, 5)):
-            s, i, kk = ix.search(Q[:B], k, with_keys=True)
-            es, ei, ek = ref_cpu.exact_search(Q[:B], V, k, metric)
-            np.testing.assert_array_equal(i, ei)
-            np.testing.assert_array_equal(kk, ek)
-        mask = rng.random(N) < 0.3
-        bits = np.zeros(((N + 31) // 32) * 32, bool)
-        bits[:N] = mask
-        words = np.packbits(bits, bitorder="little").view("<u4").astype(np.uint32)
-        s, i, kk = ix.search(Q[:260], 16, row_mask=words, with_keys=True)
-        es, ei, ek = ref_cpu.exact_search(Q[:260], V, 16, metric, row_mask=mask)
-        np.testing.assert_array_equal(i, ei)
-        np.testing.assert_array_equal(kk, ek)
-        assert ix.stat("searches_scan3") == 4
-        ix.close()
-    # 40 near copies of one row inside one workgroup's range: > KW of the query's top 50 there
-    V = rng.random((40_000, 96), dtype=np.float32)
-    V[20_000:20_040] = (V[5] + 1e-3 * rng.random((40, 96))).astype(np.float32)
-    Q = np.concatenate([V[5:6], rng.random((199, 96), dtype=np.float32)])
-    ix = vdb.NativeIndex(96, metric, precision=precision)
-    ix.set_param("scan3", 1)
-    ix.add(V)
-    s, i, kk = ix.search(Q, 50, with_keys=True)
-    es, ei, ek = ref_cpu.exact_search(Q, V, 50, metric)
-    np.testing.assert_array_equal(i, ei)
-    np.testing.assert_array_equal(kk, ek)
-    ix.close()
-
-
-@pytest.mark.parametrize("metric", ["cosine", "euclidean"])
 def test_scan2_q4_shape(vdb, metric):
     """The split pass's 128-query shape (knob "scan_q4" = 1; D <= 128, KP = 128, B >= 256):
     query block of 128 in LDS, 2 row tiles per wave, 48 kept per query and workgroup with the
@@ -846,56 +782,6 @@ def test_scan2_q4_shape(vdb, metric):
     es, ei, ek = ref_cpu.exact_search(Q, V, 100, metric)
     np.testing.assert_array_equal(i, ei)
     np.testing.assert_array_equal(kk, ek)
-    ix.close()
-
-
-@pytest.mark.parametrize("metric", ["cosine", "euclidean"])
-def test_scan8_q4_shape(vdb, metric):
-    """The int8 pass's 128-query shape (D <= 128, KP = 128, B >= 256; knob scan_q4 = 1, opt-in):
-    the query block of 128 in LDS, one row tile per wave, 48 kept per query and workgroup with the
-    drop bound raising gthr at the end.  Bit-exact vs the oracle for I8X3 (k = 100) and I8 at
-    KP = 128 (margin 100), compile-time (D = 128) and runtime (D = 64, 96) group counts, ragged
-    batches, a mask, against the 64-query shape (scan_q4 = 0), and clustered rows that put more
-    than 48 of a query's top 100 into one workgroup."""
-    rng = np.random.default_rng(71)
-    for D, N in ((128, 120_000), (64, 50_003), (96, 40_000)):
-        V = rng.random((N, D), dtype=np.float32)
-        Q = rng.random((520, D), dtype=np.float32)
-        Q[3], Q[519] = V[N - 1], V[777]
-        for prec, k, margin in (("i8x3", 100, None), ("i8", 10, 100)):
-            for q4 in (1, 0):
-                ix = vdb.NativeIndex(D, metric, precision=prec)
-                ix.set_param("scan_q4", q4)
-                if margin is not None:
-                    ix.set_param("margin", margin)
-                ix.add(V)
-                for B in (520, 256):
-                    s, i, kk = ix.search(Q[:B], k, with_keys=True)
-                    es, ei, ek = ref_cpu.exact_search(Q[:B], V, k, metric)
-                    np.testing.assert_array_equal(i, ei, err_msg=f"{prec} D {D} B {B} q4 {q4}")
-                    np.testing.assert_array_equal(kk, ek)
-                mask = rng.random(N) < 0.4
-                bits = np.zeros(((N + 31) // 32) * 32, bool)
-                bits[:N] = mask
-                words = np.packbits(bits, bitorder="little").view("<u4").astype(np.uint32)
-                s, i, kk = ix.search(Q[:300], k, row_mask=words, with_keys=True)
-                es, ei, ek = ref_cpu.exact_search(Q[:300], V, k, metric, row_mask=mask)
-                np.testing.assert_array_equal(i, ei)
-                np.testing.assert_array_equal(kk, ek)
-                assert ix.stat("searches_q4") == (3 if q4 else 0)
-                print(f"{metric} {prec} D {D} q4 {q4}: fallbacks {ix.stat('fallback_queries')}")
-                ix.close()
-    V = rng.random((60_000, 128), dtype=np.float32)
-    V[30_000:30_070] = (V[9] + 1e-3 * rng.random((70, 128))).astype(np.float32)
-    Q = np.concatenate([V[9:10], rng.random((299, 128), dtype=np.float32)])
-    ix = vdb.NativeIndex(128, metric, precision="i8x3")
-    ix.set_param("scan_q4", 1)
-    ix.add(V)
-    s, i, kk = ix.search(Q, 100, with_keys=True)
-    es, ei, ek = ref_cpu.exact_search(Q, V, 100, metric)
-    np.testing.assert_array_equal(i, ei)
-    np.testing.assert_array_equal(kk, ek)
-    assert ix.stat("searches_q4") == 1
     ix.close()
 
 

@@ -214,3 +214,21 @@ def test_graph_build_restatement_small():
             row = nbr[v][nbr[v] >= 0]
             assert row.size >= 1 and v not in row and len(set(row.tolist())) == row.size
         assert ent.tolist() == [i * 300 // 8 for i in range(8)]
+
+
+def test_l2_batch_chunked_equals_the_store_path():
+    """The chunked L2 batch (bench.py's C4 CPU baseline) returns exactly what the
+    store's per-query path (`_compiled_euclidean_distance` + stable argsort [:k]) returns, ties
+    included (duplicate rows straddling chunk boundaries)."""
+    rng = np.random.default_rng(3)
+    V = rng.random((5000, 24), dtype=np.float32)
+    V[1999:2003] = V[10]  # ties at a chunk boundary (chunk 1000 rows)
+    V[4500] = V[10]
+    Q = rng.random((7, 24), dtype=np.float32)
+    Q[0] = V[10]
+    for k in (1, 10, 37):
+        idx, dist = ref_cpu.reference_l2_batch_chunked(Q, V, k, chunk_rows=1000)
+        for b in range(Q.shape[0]):
+            ri, rs, _ = ref_cpu.reference_store_search(Q[b], V, k, "euclidean")
+            assert idx[b].tolist() == ri
+            np.testing.assert_array_equal(dist[b], np.asarray(rs, np.float32))
