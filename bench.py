@@ -239,22 +239,26 @@ def cpu_graph_baseline(V, nbr, entries, Q, k, ef, metric, gt, budget_s=15.0):
             "recall_at_10": hits / float(n * k)}
 
 
-def main_graph(args, world, rank, local, dev):
+def bench_graph(args, world, rank, local, dev, primary=True):
     """C5: the graph path at batch 1.  N>1 runs independent replicas (SURVEY.md §8e:
     each GPU holds the whole graph and serves its own queries); value = all queries
-    served / the slowest rank's time."""
+    served / the slowest rank's time.  Returns the record on rank 0 (None elsewhere);
+    primary=False: the default run's sub-record (BASELINE's rows, no tuning flags)."""
     from performance.hnsw_index import N_ENTRIES, TEAMS
+    rec = None
     if args.teams is None:
         args.teams = TEAMS
     N, D, B, k, metric, desc = CONFIGS["c5"]
-    N = args.rows or N
+    N = (args.rows if primary else None) or N
+    if rank == 0:
+        print("bench: c5 start", file=sys.stderr, flush=True)
     R = 2 * GRAPH_M
     knn = args.graph_knn or R
     ix = _vdb.NativeIndex(D, metric, local)
     ix.reserve(N)
     keep_host = world == 1 and rank == 0 and not args.no_cpu_baseline
     parts = []
-    clustered = args.data == "clustered"
+    clustered = args.data == "clustered" and primary
     cen = cluster_centres(D) if clustered else None
     for s0 in range(0, N, 8 * CHUNK_ROWS):
         part = (corpus_rows_clustered(N, D, s0, min(s0 + 8 * CHUNK_ROWS, N), centres=cen) if clustered
@@ -263,7 +267,7 @@ def main_graph(args, world, rank, local, dev):
         if keep_host:
             parts.append(part)
     t0 = time.perf_counter()
-    n_ent = args.graph_entries or N_ENTRIES
+    n_ent = (args.graph_entries if primary else None) or N_ENTRIES
     g = _vdb.NativeGraph.build(ix, degree=R, knn=knn, n_entries=n_ent)
     build_s = time.perf_counter() - t0
     g.set_param("teams", args.teams)
@@ -326,7 +330,7 @@ def main_graph(args, world, rank, local, dev):
         bl.append(time.perf_counter() - t1)
     # the same queries at other team counts (p50 over <= 100 single queries, recall)
     sweep = []
-    for tm in [int(x) for x in args.teams_sweep.split(",") if x.strip()]:
+    for tm in [int(x) for x in (args.teams_sweep if primary else "").split(",") if x.strip()]:
         if tm == args.teams:
             continue
         g.set_param("teams", tm)
@@ -389,8 +393,12 @@ def main_graph(args, world, rank, local, dev):
             V = np.concatenate(parts) if len(parts) > 1 else parts[0]
             del parts
             nbr, ent = g.to_arrays()
-            rec["cpu_baseline"] = cpu_graph_baseline(V, nbr, ent, Qt, k, GRAPH_EF, metric, gt)
-        print(json.dumps(rec), flush=True)
+            print("bench: c5 cpu baseline", file=sys.stderr, flush=True)
+            rec["cpu_baseline"] = cpu_graph_baseline(V, nbr, ent, Qt, k, GRAPH_EF, metric, gt,
+                                                     budget_s=15.0 if primary else 8.0)
+    g.close()
+    ix.close()
+    return rec
     g.close()
     if world > 1:
         dist.barrier()
@@ -490,6 +498,7 @@ def main():
     ap.add_argument("--graph-entries", type=int, default=None,
                     help="c5: entry rows of the graph (default performance/hnsw_index.py N_ENTRIES)")
     ap.add_argument("--teams-sweep", default="16,64", help="c5: extra teams settings reported beside the line")
+    ap.add_argument("--no-graph", action="store_true", help="default run: skip the c5 (graph) sub-record")
     ap.add_argument("--data", default="uniform", choices=["uniform", "clustered"],
                     help="c5: the corpus (BASELINE's uniform [0,1) rows, or rows around cluster centres: the "
                          "structured data a graph index is for)")
@@ -513,11 +522,11 @@ def main():
     else:
         torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if args.config == "c5":
-        return main_graph(args, world, rank, local, dev)
-
     cfg = args.config or "c2"
-    rec = bench_brute(cfg, args, world, rank, local, dev, primary=True)
+    if cfg == "c5":
+        rec = bench_graph(args, world, rank, local, dev)
+    else:
+        rec = bench_brute(cfg, args, world, rank, local, dev, primary=True)
     if args.config is None:
         # The default run also measures, on the same ranks, as compact sub-records (so the driver's
         # N = 1, 2, 4, 8 series carries them all):
@@ -539,6 +548,15 @@ def main():
                                                        "traffic_source", "avg_launch_ms", "precision", "basis",
                                                        "fp32_equivalent")}
         _HOST_CORPUS.clear()
+        if not args.no_other_configs and not args.no_graph:
+            # c5, BASELINE.json configs[4]: the graph path at batch 1, with the
+            # exact path's batch-1 p50 on the same queries beside it
+            sub = bench_graph(args, world, rank, local, dev, primary=False)
+            if rank == 0:
+                rec["config_c5"] = {k_: sub[k_] for k_ in ("value", "unit", "n_gpus", "steps", "ms_per_step", "p50_ms",
+                                                           "p99_ms", "recall_at_10", "exact_b1_p50_ms", "scaling",
+                                                           "dtype", "config", "build_s", "iterations_per_query",
+                                                           "visited_per_query", "roofline", "cpu_baseline") if k_ in sub}
     if rank == 0:
         print(json.dumps(rec), flush=True)
     if world > 1:

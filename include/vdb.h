@@ -131,28 +131,23 @@ int32_t vdb_index_create(int32_t dim, int32_t metric, int32_t device, vdb_index*
 int32_t vdb_index_destroy(vdb_index* idx);
 /* Pre-size the device corpus for `rows` rows (capacity otherwise doubles). */
 int32_t vdb_index_reserve(vdb_index* idx, int64_t rows);
-/* Tuning / test knobs: "precision" (VDB_PREC_*), "margin" (extra candidates
- * per query), "force_exact" (0/1), "n_wg" (candidate-pass workgroups),
- * "scan_variant" / "scan_variant_bf16x3" (0..2, kernel tiling variants),
- * "scan_sync" (candidate-pass step end: 0 auto = flag-gated for the int8 pass and for
- * rows of <= 128 dims, a per-step barrier otherwise; 1 per-step barrier,
- * 2 flag-gated compaction rounds; results identical, speed differs),
- * "scan_publish" (split pass slot publishing: -1 auto = off (round 3 measurement), 0 off,
- * 1 on), "scan_q4" (split pass 128-query shape for D <= 128, KP = 128, B >= 256: -1 auto = on,
- * 0 off, 1 on where it applies), "scan_qlds" (-1 auto: query block in LDS when it fits, 0 never),
- * "scan_pace" (int8 pass, 0 default / 1: pace the query blocks that share a row range),
- * "scan3" (large-batch shape, vdb_scan3_kernel.h: 0 default off, 1 on, -1 auto), "scan_qring" (split pass, lockstep step ends: 1 = the
- * query operand through a per-workgroup LDS ring; start value from the environment
- * variable VDB_SCAN_QRING, default 0), "gate_div" (1..64: the device-gated exact
- * fallback runs on n_cu / gate_div row ranges, one query slot each when > 1; start value
- * from VDB_GATE_DIV, default 1), "dir_bound" (0: BF16 certificate with |q| R only;
- * diagnostics), "pilot_tiles", "pilot_rank", "pilot_fused", "finish_split",
- * "no_fallback" (diagnostics: flagged queries keep the approximate order),
- * "timing" (0/1: HIP events around the candidate pass; stats "scan_ns",
- * "pipeline_ns", "timed_searches").  Stats also: "searches", "queries",
- * "fallback_queries", "overflow_queries", "capacity", "count", "device_bytes", "precision",
- * "searches_fp32" / "searches_bf16x3" / "searches_bf16" / "searches_i8" / "searches_i8x3"
- * (candidate passes run in each; with VDB_PREC_AUTO these show its choices), "auto_int8". */
+/* Knobs.  "precision" (VDB_PREC_*; default VDB_PREC_AUTO), "margin" (extra candidates
+ * per query), "force_exact" (0/1), "no_fallback" (diagnostics: flagged queries keep the
+ * approximate order), "timing" (0/1: HIP events around the candidate pass; stats "scan_ns",
+ * "pipeline_ns", "timed_searches").  Tuning knobs the bench's A/B runs use (results identical,
+ * speed differs): "n_wg" (candidate-pass workgroups), "scan_variant" / "scan_variant_bf16x3"
+ * (fp32 / split pass tilings), "scan_sync" (0 auto, 1 per-step barrier, 2 flag-gated
+ * compaction rounds), "scan_q4" (split pass 128-query shape, -1 auto / 0 / 1), "scan_qlds"
+ * (-1 auto: query block in LDS when it fits, 0 never), "scan_wide" (the wide int8 pass for rows
+ * of <= 128 dims and batches of > 256: -1 auto from 65 536 rows, 0 off, 1 always),
+ * "scan_checksum" (1 default, 0 off, 2 also I8X3's L sums), "pilot_tiles", "pilot_rank",
+ * "finish_split", "i8_refine", "i8_narrow", "device_repass", "auto_int8", "auto_i8q",
+ * "dir_bound" (0: BF16 certificate with |q| R only).  Stats also: "searches", "queries",
+ * "fallback_queries", "overflow_queries", "inconsistent_queries", "repass_queries",
+ * "capacity", "count", "device_bytes", "precision", "searches_fp32" / "searches_bf16x3" /
+ * "searches_bf16" / "searches_i8" / "searches_i8x3" / "searches_i8q" (candidate passes run in
+ * each; with VDB_PREC_AUTO these show its choices), "searches_q4", "searches_wide",
+ * "auto_int8", "i8q_off", "i8_wide", "split_copy", "split_copy_builds". */
 int32_t vdb_index_set_param(vdb_index* idx, const char* name, int64_t value);
 int32_t vdb_index_get_stat(const vdb_index* idx, const char* name, int64_t* value);
 

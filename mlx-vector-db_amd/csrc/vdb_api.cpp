@@ -589,13 +589,17 @@ bool all_finite(const float* p, int64_t n) {
 }
 
 
+// query slots of the device-gated exact scan (each loops over the flagged queries)
+constexpr int kGateSlots = 4;
+
 // Exact full scan for queries qlist[0..nq) (device list) -> writes outputs.
 // Bytes of the exact path's lists for nq queries (device-gated form: one list per CU).
 size_t exact_bytes(vdb_index* ix, int nq, int k, bool gated) {
     const int KE = std::max(32, next_pow2(k));
     const int64_t n_wg = std::min<int64_t>(std::max<int64_t>(1, ix->n_cu * (gated ? 1 : 2)),
                                            std::max<int64_t>(1, ix->count / 256));
-    return (size_t)nq * n_wg * KE * (sizeof(double) + sizeof(uint32_t)) + (size_t)nq * KE * 12 + 4096;
+    return (size_t)nq * n_wg * KE * (sizeof(double) + sizeof(uint32_t)) + (size_t)nq * KE * 12 + 4096 +
+           (gated ? exact_scan_scratch_bytes(KE, (int)n_wg, std::min(nq, kGateSlots)) : 0);
 }
 
 // Exact scan of the queries qlist[0..nq) (or 0..nq).  Device-gated form (qcount_dev):
@@ -616,7 +620,9 @@ int run_exact(vdb_index* ix, Workspace* w, const float* Qd, const double* qn64, 
     n_wg = (int)((N + rpw - 1) / rpw);
     const int n_lists = n_wg;
     const size_t list_elems = (size_t)nq * n_lists * KE;
-    const size_t bytes = list_elems * (sizeof(double) + sizeof(uint32_t)) + (size_t)nq * KE * 12 + 4096;
+    // the device-gated form keeps its top-k buffers in the workspace (no LDS, vdb_exact.hip)
+    const size_t scr = gated && done_dev ? exact_scan_scratch_bytes(KE, n_wg, std::min(nq, kGateSlots)) : 0;
+    const size_t bytes = list_elems * (sizeof(double) + sizeof(uint32_t)) + (size_t)nq * KE * 12 + 4096 + scr;
     int rc = ws_reserve_exact(w, bytes, st);
     if (rc) return rc;
     Carver c{w->exact};
@@ -624,10 +630,12 @@ int run_exact(vdb_index* ix, Workspace* w, const float* Qd, const double* qn64, 
     uint32_t* li = c.take<uint32_t>(list_elems);
     double* mk = c.take<double>((size_t)nq * KE);
     uint32_t* mi = c.take<uint32_t>((size_t)nq * KE);
+    char* gscr = scr ? c.take<char>(scr) : nullptr;
     if (gated && done_dev) {  // one launch: the last workgroup per query merges and writes (ExactTail)
         const ExactTail tail{done_dev, mk, mi, k, index_offset, out_s, out_i, out_k, row_ids, host_totals};
         HIP_TRY(launch_exact_scan(ix->metric, KE, Qd, qn64, qlist_dev, nq, ix->X, ix->G, ix->dim, ix->nrm64, mask_dev,
-                                  N, n_wg, rpw, lk, li, st, qcount_dev, ovf_dev, ix->d_totals, &tail, 4));
+                                  N, n_wg, rpw, lk, li, st, qcount_dev, ovf_dev, ix->d_totals, &tail, kGateSlots,
+                                  gscr));
         return VDB_OK;
     }
     HIP_TRY(launch_exact_scan(ix->metric, KE, Qd, qn64, qlist_dev, nq, ix->X, ix->G, ix->dim, ix->nrm64, mask_dev, N,

@@ -1151,13 +1151,27 @@ exact_scan_kernel(const float* __restrict__ Q, const double* __restrict__ qn64, 
                   const float* __restrict__ X, int G, int D, const double* __restrict__ nrm64,
                   const uint32_t* __restrict__ mask, int64_t N, int64_t rows_per_wg, int KE,
                   double* __restrict__ lk, uint32_t* __restrict__ li, const int* __restrict__ qcount, int nq_max,
-                  const int* __restrict__ ovf, unsigned long long* __restrict__ totals, ExactTail tail) {
+                  const int* __restrict__ ovf, unsigned long long* __restrict__ totals, ExactTail tail,
+                  char* __restrict__ gscr) {
+    // The per-wave top-k buffers and the tail merge's scratch: LDS, or -- the device-gated form --
+    // the workspace (gscr: this launch's [slot][range][wave] buffers, then one merge scratch per
+    // slot), so the launch holds no LDS: an empty gated launch (nothing flagged, the common case)
+    // then retires beside another batch's scan instead of waiting for a CU with free LDS (C3's
+    // scan leaves ~3 KiB of its CU's 160)
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int cap = WaveTopK<double, uint32_t>::capacity(KE);
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
-    double* bk = reinterpret_cast<double*>(smem) + (size_t)wv * cap;
-    uint32_t* bi = reinterpret_cast<uint32_t*>(smem + (size_t)4 * cap * sizeof(double)) + (size_t)wv * cap;
+    const size_t nbuf = (size_t)gridDim.y * gridDim.x * 4;  // wave buffers of the launch (gscr)
+    const size_t b0 = ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 4;
+    double* kbase = gscr ? reinterpret_cast<double*>(gscr) + b0 * cap : reinterpret_cast<double*>(smem);
+    uint32_t* ibase = gscr ? reinterpret_cast<uint32_t*>(gscr + nbuf * cap * sizeof(double)) + b0 * cap
+                           : reinterpret_cast<uint32_t*>(smem + (size_t)4 * cap * sizeof(double));
+    char* mscr = gscr ? gscr + nbuf * cap * (sizeof(double) + sizeof(uint32_t)) +
+                            (size_t)blockIdx.y * merge_block_lds<double, uint32_t>(KE)
+                      : smem;
+    double* bk = kbase + (size_t)wv * cap;
+    uint32_t* bi = ibase + (size_t)wv * cap;
     // device-gated launch (qcount): the flagged queries are known only on the device;
     // query slots qi = blockIdx.y, + gridDim.y, ... below min(*qcount, nq_max)
     int nq = (int)gridDim.y;
@@ -1192,8 +1206,8 @@ exact_scan_kernel(const float* __restrict__ Q, const double* __restrict__ qn64, 
         __syncthreads();
         if (wv == 0) {
             for (int w = 1; w < 4; ++w) {
-                const double* ok = reinterpret_cast<double*>(smem) + (size_t)w * cap;
-                const uint32_t* oi = reinterpret_cast<uint32_t*>(smem + (size_t)4 * cap * sizeof(double)) + (size_t)w * cap;
+                const double* ok = kbase + (size_t)w * cap;
+                const uint32_t* oi = ibase + (size_t)w * cap;
                 for (int e0 = 0; e0 < KE; e0 += 64) {
                     const int e = e0 + lane;
                     const bool in = e < KE && oi[e] != 0xFFFFFFFFu;
@@ -1221,7 +1235,7 @@ exact_scan_kernel(const float* __restrict__ Q, const double* __restrict__ qn64, 
                 __threadfence();
                 const size_t q0 = (size_t)qi * gridDim.x * KE;
                 merge_block<double, uint32_t>(lk + q0, li + q0, (int)gridDim.x, KE, KE, KE, tail.mk + (size_t)qi * KE,
-                                              tail.mi + (size_t)qi * KE, smem);
+                                              tail.mi + (size_t)qi * KE, mscr);
                 __syncthreads();
                 for (int e = threadIdx.x; e < tail.k; e += 256) {
                     const double key = tail.mk[(size_t)qi * KE + e];
@@ -1238,11 +1252,16 @@ exact_scan_kernel(const float* __restrict__ Q, const double* __restrict__ qn64, 
     }
 }
 
+size_t exact_scan_scratch_bytes(int KE, int n_wg, int slots) {
+    return (size_t)slots * n_wg * 4 * WaveTopK<double, uint32_t>::capacity(KE) * (sizeof(double) + sizeof(uint32_t)) +
+           (size_t)slots * merge_block_lds<double, uint32_t>(KE) + 256;
+}
+
 hipError_t launch_exact_scan(int metric, int KE, const float* Q, const double* qn64, const int* qlist, int nq,
                              const float* X, int G, int D, const double* nrm64, const uint32_t* mask, int64_t N,
                              int n_wg, int64_t rows_per_wg, double* lk, uint32_t* li, hipStream_t st,
                              const int* qcount, const int* ovf, unsigned long long* totals, const ExactTail* tail,
-                             int gate_slots) {
+                             int gate_slots, char* gscr) {
     size_t lds = (size_t)4 * WaveTopK<double, uint32_t>::capacity(KE) * (sizeof(double) + sizeof(uint32_t));
     ExactTail tl{};
     if (tail) {
@@ -1250,15 +1269,16 @@ hipError_t launch_exact_scan(int metric, int KE, const float* Q, const double* q
         tl = *tail;
         lds = std::max(lds, merge_block_lds<double, uint32_t>(KE));
     }
+    if (gscr) lds = 0;  // (the buffers in the workspace: exact_scan_scratch_bytes)
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     // gated: a few query slots per row range, each looping over the flagged queries
     const dim3 grid(n_wg, qcount ? (nq < gate_slots ? nq : gate_slots) : nq);
     if (metric == 0)
         hipLaunchKernelGGL((exact_scan_kernel<0>), grid, dim3(256), lds, st, Q, qn64, qlist, X, G, D, nrm64, mask, N,
-                           rows_per_wg, KE, lk, li, qcount, nq, ovf, totals, tl);
+                           rows_per_wg, KE, lk, li, qcount, nq, ovf, totals, tl, gscr);
     else
         hipLaunchKernelGGL((exact_scan_kernel<1>), grid, dim3(256), lds, st, Q, qn64, qlist, X, G, D, nrm64, mask, N,
-                           rows_per_wg, KE, lk, li, qcount, nq, ovf, totals, tl);
+                           rows_per_wg, KE, lk, li, qcount, nq, ovf, totals, tl, gscr);
     return hipGetLastError();
 }
 

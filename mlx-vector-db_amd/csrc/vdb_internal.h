@@ -274,7 +274,10 @@ hipError_t launch_exact_scan(int metric, int KE, const float* Q, const double* q
                              int64_t N, int n_wg, int64_t rows_per_wg,
                              double* lk, uint32_t* li, hipStream_t st, const int* qcount = nullptr,
                              const int* ovf = nullptr, unsigned long long* totals = nullptr,
-                             const ExactTail* tail = nullptr, int gate_slots = 4);
+                             const ExactTail* tail = nullptr, int gate_slots = 4, char* gscr = nullptr);
+// bytes of the device-gated exact scan's global scratch (gscr above): the per-wave top-k buffers
+// of slots x n_wg workgroups and one tail-merge scratch per slot
+size_t exact_scan_scratch_bytes(int KE, int n_wg, int slots);
 
 // Merge sorted fp64-key lists.  Element (q, j, e) lives at q*sq + j*sj + e, lists
 // have Lk entries; output [nq][KP] sorted.

@@ -25,6 +25,7 @@ from __future__ import annotations
 import json
 import logging
 import os
+import collections
 import shutil
 import threading
 import time
@@ -62,6 +63,7 @@ class MLXVectorStoreConfig:
     # join one batched device search instead of one corpus scan each (_QueryCoalescer)
     coalesce: bool = True
     coalesce_inflight: int = 2  # coalesced batches running at once (each on its own stream)
+    coalesce_linger_us: float = 0.0  # a batch leader's wait for the rest of a wave of callers
 
 
 def _as_matrix(vectors: Any) -> np.ndarray:
@@ -149,10 +151,15 @@ class _QueryCoalescer:
     of the batch's).  Callers hold the store's read lock while they wait, so every query of a
     batch sees the same rows."""
 
-    def __init__(self, run, max_batch: int = 64, max_inflight: int = 2):
+    def __init__(self, run, max_batch: int = 64, max_inflight: int = 2, linger_us: float = 0.0):
         self._run = run            # run(Q [B, D], k) -> [(indices, scores, metadata)] * B
         self._max = max_batch
         self._inflight = max(1, int(max_inflight))
+        # adaptive linger: callers come back in waves (each waits for its own result), so a leader
+        # that finds fewer pending queries than the recent batches held waits up to linger_us for
+        # the rest of the wave; a lone caller (recent batches of 1) never waits
+        self._linger = max(0.0, float(linger_us)) * 1e-6
+        self._recent = collections.deque(maxlen=8)
         self._cv = threading.Condition(threading.Lock())
         self._pending: List[list] = []
         self._running = 0
@@ -170,10 +177,21 @@ class _QueryCoalescer:
             self._pending.append(req)
             # wait for a result; whenever fewer than max_inflight batches run, lead the next one:
             # the oldest pending request's k class, FIFO (a leader may serve others before its own)
+            lingered = False
             while req[2] is None and req[3] is None:
                 if self._running >= self._inflight or not self._pending:
                     self._cv.wait()
                     continue
+                expect = min(self._max, max(self._recent)) if self._recent else 1
+                if self._linger > 0.0 and not lingered and len(self._pending) < expect:
+                    lingered = True
+                    deadline = time.perf_counter() + self._linger
+                    while len(self._pending) < expect and req[2] is None and req[3] is None:
+                        rem = deadline - time.perf_counter()
+                        if rem <= 0.0:
+                            break
+                        self._cv.wait(rem)
+                    continue  # (another leader may have taken the requests meanwhile)
                 kc = self._kclass(self._pending[0][1])
                 batch, rest = [], []
                 for r in self._pending:
@@ -194,6 +212,7 @@ class _QueryCoalescer:
                     self._running -= 1
                     self.batches += 1
                     self.queries += len(batch)
+                    self._recent.append(len(batch))
                     self._cv.notify_all()
         finally:
             self._cv.release()
@@ -221,7 +240,8 @@ class MLXVectorStore:
         self._hnsw_index = None
         self._files = StoreFiles(self.store_path)
         self._coalescer = _QueryCoalescer(lambda Q, k: self._brute_force_search(Q, k, None),
-                                          max_inflight=self.config.coalesce_inflight)
+                                          max_inflight=self.config.coalesce_inflight,
+                                          linger_us=self.config.coalesce_linger_us)
         if self.config.enable_hnsw:  # service/optimized_vector_store.py:72-78
             from performance.hnsw_index import ProductionHNSWIndex
             self._hnsw_index = ProductionHNSWIndex(self.config.dimension, self.store_path, self.config.metric,

@@ -220,6 +220,74 @@ def test_c6_10m_x_128_cosine_b64_top10(vdb):
     _report("c6_fp32_ref.json", rep)
 
 
+def _hostile_rows(seed, n, D):
+    """Heavy-tailed rows (a Gaussian scale mixture: z1 exp(0.75 z2), tails far past a normal's),
+    generated per 1 M-row chunk."""
+    out = np.empty((n, D), np.float32)
+    for s0 in range(0, n, 1 << 20):
+        g = np.random.default_rng([seed, s0])
+        m = min(1 << 20, n - s0)
+        z = g.standard_normal((m, D), dtype=np.float32)
+        out[s0:s0 + m] = z * np.exp(np.float32(0.75) * g.standard_normal((m, D), dtype=np.float32))
+    return out
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("metric", ["cosine", "euclidean"])
+def test_certificate_on_data_hostile_to_the_int8_copy(vdb, metric):
+    """the headline's exactness rests on the int8 pass's certificate, so run it
+    at full size on data hostile to the quantisation: heavy-tailed rows; a first add whose mean
+    differs from the later adds' (the centring row and the quantisation step come from the
+    first add); 24 rows of 1000x the norm in a later add (they clip in the int8 copy and their
+    residual enters the bound).  Cosine at C2's shape (1M x 768, B = 64, k = 10: the I8 pass),
+    L2 at C4's (10M x 128, B = 512, k = 100: the wide I8Q pass).  Queries: copies of the big
+    rows, copies of ordinary rows, heavy-tailed queries from both means.  Every query's list is
+    checked for the properties, a spread of queries (the planted ones included) bit-exact
+    against the oracle (indices and fp64 keys) on two searches; fallbacks are counted and
+    reported (a fallback is exact, only slower)."""
+    if metric == "cosine":
+        N, D, B, k = 1_000_000, 768, 64, 10
+    else:
+        N, D, B, k = 10_000_000, 128, 512, 100
+    first = N // 16
+    V = _hostile_rows(31, N, D)
+    V[:first] += np.float32(4.0)  # the first add's mean differs
+    rng = np.random.default_rng(32)
+    big = (rng.choice(N - first, 24, replace=False) + first).astype(np.int64)
+    V[big] *= np.float32(1000.0)
+    Q = _hostile_rows(33, B, D)
+    Q[: B // 2] += np.float32(4.0)
+    plant = {}
+    for j in range(8):  # copies of big rows and of ordinary rows, spread over the query blocks
+        b = (j * B) // 8
+        r = int(big[j]) if j % 2 == 0 else int(rng.integers(0, N))
+        Q[b] = V[r]
+        plant[b] = r
+    ix = vdb.NativeIndex(D, metric)
+    ix.reserve(N)
+    ix.add(V[:first])
+    for s0 in range(first, N, 1 << 21):
+        ix.add(V[s0:s0 + (1 << 21)])
+    sub = sorted(set(plant) | set(range(1, B, max(1, B // 12))))
+    es, ei, ek = ref_cpu.exact_search(Q[sub], V, k, metric)
+    fbs, incons = [], []
+    for _ in range(2):
+        fb0, ic0 = ix.stat("fallback_queries"), ix.stat("inconsistent_queries")
+        s, i, kk = ix.search(Q, k, with_keys=True)
+        fbs.append(ix.stat("fallback_queries") - fb0)
+        incons.append(ix.stat("inconsistent_queries") - ic0)
+        _properties(s, i, metric, N)
+        for b, r in plant.items():
+            assert i[b, 0] == r, (b, r, i[b, :3])
+        np.testing.assert_array_equal(i[sub], ei)
+        np.testing.assert_array_equal(kk[sub], ek)
+    by_prec = {p: ix.stat(f"searches_{p}") for p in ("bf16", "bf16x3", "fp32", "i8", "i8x3", "i8q")}
+    _report(f"hostile_{metric}.json", {"rows": N, "dim": D, "batch": B, "k": k, "queries_checked_exactly": len(sub),
+                                       "fallback_queries_per_search": fbs, "inconsistent_queries_per_search": incons,
+                                       "searches_by_precision": by_prec, "searches_wide": ix.stat("searches_wide")})
+    ix.close()
+
+
 @pytest.mark.timeout(600)
 def test_c5_graph_5m_x_384(vdb):
     from performance.hnsw_index import N_ENTRIES, TEAMS
