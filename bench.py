@@ -399,10 +399,6 @@ def bench_graph(args, world, rank, local, dev, primary=True):
     g.close()
     ix.close()
     return rec
-    g.close()
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
 
 
 def _rank_entry(local_rank, world, port, argv):
@@ -771,6 +767,8 @@ def bench_brute(cfg, args, world, rank, local, dev, primary=True):
                    "note": "SURVEY.md §8(d) fp32 work per launch (2BND flops, 4 B/element; c3: 2 B) over the scan's "
                            "launch time: a throughput, not a roofline fraction (the scan reads the int8 / bf16 "
                            "copy, not the fp32 rows)"}
+        kname = ("scan8w_kernel" if ix.stat("searches_wide") > 0 else "scan8_kernel") if prec in ("i8", "i8x3", "i8q") \
+            else {"fp32": "scan_topk"}.get(prec, "scan2_kernel")
         traffic = None
         traffic_src = None
         cands = [args.pmc_json] if (args.pmc_json and primary) else sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc.json")))
@@ -780,7 +778,7 @@ def bench_brute(cfg, args, world, rank, local, dev, primary=True):
             except (OSError, ValueError):
                 continue
             if (pm.get("config") == cfg and pm.get("n_gpus") == world and "hbm_bytes_per_launch" in pm
-                    and pm.get("precision", "fp32") == prec):
+                    and pm.get("precision", "fp32") == prec and kname + "<" in pm.get("kernel", kname + "<")):
                 traffic = pm["hbm_bytes_per_launch"]
                 traffic_src = os.path.relpath(path, ROOT)
                 break
@@ -807,7 +805,7 @@ def bench_brute(cfg, args, world, rank, local, dev, primary=True):
                        "metric": metric, "parallelism": f"row-shard x{world}" if world > 1 else "single GPU",
                        "rows_per_gpu": n_local},
             "roofline": dict(roof, traffic=traffic,
-                             kernel={"fp32": "scan_topk", "i8": "scan8_kernel", "i8x3": "scan8_kernel", "i8q": "scan8_kernel"}.get(prec, "scan2_kernel"),
+                             kernel=kname,
                              fp32_equivalent=fp32_eq, precision=prec,
                              precision_requested=args.precision, searches_by_precision=by_prec,
                              traffic_source=traffic_src, algorithmic_bytes=hbm_bytes, algorithmic_flops=mfma_flops,
@@ -829,8 +827,6 @@ def bench_brute(cfg, args, world, rank, local, dev, primary=True):
             rec["cpu_baseline"] = cpu_baseline(V, Q, k, metric, budget_s=10.0 if primary else 6.0)
     ix.close()
     return rec
-
-
 
 
 if __name__ == "__main__":

@@ -7,7 +7,7 @@ ranks / certificate, averaged over the batch of the last search.
 import ctypes, os, sys
 import numpy as np
 ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), "..", ".."))
-os.environ["VDB_LIB"] = os.path.join(ROOT, "mlx-vector-db_amd", "lib", "libvdb_amd_stamp.so")
+os.environ.setdefault("VDB_LIB", os.path.join(ROOT, "mlx-vector-db_amd", "lib", "libvdb_amd_st.so"))
 sys.path.insert(0, os.path.join(ROOT, "mlx-vector-db_amd")); sys.path.insert(0, ROOT)
 import torch  # noqa
 from service import _vdb

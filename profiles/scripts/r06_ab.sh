@@ -12,6 +12,6 @@ for r in $(seq 1 ${ROUNDS:-2}); do
       > gpurun_out/r06_ab/${label}_$r.json 2> gpurun_out/r06_ab/${label}_$r.err || { echo "FAIL $label"; tail -5 gpurun_out/r06_ab/${label}_$r.err; exit 1; }
     python3 -c "
 import json,sys; d=json.load(open('gpurun_out/r06_ab/${label}_$r.json')); r=d['roofline']
-print('$label', $r, 'qps %.0f' % d['value'], 'step %.4f' % d['ms_per_step'], 'scan %.4f' % r['avg_launch_ms'], r['precision'], 'fb', d['fallback_queries_timed'])"
+print('$label', $r, 'qps %.0f' % d['value'], 'step %.4f' % d['ms_per_step'], 'p50 %.4f' % d['p50_ms'], 'scan %.4f' % r['avg_launch_ms'], r['precision'], 'fb', d['fallback_queries_timed'])"
   done
 done

@@ -87,3 +87,27 @@ def test_max_batch(max_batch):
     for th in ths:
         th.join()
     assert co.queries == 8 and max(b for b, _ in calls) <= max_batch
+
+
+def test_linger_gathers_the_wave_and_a_lone_caller_never_waits():
+    """Adaptive linger: after batches of 4, a leader that finds 1 pending query waits (up to the
+    linger) for the rest of the wave; a caller alone (recent batches of 1) runs at once."""
+    calls = []
+    co = _QueryCoalescer(_fake_search(calls, delay=0.002), max_inflight=1, linger_us=200_000)
+    t0 = time.perf_counter()
+    for r in range(3):  # alone: no linger, whatever its length
+        assert co.query(np.array([r, 0], np.float32), 1)[0] == [r * 100]
+    assert time.perf_counter() - t0 < 0.15 and [b for b, _ in calls] == [1, 1, 1]
+    co._recent.extend([4] * 8)  # as after waves of 4 callers
+    res = {}
+
+    def worker(t, delay):
+        time.sleep(delay)
+        res[t] = co.query(np.array([10 + t, 0], np.float32), 2)[0]
+    ths = [threading.Thread(target=worker, args=(t, 0.01 * t)) for t in range(4)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    assert res == {t: [(10 + t) * 100, (10 + t) * 100 + 1] for t in range(4)}
+    assert calls[3:] == [(4, 2)]  # the staggered wave ran as one batch
