@@ -79,6 +79,10 @@ struct Workspace {
     char* exact = nullptr;  // exact-path lists, grown on demand
     size_t exact_bytes = 0;
     int* host_flag = nullptr;  // pinned
+    // pinned staging of a host-memory search: the queries up, the results down (read with the
+    // certificate's flags in one synchronisation; grown on demand)
+    char* host_io = nullptr;
+    size_t host_io_bytes = 0;
     hipEvent_t done = nullptr;
     // timing (vdb_index_set_param "timing"): a ring of event sets, one per timed search
     // (scan start / scan end / finish end / pilot start), read once complete, so timed
@@ -229,10 +233,12 @@ void free_workspace_memory(Workspace* w) {
     if (w->dev) (void)hipFree(w->dev);
     if (w->exact) (void)hipFree(w->exact);
     if (w->host_flag) (void)hipHostFree(w->host_flag);
+    if (w->host_io) (void)hipHostFree(w->host_io);
     w->dev = nullptr;
     w->exact = nullptr;
     w->host_flag = nullptr;
-    w->dev_bytes = w->exact_bytes = 0;
+    w->host_io = nullptr;
+    w->dev_bytes = w->exact_bytes = w->host_io_bytes = 0;
 }
 
 int wait_idle(vdb_index* ix);
@@ -565,6 +571,20 @@ int ws_reserve(Workspace* w, size_t bytes, hipStream_t st) {
         size_t nb = std::max(bytes, w->dev_bytes * 2);
         HIP_TRY(hipMalloc(&w->dev, nb));
         w->dev_bytes = nb;
+    }
+    return VDB_OK;
+}
+
+// The pinned staging of a host-memory search (the previous host search on this workspace
+// synchronised before returning, so nothing reads the old buffer).
+int ws_host_io(Workspace* w, size_t bytes) {
+    if (bytes > w->host_io_bytes) {
+        const size_t nb = std::max(bytes, w->host_io_bytes * 2);
+        if (w->host_io) (void)hipHostFree(w->host_io);
+        w->host_io = nullptr;
+        w->host_io_bytes = 0;
+        HIP_TRY(hipHostMalloc(&w->host_io, nb, hipHostMallocDefault));
+        w->host_io_bytes = nb;
     }
     return VDB_OK;
 }
@@ -1635,8 +1655,17 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     float* out_s = out_scores;
     int64_t* out_i = out_indices;
     double* out_k = out_keys;
+    // host memory: the queries go up and the results come down through the workspace's pinned
+    // staging (asynchronous copies; the results are read in the same synchronisation as the
+    // certificate's flags, and copied out on the host when nothing was flagged)
+    const size_t io_q = mem == VDB_MEM_HOST ? (size_t)B * D * 4 : 0;
+    const size_t io_r = (size_t)B * k * (4 + 8 + (out_keys ? 8 : 0));
+    bool staged = false;
     if (mem == VDB_MEM_HOST) {
-        HIP_TRY(hipMemcpyAsync(Qraw, queries, (size_t)B * D * 4, hipMemcpyHostToDevice, st));
+        rc = ws_host_io(w, io_q + io_r);
+        if (rc) return rc;
+        std::memcpy(w->host_io, queries, io_q);
+        HIP_TRY(hipMemcpyAsync(Qraw, w->host_io, io_q, hipMemcpyHostToDevice, st));
         Qd = Qraw;
         if (row_mask && N > 0) {
             HIP_TRY(hipMemcpyAsync(maskd, row_mask, (size_t)mask_words * 4, hipMemcpyHostToDevice, st));
@@ -1846,8 +1875,16 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
             }
             HIP_TRY(hipMemcpyAsync(w->host_flag, flags, sizeof(int), hipMemcpyDeviceToHost, st));
             HIP_TRY(hipMemcpyAsync(w->host_flag + 1, flags + B + 1, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
+            if (mem == VDB_MEM_HOST) {  // (valid when nothing was flagged: nothing rewrites them then)
+                char* r = w->host_io + io_q;
+                HIP_TRY(hipMemcpyAsync(r, out_s, (size_t)B * k * 4, hipMemcpyDeviceToHost, st));
+                HIP_TRY(hipMemcpyAsync(r + (size_t)B * k * 4, out_i, (size_t)B * k * 8, hipMemcpyDeviceToHost, st));
+                if (out_keys)
+                    HIP_TRY(hipMemcpyAsync(r + (size_t)B * k * 12, out_k, (size_t)B * k * 8, hipMemcpyDeviceToHost, st));
+            }
             HIP_TRY(hipStreamSynchronize(st));
             n_flag = w->host_flag[0];
+            staged = mem == VDB_MEM_HOST && n_flag == 0;
             if (prec == PREC_I8 && n_flag > 0) ix->i8_wide = true;
             ix->n_overflow += w->host_flag[1];
             ix->n_incons += w->host_flag[2];
@@ -1891,7 +1928,12 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
             if (rc) return rc;
         }
     }
-    if (mem == VDB_MEM_HOST) {
+    if (mem == VDB_MEM_HOST && staged) {
+        const char* r = w->host_io + io_q;
+        std::memcpy(out_scores, r, (size_t)B * k * 4);
+        std::memcpy(out_indices, r + (size_t)B * k * 4, (size_t)B * k * 8);
+        if (out_keys) std::memcpy(out_keys, r + (size_t)B * k * 12, (size_t)B * k * 8);
+    } else if (mem == VDB_MEM_HOST) {
         HIP_TRY(hipMemcpyAsync(out_scores, out_s, (size_t)B * k * 4, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipMemcpyAsync(out_indices, out_i, (size_t)B * k * 8, hipMemcpyDeviceToHost, st));
         if (out_keys) HIP_TRY(hipMemcpyAsync(out_keys, out_k, (size_t)B * k * 8, hipMemcpyDeviceToHost, st));
