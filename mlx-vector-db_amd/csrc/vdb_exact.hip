@@ -283,7 +283,9 @@ constexpr int FIN_WAVES = VDB_FIN_WAVES;
 
 #ifdef VDB_STAMP
 // Diagnostic build only: per-query phase timestamps of finish_kernel + list length.
-__device__ unsigned long long g_fin_stamps[8192][8];
+// [0..5] phase starts / end, [6] refinement ticks | rerank set << 40, [7] list length, [8..15]
+// sub-phase stamps of the certificate and the refinement (thread 0's view)
+__device__ unsigned long long g_fin_stamps[8192][16];
 #define FIN_STAMP(i) do { if (threadIdx.x == 0) g_fin_stamps[blockIdx.x][i] = __builtin_amdgcn_s_memtime(); } while (0)
 #else
 #define FIN_STAMP(i) do { } while (0)
@@ -622,6 +624,7 @@ __global__ void __launch_bounds__(64 * FW) finish_kernel(FinishArgs a) {
             if (g < KP && ge >= KP) s_akp = ck;
         }
     }
+    FIN_STAMP(13);
     // bf16 corpus rounding: |q.(y - bf16(y))| <= bq, Cauchy-Schwarz |q| R or, along the index's
     // residual direction, |q - c dir| R + |c| M with c = q.dir (vdb_ingest.hip resid_dir_kernel);
     // cosine on the unit query
@@ -705,7 +708,9 @@ __global__ void __launch_bounds__(64 * FW) finish_kernel(FinishArgs a) {
         ck_h = x;
         ck_l = y;
     }
+    FIN_STAMP(14);
     __syncthreads();
+    FIN_STAMP(15);
     if (tid == 0) {
         if (a.chkp) {
             const uint32_t eh = (a.chke ? ck_eh : s_ckeh) + (a.chkr ? *a.chkr : 0u);
@@ -805,6 +810,7 @@ __global__ void __launch_bounds__(64 * FW) finish_kernel(FinishArgs a) {
         // <= 256 |r|), the subtraction of 128 sum(r), r = q' - s_q qh itself (<= 2 ulp of |q'|
         // per element), times f s_x; plus (per row) the roundings of a'
         const float bq2 = fsx * (((float)a.Dp + 8.0f) * 5.97e-8f * 256.0f * rabs + 1.2e-7f * qmx * 127.0f * (float)a.D);
+        FIN_STAMP(8);
         for (int j0 = wv * NBR; j0 < m; j0 += FIN_WAVES * NBR) {
             float sum[NBR];
 #pragma unroll
@@ -846,7 +852,9 @@ __global__ void __launch_bounds__(64 * FW) finish_kernel(FinishArgs a) {
                 atomicMax(&s_cbmax, __float_as_uint((bq2 + bmax) * 1.01f));
             }
         }
+        FIN_STAMP(9);
         __syncthreads();
+        FIN_STAMP(10);
         // a'_k by rank counting over (a' desc, row asc), TPC threads per candidate
         for (int jt = tid; jt < KP * TPC; jt += 64 * FIN_WAVES) {  // (the value alone, as above)
             const int j = jt / TPC, sub = jt % TPC;
@@ -875,6 +883,7 @@ __global__ void __launch_bounds__(64 * FW) finish_kernel(FinishArgs a) {
             if (sub == 0 && j < m && g < a.k && ge >= a.k) s_ak2 = cj;
         }
         __syncthreads();
+        FIN_STAMP(11);
         if (tid == 0) {
             const double ak2 = (double)s_ak2;
             const double qe2 = a.qerr2 ? (double)a.qerr2[b] : 0.0;
@@ -885,6 +894,7 @@ __global__ void __launch_bounds__(64 * FW) finish_kernel(FinishArgs a) {
             s_e2 = e2;
         }
         __syncthreads();
+        FIN_STAMP(12);
     }
     if (s_cut > -INFINITY) {
         const double cut = s_cut;
@@ -1286,6 +1296,6 @@ hipError_t launch_exact_scan(int metric, int KE, const float* Q, const double* q
 
 #ifdef VDB_STAMP
 extern "C" int vdb_debug_finish_stamps(unsigned long long* out, int n) {
-    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(vdb::g_fin_stamps), (size_t)n * 8 * sizeof(unsigned long long));
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(vdb::g_fin_stamps), (size_t)n * 16 * sizeof(unsigned long long));
 }
 #endif

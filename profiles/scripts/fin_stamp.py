@@ -27,9 +27,9 @@ Q = np.random.default_rng(1).random((B, D), dtype=np.float32)
 for _ in range(3):
     ix.search(Q, k)
 lib = _vdb.load_library()
-fb = (ctypes.c_ulonglong * (B * 8))()
+fb = (ctypes.c_ulonglong * (B * 16))()
 lib.vdb_debug_finish_stamps(fb, B)
-f = np.array(fb, dtype=np.uint64).reshape(B, 8).astype(np.float64)
+f = np.array(fb, dtype=np.uint64).reshape(B, 16).astype(np.float64)
 rs = f[:, 6].astype(np.uint64) >> np.uint64(40)
 rt = (f[:, 6].astype(np.uint64) & np.uint64((1 << 40) - 1)).astype(np.float64)
 print(f"{cfg} {prec} N {N} B {B}: list length mean {f[:, 7].mean():.0f} p50 {np.median(f[:, 7]):.0f} max {f[:, 7].max():.0f}; "
@@ -38,3 +38,10 @@ for i, name in enumerate(["load", "select", "cert+refine+cut", "exact keys", "ra
     d = f[:, i + 1] - f[:, i]
     print(f"  {name:16s} mean {d.mean():9.0f}  max {d.max():9.0f}  (s_memtime ticks)")
 print(f"    (of which refinement + cut: mean {rt.mean():.0f})")
+sub = [("select end -> a_k counts", 2, 13), ("a_k counts -> pre-cert sync", 13, 14), ("pre-cert sync", 14, 15),
+       ("cert (tid 0) + sync + refine setup", 15, 8), ("refine rows (wave 0)", 8, 9), ("refine sync", 9, 10),
+       ("a'_k counts + sync", 10, 11), ("e2 (tid 0) + sync", 11, 12), ("cut", 12, 3)]
+for name, i, j in sub:
+    d = f[:, j] - f[:, i]
+    if (f[:, i] > 0).all() and (f[:, j] > 0).all():
+        print(f"    {name:36s} mean {d.mean():9.0f}  max {d.max():9.0f}")

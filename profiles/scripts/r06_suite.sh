@@ -12,4 +12,5 @@ import json; d=json.loads(open('$O/bench.json').read().strip().splitlines()[-1])
 print('c2', round(d['value']), d['ms_per_step'], d['roofline']['avg_launch_ms'], 'cpu', d.get('cpu_baseline',{}).get('value'))
 for k in ('metric_workload_10m_x_128','config_c3','config_c4'):
   s=d.get(k); print(k, round(s['value']), s['ms_per_step'], s['roofline']['avg_launch_ms'], round(s['roofline']['frac'],3), 'cpu', s.get('cpu_baseline',{}).get('value'))
+c5=d.get('config_c5') or {}; print('c5', {k: c5.get(k) for k in ('value','p50_ms','recall_at_10','exact_b1_p50_ms')}, 'cpu', (c5.get('cpu_baseline') or {}).get('value'))
 print(d['serving'])"
