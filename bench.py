@@ -542,7 +542,7 @@ def main():
                 rec[key]["roofline"] = {
                     k_: sub["roofline"][k_] for k_ in ("bound", "achieved", "peak", "unit", "frac", "traffic",
                                                        "traffic_source", "avg_launch_ms", "precision", "basis",
-                                                       "fp32_equivalent")}
+                                                       "kernel", "algorithmic_bytes", "fp32_equivalent")}
         _HOST_CORPUS.clear()
         if not args.no_other_configs and not args.no_graph:
             # c5, BASELINE.json configs[4]: the graph path at batch 1, with the
