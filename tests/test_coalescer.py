@@ -111,3 +111,37 @@ def test_linger_gathers_the_wave_and_a_lone_caller_never_waits():
         th.join()
     assert res == {t: [(10 + t) * 100, (10 + t) * 100 + 1] for t in range(4)}
     assert calls[3:] == [(4, 2)]  # the staggered wave ran as one batch
+
+
+@pytest.mark.parametrize("inflight,linger", [(1, 0), (2, 0), (2, 300), (3, 50)])
+def test_many_callers_every_slot_returns(inflight, linger):
+    """8 callers x 40 queries, mixed k classes (k <= 16 / <= 200 / larger), a search of random
+    length: every caller gets its own answer, and the leadership slots all come back (nothing is
+    left running or pending)."""
+    rng = np.random.default_rng(inflight * 1000 + linger)
+    delays = iter(rng.random(10_000) * 2e-3)
+    calls = []
+
+    def run(Q, k):
+        calls.append((Q.shape[0], k))
+        time.sleep(next(delays))
+        return [([int(q[0]) * 1000 + j for j in range(k)], [0.0] * k, [{}] * k) for q in Q]
+    co = _QueryCoalescer(run, max_batch=5, max_inflight=inflight, linger_us=linger)
+    bad = []
+
+    def worker(t):
+        for r in range(40):
+            key = t * 100 + r
+            k = [3, 40, 250][(t + r) % 3]
+            ix, _, _ = co.query(np.array([key, 0], np.float32), k)
+            if ix != [key * 1000 + j for j in range(k)]:
+                bad.append((t, r))
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join(timeout=60)
+    assert not any(th.is_alive() for th in ths)
+    assert bad == [] and co.queries == 320
+    assert co._running == 0 and co._pending == []
+    assert max(b for b, _ in calls) <= 5
