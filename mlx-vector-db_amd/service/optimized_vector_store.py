@@ -163,9 +163,8 @@ class _QueryCoalescer:
         self._linger = max(0.0, float(linger_us)) * 1e-6
         self._recent = collections.deque(maxlen=8)
         self._cv = threading.Condition(threading.Lock())
-        self._pending: List[_Request] = []
-        self._running = 0   # leadership slots taken (batches running or about to)
-        self._lingering = 0
+        self._pending: List[list] = []
+        self._running = 0
         self.batches = 0
         self.queries = 0
 
@@ -174,102 +173,54 @@ class _QueryCoalescer:
         return 0 if k <= 16 else 1 if k <= 200 else 2
 
     def query(self, q: np.ndarray, k: int):
-        """Each caller sleeps on its own event: a finished batch wakes exactly its callers, and a
-        freed leadership slot is handed to the oldest pending caller (which leads the next batch),
-        instead of a broadcast that wakes every waiting thread (each then takes the GIL only to
-        sleep again: the serving path's host turnaround).  Flags change, and wake
-        events are set and cleared, under the coalescer's lock, so no wake-up is lost."""
-        req = _Request(q, int(k))
-        with self._cv:
+        req = [q, int(k), None, None]  # query, k, result, error
+        self._cv.acquire()
+        try:
             self._pending.append(req)
-            if self._lingering:
-                self._cv.notify_all()
-            if self._running < self._inflight:
-                self._running += 1
-                req.holding = True
-        while True:
-            if req.holding:
-                if not req.done:
-                    self._lead()
-                with self._cv:
-                    if req.done or req not in self._pending:
-                        self._release(req)  # served, or in another leader's batch
-                    else:
-                        continue  # still pending (another k class, past max_batch): lead again
-            with self._cv:
-                if req.lead:  # a slot handed over: lead (or pass it on if already served)
-                    req.lead = False
-                    req.holding = True
+            # wait for a result; whenever fewer than max_inflight batches run, lead the next one:
+            # the oldest pending request's k class, FIFO (a leader may serve others before its own)
+            lingered = False
+            while req[2] is None and req[3] is None:
+                if self._running >= self._inflight or not self._pending:
+                    self._cv.wait()
                     continue
-                if req.done:
-                    return req.outcome()
-                req.wake.clear()
-            req.wake.wait()
-
-    def _release(self, req):
-        """(lock held) req's thread gives up its leadership slot: to the oldest pending caller
-        that neither holds one nor has one on its way, or back to the pool."""
-        req.holding = False
-        for r in self._pending:
-            if not r.lead and not r.holding:
-                r.lead = True
-                r.wake.set()
-                return
-        self._running -= 1
-
-    def _lead(self):
-        """Run one batch: the oldest pending request's k class, FIFO, up to max_batch; first, if
-        fewer queries are pending than recent batches held, linger for the rest of the wave."""
-        with self._cv:
-            expect = min(self._max, max(self._recent)) if self._recent else 1
-            if self._linger > 0.0 and len(self._pending) < expect:
-                deadline = time.perf_counter() + self._linger
-                self._lingering += 1
-                try:
-                    while len(self._pending) < expect:
+                expect = min(self._max, max(self._recent)) if self._recent else 1
+                if self._linger > 0.0 and not lingered and len(self._pending) < expect:
+                    lingered = True
+                    deadline = time.perf_counter() + self._linger
+                    while len(self._pending) < expect and req[2] is None and req[3] is None:
                         rem = deadline - time.perf_counter()
                         if rem <= 0.0:
                             break
                         self._cv.wait(rem)
+                    continue  # (another leader may have taken the requests meanwhile)
+                kc = self._kclass(self._pending[0][1])
+                batch, rest = [], []
+                for r in self._pending:
+                    (batch if len(batch) < self._max and self._kclass(r[1]) == kc else rest).append(r)
+                self._pending = rest
+                self._running += 1
+                self._cv.release()
+                try:
+                    kmax = max(r[1] for r in batch)
+                    res = self._run(np.stack([r[0] for r in batch]), kmax)
+                    for r, (ix, sc, md) in zip(batch, res):
+                        r[2] = (ix[:r[1]], sc[:r[1]], md[:r[1]])
+                except BaseException as e:  # every caller of the batch sees the failure
+                    for r in batch:
+                        r[3] = e
                 finally:
-                    self._lingering -= 1
-            if not self._pending:
-                return
-            kc = self._kclass(self._pending[0].k)
-            batch, rest = [], []
-            for r in self._pending:
-                (batch if len(batch) < self._max and self._kclass(r.k) == kc else rest).append(r)
-            self._pending = rest
-        try:
-            kmax = max(r.k for r in batch)
-            res = self._run(np.stack([r.q for r in batch]), kmax)
-            for r, (ix, sc, md) in zip(batch, res):
-                r.result = (ix[:r.k], sc[:r.k], md[:r.k])
-        except BaseException as e:  # every caller of the batch sees the failure
-            for r in batch:
-                r.error = e
-        with self._cv:
-            self.batches += 1
-            self.queries += len(batch)
-            self._recent.append(len(batch))
-            for r in batch:
-                r.done = True
-                r.wake.set()
-
-
-class _Request:
-    __slots__ = ("q", "k", "result", "error", "done", "lead", "holding", "wake")
-
-    def __init__(self, q, k):
-        self.q, self.k = q, k
-        self.result = self.error = None
-        self.done = self.lead = self.holding = False
-        self.wake = threading.Event()
-
-    def outcome(self):
-        if self.error is not None:
-            raise self.error
-        return self.result
+                    self._cv.acquire()
+                    self._running -= 1
+                    self.batches += 1
+                    self.queries += len(batch)
+                    self._recent.append(len(batch))
+                    self._cv.notify_all()
+        finally:
+            self._cv.release()
+        if req[3] is not None:
+            raise req[3]
+        return req[2]
 
 
 class MLXVectorStore:
