@@ -1475,8 +1475,12 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     // (C4, and each rank of its row-sharded run): all queries of a 512-query block in one
     // workgroup, the corpus staged once through LDS; one workgroup per CU, tiles dealt round-robin
     const int64_t n_tiles_all = round_up(N, 32) / 32;
-    const bool wide8 = i8_pass && !exact_all && !opt.gate && scan8w_ok(Gs, B) && N > 0 &&
-                       (ix->scan_wide == 1 || (ix->scan_wide < 0 && N >= kWideMinRows));
+    // ... and its long-row form (vdb_scan8wl.hip): the I8 cosine pass for 16..48 groups and
+    // batches of 129..256 (C3), all queries of the batch in one workgroup's registers
+    const bool wide_long = i8_pass && !exact_all && !opt.gate && scan8wl_ok(prec, ix->metric, Gs, B) && N > 0 &&
+                           (ix->scan_wide == 1 || (ix->scan_wide < 0 && N >= kWideMinRows));
+    const bool wide8 = wide_long || (i8_pass && !exact_all && !opt.gate && scan8w_ok(Gs, B) && N > 0 &&
+                                     (ix->scan_wide == 1 || (ix->scan_wide < 0 && N >= kWideMinRows)));
     const int n_seg8 = wide8 ? (int)std::min<int64_t>(FIN_SEG_MAX, round_up(std::min<int64_t>(ix->n_cu, n_tiles_all), 8)) : 0;
     // query rows per candidate-pass block: the int8 pass keeps 64 at KP = 256 (KW = 64 kept per
     // workgroup, vdb_scan8_kernel.h), the split pass 32 there
@@ -1737,7 +1741,10 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
             if (timed) HIP_TRY(hipEventRecord(tev[0], st));
             if (q4) ix->n_q4++;
             if (wide8) ix->n_wide++;
-            if (wide8)
+            if (wide_long)
+                HIP_TRY(launch_scan8wl(prec, ix->metric, Xscan, md, Qt, q8lsl, q8scal, Gs, N, B, n_seg8, gl_s, gl_i,
+                                       gl_cap, segc, gthr, chkp, st));
+            else if (wide8)
                 HIP_TRY(launch_scan8w(prec, ix->metric, Xscan, rs8, md, Qt, q8lsl, q8scal, Gs, N, B, Bp, n_seg8, gl_s, gl_i,
                                       gl_cap, segc, gthr, chkp, Bp, chk_l ? 1 : 0, st));
             else if (i8_pass)

@@ -429,24 +429,40 @@ __global__ void __launch_bounds__(64 * FW) finish_kernel(FinishArgs a) {
     __syncthreads();
     // the wide int8 pass's lists: one segment of W8_CH slots per scan workgroup, wave wv taking
     // segments wv, wv + FW, ...; a segment that overflowed sends the query to the exact path
-    for (int sg = a.seg_cnt ? wv : a.seg_n; sg < a.seg_n; sg += FIN_WAVES) {
-        const uint32_t cnt = a.seg_cnt[(size_t)b * a.seg_n + sg];
+    // (lane l of wave wv takes segment 64 (wv + FW i) + l: one round of count loads, then one
+    // round per entry slot up to the wave's fullest segment -- typically a few entries each;
+    // one wave per segment took a dependent round trip per segment, 32 per wave at C3 / C4)
+    for (int sg0 = a.seg_cnt ? wv * 64 : a.seg_n; sg0 < a.seg_n; sg0 += FIN_WAVES * 64) {
+        const int sg = sg0 + lane;
+        uint32_t cnt = sg < a.seg_n ? a.seg_cnt[(size_t)b * a.seg_n + sg] : 0u;
         if (cnt > (uint32_t)W8_CH) {
-            if (lane == 0) s_ovf = 1;
-            continue;
+            s_ovf = 1;
+            cnt = 0;
         }
-        const bool in = lane < (int)cnt;
-        const uint32_t key = in ? order_key(ls[(size_t)sg * W8_CH + lane]) : 0u;
-        const uint32_t row = in ? li[(size_t)sg * W8_CH + lane] : 0u;
-        const bool keep = in && key >= tkey;
-        const unsigned long long bm = __ballot(keep);
-        int base = 0;
-        if (lane == 0 && bm) base = atomicAdd(&s_n, __popcll(bm));
-        base = __shfl(base, 0, 64);
-        if (keep) {
-            const int pos = base + __popcll(bm & ((1ull << lane) - 1ull));
-            s_key[pos] = key;
-            s_row[pos] = row;
+        uint32_t most = cnt;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) most = max(most, (uint32_t)__shfl_xor((int)most, off, 64));
+        for (uint32_t j = 0; j < most; j += 4) {
+            uint32_t key[4], row[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {  // (four entry slots' loads in flight together)
+                const bool in = j + u < cnt;
+                key[u] = in ? order_key(ls[(size_t)sg * W8_CH + j + u]) : 0u;
+                row[u] = in ? li[(size_t)sg * W8_CH + j + u] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const bool keep = j + u < cnt && key[u] >= tkey;
+                const unsigned long long bm = __ballot(keep);
+                int base = 0;
+                if (lane == 0 && bm) base = atomicAdd(&s_n, __popcll(bm));
+                base = __shfl(base, 0, 64);
+                if (keep) {
+                    const int pos = base + __popcll(bm & ((1ull << lane) - 1ull));
+                    s_key[pos] = key[u];
+                    s_row[pos] = row[u];
+                }
+            }
         }
     }
     for (int e0 = wv * 64; e0 < c; e0 += 64 * FIN_WAVES) {

@@ -68,6 +68,12 @@ int scan8_rows_per_step(int prec, int metric);  // (64 queries per block of the 
 // (workgroup, query) segment of the candidate lists
 constexpr int W8_CH = 32;
 bool scan8w_ok(int G8, int B);
+// its long-row form (vdb_scan8wl.hip): I8 cosine, 16 / 24 / 32 / 48 groups, 129..256 queries
+bool scan8wl_ok(int prec, int metric, int G8, int B);
+hipError_t launch_scan8wl(int prec, int metric, const float* Xq, const uint32_t* mask, const float* Qq,
+                          const float* lsl, const float* qscal, int G8, int64_t N, int B, int n_seg, float* gl_s,
+                          uint32_t* gl_i, int64_t gl_cap, uint32_t* seg_cnt, const uint32_t* gthr, uint32_t* chkp,
+                          hipStream_t st);
 hipError_t launch_scan8w(int prec, int metric, const float* Xq, const int* rs8, const uint32_t* mask, const float* Qq,
                          const float* lsl, const float* qscal, int G8, int64_t N, int B, int Bp, int n_seg,
                          float* gl_s, uint32_t* gl_i, int64_t gl_cap, uint32_t* seg_cnt, const uint32_t* gthr,

@@ -137,3 +137,52 @@ def test_wide_pass_device_memory_queued(vdb):
         np.testing.assert_array_equal(kd.cpu().numpy(), ek)
     assert ix.stat("searches_wide") == 3
     ix.close()
+
+
+# ---- the long-row form (vdb_scan8wl.hip): I8 cosine, 512..1536-dim rows, 129..256 queries ----
+
+@pytest.mark.parametrize("precision", ["i8", "auto"])
+@pytest.mark.parametrize("N,D,B,k", [(20000, 1536, 256, 10), (33333, 1500, 200, 10), (9001, 1024, 129, 50),
+                                     (300, 768, 256, 16), (41000, 512, 256, 100), (70001, 1536, 256, 10)])
+def test_wide_long_pass_matches_oracle(vdb, precision, N, D, B, k):
+    rng = np.random.default_rng(N + D + B + 7)
+    V = rng.random((N, D), dtype=np.float32)
+    Q = rng.random((B, D), dtype=np.float32)
+    Q[0] = V[N // 2]
+    Q[B - 1] = V[N - 1]
+    ix = vdb.NativeIndex(D, "cosine", precision=precision)
+    ix.set_param("scan_wide", 1)
+    ix.add(V)
+    _search_check(ix, Q, V, k, "cosine")
+    wide = ix.stat("searches_wide")
+    i8 = ix.stat("searches_i8")
+    print(f"long D {D} B {B} k {k} {precision}: wide {wide} i8 {i8} fallbacks {ix.stat('fallback_queries')}"
+          f" overflow {ix.stat('overflow_queries')}")
+    if precision == "i8":
+        assert wide == 1
+    ix.close()
+
+
+def test_wide_long_pass_mask_overflow_and_clusters(vdb):
+    rng = np.random.default_rng(21)
+    N, D, B = 80_000, 1536, 256
+    V = rng.random((N, D), dtype=np.float32)
+    V[40_000:44_000] = (V[17] + 2e-3 * rng.random((4000, D))).astype(np.float32)  # one cluster of near-duplicates
+    Q = np.concatenate([V[17:18], V[41_000:41_001], rng.random((B - 2, D), dtype=np.float32)])
+    ix = vdb.NativeIndex(D, "cosine", precision="i8")  # auto rows threshold: the wide pass from 65 536 rows
+    for s in range(0, N, 25_000):
+        ix.add(V[s:s + 25_000])
+    _search_check(ix, Q, V, 10, "cosine")
+    mask = rng.random(N) < 0.4
+    _search_check(ix, Q, V, 10, "cosine", mask=mask)
+    assert ix.stat("searches_wide") == 2
+    # without a pilot bound every segment overflows: every query takes the exact path (still exact)
+    ix.set_param("pilot_tiles", 0)
+    _search_check(ix, Q[:150], V, 10, "cosine")
+    assert ix.stat("searches_wide") == 3 and ix.stat("overflow_queries") >= 150
+    # the 64-query shape on the same index gives the same results
+    ix.set_param("pilot_tiles", -1)
+    ix.set_param("scan_wide", 0)
+    _search_check(ix, Q, V, 10, "cosine", mask=mask)
+    assert ix.stat("searches_wide") == 3
+    ix.close()
