@@ -43,11 +43,19 @@ constexpr int W8L_QB = W8L_NW * 32;        // queries per workgroup: 256
 #endif
 constexpr int W8L_PD = VDB_W8L_PD;  // LDS reads in flight ahead of the MFMA chain
 #ifndef VDB_W8L_NSLOT
-#define VDB_W8L_NSLOT 3
+#define VDB_W8L_NSLOT 6
 #endif
 
+// ring slots: as many row tiles as fit the LDS beside the segment counters, at most VDB_W8L_NSLOT
+// (1536 dims: 3 tiles of 48 KiB; 768: 6 of 24 KiB)
 template <int G>
-__host__ __device__ constexpr int w8l_nslot() { return G * 1024 * VDB_W8L_NSLOT + W8L_QB * 4 <= 160 * 1024 ? VDB_W8L_NSLOT : 2; }
+__host__ __device__ constexpr int w8l_nslot() {
+    return (160 * 1024 - W8L_QB * 4) / (G * 1024) < VDB_W8L_NSLOT ? (160 * 1024 - W8L_QB * 4) / (G * 1024) : VDB_W8L_NSLOT;
+}
+// the stage wait: this wave's loads of the Y tiles younger than the one about to be scored may stay
+// in flight (LPW each), then the workgroup barrier
+template <int N>
+__device__ __forceinline__ void w8l_wait_bar() { asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory"); }
 template <int G>
 __host__ __device__ constexpr size_t w8l_lds_bytes() { return (size_t)w8l_nslot<G>() * G * 1024 + (size_t)W8L_QB * 4; }
 
@@ -108,11 +116,14 @@ scan8wl_kernel(const float* __restrict__ Xq, const uint32_t* __restrict__ mask, 
         // may stay in flight (LPW each; fewer issued near the end: wait for all then); after the
         // barrier every wave's have, and every wave is done with tile m - 1, whose slot tile
         // m + NSLOT - 1 now refills
-        const int64_t younger = min<int64_t>(NSLOT - 2, my_tiles - 1 - m);
-        if (NSLOT == 3 && younger == 1)
-            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(LPW) : "memory");
-        else
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        static_assert(NSLOT >= 2 && NSLOT <= 6 && (NSLOT - 2) * LPW <= 63, "vmcnt range");
+        switch ((int)min<int64_t>(NSLOT - 2, my_tiles - 1 - m)) {
+            case 4: w8l_wait_bar<4 * LPW>(); break;
+            case 3: w8l_wait_bar<3 * LPW>(); break;
+            case 2: w8l_wait_bar<2 * LPW>(); break;
+            case 1: w8l_wait_bar<LPW>(); break;
+            default: w8l_wait_bar<0>(); break;
+        }
         if (m + NSLOT - 1 < my_tiles) issue(m + NSLOT - 1);
         if (!active) continue;
         const int64_t t = m * n_seg + w;
@@ -194,7 +205,7 @@ scan8wl_kernel(const float* __restrict__ Xq, const uint32_t* __restrict__ mask, 
 }
 
 bool scan8wl_ok(int prec, int metric, int G8, int B) {
-    return prec == PREC_I8 && metric == 0 && B > 128 && B <= W8L_QB && (G8 == 16 || G8 == 24 || G8 == 32 || G8 == 48);
+    return prec == PREC_I8 && metric == 0 && B >= 1 && B <= W8L_QB && (G8 == 16 || G8 == 24 || G8 == 32 || G8 == 48);
 }
 
 template <int G, bool NT>
