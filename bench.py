@@ -767,7 +767,9 @@ def bench_brute(cfg, args, world, rank, local, dev, primary=True):
                    "note": "SURVEY.md §8(d) fp32 work per launch (2BND flops, 4 B/element; c3: 2 B) over the scan's "
                            "launch time: a throughput, not a roofline fraction (the scan reads the int8 / bf16 "
                            "copy, not the fp32 rows)"}
-        kname = ("scan8w_kernel" if ix.stat("searches_wide") > 0 else "scan8_kernel") if prec in ("i8", "i8x3", "i8q") \
+        wide = ix.stat("searches_wide") > 0  # (rows of > 128 dims: the long-row form, vdb_scan8wl.hip)
+        kname = (("scan8wl_kernel" if D > 128 else "scan8w_kernel") if wide else "scan8_kernel") \
+            if prec in ("i8", "i8x3", "i8q") \
             else {"fp32": "scan_topk"}.get(prec, "scan2_kernel")
         traffic = None
         traffic_src = None
