@@ -1476,12 +1476,14 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     // workgroup, the corpus staged once through LDS; one workgroup per CU, tiles dealt round-robin
     const int64_t n_tiles_all = round_up(N, 32) / 32;
     // ... and its long-row form (vdb_scan8wl.hip): the I8 cosine pass for 16..48 groups and up to
-    // 256 queries, all of them in one workgroup's registers.  Auto: batches of 129..256 (C3: 420 ->
-    // 494 K QPS) and small ones (C2 rows, one stream: B = 2 / 4 / 8 scans 128 -> 115 / 117 / 121
-    // us; B = 16 even, 32 and 64 slower; 1536-dim rows faster at 2 and 16 too, profiles/r06_wl3)
+    // 256 queries, all of them in one workgroup's registers, two waves per query tile for batches
+    // of <= 128 with rows of <= 1024 dims.  Auto (profiles/r06_wl3, r06_rl4): every batch for rows
+    // of <= 1024 dims (C2, B = 64: scan 0.142 -> 0.117 ms, 410 -> 432 K QPS; B = 2 / 32 / 128
+    // faster too); at 1536 dims batches of <= 16 and > 96 (C3: 420 -> 494 K; B = 32 even, 64
+    // slower).
     const bool wide_long = i8_pass && !exact_all && !opt.gate && scan8wl_ok(prec, ix->metric, Gs, B) && N > 0 &&
                            (ix->scan_wide == 1 ||
-                            (ix->scan_wide < 0 && N >= kWideMinRows && (B > 128 || B <= 8 || (Gs >= 48 && B <= 16))));
+                            (ix->scan_wide < 0 && N >= kWideMinRows && (Gs <= 32 || B <= 16 || B > 96)));
     const bool wide8 = wide_long || (i8_pass && !exact_all && !opt.gate && scan8w_ok(Gs, B) && N > 0 &&
                                      (ix->scan_wide == 1 || (ix->scan_wide < 0 && N >= kWideMinRows)));
     const int n_seg8 = wide8 ? (int)std::min<int64_t>(FIN_SEG_MAX, round_up(std::min<int64_t>(ix->n_cu, n_tiles_all), 8)) : 0;

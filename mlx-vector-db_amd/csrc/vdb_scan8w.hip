@@ -110,7 +110,6 @@ scan8w_kernel(const float* __restrict__ Xq, const int* __restrict__ rs8, const u
     constexpr int LPW = XPL * NTILE * G / NW;  // corpus loads per wave and stage
     static_assert(XPL * NTILE * G == LPW * NW, "corpus loads spread evenly over the waves");
     extern __shared__ __attribute__((aligned(16))) char s_dyn[];
-    int* s_seg = (int*)(s_dyn + 2 * SLOT_B);  // [NW][QW]: this workgroup's entries per query
 
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -122,7 +121,12 @@ scan8w_kernel(const float* __restrict__ Xq, const int* __restrict__ rs8, const u
     const int64_t n_stages = (my_tiles + NTILE - 1) / NTILE;
     const uint32_t ring = w8_lds_addr(s_dyn);
 
-    if (lane < QW) s_seg[wv * QW + lane] = 0;
+    // this workgroup's entries per query tile of the lane, in registers: a query tile belongs to
+    // one wave, so lanes l and l + 32 (the tile's two row halves) count it together (no LDS
+    // atomic round trip on the insertion path)
+    int cnt[QT];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) cnt[qt] = 0;
 
     // This wave's share of stage m's LDS-DMA loads into slot sl: LPW of the stage's 64 corpus
     // blocks (1 KiB each: row tile, group, plane) and, L2, waves 0 .. NTILE / 8 - 1 one 1 KiB piece
@@ -335,8 +339,11 @@ scan8w_kernel(const float* __restrict__ Xq, const int* __restrict__ rs8, const u
                     pm |= (sv[v] > th ? 1u : 0u) << v;
                 }
                 pm &= cand;
-                int pos = 0;
-                if (pm != 0u) pos = atomicAdd(&s_seg[wv * QW + ql], __builtin_popcount(pm));
+                const int np = __builtin_popcount(pm);
+                const int np_hi = __shfl_xor(np, 32, 64);  // (the other row half's)
+                int pos = (qt == 0 ? cnt[0] : cnt[QT - 1]) + (lane >= 32 ? np_hi : 0);
+                if (qt == 0) cnt[0] += np + np_hi;
+                else cnt[QT - 1] += np + np_hi;
                 const uint32_t rb = (uint32_t)(t * 32) + 4u * (uint32_t)(lane >> 5);
                 float* ls = gl_s + (size_t)qg * gl_cap + (size_t)w * W8_CH;
                 uint32_t* li = gl_i + (size_t)qg * gl_cap + (size_t)w * W8_CH;
@@ -358,7 +365,9 @@ scan8w_kernel(const float* __restrict__ Xq, const int* __restrict__ rs8, const u
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (!active) return;
     // this workgroup's entries per query (the finish's segment counts; > W8_CH = overflowed)
-    if (lane < QW && q0 + lane < B) seg_cnt[(size_t)(q0 + lane) * n_seg + w] = (uint32_t)s_seg[wv * QW + lane];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt)
+        if (lane < 32 && q0 + qt * 32 + lane < B) seg_cnt[(size_t)(q0 + qt * 32 + lane) * n_seg + w] = (uint32_t)cnt[qt];
     // the checksum's partial sums: the tile's two row halves (lanes l, l + 32), one word per
     // (plane, query, workgroup)
     if (chkp) {

@@ -188,11 +188,12 @@ def test_wide_long_pass_mask_overflow_and_clusters(vdb):
     ix.close()
 
 
-@pytest.mark.parametrize("B", [1, 2, 5, 8, 16])
-@pytest.mark.parametrize("D", [768, 1536, 1000])
+@pytest.mark.parametrize("B", [1, 2, 5, 8, 16, 33, 64, 100])
+@pytest.mark.parametrize("D", [768, 1536, 1000, 512])
 def test_wide_long_pass_small_batches_under_auto(vdb, B, D):
-    """Auto takes the long-row wide pass for small batches too (B <= 8; <= 16 at 1536 dims) from
-    65 536 rows: the serving path's single queries."""
+    """Auto takes the long-row wide pass from 65 536 rows for every batch of rows of <= 1024 dims
+    (two waves per query tile up to 128 queries) and for batches of <= 16 / > 96 at 1536 dims:
+    C2's batches and the serving path's single queries."""
     rng = np.random.default_rng(B * 7 + D)
     N = 66_000
     V = rng.random((N, D), dtype=np.float32)
@@ -202,6 +203,6 @@ def test_wide_long_pass_small_batches_under_auto(vdb, B, D):
     ix.add(V)
     _search_check(ix, Q, V, 10, "cosine")
     G8 = ((D + 63) // 64 * 64) // 32
-    expect = G8 in (16, 24, 32, 48) and (B <= 8 or (G8 >= 48 and B <= 16)) and ix.stat("searches_i8") == 1
+    expect = G8 in (16, 24, 32, 48) and (G8 <= 32 or B <= 16 or B > 96) and ix.stat("searches_i8") == 1
     assert ix.stat("searches_wide") == (1 if expect else 0)
     ix.close()
