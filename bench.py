@@ -768,7 +768,9 @@ def bench_brute(cfg, args, world, rank, local, dev, primary=True):
                            "launch time: a throughput, not a roofline fraction (the scan reads the int8 / bf16 "
                            "copy, not the fp32 rows)"}
         wide = ix.stat("searches_wide") > 0  # (rows of > 128 dims: the long-row form, vdb_scan8wl.hip)
-        kname = (("scan8wl_kernel" if D > 128 else "scan8w_kernel") if wide else "scan8_kernel") \
+        G8 = (D + 63) // 64 * 2  # 32-dim groups; the long-row form's two-waves-per-query-tile kernel below 129 queries
+        long_k = "scan8wl_kernel" if (Bg + 31) // 32 <= 4 and G8 <= 32 else "scan8wl1_kernel"
+        kname = ((long_k if D > 128 else "scan8w_kernel") if wide else "scan8_kernel") \
             if prec in ("i8", "i8x3", "i8q") \
             else {"fp32": "scan_topk"}.get(prec, "scan2_kernel")
         traffic = None
