@@ -468,6 +468,8 @@ def main():
     ap.add_argument("--pilot-rank", type=int, default=None, help="rank of the pilot bound (tuning; default: Poisson rule)")
     ap.add_argument("--k", type=int, default=None, help="tuning: the config at another k (not the config's line)")
     ap.add_argument("--finish-split", type=int, default=None, help="workgroups per query in the finish (tuning)")
+    ap.add_argument("--finish-small", type=int, default=None,
+                    help="the finish's 4-wave form beside a long-row wide scan: -1 auto, 0 off, 1 on (tuning)")
     ap.add_argument("--i8-refine", type=int, default=None, help="finish's I8 refinement: -1 auto (rows >= 512 dims), 0 off, 1 on (tuning)")
     ap.add_argument("--plant-close", type=int, default=None,
                     help="one GPU: P queries per batch with 300 rows the int8 pass cannot separate (re-pass test)")
@@ -602,6 +604,8 @@ def bench_brute(cfg, args, world, rank, local, dev, primary=True):
         ix.set_param("pilot_rank", args.pilot_rank)
     if args.finish_split is not None:
         ix.set_param("finish_split", args.finish_split)
+    if args.finish_small is not None:
+        ix.set_param("finish_small", args.finish_small)
     if args.device_repass is not None:
         ix.set_param("device_repass", args.device_repass)
     if args.i8_refine is not None:

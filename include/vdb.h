@@ -141,7 +141,8 @@ int32_t vdb_index_reserve(vdb_index* idx, int64_t rows);
  * (-1 auto: query block in LDS when it fits, 0 never), "scan_wide" (the wide int8 pass for rows
  * of <= 128 dims and batches of > 256: -1 auto from 65 536 rows, 0 off, 1 always),
  * "scan_checksum" (1 default, 0 off, 2 also I8X3's L sums), "pilot_tiles", "pilot_rank",
- * "finish_split", "i8_refine", "i8_narrow", "device_repass", "auto_int8", "auto_i8q",
+ * "finish_split", "finish_small" (-1 auto: the finish's 4-wave form beside a long-row
+ * wide scan for batches of >= 32, 0 off, 1 on), "i8_refine", "i8_narrow", "device_repass", "auto_int8", "auto_i8q",
  * "dir_bound" (0: BF16 certificate with |q| R only).  Stats also: "searches", "queries",
  * "fallback_queries", "overflow_queries", "inconsistent_queries", "repass_queries",
  * "capacity", "count", "device_bytes", "precision", "searches_fp32" / "searches_bf16x3" /

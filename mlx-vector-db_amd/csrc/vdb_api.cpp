@@ -181,6 +181,9 @@ struct vdb_index {
     int64_t pilot_rank_override = 0;  // tuning: rank of the pilot bound (0 = the Poisson rule)
     bool no_dir_bound = false;    // diagnostics: PREC_BF16 certificate with Cauchy-Schwarz only
     int64_t finish_split = 1;  // workgroups per query in the finish kernel (tuning)
+    // the finish's small form (4 waves, 4096-entry buffer) that fits beside a long-row wide scan:
+    // -1 auto (with that scan at <= 1024 dims), 0 off, 1 on
+    int64_t finish_small = -1;
     int64_t scan_qlds = -1;    // split pass: query block in LDS when it fits (-1 auto), 0 never
     // the finish's I8 refinement (i8_refine): -1 auto = rows of kRefineMinDp dims or more (C3 +6%,
     // C2 neutral, C6 -1%: shorter rows rerank cheaply; profiles/r04_mx1); 0 off; 1 on
@@ -857,6 +860,9 @@ int32_t vdb_index_set_param(vdb_index* ix, const char* name, int64_t value) {
         ix->timing = value != 0;
     } else if (n == "no_fallback") {
         ix->no_fallback = value != 0;
+    } else if (n == "finish_small") {
+        if (value < -1 || value > 1) return set_error(VDB_ERR_INVALID, "finish_small must be -1, 0 or 1");
+        ix->finish_small = value;
     } else if (n == "finish_split") {
         if (value < 1 || value > 8) return set_error(VDB_ERR_INVALID, "finish_split must be in [1, 8]");
         ix->finish_split = value;
@@ -1823,6 +1829,11 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
             fa.qconst = fa.mu == q_mu && fa.dir == q_dir ? qconst : nullptr;  // (prep_queries' constants)
             fa.seg_cnt = segc;
             fa.seg_n = n_seg8;
+            // auto: batches of >= 32 (throughput: C2 under three streams 437 -> 453 K QPS, the finish
+            // beside the next batch's scan), not single queries (one batch alone its 4 waves are
+            // slower: C2 B = 2 step 0.195 -> 0.217 ms; B = 64 p50 0.213 -> 0.240; profiles/r06_fs)
+            fa.small = D <= 1024 && (ix->finish_small == 1 ||
+                                     (ix->finish_small < 0 && wide_long && Gs <= 32 && B >= 32)) ? 1 : 0;
             fa.split = fin_split; fa.sx_ek = fx_ek; fa.sx_ck = fx_ck; fa.sx_cr = fx_cr; fa.sx_n = fx_n; fa.done = done;
             HIP_TRY(launch_finish(ix->metric, KP, fa, B, st));
             if (timed) HIP_TRY(hipEventRecord(tev[2], st));

@@ -337,10 +337,16 @@ __device__ __forceinline__ void exact_keys_batch(const float* __restrict__ q, do
 // FW waves per workgroup: 16 (FIN_WAVES), or 8 for rows of more than 1024 dims (no spills at the
 // 8-piece exact keys: C3 400-413 K -> 419-421 K QPS; C2 / C4 / C6 -0.5..-1% at 8, so they keep 16;
 // profiles/r05_ab/ab34_finish_waves.log)
-template <int METRIC, int KP, int FW = FIN_WAVES>
-__global__ void __launch_bounds__(64 * FW) finish_kernel(FinishArgs a) {
+// The small form (FW = 4, CAP = FIN_CAP_SMALL: 4 waves of <= 128 VGPRs, ~45 KiB of LDS) fits beside a
+// long-row wide scan workgroup (vdb_scan8wl.hip: 8 waves of 170 VGPRs, 98 KiB of LDS at 768 dims),
+// so under several streams a batch's finish runs beside the next batch's scan instead of after it;
+// a list longer than CAP goes to the exact path.
+constexpr int FIN_CAP_SMALL = 4096;
+template <int METRIC, int KP, int FW = FIN_WAVES, int CAP = FIN_CAP>
+__global__ void __launch_bounds__(64 * FW, FW <= 4 ? 4 : 1) finish_kernel(FinishArgs a) {
     constexpr int FIN_WAVES = FW;  // (shadows the default inside this kernel)
-    constexpr int FIN_NB4 = FW > 8 ? 3 : 6;
+    constexpr int FIN_NB4 = FW > 8 || FW <= 4 ? 3 : 6;
+    constexpr int FIN_CAP = CAP;   // (likewise)
     __shared__ uint32_t s_key[FIN_CAP];
     __shared__ uint32_t s_row[FIN_CAP];
     __shared__ __attribute__((aligned(16))) uint32_t s_ck[KP];
@@ -459,8 +465,10 @@ __global__ void __launch_bounds__(64 * FW) finish_kernel(FinishArgs a) {
                 base = __shfl(base, 0, 64);
                 if (keep) {
                     const int pos = base + __popcll(bm & ((1ull << lane) - 1ull));
-                    s_key[pos] = key[u];
-                    s_row[pos] = row[u];
+                    if (pos < FIN_CAP) {  // (more: the list overflows this form's buffer, below)
+                        s_key[pos] = key[u];
+                        s_row[pos] = row[u];
+                    }
                 }
             }
         }
@@ -481,7 +489,7 @@ __global__ void __launch_bounds__(64 * FW) finish_kernel(FinishArgs a) {
         }
     }
     __syncthreads();
-    if (s_ovf) {  // (uniform: every thread returns)
+    if (s_ovf || s_n > FIN_CAP) {  // (uniform: every thread returns)
         if (tid == 0 && sp == 0) {
             const int pos = atomicAdd(a.flag_count, 1);
             a.flag_list[pos] = b;
@@ -1155,7 +1163,9 @@ hipError_t launch_finish(int metric, int KP, const FinishArgs& a, int B, hipStre
     const bool w8 = FIN_WAVES > 8 && a.D > 1024;
 #define VDB_FIN(M, KPV)                                                                                    \
     if (metric == M && KP == KPV) {                                                                        \
-        if (w8)                                                                                            \
+        if (a.small)                                                                                       \
+            hipLaunchKernelGGL((finish_kernel<M, KPV, 4, FIN_CAP_SMALL>), dim3(B, a.split), dim3(64 * 4), 0, st, a); \
+        else if (w8)                                                                                       \
             hipLaunchKernelGGL((finish_kernel<M, KPV, 8>), dim3(B, a.split), dim3(64 * 8), 0, st, a);      \
         else                                                                                               \
             hipLaunchKernelGGL((finish_kernel<M, KPV>), dim3(B, a.split), dim3(64 * FIN_WAVES), 0, st, a); \

@@ -203,6 +203,7 @@ hipError_t launch_rerank(int metric, int KP, const RerankArgs& a, int B, hipStre
 
 // Fused select (top KP of each global candidate list) + exact rerank + certificate.
 struct FinishArgs {
+    int small = 0;  // the 4-wave form with a 4096-entry buffer (vdb_exact.hip FIN_CAP_SMALL)
     const float* gl_s; const uint32_t* gl_i; const uint32_t* gl_cnt; int64_t gl_cap;
     const float* Q; const double* qn64; const float* X; int G; int D; const double* nrm64;
     int k; double eps_rel; double xmax;

@@ -206,3 +206,24 @@ def test_wide_long_pass_small_batches_under_auto(vdb, B, D):
     expect = G8 in (16, 24, 32, 48) and (G8 <= 32 or B <= 16 or B > 96) and ix.stat("searches_i8") == 1
     assert ix.stat("searches_wide") == (1 if expect else 0)
     ix.close()
+
+
+@pytest.mark.parametrize("small", [0, 1])
+@pytest.mark.parametrize("N,D,B,k", [(70_001, 768, 64, 10), (66_000, 1000, 8, 10), (70_000, 512, 120, 50)])
+def test_finish_small_form_matches_oracle(vdb, small, N, D, B, k):
+    """The finish's 4-wave form (4096-entry buffer) beside the long-row wide scan, and the
+    16-wave form, give the same exact results; a list past 4096 entries (no pilot bound) goes to
+    the exact path."""
+    rng = np.random.default_rng(N + D + small)
+    V = rng.random((N, D), dtype=np.float32)
+    Q = rng.random((B, D), dtype=np.float32)
+    Q[0] = V[7]
+    ix = vdb.NativeIndex(D, "cosine", precision="i8")
+    ix.set_param("scan_wide", 1)
+    ix.set_param("finish_small", small)
+    ix.add(V)
+    _search_check(ix, Q, V, k, "cosine")
+    ix.set_param("pilot_tiles", 0)  # every row passes: segments overflow (exact path, still exact)
+    _search_check(ix, Q, V, k, "cosine")
+    assert ix.stat("overflow_queries") >= B
+    ix.close()
