@@ -1491,7 +1491,7 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
                            (ix->scan_wide == 1 ||
                             (ix->scan_wide < 0 && N >= kWideMinRows && (Gs <= 32 || B <= 16 || B > 96)));
     const bool wide8 = wide_long || (i8_pass && !exact_all && !opt.gate && scan8w_ok(Gs, B) && N > 0 &&
-                                     (ix->scan_wide == 1 || (ix->scan_wide < 0 && N >= kWideMinRows)));
+                                     (ix->scan_wide == 1 || (ix->scan_wide < 0 && N >= kWideMinRows && B > 256)));
     const int n_seg8 = wide8 ? (int)std::min<int64_t>(FIN_SEG_MAX, round_up(std::min<int64_t>(ix->n_cu, n_tiles_all), 8)) : 0;
     // query rows per candidate-pass block: the int8 pass keeps 64 at KP = 256 (KW = 64 kept per
     // workgroup, vdb_scan8_kernel.h), the split pass 32 there

@@ -384,7 +384,7 @@ scan8w_kernel(const float* __restrict__ Xq, const int* __restrict__ rs8, const u
     }
 }
 
-bool scan8w_ok(int G8, int B) { return G8 == W8_G && B > 256; }
+bool scan8w_ok(int G8, int B) { return G8 == W8_G && B >= 1; }
 int scan8w_qblocks(int B) { return (B + W8_QB - 1) / W8_QB; }
 
 template <int P, int M, bool NT>
