@@ -1246,6 +1246,12 @@ constexpr int64_t kI8NarrowRows = 512 * 1024;
 constexpr int64_t kI8NarrowRowsShort = 4 * 1024 * 1024;  // rows of <= 128 dims
 // the wide int8 pass under scan_wide auto: from this many rows (smaller indexes: the 64-query shape)
 constexpr int64_t kWideMinRows = 65536;
+// ... and, for batches of <= 256 (a 64-query block's stage tiles split over 2..8 waves), up to this
+// many rows: the c6 shard of an 8-way run (1.25M x 128, B = 64) 1.03 -> 1.25 M QPS per rank, scan
+// 60 -> 40 us; at 10M rows the scan is faster (0.218 -> 0.206 ms) but the three-stream step slower
+// (0.235 -> 0.245: its 134 KiB of LDS leave no room for the other streams' side kernels),
+// profiles/r06_c6w2
+constexpr int64_t kWideSplitMaxRows = 2500000;
 // the finish holds every segment's entries: at most FIN_CAP (16 K) / W8_CH segments
 constexpr int FIN_SEG_MAX = 512;
 // i8_refine auto: the finish refines I8 candidates' scores for padded rows of this many dims or more
@@ -1491,7 +1497,8 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
                            (ix->scan_wide == 1 ||
                             (ix->scan_wide < 0 && N >= kWideMinRows && (Gs <= 32 || B <= 16 || B > 96)));
     const bool wide8 = wide_long || (i8_pass && !exact_all && !opt.gate && scan8w_ok(Gs, B) && N > 0 &&
-                                     (ix->scan_wide == 1 || (ix->scan_wide < 0 && N >= kWideMinRows && B > 256)));
+                                     (ix->scan_wide == 1 ||
+                                      (ix->scan_wide < 0 && N >= kWideMinRows && (B > 256 || N <= kWideSplitMaxRows))));
     const int n_seg8 = wide8 ? (int)std::min<int64_t>(FIN_SEG_MAX, round_up(std::min<int64_t>(ix->n_cu, n_tiles_all), 8)) : 0;
     // query rows per candidate-pass block: the int8 pass keeps 64 at KP = 256 (KW = 64 kept per
     // workgroup, vdb_scan8_kernel.h), the split pass 32 there

@@ -70,7 +70,7 @@ __host__ __device__ constexpr size_t w8_slot_bytes() {
     return (size_t)w8_ntile<PREC>() * W8_G * Planes8<PREC>::XPL * 1024 + (METRIC == 1 ? (size_t)w8_ntile<PREC>() * 128 : 0);
 }
 template <int PREC, int METRIC>
-__host__ __device__ constexpr size_t w8_lds_bytes() { return 2 * w8_slot_bytes<PREC, METRIC>() + (size_t)W8_QB * 4; }
+__host__ __device__ constexpr size_t w8_lds_bytes() { return 2 * w8_slot_bytes<PREC, METRIC>() + (size_t)3 * W8_QB * 4; }
 
 // the LDS byte address of a __shared__ object (the LDS-DMA destination base is an address, M0)
 __device__ __forceinline__ uint32_t w8_lds_addr(const void* p) {
@@ -97,7 +97,7 @@ scan8w_kernel(const float* __restrict__ Xq, const int* __restrict__ rs8, const u
               const float* __restrict__ Qq, const float* __restrict__ lsl, const float* __restrict__ qscal, int64_t N,
               int B, int Bp, float* __restrict__ gl_s, uint32_t* __restrict__ gl_i, int64_t gl_cap,
               uint32_t* __restrict__ seg_cnt, const uint32_t* __restrict__ gthr, uint32_t* __restrict__ chkp, int chk_ld,
-              int chk_l) {
+              int chk_l, int rw) {
     constexpr int G = W8_G, QT = W8_QT, NW = W8_NW;
     constexpr int XPL = Planes8<PREC>::XPL, QPL = Planes8<PREC>::QPL;
     constexpr bool HL = Planes8<PREC>::L;
@@ -114,8 +114,15 @@ scan8w_kernel(const float* __restrict__ Xq, const int* __restrict__ rs8, const u
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int w = blockIdx.x, n_seg = gridDim.x;
-    const int q0 = (blockIdx.y * NW + wv) * QW;  // this wave's queries q0 .. q0 + QW - 1
+    // rw waves per 64-query block (a small batch: the stage's tiles split over them, tile i to
+    // wave i mod rw of the block; rw = 1 for C4's 512 queries)
+    const int n_qb = NW / rw, qbl = wv % n_qb, rl = wv / n_qb;
+    const int q0 = (blockIdx.y * n_qb + qbl) * QW;  // this wave's queries q0 .. q0 + QW - 1
     const bool active = q0 < Bp;                 // (wave-uniform: a block past the padded batch only loads)
+    int* s_seg = (int*)(s_dyn + 2 * SLOT_B);     // rw > 1: [n_qb * QW] entries per query of the workgroup
+    uint32_t* s_ck = (uint32_t*)(s_seg + W8_QB);  //          and its checksum words [2][n_qb * QW]
+    if (rw > 1)
+        for (int i = threadIdx.x; i < 3 * W8_QB; i += 64 * NW) s_seg[i] = 0;
     const int64_t T = (N + 31) >> 5;
     const int64_t my_tiles = T > w ? (T - 1 - w) / n_seg + 1 : 0;
     const int64_t n_stages = (my_tiles + NTILE - 1) / NTILE;
@@ -212,7 +219,7 @@ scan8w_kernel(const float* __restrict__ Xq, const int* __restrict__ rs8, const u
         i32x4 rr[4];
         ld_tile(0, xr, rr);
 #endif
-        for (int i = 0; i < n_here; ++i) {
+        for (int i = rl; i < n_here; i += rw) {
             const int64_t t = (m * NTILE + i) * n_seg + w;
 #if VDB_W8_PF
             f32x4 xn[G][1][XPL];
@@ -339,11 +346,16 @@ scan8w_kernel(const float* __restrict__ Xq, const int* __restrict__ rs8, const u
                     pm |= (sv[v] > th ? 1u : 0u) << v;
                 }
                 pm &= cand;
-                const int np = __builtin_popcount(pm);
-                const int np_hi = __shfl_xor(np, 32, 64);  // (the other row half's)
-                int pos = (qt == 0 ? cnt[0] : cnt[QT - 1]) + (lane >= 32 ? np_hi : 0);
-                if (qt == 0) cnt[0] += np + np_hi;
-                else cnt[QT - 1] += np + np_hi;
+                int pos;
+                if (rw == 1) {
+                    const int np = __builtin_popcount(pm);
+                    const int np_hi = __shfl_xor(np, 32, 64);  // (the other row half's)
+                    pos = (qt == 0 ? cnt[0] : cnt[QT - 1]) + (lane >= 32 ? np_hi : 0);
+                    if (qt == 0) cnt[0] += np + np_hi;
+                    else cnt[QT - 1] += np + np_hi;
+                } else {  // (the block's rw waves share the segment)
+                    pos = pm != 0u ? atomicAdd(&s_seg[qbl * QW + ql], __builtin_popcount(pm)) : 0;
+                }
                 const uint32_t rb = (uint32_t)(t * 32) + 4u * (uint32_t)(lane >> 5);
                 float* ls = gl_s + (size_t)qg * gl_cap + (size_t)w * W8_CH;
                 uint32_t* li = gl_i + (size_t)qg * gl_cap + (size_t)w * W8_CH;
@@ -363,6 +375,32 @@ scan8w_kernel(const float* __restrict__ Xq, const int* __restrict__ rs8, const u
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (rw > 1) {
+        // the rw waves' checksum partial sums of each query summed in LDS, then one word per
+        // (plane, query, workgroup), and the segment counts
+        if (active && chkp) {
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt) {
+                const uint32_t hsum = ckh[qt] + (uint32_t)__shfl_xor((int)ckh[qt], 32, 64);
+                const uint32_t lsum = ckl[qt] + (uint32_t)__shfl_xor((int)ckl[qt], 32, 64);
+                if (lane < 32) {
+                    atomicAdd(&s_ck[qbl * QW + qt * 32 + lane], hsum);
+                    if (HL && chk_l) atomicAdd(&s_ck[W8_QB + qbl * QW + qt * 32 + lane], lsum);
+                }
+            }
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < n_qb * QW; i += 64 * NW) {
+            const int q = blockIdx.y * n_qb * QW + i;
+            if (q >= B) continue;
+            seg_cnt[(size_t)q * n_seg + w] = (uint32_t)s_seg[i];
+            if (chkp) {
+                chkp[(size_t)q * n_seg + w] = s_ck[i];
+                if (HL && chk_l) chkp[((size_t)chk_ld + q) * n_seg + w] = s_ck[W8_QB + i];
+            }
+        }
+        return;
+    }
     if (!active) return;
     // this workgroup's entries per query (the finish's segment counts; > W8_CH = overflowed)
 #pragma unroll
@@ -385,7 +423,13 @@ scan8w_kernel(const float* __restrict__ Xq, const int* __restrict__ rs8, const u
 }
 
 bool scan8w_ok(int G8, int B) { return G8 == W8_G && B >= 1; }
-int scan8w_qblocks(int B) { return (B + W8_QB - 1) / W8_QB; }
+// waves per 64-query block: the whole workgroup for a batch of <= 64 queries, 4 / 2 for <= 128 /
+// <= 256, one for C4's 512
+int scan8w_rw(int B) { return B <= 64 ? 8 : B <= 128 ? 4 : B <= 256 ? 2 : 1; }
+int scan8w_qblocks(int B) {
+    const int per_wg = W8_QB / scan8w_rw(B);
+    return (B + per_wg - 1) / per_wg;
+}
 
 template <int P, int M, bool NT>
 static hipError_t scan8w_launch(const float* Xq, const int* rs8, const uint32_t* mask, const float* Qq, const float* lsl,
@@ -402,7 +446,7 @@ static hipError_t scan8w_launch(const float* Xq, const int* rs8, const uint32_t*
         lds_set = true;
     }
     hipLaunchKernelGGL(k, dim3((unsigned)n_seg, (unsigned)scan8w_qblocks(B)), dim3(64 * W8_NW), lds, st, Xq, rs8, mask, Qq,
-                       lsl, qscal, N, B, Bp, gl_s, gl_i, gl_cap, seg_cnt, gthr, chkp, chk_ld, chk_l);
+                       lsl, qscal, N, B, Bp, gl_s, gl_i, gl_cap, seg_cnt, gthr, chkp, chk_ld, chk_l, scan8w_rw(B));
     return hipGetLastError();
 }
 

@@ -227,3 +227,24 @@ def test_finish_small_form_matches_oracle(vdb, small, N, D, B, k):
     _search_check(ix, Q, V, k, "cosine")
     assert ix.stat("overflow_queries") >= B
     ix.close()
+
+
+@pytest.mark.parametrize("metric,precision", [("cosine", "i8"), ("euclidean", "i8q"), ("euclidean", "i8x3")])
+@pytest.mark.parametrize("B", [1, 37, 64, 100, 200, 256])
+def test_wide_pass_small_batches_split_tiles(vdb, metric, precision, B):
+    """The short-row wide pass forced on for batches of <= 256: rw = 8 / 4 / 2 waves per 64-query
+    block share each stage's tiles, their segment counters and checksum words in LDS."""
+    rng = np.random.default_rng(B + len(metric) + len(precision))
+    N, D, k = 40_003, 128, 20
+    V = rng.random((N, D), dtype=np.float32)
+    Q = rng.random((B, D), dtype=np.float32)
+    Q[0] = V[N - 1]
+    ix = vdb.NativeIndex(D, metric, precision=precision)
+    ix.set_param("scan_wide", 1)
+    ix.add(V)
+    _search_check(ix, Q, V, k, metric)
+    mask = rng.random(N) < 0.5
+    _search_check(ix, Q, V, k, metric, mask=mask)
+    assert ix.stat("searches_wide") == 2
+    assert ix.stat("inconsistent_queries") == 0
+    ix.close()
