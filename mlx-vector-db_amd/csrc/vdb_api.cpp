@@ -1499,7 +1499,9 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
     const bool wide8 = wide_long || (i8_pass && !exact_all && !opt.gate && scan8w_ok(Gs, B) && N > 0 &&
                                      (ix->scan_wide == 1 ||
                                       (ix->scan_wide < 0 && N >= kWideMinRows && (B > 256 || N <= kWideSplitMaxRows))));
-    const int n_seg8 = wide8 ? (int)std::min<int64_t>(FIN_SEG_MAX, round_up(std::min<int64_t>(ix->n_cu, n_tiles_all), 8)) : 0;
+    const int n_seg8 = !wide8 ? 0
+                       : ix->n_wg_override > 0 ? (int)std::min<int64_t>(FIN_SEG_MAX, std::min<int64_t>(ix->n_wg_override, n_tiles_all))
+                                               : (int)std::min<int64_t>(FIN_SEG_MAX, round_up(std::min<int64_t>(ix->n_cu, n_tiles_all), 8));
     // query rows per candidate-pass block: the int8 pass keeps 64 at KP = 256 (KW = 64 kept per
     // workgroup, vdb_scan8_kernel.h), the split pass 32 there
     const int QB = q4 ? 128 : i8_pass ? 64 : KP == 256 ? 32 : 64;
