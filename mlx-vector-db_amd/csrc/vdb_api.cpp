@@ -1841,8 +1841,10 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
             // auto: batches of >= 32 (throughput: C2 under three streams 437 -> 453 K QPS, the finish
             // beside the next batch's scan), not single queries (one batch alone its 4 waves are
             // slower: C2 B = 2 step 0.195 -> 0.217 ms; B = 64 p50 0.213 -> 0.240; profiles/r06_fs)
+            // (and beside the short-row wide pass's small stage, batches of 32..256 at <= 128 dims)
             fa.small = D <= 1024 && (ix->finish_small == 1 ||
-                                     (ix->finish_small < 0 && wide_long && Gs <= 32 && B >= 32)) ? 1 : 0;
+                                     (ix->finish_small < 0 && B >= 32 &&
+                                      ((wide_long && Gs <= 32) || (wide8 && !wide_long && B <= 256)))) ? 1 : 0;
             fa.split = fin_split; fa.sx_ek = fx_ek; fa.sx_ck = fx_ck; fa.sx_cr = fx_cr; fa.sx_n = fx_n; fa.done = done;
             HIP_TRY(launch_finish(ix->metric, KP, fa, B, st));
             if (timed) HIP_TRY(hipEventRecord(tev[2], st));

@@ -63,14 +63,16 @@ constexpr int W8_QW = W8_QT * 32;    // queries per wave
 constexpr int W8_QB = W8_NW * W8_QW;  // queries per workgroup
 static_assert(W8_QB == 512, "512 queries per workgroup");
 
-template <int PREC>
-__host__ __device__ constexpr int w8_ntile() { return Planes8<PREC>::XPL == 2 ? 8 : 16; }
-template <int PREC, int METRIC>
+// SM: the small stage (8 one-plane row tiles, 32 KiB per slot) of batches of <= 256 queries: the
+// pass then leaves LDS for the finish's small form beside it (vdb_exact.hip FIN_CAP_SMALL)
+template <int PREC, bool SM = false>
+__host__ __device__ constexpr int w8_ntile() { return Planes8<PREC>::XPL == 2 || SM ? 8 : 16; }
+template <int PREC, int METRIC, bool SM = false>
 __host__ __device__ constexpr size_t w8_slot_bytes() {
-    return (size_t)w8_ntile<PREC>() * W8_G * Planes8<PREC>::XPL * 1024 + (METRIC == 1 ? (size_t)w8_ntile<PREC>() * 128 : 0);
+    return (size_t)w8_ntile<PREC, SM>() * W8_G * Planes8<PREC>::XPL * 1024 + (METRIC == 1 ? (size_t)w8_ntile<PREC, SM>() * 128 : 0);
 }
-template <int PREC, int METRIC>
-__host__ __device__ constexpr size_t w8_lds_bytes() { return 2 * w8_slot_bytes<PREC, METRIC>() + (size_t)3 * W8_QB * 4; }
+template <int PREC, int METRIC, bool SM = false>
+__host__ __device__ constexpr size_t w8_lds_bytes() { return 2 * w8_slot_bytes<PREC, METRIC, SM>() + (size_t)3 * W8_QB * 4; }
 
 // the LDS byte address of a __shared__ object (the LDS-DMA destination base is an address, M0)
 __device__ __forceinline__ uint32_t w8_lds_addr(const void* p) {
@@ -91,7 +93,7 @@ __device__ __forceinline__ void w8_glds(const void* gsrc, uint32_t lds) {
                      : "=&s"(keep) : "v"(gsrc), "s"(lds) : "memory");
 }
 
-template <int PREC, int METRIC, bool NT>
+template <int PREC, int METRIC, bool NT, bool SM>
 __global__ void __launch_bounds__(64 * W8_NW, 1)
 scan8w_kernel(const float* __restrict__ Xq, const int* __restrict__ rs8, const uint32_t* __restrict__ mask,
               const float* __restrict__ Qq, const float* __restrict__ lsl, const float* __restrict__ qscal, int64_t N,
@@ -101,10 +103,10 @@ scan8w_kernel(const float* __restrict__ Xq, const int* __restrict__ rs8, const u
     constexpr int G = W8_G, QT = W8_QT, NW = W8_NW;
     constexpr int XPL = Planes8<PREC>::XPL, QPL = Planes8<PREC>::QPL;
     constexpr bool HL = Planes8<PREC>::L;
-    constexpr int NTILE = w8_ntile<PREC>();
+    constexpr int NTILE = w8_ntile<PREC, SM>();
     constexpr size_t TILE_B = (size_t)G * XPL * 1024;
     constexpr size_t CORP_B = NTILE * TILE_B;
-    constexpr size_t SLOT_B = w8_slot_bytes<PREC, METRIC>();
+    constexpr size_t SLOT_B = w8_slot_bytes<PREC, METRIC, SM>();
     constexpr size_t GSTEP = 8 * BLOCK_FLOATS, PLANE = 4 * BLOCK_FLOATS;
     constexpr int QW = W8_QW;
     constexpr int LPW = XPL * NTILE * G / NW;  // corpus loads per wave and stage
@@ -431,13 +433,13 @@ int scan8w_qblocks(int B) {
     return (B + per_wg - 1) / per_wg;
 }
 
-template <int P, int M, bool NT>
+template <int P, int M, bool NT, bool SM>
 static hipError_t scan8w_launch(const float* Xq, const int* rs8, const uint32_t* mask, const float* Qq, const float* lsl,
                                 const float* qscal, int64_t N, int B, int Bp, int n_seg, float* gl_s, uint32_t* gl_i,
                                 int64_t gl_cap, uint32_t* seg_cnt, const uint32_t* gthr, uint32_t* chkp, int chk_ld,
                                 int chk_l, hipStream_t st) {
-    auto k = scan8w_kernel<P, M, NT>;
-    constexpr size_t lds = w8_lds_bytes<P, M>();
+    auto k = scan8w_kernel<P, M, NT, SM>;
+    constexpr size_t lds = w8_lds_bytes<P, M, SM>();
     static_assert(lds <= 160 * 1024, "LDS");
     static std::atomic<bool> lds_set{false};
     if (!lds_set.load()) {
@@ -459,12 +461,19 @@ hipError_t launch_scan8w(int prec, int metric, const float* Xq, const int* rs8, 
     // the corpus is read once per query block: non-temporal with one (C4), default policy with
     // several (they share each tile through the XCD's L2)
     const bool nt = scan8w_qblocks(B) == 1;
+    const bool sm = scan8w_rw(B) > 1;
 #define W8_CASE(P, M)                                                                                                 \
-    if (prec == P && metric == M)                                                                                     \
-        return nt ? scan8w_launch<P, M, true>(Xq, rs8, mask, Qq, lsl, qscal, N, B, Bp, n_seg, gl_s, gl_i, gl_cap,     \
-                                              seg_cnt, gthr, chkp, chk_ld, chk_l, st)                                 \
-                  : scan8w_launch<P, M, false>(Xq, rs8, mask, Qq, lsl, qscal, N, B, Bp, n_seg, gl_s, gl_i, gl_cap,    \
-                                               seg_cnt, gthr, chkp, chk_ld, chk_l, st);
+    if (prec == P && metric == M) {                                                                                   \
+        if (sm)                                                                                                       \
+            return nt ? scan8w_launch<P, M, true, true>(Xq, rs8, mask, Qq, lsl, qscal, N, B, Bp, n_seg, gl_s, gl_i,   \
+                                                        gl_cap, seg_cnt, gthr, chkp, chk_ld, chk_l, st)              \
+                      : scan8w_launch<P, M, false, true>(Xq, rs8, mask, Qq, lsl, qscal, N, B, Bp, n_seg, gl_s, gl_i,  \
+                                                         gl_cap, seg_cnt, gthr, chkp, chk_ld, chk_l, st);            \
+        return nt ? scan8w_launch<P, M, true, false>(Xq, rs8, mask, Qq, lsl, qscal, N, B, Bp, n_seg, gl_s, gl_i,      \
+                                                     gl_cap, seg_cnt, gthr, chkp, chk_ld, chk_l, st)                 \
+                  : scan8w_launch<P, M, false, false>(Xq, rs8, mask, Qq, lsl, qscal, N, B, Bp, n_seg, gl_s, gl_i,     \
+                                                      gl_cap, seg_cnt, gthr, chkp, chk_ld, chk_l, st);               \
+    }
     W8_CASE(PREC_I8Q, 1) W8_CASE(PREC_I8X3, 1) W8_CASE(PREC_I8, 1)
     W8_CASE(PREC_I8Q, 0) W8_CASE(PREC_I8X3, 0) W8_CASE(PREC_I8, 0)
 #undef W8_CASE
