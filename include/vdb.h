@@ -138,8 +138,10 @@ int32_t vdb_index_reserve(vdb_index* idx, int64_t rows);
  * speed differs): "n_wg" (candidate-pass workgroups), "scan_variant" / "scan_variant_bf16x3"
  * (fp32 / split pass tilings), "scan_sync" (0 auto, 1 per-step barrier, 2 flag-gated
  * compaction rounds), "scan_q4" (split pass 128-query shape, -1 auto / 0 / 1), "scan_qlds"
- * (-1 auto: query block in LDS when it fits, 0 never), "scan_wide" (the wide int8 pass for rows
- * of <= 128 dims and batches of > 256: -1 auto from 65 536 rows, 0 off, 1 always),
+ * (-1 auto: query block in LDS when it fits, 0 never), "scan_wide" (the wide int8 passes, all
+ * queries of a batch in one workgroup's registers: -1 auto from 65 536 rows -- rows of <= 128
+ * dims with > 256 queries, or <= 256 up to 2.5M rows; I8 cosine rows of 512..1536 dims with
+ * <= 256 queries (1536: <= 16 or > 96) -- 0 off, 1 whenever the shape allows),
  * "scan_checksum" (1 default, 0 off, 2 also I8X3's L sums), "pilot_tiles", "pilot_rank",
  * "finish_split", "finish_small" (-1 auto: the finish's 4-wave form beside a long-row
  * wide scan for batches of >= 32, 0 off, 1 on), "i8_refine", "i8_narrow", "device_repass", "auto_int8", "auto_i8q",
