@@ -487,6 +487,18 @@ Workspace* acquire_ws(vdb_index* ix, hipStream_t st, bool own = false) {
     return w;
 }
 
+// Another search of this index on the device right now (being queued, or queued and not finished):
+// the finish's small form pays off only when it can run beside another batch's scan.
+bool others_in_flight(vdb_index* ix, const Workspace* self) {
+    std::lock_guard<std::mutex> g(ix->ws_mu);
+    for (Workspace* w : ix->pool) {
+        if (w == self) continue;
+        if (w->busy) return true;
+        if (w->used && w->done && hipEventQuery(w->done) == hipErrorNotReady) return true;
+    }
+    return false;
+}
+
 void release_ws(vdb_index* ix, Workspace* w, hipStream_t st) {
     if (w->done == nullptr) (void)hipEventCreateWithFlags(&w->done, hipEventDisableTiming);
     (void)hipEventRecord(w->done, st);
@@ -1841,10 +1853,13 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
             // auto: batches of >= 32 (throughput: C2 under three streams 437 -> 453 K QPS, the finish
             // beside the next batch's scan), not single queries (one batch alone its 4 waves are
             // slower: C2 B = 2 step 0.195 -> 0.217 ms; B = 64 p50 0.213 -> 0.240; profiles/r06_fs)
-            // (and beside the short-row wide pass's small stage, batches of 32..256 at <= 128 dims)
+            // (and beside the short-row wide pass's small stage, batches of 32..256 at <= 128 dims);
+            // auto also only while another search of the index is in flight: a batch alone keeps the
+            // 16-wave form (its latency, the bench's p50)
             fa.small = D <= 1024 && (ix->finish_small == 1 ||
                                      (ix->finish_small < 0 && B >= 32 &&
-                                      ((wide_long && Gs <= 32) || (wide8 && !wide_long && B <= 256)))) ? 1 : 0;
+                                      ((wide_long && Gs <= 32) || (wide8 && !wide_long && B <= 256)) &&
+                                      others_in_flight(ix, w))) ? 1 : 0;
             fa.split = fin_split; fa.sx_ek = fx_ek; fa.sx_ck = fx_ck; fa.sx_cr = fx_cr; fa.sx_n = fx_n; fa.done = done;
             HIP_TRY(launch_finish(ix->metric, KP, fa, B, st));
             if (timed) HIP_TRY(hipEventRecord(tev[2], st));
