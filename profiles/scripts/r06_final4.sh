@@ -3,8 +3,8 @@
 # strong-scaled per-rank shard lines (c6 / c4 at 1.25M rows) with a one-stream trace of c6's.
 set -o pipefail
 export TMPDIR=/tmp
-TAG=r06_final4 bash profiles/scripts/r06_suite.sh || exit 1
-O=gpurun_out/r06_final4
+TAG=${TAG:-r06_final4} bash profiles/scripts/r06_suite.sh || exit 1
+O=gpurun_out/${TAG:-r06_final4}
 for c in c6 c4; do
   timeout -k 10 200 python3 bench.py --config $c --rows 1250000 --steps 200 --warmup 20 --no-cpu-baseline > $O/shard_${c}_line.json 2> $O/shard_${c}.err || { tail -5 $O/shard_${c}.err; exit 1; }
 done
