@@ -66,7 +66,10 @@ static_assert(W8_QB == 512, "512 queries per workgroup");
 // SM: the small stage (8 one-plane row tiles, 32 KiB per slot) of batches of <= 256 queries: the
 // pass then leaves LDS for the finish's small form beside it (vdb_exact.hip FIN_CAP_SMALL)
 template <int PREC, bool SM = false>
-__host__ __device__ constexpr int w8_ntile() { return Planes8<PREC>::XPL == 2 || SM ? 8 : 16; }
+#ifndef VDB_W8_SM_NTILE
+#define VDB_W8_SM_NTILE 8
+#endif
+__host__ __device__ constexpr int w8_ntile() { return Planes8<PREC>::XPL == 2 ? 8 : SM ? VDB_W8_SM_NTILE : 16; }
 template <int PREC, int METRIC, bool SM = false>
 __host__ __device__ constexpr size_t w8_slot_bytes() {
     return (size_t)w8_ntile<PREC, SM>() * W8_G * Planes8<PREC>::XPL * 1024 + (METRIC == 1 ? (size_t)w8_ntile<PREC, SM>() * 128 : 0);
@@ -103,7 +106,8 @@ scan8w_kernel(const float* __restrict__ Xq, const int* __restrict__ rs8, const u
     constexpr int G = W8_G, QT = W8_QT, NW = W8_NW;
     constexpr int XPL = Planes8<PREC>::XPL, QPL = Planes8<PREC>::QPL;
     constexpr bool HL = Planes8<PREC>::L;
-    constexpr int NTILE = w8_ntile<PREC, SM>();
+    constexpr int NTILE = METRIC == 1 && SM ? 8 : w8_ntile<PREC, SM>();  // (L2: the start values load 8 tiles per wave)
+    static_assert(METRIC == 0 || NTILE % 8 == 0, "L2 start values: 8 row tiles per loading wave");
     constexpr size_t TILE_B = (size_t)G * XPL * 1024;
     constexpr size_t CORP_B = NTILE * TILE_B;
     constexpr size_t SLOT_B = w8_slot_bytes<PREC, METRIC, SM>();
