@@ -26,7 +26,7 @@ try:
         t0 = time.perf_counter(); st.query(q, k); lat.append(time.perf_counter() - t0)
     print(f"batch-1 p50 {np.median(lat) * 1e3:.3f} ms", flush=True)
     for rep in range(2):
-        for mode in ("direct", (2, 0), (2, 150), (2, 300), (2, 600), (3, 300), (1, 300)):
+        for mode in ((2, 300), (2, 100), (2, 600), (3, 300), (2, 0), (1, 200)):
             st.config.coalesce = mode != "direct"
             if mode != "direct":
                 st._coalescer._inflight, st._coalescer._linger = mode[0], mode[1] * 1e-6
