@@ -1755,7 +1755,7 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
                 if (i8_pass) {
                     HIP_TRY(launch_pilot8(prec, ix->metric, Xscan, ix->rinit32, md, Qt, q8scal, Gs, N, B,
                                           (B + QB_pilot - 1) / QB_pilot, QB_pilot, n_pilot, pslots, st,
-                                          chke ? ix->d_csum : nullptr, chke));
+                                          chke ? ix->d_csum : nullptr, chke, wide_long));
                     HIP_TRY(launch_pilot_bound(pslots, B, pilot_rank, gthr, st));
                 } else if (split_pass) {
                     HIP_TRY(launch_pilot2(prec, ix->metric, pilot_rank, Xscan, ix->rinit32, md, Qt, Gs, N, B,

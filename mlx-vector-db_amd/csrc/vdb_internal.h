@@ -62,7 +62,7 @@ hipError_t launch_sink_row8(float* Xq, int64_t row, int G8, hipStream_t st);
 hipError_t launch_pilot8(int prec, int metric, const float* Xq, const float* rinit, const uint32_t* mask,
                          const float* Qq, const float* qscal, int G8, int64_t N, int B, int n_qblocks, int QB,
                          int n_sample, uint32_t* pslots, hipStream_t st, const uint32_t* csum = nullptr,
-                         uint32_t* chke = nullptr);
+                         uint32_t* chke = nullptr, bool wide = false);
 int scan8_rows_per_step(int prec, int metric);  // (64 queries per block of the int8 pass)
 // the wide int8 pass (vdb_scan8w.hip): rows of 4 groups, batches of more than 256; W8_CH slots per
 // (workgroup, query) segment of the candidate lists

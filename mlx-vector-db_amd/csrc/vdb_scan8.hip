@@ -382,8 +382,10 @@ constexpr int PILOT8_WAVES = 4;
 #ifndef VDB_PILOT8_W1
 #define VDB_PILOT8_W1 0
 #endif
-__host__ __device__ inline int pilot8_w(int G8) {
-    return VDB_PILOT8_W1 || G8 > 24 ? 1 : G8 >= 16 ? 4 : G8 >= 8 ? 2 : 1;
+// (wide: the batch's scan is a long-row wide pass, whose 8 waves of 255 registers leave nothing
+// beside it, so the pilot only has to be fast alone: four waves per tile, C3 63 -> ~35 us)
+__host__ __device__ inline int pilot8_w(int G8, bool wide = false) {
+    return VDB_PILOT8_W1 || (G8 > 24 && !wide) ? 1 : G8 >= 16 ? 4 : G8 >= 8 ? 2 : 1;
 }
 
 // The checksum's expected values (vdb_scan8_kernel.h), one query per wave of the pilot's first
@@ -434,7 +436,7 @@ __global__ void __launch_bounds__(64 * PILOT8_WAVES)
 pilot8_scores_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, const uint32_t* __restrict__ mask,
                      const float* __restrict__ Qq, const float* __restrict__ qscal, int G, int64_t N, int B, int n_qb,
                      int64_t n_tiles, int n_sample, uint32_t* __restrict__ pslots,
-                     const uint32_t* __restrict__ csum, uint32_t* __restrict__ chke) {
+                     const uint32_t* __restrict__ csum, uint32_t* __restrict__ chke, int W) {
     constexpr int QB = 32 * QT;
     constexpr int XPL = Planes8<PREC>::XPL;
     constexpr size_t GSTEP = 8 * BLOCK_FLOATS, PLANE = 4 * BLOCK_FLOATS;
@@ -447,7 +449,6 @@ pilot8_scores_kernel(const float* __restrict__ Xq, const float* __restrict__ rin
     PartT* s_part = (PartT*)s_pdyn;
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
-    const int W = pilot8_w(G);
     const int part = wv % W;
     const int i = blockIdx.x * (PILOT8_WAVES / W) + wv / W;
     const bool live = i < n_sample;
@@ -618,11 +619,13 @@ pilot8_g4_kernel(const float* __restrict__ Xq, const float* __restrict__ rinit, 
 
 hipError_t launch_pilot8(int prec, int metric, const float* Xq, const float* rinit, const uint32_t* mask,
                          const float* Qq, const float* qscal, int G8, int64_t N, int B, int n_qblocks, int QB,
-                         int n_sample, uint32_t* pslots, hipStream_t st, const uint32_t* csum, uint32_t* chke) {
+                         int n_sample, uint32_t* pslots, hipStream_t st, const uint32_t* csum, uint32_t* chke,
+                         bool wide) {
     const int64_t n_tiles = (N + 31) / 32;
+    const int W = pilot8_w(G8, wide);
     if (n_sample > n_tiles) n_sample = (int)n_tiles;
     if (n_sample <= 0) return hipSuccess;
-    const int tpb = G8 == 4 ? PILOT8_WAVES : PILOT8_WAVES / pilot8_w(G8);
+    const int tpb = G8 == 4 ? PILOT8_WAVES : PILOT8_WAVES / W;
     // (with the checksum's expectations: at least B / PILOT8_WAVES workgroups, one query per wave;
     // past n_sample they score nothing)
     const int gx = (n_sample + tpb - 1) / tpb;
@@ -635,9 +638,9 @@ hipError_t launch_pilot8(int prec, int metric, const float* Xq, const float* rin
         launched = true;                                                                                         \
     }                                                                                                            \
     if (!launched && prec == P && metric == M && QB == 32 * QTV) {                                               \
-        const size_t lds = pilot8_w(G8) > 1 ? (size_t)PILOT8_WAVES * (P == PREC_I8 ? 1 : 2) * QTV * 16 * 64 * 4 : 0; \
+        const size_t lds = W > 1 ? (size_t)PILOT8_WAVES * (P == PREC_I8 ? 1 : 2) * QTV * 16 * 64 * 4 : 0;            \
         hipLaunchKernelGGL((pilot8_scores_kernel<P, M, QTV>), grid, dim3(64 * PILOT8_WAVES), lds, st, Xq, rinit, \
-                           mask, Qq, qscal, G8, N, B, n_qblocks, n_tiles, n_sample, pslots, csum, chke);        \
+                           mask, Qq, qscal, G8, N, B, n_qblocks, n_tiles, n_sample, pslots, csum, chke, W);     \
         launched = true;                                                                                         \
     }
     VDB_PILOT8(PREC_I8, 0, 2) VDB_PILOT8(PREC_I8, 1, 2) VDB_PILOT8(PREC_I8, 0, 1) VDB_PILOT8(PREC_I8, 1, 1)
