@@ -178,8 +178,10 @@ constexpr int FIN_NB4 = VDB_FIN_WAVES > 8 ? 3 : 6;  // rows per wave per batch o
 // of row pieces in flight per wave; the loop form below keeps one 1 KiB piece per row in flight
 // and ran C3's exact keys at 150 us for 256 candidates x 256 queries, profiles/r04 fin stamps)
 constexpr int FIN_MP8 = 8;
+// (2 rows: C3 p50 0.522 -> 0.516 ms, QPS +0.3% now that its finish never runs beside the long-row
+// wide scan, profiles/r06_nb2; 175 VGPRs, no spills; round 5 had measured 1 better beside scan8)
 #ifndef VDB_FIN_NB8
-#define VDB_FIN_NB8 1
+#define VDB_FIN_NB8 2
 #endif
 constexpr int FIN_NB8 = VDB_FIN_NB8;
 
