@@ -1853,12 +1853,14 @@ static int32_t search_locked(vdb_index* ix, const float* queries, int32_t B, int
             // auto: batches of >= 32 (throughput: C2 under three streams 437 -> 453 K QPS, the finish
             // beside the next batch's scan), not single queries (one batch alone its 4 waves are
             // slower: C2 B = 2 step 0.195 -> 0.217 ms; B = 64 p50 0.213 -> 0.240; profiles/r06_fs)
-            // (and beside the short-row wide pass's small stage, batches of 32..256 at <= 128 dims);
+            // (and with the short-row wide pass, <= 128 dims: beside its small stage for <= 256
+            // queries; for C4's 512 three workgroups per CU instead of one, 366 -> 374 K QPS,
+            // profiles/r06_c4f);
             // auto also only while another search of the index is in flight: a batch alone keeps the
             // 16-wave form (its latency, the bench's p50)
             fa.small = D <= 1024 && (ix->finish_small == 1 ||
                                      (ix->finish_small < 0 && B >= 32 &&
-                                      ((wide_long && Gs <= 32) || (wide8 && !wide_long && B <= 256)) &&
+                                      ((wide_long && Gs <= 32) || (wide8 && !wide_long)) &&
                                       others_in_flight(ix, w))) ? 1 : 0;
             fa.split = fin_split; fa.sx_ek = fx_ek; fa.sx_ck = fx_ck; fa.sx_cr = fx_cr; fa.sx_n = fx_n; fa.done = done;
             HIP_TRY(launch_finish(ix->metric, KP, fa, B, st));
