@@ -1,6 +1,9 @@
 """Gap analysis of a three-stream kernel trace (rocprofv3 --kernel-trace csv): over the timed
 steady state, the share of wall time with a scan kernel running, and what runs (or nothing)
-while none does.  Usage: timeline6.py run_kernel_trace.csv"""
+while none does.  Usage: timeline6.py run_kernel_trace.csv
+Measured in round 6: under --kernel-trace the three streams' launches ran one at a time (C2: 240
+us per step traced against 145 us untraced, no kernel overlapping another), so the trace shows the
+serial chain per batch, not the overlap the bench gets."""
 import csv
 import sys
 from collections import defaultdict
