@@ -1010,7 +1010,11 @@ __global__ void __launch_bounds__(64 * FW, FW <= 4 ? 4 : 1) finish_kernel(Finish
             }
         }
     };
-    if (np <= FIN_MP) {
+    // launch_finish runs the 16- and 4-wave forms for D <= 1024 alone (when the default form has
+    // more than 8 waves), so they compile the register path only: 212 -> 0 bytes of scratch per
+    // lane, c4 shard +1.5% (profiles/r06_nosp; the 8-wave form keeps every path: pruned, C3 -1%)
+    constexpr bool kShortOnly = FW != 8 && VDB_FIN_WAVES > 8;
+    if (kShortOnly || np <= FIN_MP) {
         keys_regs(std::integral_constant<int, FIN_MP>{}, std::integral_constant<int, FIN_NB4>{});
     } else if (np <= FIN_MP8) {
         for (int j0 = wv * FIN_NB8; j0 < mx; j0 += FIN_WAVES * FIN_NB8) {
@@ -1030,7 +1034,7 @@ __global__ void __launch_bounds__(64 * FW, FW <= 4 ? 4 : 1) finish_kernel(Finish
                     if (u < nb) xek[j0 + u] = keys[u];
             }
         }
-    } else
+    } else if (!kShortOnly)
     for (int j0 = wv * FIN_NB; j0 < mx; j0 += FIN_WAVES * FIN_NB) {
         uint32_t rows[FIN_NB];
         double xn[FIN_NB];
@@ -1163,6 +1167,8 @@ hipError_t launch_finish(int metric, int KP, const FinishArgs& a, int B, hipStre
     if (a.split < 1 || (a.split > 1 && (!a.sx_ek || !a.sx_ck || !a.sx_cr || !a.sx_n || !a.done)))
         return hipErrorInvalidValue;
     const bool w8 = FIN_WAVES > 8 && a.D > 1024;
+    // (the forms' exact-key paths are compiled per row length, finish_kernel kShortOnly)
+    if (a.small && a.D > 1024) return hipErrorInvalidValue;
 #define VDB_FIN(M, KPV)                                                                                    \
     if (metric == M && KP == KPV) {                                                                        \
         if (a.small)                                                                                       \
