@@ -1,9 +1,9 @@
 """Gap analysis of a three-stream kernel trace (rocprofv3 --kernel-trace csv): over the timed
 steady state, the share of wall time with a scan kernel running, and what runs (or nothing)
 while none does.  Usage: timeline6.py run_kernel_trace.csv
-Measured in round 6: under --kernel-trace the three streams' launches ran one at a time (C2: 240
-us per step traced against 145 us untraced, no kernel overlapping another), so the trace shows the
-serial chain per batch, not the overlap the bench gets."""
+The window is the densest run of 40 consecutive launches of the scan kernel named by the optional
+second argument (the bench's timed three-stream loop; its p50 loop after it runs one batch at a
+time with a host sync per batch, which an earlier version of this script took by mistake)."""
 import csv
 import sys
 from collections import defaultdict
@@ -16,9 +16,11 @@ for r in rows:
     short = n.split('(')[0].replace('void ', '').replace('vdb::', '')
     ev.append((s, e, short, int(r.get('Stream_Id', 0) or 0)))
 ev.sort()
-scans = [x for x in ev if 'scan8' in x[2] and 'exact' not in x[2]]
-# steady state: the last 40 scans
-scans = scans[-40:]
+pat = sys.argv[2] if len(sys.argv) > 2 else 'scan8'
+scans = [x for x in ev if pat in x[2] and 'exact' not in x[2]]
+# steady state: the densest 40 consecutive scans (the timed loop)
+j = min(range(len(scans) - 39), key=lambda i: scans[i + 39][1] - scans[i][0])
+scans = scans[j:j + 40]
 t0, t1 = scans[0][0], scans[-1][1]
 win = [x for x in ev if x[1] > t0 and x[0] < t1]
 # sweep over time points
